@@ -1,0 +1,157 @@
+/*
+ * qasr_capi.h -- C-ABI of the MI355X-native Qwen3-ASR engine (libqasr.so).
+ *
+ * The reference has no plugin registry; its hot-path boundary is the C++
+ * class API listed below.  Each entry point here replaces one of those calls
+ * (SURVEY.md §8(b)); plain pointers and sizes only, no torch / HIP types.
+ *
+ *   qasr_model_load / qasr_model_free
+ *       <- Qwen3ASR::load_model           src/qwen3_asr.cpp:21-42
+ *          (AudioEncoder::load_model      src/audio_encoder.cpp:42-83,
+ *           TextDecoder::load_model       src/text_decoder.cpp:38-114,
+ *           GGUFLoader::load              src/gguf_loader.cpp:17-53)
+ *   qasr_ctx_create / qasr_ctx_free
+ *       <- TextDecoder::init_kv_cache     src/text_decoder.cpp:337-386
+ *   qasr_mel
+ *       <- log_mel_spectrogram            src/mel_spectrogram.h:53-55 / .cpp:484-628
+ *   qasr_encode, qasr_encode_conv
+ *       <- AudioEncoder::encode           src/audio_encoder.h:27 / .cpp:312-601
+ *          AudioEncoder::encode_conv_only src/audio_encoder.h:30
+ *   qasr_prefill
+ *       <- TextDecoder::forward_with_audio src/text_decoder.h:134-137 / .cpp:588-684
+ *   qasr_decode_step
+ *       <- TextDecoder::forward           src/text_decoder.h:125-126 / .cpp:583-586
+ *          + Qwen3ASR::sample_greedy      src/qwen3_asr.cpp:305-317 (fused argmax)
+ *   qasr_transcribe_batch / qasr_stage_audio + qasr_run
+ *       <- Qwen3ASR::transcribe_internal  src/qwen3_asr.cpp:81-149
+ *          + decode_greedy                src/qwen3_asr.cpp:216-303
+ *   qasr_detokenize / qasr_tokenize
+ *       <- TextDecoder::decode_tokens / tokenize src/text_decoder.cpp:1069-1103
+ *
+ * Conventions (mirroring the reference's):
+ *   - return value: 0 = OK, nonzero = error; message via qasr_last_error().
+ *     Nothing throws across the boundary.
+ *   - host pointers are caller-owned; outputs are written into caller
+ *     buffers sized by the documented formula (query helpers provided).
+ *   - a context owns its device buffers, KV cache and HIP stream; calls on
+ *     one context are stream-ordered and NOT thread-safe (one context per
+ *     host thread), exactly as the reference's objects.
+ *   - layouts: mel [128][T] mel-major; features [N][1024] row-major; logits
+ *     [151936] fp32 (last row only); token ids int32.
+ */
+#ifndef QASR_CAPI_H
+#define QASR_CAPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct qasr_model qasr_model;
+typedef struct qasr_ctx qasr_ctx;
+
+#define QASR_OK 0
+#define QASR_ERR_ARG 1
+#define QASR_ERR_IO 2
+#define QASR_ERR_FORMAT 3
+#define QASR_ERR_DEVICE 4
+#define QASR_ERR_STATE 5
+
+typedef struct {
+    /* audio encoder (src/gguf_loader.h:15-25) */
+    int32_t enc_layers, d_model, enc_heads, enc_ffn, conv_channels, n_mel;
+    float enc_eps;
+    /* text decoder (src/text_decoder.h:15-31) */
+    int32_t vocab_size, hidden_size, dec_layers, n_heads, n_kv_heads, head_dim, dec_ffn;
+    float rms_eps, rope_theta;
+    int32_t eos_id, pad_id, audio_start_id, audio_end_id, audio_pad_id;
+    int32_t weight_type; /* ggml type of the 2-D linear weights: 1 = F16, 8 = Q8_0 */
+} qasr_hparams;
+
+typedef struct {
+    double t_mel_ms, t_encode_ms, t_prefill_ms, t_decode_ms, t_total_ms;  /* device (HIP event) time */
+    int32_t n_decode_steps;
+} qasr_timings;
+
+/* ---- errors / version ---------------------------------------------------- */
+const char *qasr_last_error(void);                 /* thread-local last message */
+const char *qasr_version(void);
+int qasr_device_count(int *n);
+
+/* ---- model ---------------------------------------------------------------- */
+int qasr_model_load(const char *gguf_path, int device, qasr_model **out);
+void qasr_model_free(qasr_model *m);
+int qasr_model_hparams(const qasr_model *m, qasr_hparams *out);
+/* device bytes held by the weight arena */
+int64_t qasr_model_device_bytes(const qasr_model *m);
+
+/* ---- context -------------------------------------------------------------- */
+/* max_batch: clips per call; max_ctx: decoder positions per sequence
+ * (prompt + max_tokens, src/qwen3_asr.cpp:223). */
+int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_ctx **out);
+void qasr_ctx_free(qasr_ctx *c);
+
+/* ---- size helpers (host-only arithmetic) ---------------------------------- */
+int qasr_mel_frames(int n_samples);               /* n/160 (src/mel_spectrogram.cpp:517-522) */
+int qasr_encoder_frames(int n_mel_frames);        /* src/audio_encoder.cpp:304-343 */
+int qasr_prompt_len(int n_audio_frames);          /* n + 15 (src/qwen3_asr.cpp:170-209) */
+/* build the reference chat prompt (no system prompt); returns P, writes
+ * ids[P] and the first <|audio_pad|> index to *audio_pos. */
+int qasr_build_prompt(const qasr_model *m, int n_audio_frames, int32_t *ids, int *audio_pos);
+
+/* ---- stages (host buffers in/out; each call synchronises its stream) ---- */
+/* B clips: pcm[b] has n[b] samples; mel_out receives B blocks of [128][T_b]
+ * back to back, T_b = qasr_mel_frames(n[b]). */
+int qasr_mel(qasr_ctx *c, const float *const *pcm, const int *n, int B, float *mel_out);
+/* mel: B blocks [128][T_b] back to back; feats: [sum N_b][hidden] */
+int qasr_encode(qasr_ctx *c, const float *mel, const int *T, int B, float *feats);
+/* conv front-end + positional embedding only: [sum N_b][d_model] */
+int qasr_encode_conv(qasr_ctx *c, const float *mel, const int *T, int B, float *out);
+/* Prefill B sequences from n_past = 0 (the KV cache of sequence b is reset).
+ * ids: sum P_b tokens back to back; feats: sum N_b rows of [hidden];
+ * audio_pos[b]: first pad index (splice rows [audio_pos, audio_pos+N_b));
+ * logits_last (optional) [B][vocab]; argmax (optional) [B]. */
+int qasr_prefill(qasr_ctx *c, const int32_t *ids, const int *P, const float *feats,
+                 const int *audio_pos, const int *N, int B, float *logits_last, int32_t *argmax);
+/* One decode step for B sequences at positions n_past[b] (token tok[b]). */
+int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_past, int B,
+                     float *logits, int32_t *argmax);
+
+/* ---- whole path ----------------------------------------------------------- */
+/* Stage PCM into device HBM (one H2D copy); qasr_run then works from HBM. */
+int qasr_stage_audio(qasr_ctx *c, const float *const *pcm, const int *n, int B);
+/* Greedy transcription of the staged clips: tokens [B][max_tokens],
+ * n_tokens[B] (trailing EOS popped as src/qwen3_asr.cpp:298-300).
+ * ignore_eos != 0: fixed budget of max_tokens steps (throughput mode). */
+int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *tokens, int *n_tokens,
+             qasr_timings *t);
+/* Optional system-prompt token ids inserted by qasr_run after
+ * "<|im_start|>system\n" (src/qwen3_asr.cpp:186-190); n = 0 clears. */
+int qasr_set_system_prompt(qasr_ctx *c, const int32_t *ids, int n);
+int qasr_transcribe_batch(qasr_ctx *c, const float *const *pcm, const int *n, int B, int max_tokens,
+                          int ignore_eos, int32_t *tokens, int *n_tokens, qasr_timings *t);
+
+/* ---- text (host) ---------------------------------------------------------- */
+/* UTF-8 text for ids (special <|..|> and [PAD..] tokens skipped); returns the
+ * byte length (excluding NUL), writes at most cap-1 bytes + NUL. */
+int qasr_detokenize(const qasr_model *m, const int32_t *ids, int n, char *out, int cap);
+/* byte-level BPE; returns number of ids (writes at most cap). */
+int qasr_tokenize(const qasr_model *m, const char *text, int32_t *ids, int cap);
+
+/* ---- host utilities (no device needed) ------------------------------------ */
+/* PCM16 RIFF reader (src/mel_spectrogram.cpp:130-221); returns n or -1.
+ * out may be NULL to query n. */
+int qasr_load_wav(const char *path, float *out, int max_n, int *sample_rate);
+int qasr_write_wav(const char *path, const float *pcm, int n, int sample_rate);
+/* deterministic synthetic clip: seed 1000+i recipe */
+int qasr_synth_pcm(uint64_t seed, int n_samples, float *out);
+/* synthetic GGUF with the reference tensor names/shapes/dtypes.
+ * config: "full" (Qwen3-ASR-0.6B dims) or "tiny" (test dims);
+ * wtype: 1 = f16, 8 = q8_0 for linear weights. */
+int qasr_write_synthetic_gguf(const char *path, const char *config, uint64_t seed, int wtype);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,95 @@
+// qwen3_asr.h -- C++17 pipeline API, kept verbatim from the reference's
+// src/qwen3_asr.h:15-116 (transcribe_params / transcribe_result / Qwen3ASR),
+// implemented over the C-ABI of libqasr.so (include/qasr_capi.h) instead of
+// ggml graphs.  Existing callers of the reference library recompile against
+// this header unchanged.
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "qasr_capi.h"
+
+namespace qwen3_asr {
+
+// src/text_decoder.h:15-31
+struct text_decoder_config {
+    int32_t vocab_size = 151936;
+    int32_t hidden_size = 1024;
+    int32_t n_decoder_layers = 28;
+    int32_t n_attention_heads = 16;
+    int32_t n_key_value_heads = 8;
+    int32_t intermediate_size = 3072;
+    int32_t head_dim = 128;
+    float rms_norm_eps = 1e-6f;
+    float rope_theta = 1000000.0f;
+    int32_t pad_token_id = 151643;
+    int32_t eos_token_id = 151645;
+    int32_t audio_start_token_id = 151669;
+    int32_t audio_end_token_id = 151670;
+    int32_t audio_pad_token_id = 151676;
+};
+
+// src/qwen3_asr.h:15-34
+struct transcribe_params {
+    int32_t max_tokens = 1024;
+    std::string language = "";       // accepted, ignored (as src/qwen3_asr.cpp:211)
+    std::string system_prompt = "";
+    int32_t n_threads = 4;            // accepted for API compatibility (no host threads on the hot path)
+    bool print_progress = false;
+    bool print_timing = true;
+};
+
+// src/qwen3_asr.h:37-49
+struct transcribe_result {
+    std::string text;
+    std::vector<int32_t> tokens;
+    bool success = false;
+    std::string error_msg;
+    int64_t t_load_ms = 0;
+    int64_t t_mel_ms = 0;
+    int64_t t_encode_ms = 0;
+    int64_t t_decode_ms = 0;   // prefill + greedy loop, as the reference's decode_greedy
+    int64_t t_total_ms = 0;
+};
+
+using progress_callback_t = std::function<void(int tokens_generated, int max_tokens)>;
+
+// src/qwen3_asr.h:55-116
+class Qwen3ASR {
+public:
+    Qwen3ASR();
+    ~Qwen3ASR();
+    Qwen3ASR(const Qwen3ASR &) = delete;
+    Qwen3ASR &operator=(const Qwen3ASR &) = delete;
+
+    bool load_model(const std::string &model_path);
+    transcribe_result transcribe(const std::string &audio_path, const transcribe_params &params = transcribe_params());
+    transcribe_result transcribe(const float *samples, int n_samples, const transcribe_params &params = transcribe_params());
+    void set_progress_callback(progress_callback_t callback);
+    const std::string &get_error() const { return error_msg_; }
+    bool is_loaded() const { return model_ != nullptr; }
+    const text_decoder_config &get_config() const { return config_; }
+
+    // MI355X additions: device selection and batched transcription.
+    void set_device(int device) { device_ = device; }
+    std::vector<transcribe_result> transcribe_batch(const std::vector<std::vector<float>> &clips,
+                                                    const transcribe_params &params = transcribe_params());
+
+private:
+    transcribe_result transcribe_internal(const float *samples, int n_samples, const transcribe_params &params);
+    bool ensure_ctx(int batch, int n_ctx);
+
+    qasr_model *model_ = nullptr;
+    qasr_ctx *ctx_ = nullptr;
+    int ctx_batch_ = 0, ctx_len_ = 0, device_ = 0;
+    text_decoder_config config_;
+    std::string error_msg_;
+    progress_callback_t progress_callback_;
+};
+
+bool load_audio_file(const std::string &path, std::vector<float> &samples, int &sample_rate);
+
+}  // namespace qwen3_asr

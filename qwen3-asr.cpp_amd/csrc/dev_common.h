@@ -1,0 +1,66 @@
+// dev_common.h -- shared device helpers for the gfx950 kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef _Float16 f16;
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define WAVE 64
+
+__device__ __forceinline__ float h2f(f16 h) { return (float)h; }
+// fp32 -> fp16 round-to-nearest-even (v_cvt_f16_f32 under the default mode),
+// identical to ggml's GGML_CPU_FP32_TO_FP16 / F16C _cvtss_sh(x, 0).
+__device__ __forceinline__ f16 f2h(float f) { return (f16)f; }
+__device__ __forceinline__ float u16_to_f(uint16_t u) { return (float)__builtin_bit_cast(f16, u); }
+__device__ __forceinline__ uint16_t f_to_u16(float f) { return __builtin_bit_cast(uint16_t, (f16)f); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// total order on finite doubles as unsigned 64-bit keys (for atomicMax)
+__device__ __forceinline__ unsigned long long dkey(double d) {
+    unsigned long long u = __double_as_longlong(d);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double dkey_inv(unsigned long long k) {
+    unsigned long long u = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+    return __longlong_as_double(u);
+}
+// argmax key: larger value wins, ties -> lower index (src/qwen3_asr.cpp:309-313 strict '>')
+__device__ __forceinline__ unsigned long long argmax_key(float v, int idx) {
+    uint32_t u = __float_as_uint(v);
+    u = (u >> 31) ? ~u : (u | 0x80000000u);
+    return ((unsigned long long)u << 32) | (unsigned long long)(0xffffffffu - (uint32_t)idx);
+}
+__device__ __forceinline__ int argmax_key_idx(unsigned long long k) { return (int)(0xffffffffu - (uint32_t)(k & 0xffffffffu)); }
+
+// non-contracted fp32 ops (ggml computes these as separate ops, each rounded)
+__device__ __forceinline__ float fmul_rn(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float fadd_rn(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float fsub_rn(float a, float b) { return __fsub_rn(a, b); }
+
+// ggml tanh-GELU through the fp16 table (GGML_GELU_FP16)
+__device__ __forceinline__ float gelu_lut(float x, const uint16_t *__restrict__ lut) {
+    if (x <= -10.0f) return 0.0f;
+    if (x >= 10.0f) return x;
+    return u16_to_f(lut[f_to_u16(x)]);
+}

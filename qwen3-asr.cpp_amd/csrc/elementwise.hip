@@ -1,0 +1,217 @@
+// elementwise.hip -- memory-bound kernels: conv1, norms, embedding/splice,
+// argmax finish and decode-step bookkeeping.
+#include "dev_common.h"
+#include "kernels.h"
+
+namespace qasr {
+
+__device__ __forceinline__ int find_chunk_e(const int *__restrict__ starts, int n, int r) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (starts[mid] <= r) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// ------------------------------------------------------------------ conv1
+// src/audio_encoder.cpp:105-112: ggml_conv_2d(1 -> C) = im2col(fp16) x fp16
+// kernel.  K = 9 is below ggml's SIMD step, so ggml's vec_dot_f16 sums the 9
+// exact fp16 products in double (its scalar leftover loop); we do the same.
+// One wave per output position; lanes sweep the C output channels (coalesced
+// NHWC stores).
+__global__ __launch_bounds__(256) void conv1_kernel(const float *__restrict__ mel, const ChunkDesc *__restrict__ chunks,
+                                                    const int *__restrict__ row1_start, int n_chunks, int rows1,
+                                                    const uint16_t *__restrict__ w, const float *__restrict__ b,
+                                                    const uint16_t *__restrict__ lut, int C, uint16_t *__restrict__ act1) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows1) return;
+    const int c = find_chunk_e(row1_start, n_chunks, row);
+    const ChunkDesc cd = chunks[c];
+    const int local = row - cd.row1;
+    const int oh = local / cd.W1, ow = local - oh * cd.W1;
+    float in[9];
+#pragma unroll
+    for (int kh = 0; kh < 3; kh++)
+#pragma unroll
+        for (int kw = 0; kw < 3; kw++) {
+            const int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;   // ih: mel bin, iw: frame in chunk
+            float v = 0.0f;
+            if (ih >= 0 && ih < 128 && iw >= 0 && iw < cd.L) v = mel[cd.mel_off + (long)ih * cd.T + iw];
+            in[kh * 3 + kw] = h2f(f2h(v));
+        }
+    for (int oc = lane; oc < C; oc += 64) {
+        double s = 0.0;
+#pragma unroll
+        for (int t = 0; t < 9; t++) s += (double)(in[t] * u16_to_f(w[oc * 9 + t]));
+        const float v = fadd_rn((float)s, b[oc]);
+        act1[(long)row * C + oc] = f_to_u16(gelu_lut(v, lut));
+    }
+}
+
+void launch_conv1(const float *mel, const ChunkDesc *chunks, const int *row1_start, int n_chunks, int rows1,
+                  const uint16_t *w, const float *b, const uint16_t *gelu, int C, uint16_t *act1, hipStream_t s) {
+    if (rows1 <= 0) return;
+    hipLaunchKernelGGL(conv1_kernel, dim3((rows1 + 3) / 4), dim3(256), 0, s, mel, chunks, row1_start, n_chunks, rows1, w, b,
+                       gelu, C, act1);
+}
+
+// ------------------------------------------------------------------ norms
+// ggml_norm: mean and centred variance summed in double, scale = 1/sqrtf(var+eps);
+// then ggml_mul(w), ggml_add(b) as separately rounded fp32 ops; output rounded
+// to fp16 (what the following ggml_mul_mat does to its input).
+template <int D>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict__ x, int M, const float *__restrict__ w,
+                                                        const float *__restrict__ b, float eps, uint16_t *__restrict__ y) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= M) return;
+    constexpr int PER = (D + 63) / 64;
+    const float *xr = x + (long)row * D;
+    float v[PER];
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+        const int k = lane + 64 * i;
+        v[i] = k < D ? xr[k] : 0.0f;
+        s += (double)v[i];
+    }
+    s = wave_sum_d(s);
+    const float mean = (float)(s / D);
+    double s2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+        const int k = lane + 64 * i;
+        if (k < D) {
+            v[i] = fsub_rn(v[i], mean);
+            s2 += (double)fmul_rn(v[i], v[i]);
+        }
+    }
+    s2 = wave_sum_d(s2);
+    const float var = (float)(s2 / D);
+    const float scale = 1.0f / sqrtf(var + eps);
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+        const int k = lane + 64 * i;
+        if (k < D) {
+            float t = fmul_rn(v[i], scale);
+            if (w) t = fmul_rn(t, w[k]);
+            if (b) t = fadd_rn(t, b[k]);
+            y[(long)row * D + k] = f_to_u16(t);
+        }
+    }
+}
+
+void launch_layernorm_f16(const float *x, int M, int D, const float *w, const float *b, float eps, uint16_t *y, hipStream_t s) {
+    if (M <= 0) return;
+    dim3 grid((M + 3) / 4);
+    switch (D) {
+        case 896: hipLaunchKernelGGL(layernorm_kernel<896>, grid, dim3(256), 0, s, x, M, w, b, eps, y); break;
+        case 256: hipLaunchKernelGGL(layernorm_kernel<256>, grid, dim3(256), 0, s, x, M, w, b, eps, y); break;
+        case 1024: hipLaunchKernelGGL(layernorm_kernel<1024>, grid, dim3(256), 0, s, x, M, w, b, eps, y); break;
+        default: hipLaunchKernelGGL(layernorm_kernel<2048>, grid, dim3(256), 0, s, x, M, w, b, eps, y); break;
+    }
+}
+
+// ggml_rms_norm: sum of squares (fp32 products) in double; scale = 1/sqrtf(mean+eps)
+template <int D>
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const float *__restrict__ x, int ldx, const int *__restrict__ row_idx, int M,
+                                                      const float *__restrict__ w, float eps, uint16_t *__restrict__ y) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= M) return;
+    constexpr int PER = (D + 63) / 64;
+    const int src = row_idx ? row_idx[row] : row;
+    const float *xr = x + (long)src * ldx;
+    float v[PER];
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+        const int k = lane + 64 * i;
+        v[i] = k < D ? xr[k] : 0.0f;
+        s += (double)fmul_rn(v[i], v[i]);
+    }
+    s = wave_sum_d(s);
+    const float mean = (float)(s / D);
+    const float scale = 1.0f / sqrtf(mean + eps);
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+        const int k = lane + 64 * i;
+        if (k < D) y[(long)row * D + k] = f_to_u16(fmul_rn(fmul_rn(v[i], scale), w[k]));
+    }
+}
+
+void launch_rmsnorm_f16(const float *x, int ldx, const int *row_idx, int M, int D, const float *w, float eps, uint16_t *y,
+                        hipStream_t s) {
+    if (M <= 0) return;
+    dim3 grid((M + 3) / 4);
+    switch (D) {
+        case 1024: hipLaunchKernelGGL(rmsnorm_kernel<1024>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y); break;
+        case 256: hipLaunchKernelGGL(rmsnorm_kernel<256>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y); break;
+        default: hipLaunchKernelGGL(rmsnorm_kernel<2048>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y); break;
+    }
+}
+
+// --------------------------------------------------------- embedding/splice
+__global__ __launch_bounds__(256) void embed_kernel(const int32_t *__restrict__ ids, int rows, const uint16_t *__restrict__ embd,
+                                                    int hidden, const float *__restrict__ audio,
+                                                    const int *__restrict__ row_audio, float *__restrict__ x) {
+    const int row = blockIdx.x;
+    if (row >= rows) return;
+    const int ar = row_audio ? row_audio[row] : -1;
+    float *dst = x + (long)row * hidden;
+    if (ar >= 0) {
+        const float *srcp = audio + (long)ar * hidden;
+        for (int k = threadIdx.x; k < hidden; k += 256) dst[k] = srcp[k];
+    } else {
+        const uint16_t *srcp = embd + (long)ids[row] * hidden;
+        for (int k = threadIdx.x; k < hidden; k += 256) dst[k] = u16_to_f(srcp[k]);
+    }
+}
+
+void launch_embed(const int32_t *ids, int rows, const uint16_t *embd, int hidden, const float *audio, const int *row_audio,
+                  float *x, hipStream_t s) {
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(embed_kernel, dim3(rows), dim3(256), 0, s, ids, rows, embd, hidden, audio, row_audio, x);
+}
+
+// ------------------------------------------------------------ argmax etc.
+__global__ void argmax_finish_kernel(const unsigned long long *__restrict__ amax, int B, int32_t *__restrict__ ids,
+                                     int32_t *__restrict__ hist, int hist_stride, const int *__restrict__ step) {
+    const int b = threadIdx.x;
+    if (b >= B) return;
+    const int id = argmax_key_idx(amax[b]);
+    ids[b] = id;
+    if (hist) hist[(long)b * hist_stride + *step] = id;
+}
+
+void launch_argmax_finish(const unsigned long long *amax, int B, int32_t *ids, int32_t *hist, int hist_stride, const int *step,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(argmax_finish_kernel, dim3(1), dim3(256), 0, s, amax, B, ids, hist, hist_stride, step);
+}
+
+__global__ void fill_u64_kernel(unsigned long long *p, int n, unsigned long long v) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+void launch_fill_u64(unsigned long long *p, int n, unsigned long long v, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(fill_u64_kernel, dim3((n + 255) / 256), dim3(256), 0, s, p, n, v);
+}
+
+__global__ void step_advance_kernel(int *row_pos, int *n_kv, int *step, int B) {
+    const int b = threadIdx.x;
+    if (b < B) {
+        row_pos[b] += 1;
+        n_kv[b] += 1;
+    }
+    if (b == 0) *step += 1;
+}
+
+void launch_step_advance(int *row_pos, int *n_kv, int *step, int B, hipStream_t s) {
+    hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(256), 0, s, row_pos, n_kv, step, B);
+}
+
+}  // namespace qasr

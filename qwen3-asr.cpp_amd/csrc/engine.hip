@@ -1,0 +1,1048 @@
+// engine.hip -- C-ABI implementation (include/qasr_capi.h): device weight
+// arena, per-context buffers, and the hot path
+//   PCM -> mel -> conv front-end -> encoder -> prompt + splice -> prefill ->
+//   greedy decode (HIP-graph replayed step) -> token ids
+// restating Qwen3ASR::transcribe_internal (src/qwen3_asr.cpp:81-149) on HIP.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/qasr_capi.h"
+#include "../host/gguf.h"
+#include "../host/qasr_host.h"
+#include "kernels.h"
+
+using namespace qasr;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(x)                                                                                  \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) return fail(QASR_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// ------------------------------------------------------------------ model
+struct EncLayer {
+    uint16_t *wqkv, *wo, *w1, *w2;
+    float *bqkv, *bo, *b1, *b2, *ln1_w, *ln1_b, *ln2_w, *ln2_b;
+};
+struct DecLayer {
+    float *attn_norm, *q_norm, *k_norm, *ffn_norm;
+    uint16_t *wqkv, *wo, *wgu, *wd;
+};
+
+struct qasr_model {
+    Hparams hp;
+    int device = 0;
+    Tokenizer tok;
+    char *arena = nullptr;
+    size_t arena_bytes = 0;
+    uint16_t *conv1_w, *conv2_w, *conv3_w, *conv_out_w, *proj1_w, *proj2_w, *embd;
+    float *conv1_b, *conv2_b, *conv3_b, *ln_post_w, *ln_post_b, *proj1_b, *proj2_b, *out_norm;
+    std::vector<EncLayer> enc;
+    std::vector<DecLayer> dec;
+    uint16_t *gelu;
+    float *pe, *filters;
+    double2 *tw;
+    double *hann;
+    ~qasr_model() {
+        if (arena) {
+            (void)hipSetDevice(device);
+            (void)hipFree(arena);
+        }
+    }
+};
+
+// --------------------------------------------------------------- context
+struct DevBuf {
+    void *p = nullptr;
+    size_t n = 0;
+    template <class T> T *as() const { return (T *)p; }
+};
+
+struct qasr_ctx {
+    qasr_model *m = nullptr;
+    int max_batch = 0, max_ctx = 0;
+    hipStream_t st = nullptr;
+    hipEvent_t ev[8] = {};
+    uint16_t *kc = nullptr, *vc = nullptr;
+    float *rope = nullptr;
+    std::vector<DevBuf> owned;     // everything hipMalloc'ed by the context
+    // grow-on-demand scratch
+    DevBuf pcm, mel, meltmp, melmax, melclips, melblocks;
+    DevBuf chunks, rs1, rs2, rs3, pepos, act1, act2, act3;
+    DevBuf ex, exh, eqkv, eatt, eff, feats, segs;
+    DevBuf px, pxh, pqkv, pq, patt, pact, prow, plast, pids, pxl;
+    // fixed decode state (sized by max_batch)
+    int32_t *d_tok = nullptr, *d_hist = nullptr;
+    int *d_pos = nullptr, *d_nkv = nullptr, *d_slot = nullptr, *d_step = nullptr;
+    float *d_x = nullptr, *d_qkv = nullptr, *d_part_o = nullptr, *d_part_ml = nullptr, *d_logits = nullptr;
+    uint16_t *d_q = nullptr, *d_att = nullptr, *d_act = nullptr, *d_xh = nullptr;
+    unsigned long long *d_amax = nullptr;
+    int max_splits = 0, split_len = 256, hist_cap = 0;
+    // pinned host staging for small per-call tables (reset at each top-level call)
+    char *pin = nullptr;
+    size_t pin_cap = 0, pin_used = 0;
+    std::vector<int32_t> sys_ids;
+    // staged audio
+    std::vector<int> staged_n;
+    std::vector<long> staged_off;
+    // decode graph
+    hipGraphExec_t graph = nullptr;
+    int graph_B = -1;
+    bool graph_logits = false;
+    ~qasr_ctx() {
+        (void)hipSetDevice(m->device);
+        if (graph) (void)hipGraphExecDestroy(graph);
+        for (auto &b : owned) (void)hipFree(b.p);
+        for (auto &e : ev) if (e) (void)hipEventDestroy(e);
+        if (pin) (void)hipHostFree(pin);
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+
+static int dev_alloc(qasr_ctx *c, void **p, size_t bytes) {
+    HIPCHK(hipMalloc(p, bytes ? bytes : 256));
+    c->owned.push_back({*p, bytes});
+    return 0;
+}
+
+// grow a scratch buffer (contents are not preserved)
+static int ensure(qasr_ctx *c, DevBuf &b, size_t bytes) {
+    if (b.n >= bytes && b.p) return 0;
+    if (b.p) {
+        HIPCHK(hipStreamSynchronize(c->st));
+        for (auto it = c->owned.begin(); it != c->owned.end(); ++it)
+            if (it->p == b.p) { c->owned.erase(it); break; }
+        HIPCHK(hipFree(b.p));
+        b.p = nullptr;
+    }
+    size_t n = std::max<size_t>(bytes + bytes / 4, 4096);
+    HIPCHK(hipMalloc(&b.p, n));
+    b.n = n;
+    c->owned.push_back({b.p, n});
+    return 0;
+}
+
+// Small per-call tables go through a pinned staging area so the async copy
+// never reads a host vector that has gone out of scope.
+template <class T>
+static int upload(qasr_ctx *c, DevBuf &b, const std::vector<T> &v) {
+    const size_t bytes = v.size() * sizeof(T);
+    int rc = ensure(c, b, bytes);
+    if (rc || !bytes) return rc;
+    const size_t need = (bytes + 255) / 256 * 256;
+    if (c->pin_used + need > c->pin_cap) {
+        HIPCHK(hipStreamSynchronize(c->st));   // every earlier staged copy has landed
+        c->pin_used = 0;
+        if (need > c->pin_cap) {
+            if (c->pin) HIPCHK(hipHostFree(c->pin));
+            c->pin_cap = std::max<size_t>(need * 2, 1 << 20);
+            HIPCHK(hipHostMalloc((void **)&c->pin, c->pin_cap, hipHostMallocDefault));
+        }
+    }
+    char *h = c->pin + c->pin_used;
+    c->pin_used += need;
+    memcpy(h, v.data(), bytes);
+    HIPCHK(hipMemcpyAsync(b.p, h, bytes, hipMemcpyHostToDevice, c->st));
+    return 0;
+}
+
+// ----------------------------------------------------------------- errors
+extern "C" const char *qasr_last_error(void) { return g_err.c_str(); }
+extern "C" const char *qasr_version(void) { return "qasr-mi355x 0.1.0 (gfx950)"; }
+extern "C" int qasr_device_count(int *n) {
+    int k = 0;
+    if (hipGetDeviceCount(&k) != hipSuccess) k = 0;
+    if (n) *n = k;
+    return 0;
+}
+
+// -------------------------------------------------------------- loading
+struct Up {
+    std::string name;
+    size_t bytes;
+    void **dst;
+    std::function<void(uint8_t *)> fill;
+};
+
+static bool check_shape(const gguf_tensor *t, std::vector<int64_t> ne, uint32_t want_type, std::string &err) {
+    if (!t) { err = "missing tensor"; return false; }
+    int64_t n = 1, m = 1;
+    for (auto v : ne) n *= v;
+    for (auto v : t->ne) m *= v;
+    if (n != m) {
+        err = "tensor " + t->name + ": expected " + std::to_string(n) + " elements, file has " + std::to_string(m);
+        return false;
+    }
+    if (t->type != want_type) {
+        err = "tensor " + t->name + ": unsupported ggml type " + std::to_string(t->type) +
+              (want_type == DT_F16 ? " (this build supports F16 2-D weights)" : " (expected F32)");
+        return false;
+    }
+    return true;
+}
+
+extern "C" int qasr_model_load(const char *path, int device, qasr_model **out) {
+    if (!path || !out) return fail(QASR_ERR_ARG, "null argument");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(QASR_ERR_DEVICE, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(QASR_ERR_ARG, "bad device index");
+    HIPCHK(hipSetDevice(device));
+    GGUFFile f;
+    if (!f.open(path)) return fail(QASR_ERR_IO, f.error());
+    std::unique_ptr<qasr_model> m(new qasr_model());
+    m->device = device;
+    m->hp = read_hparams(f);
+    const Hparams &hp = m->hp;
+    std::string err;
+    if (!m->tok.load(f, err)) return fail(QASR_ERR_FORMAT, err);
+    if (hp.d_model / hp.enc_heads != 64 || hp.d_model % hp.enc_heads)
+        return fail(QASR_ERR_FORMAT, "encoder head_dim must be 64");
+    if (hp.head_dim != 128 || hp.n_head != 2 * hp.n_kv_head)
+        return fail(QASR_ERR_FORMAT, "decoder must have head_dim 128 and GQA ratio 2");
+    if (hp.n_mel != 128) return fail(QASR_ERR_FORMAT, "n_mel must be 128");
+    if (hp.conv_ch % 32 || hp.dec_ffn % 16) return fail(QASR_ERR_FORMAT, "unsupported conv/ffn width");
+
+    const int C = hp.conv_ch, D = hp.d_model, FF = hp.enc_ffn, H = hp.hidden, V = hp.vocab;
+    const int QD = hp.n_head * 128, KD = hp.n_kv_head * 128, F = hp.dec_ffn;
+    m->enc.resize(hp.enc_layers);
+    m->dec.resize(hp.dec_layers);
+    std::vector<Up> ups;
+    auto T = [&](const std::string &n) { return f.tensor(n); };
+    auto need = [&](const std::string &n, std::vector<int64_t> ne, uint32_t ty) -> const gguf_tensor * {
+        const gguf_tensor *t = T(n);
+        std::string e;
+        if (!t) { if (err.empty()) err = "missing tensor: " + n; return nullptr; }
+        if (!check_shape(t, ne, ty, e)) { if (err.empty()) err = e; return nullptr; }
+        return t;
+    };
+    auto copy_f32 = [&](const std::string &n, int64_t len, float **dst) {
+        const gguf_tensor *t = need(n, {len}, DT_F32);
+        if (!t) return;
+        ups.push_back({n, (size_t)len * 4, (void **)dst, [t, len](uint8_t *o) { memcpy(o, t->data, (size_t)len * 4); }});
+    };
+    auto copy_f16 = [&](const std::string &n, std::vector<int64_t> ne, uint16_t **dst) {
+        const gguf_tensor *t = need(n, ne, DT_F16);
+        if (!t) return;
+        size_t bytes = t->nbytes;
+        ups.push_back({n, bytes, (void **)dst, [t, bytes](uint8_t *o) { memcpy(o, t->data, bytes); }});
+    };
+    // conv kernels: [oc][ic][kh][kw] -> [oc][kh][kw][ic] (im2col K order of the implicit GEMM)
+    auto conv_w = [&](const std::string &n, int IC, uint16_t **dst) {
+        const gguf_tensor *t = need(n, {3, 3, IC, C}, DT_F16);
+        if (!t) return;
+        ups.push_back({n, (size_t)C * IC * 9 * 2, (void **)dst, [t, IC, C](uint8_t *o) {
+                           const uint16_t *s = (const uint16_t *)t->data;
+                           uint16_t *d = (uint16_t *)o;
+                           for (int oc = 0; oc < C; oc++)
+                               for (int ic = 0; ic < IC; ic++)
+                                   for (int k = 0; k < 9; k++) d[((size_t)oc * 9 + k) * IC + ic] = s[((size_t)oc * IC + ic) * 9 + k];
+                       }});
+    };
+    copy_f16("audio.encoder.conv1.weight", {3, 3, 1, C}, &m->conv1_w);
+    copy_f32("audio.encoder.conv1.bias", C, &m->conv1_b);
+    conv_w("audio.encoder.conv2.weight", C, &m->conv2_w);
+    copy_f32("audio.encoder.conv2.bias", C, &m->conv2_b);
+    conv_w("audio.encoder.conv3.weight", C, &m->conv3_w);
+    copy_f32("audio.encoder.conv3.bias", C, &m->conv3_b);
+    {   // conv_out: input feature c*16+h (src/audio_encoder.cpp:133-142) -> h*C + c
+        const gguf_tensor *t = need("audio.encoder.conv_out.weight", {(int64_t)C * 16, D}, DT_F16);
+        if (t)
+            ups.push_back({t->name, (size_t)D * C * 16 * 2, (void **)&m->conv_out_w, [t, C, D](uint8_t *o) {
+                               const uint16_t *s = (const uint16_t *)t->data;
+                               uint16_t *d = (uint16_t *)o;
+                               for (int n = 0; n < D; n++)
+                                   for (int c = 0; c < C; c++)
+                                       for (int h = 0; h < 16; h++) d[(size_t)n * C * 16 + h * C + c] = s[(size_t)n * C * 16 + c * 16 + h];
+                           }});
+    }
+    for (int l = 0; l < hp.enc_layers; l++) {
+        const std::string p = "audio.encoder.blk." + std::to_string(l) + ".";
+        EncLayer &L = m->enc[l];
+        const gguf_tensor *q = need(p + "attn_q.weight", {D, D}, DT_F16), *k = need(p + "attn_k.weight", {D, D}, DT_F16),
+                          *v = need(p + "attn_v.weight", {D, D}, DT_F16);
+        const gguf_tensor *qb = need(p + "attn_q.bias", {D}, DT_F32), *kb = need(p + "attn_k.bias", {D}, DT_F32),
+                          *vb = need(p + "attn_v.bias", {D}, DT_F32);
+        if (q && k && v && qb && kb && vb) {
+            const size_t mb = (size_t)D * D * 2;
+            ups.push_back({p + "qkv", 3 * mb, (void **)&L.wqkv, [q, k, v, mb](uint8_t *o) {
+                               memcpy(o, q->data, mb); memcpy(o + mb, k->data, mb); memcpy(o + 2 * mb, v->data, mb); }});
+            const size_t bb = (size_t)D * 4;
+            ups.push_back({p + "bqkv", 3 * bb, (void **)&L.bqkv, [qb, kb, vb, bb](uint8_t *o) {
+                               memcpy(o, qb->data, bb); memcpy(o + bb, kb->data, bb); memcpy(o + 2 * bb, vb->data, bb); }});
+        }
+        copy_f16(p + "attn_out.weight", {D, D}, &L.wo);
+        copy_f32(p + "attn_out.bias", D, &L.bo);
+        copy_f32(p + "attn_norm.weight", D, &L.ln1_w);
+        copy_f32(p + "attn_norm.bias", D, &L.ln1_b);
+        copy_f16(p + "ffn_up.weight", {D, FF}, &L.w1);
+        copy_f32(p + "ffn_up.bias", FF, &L.b1);
+        copy_f16(p + "ffn_down.weight", {FF, D}, &L.w2);
+        copy_f32(p + "ffn_down.bias", D, &L.b2);
+        copy_f32(p + "ffn_norm.weight", D, &L.ln2_w);
+        copy_f32(p + "ffn_norm.bias", D, &L.ln2_b);
+    }
+    copy_f32("audio.encoder.ln_post.weight", D, &m->ln_post_w);
+    copy_f32("audio.encoder.ln_post.bias", D, &m->ln_post_b);
+    copy_f16("audio.encoder.proj1.weight", {D, D}, &m->proj1_w);
+    copy_f32("audio.encoder.proj1.bias", D, &m->proj1_b);
+    copy_f16("audio.encoder.proj2.weight", {D, H}, &m->proj2_w);
+    copy_f32("audio.encoder.proj2.bias", H, &m->proj2_b);
+    copy_f16("token_embd.weight", {H, V}, &m->embd);   // tied LM head (src/text_decoder.cpp:264-265)
+    copy_f32("output_norm.weight", H, &m->out_norm);
+    for (int l = 0; l < hp.dec_layers; l++) {
+        const std::string p = "blk." + std::to_string(l) + ".";
+        DecLayer &L = m->dec[l];
+        copy_f32(p + "attn_norm.weight", H, &L.attn_norm);
+        copy_f32(p + "attn_q_norm.weight", 128, &L.q_norm);
+        copy_f32(p + "attn_k_norm.weight", 128, &L.k_norm);
+        copy_f32(p + "ffn_norm.weight", H, &L.ffn_norm);
+        const gguf_tensor *q = need(p + "attn_q.weight", {H, QD}, DT_F16), *k = need(p + "attn_k.weight", {H, KD}, DT_F16),
+                          *v = need(p + "attn_v.weight", {H, KD}, DT_F16);
+        if (q && k && v) {
+            const size_t qb = (size_t)QD * H * 2, kb = (size_t)KD * H * 2;
+            ups.push_back({p + "qkv", qb + 2 * kb, (void **)&L.wqkv, [q, k, v, qb, kb](uint8_t *o) {
+                               memcpy(o, q->data, qb); memcpy(o + qb, k->data, kb); memcpy(o + qb + kb, v->data, kb); }});
+        }
+        copy_f16(p + "attn_output.weight", {QD, H}, &L.wo);
+        const gguf_tensor *gt = need(p + "ffn_gate.weight", {H, F}, DT_F16), *ut = need(p + "ffn_up.weight", {H, F}, DT_F16);
+        if (gt && ut)   // interleave 16-row blocks: [gate 16q..16q+15 | up 16q..16q+15]
+            ups.push_back({p + "gu", (size_t)2 * F * H * 2, (void **)&L.wgu, [gt, ut, F, H](uint8_t *o) {
+                               const uint16_t *gs = (const uint16_t *)gt->data, *us = (const uint16_t *)ut->data;
+                               uint16_t *d = (uint16_t *)o;
+                               for (int r = 0; r < 2 * F; r++) {
+                                   const int q = r / 32, w = r % 32;
+                                   const uint16_t *src = w < 16 ? gs + (size_t)(16 * q + w) * H : us + (size_t)(16 * q + w - 16) * H;
+                                   memcpy(d + (size_t)r * H, src, (size_t)H * 2);
+                               }
+                           }});
+        copy_f16(p + "ffn_down.weight", {F, H}, &L.wd);
+    }
+    if (!err.empty()) return fail(QASR_ERR_FORMAT, err);
+    // constant tables
+    std::vector<uint16_t> lut;
+    gelu_table(lut);
+    ups.push_back({"gelu", lut.size() * 2, (void **)&m->gelu, [lut](uint8_t *o) { memcpy(o, lut.data(), lut.size() * 2); }});
+    std::vector<float> pe;
+    sinusoidal_pe(pe, 13, D);   // a 100-frame chunk yields at most 13 frames
+    ups.push_back({"pe", pe.size() * 4, (void **)&m->pe, [pe](uint8_t *o) { memcpy(o, pe.data(), pe.size() * 4); }});
+    std::vector<float> fl;
+    mel_filters(fl);
+    ups.push_back({"filters", fl.size() * 4, (void **)&m->filters, [fl](uint8_t *o) { memcpy(o, fl.data(), fl.size() * 4); }});
+    std::vector<double> tw, hn;
+    dft_twiddles(tw);
+    hann_window(hn);
+    ups.push_back({"tw", tw.size() * 8, (void **)&m->tw, [tw](uint8_t *o) { memcpy(o, tw.data(), tw.size() * 8); }});
+    ups.push_back({"hann", hn.size() * 8, (void **)&m->hann, [hn](uint8_t *o) { memcpy(o, hn.data(), hn.size() * 8); }});
+
+    size_t total = 0;
+    std::vector<size_t> offs(ups.size());
+    for (size_t i = 0; i < ups.size(); i++) {
+        offs[i] = total;
+        total += (ups[i].bytes + 255) / 256 * 256;
+    }
+    HIPCHK(hipMalloc((void **)&m->arena, total));
+    m->arena_bytes = total;
+    std::vector<uint8_t> host;
+    for (size_t i = 0; i < ups.size(); i++) {
+        host.resize(ups[i].bytes);
+        ups[i].fill(host.data());
+        HIPCHK(hipMemcpy(m->arena + offs[i], host.data(), ups[i].bytes, hipMemcpyHostToDevice));
+        *ups[i].dst = m->arena + offs[i];
+    }
+    *out = m.release();
+    return 0;
+}
+
+extern "C" void qasr_model_free(qasr_model *m) { delete m; }
+
+extern "C" int qasr_model_hparams(const qasr_model *m, qasr_hparams *o) {
+    if (!m || !o) return fail(QASR_ERR_ARG, "null argument");
+    const Hparams &h = m->hp;
+    *o = qasr_hparams{h.enc_layers, h.d_model, h.enc_heads, h.enc_ffn, h.conv_ch, h.n_mel, h.enc_eps,
+                      h.vocab, h.hidden, h.dec_layers, h.n_head, h.n_kv_head, h.head_dim, h.dec_ffn, h.rms_eps, h.rope_theta,
+                      h.eos_id, h.pad_id, h.audio_start_id, h.audio_end_id, h.audio_pad_id, h.weight_type};
+    return 0;
+}
+
+extern "C" int64_t qasr_model_device_bytes(const qasr_model *m) { return m ? (int64_t)m->arena_bytes : 0; }
+
+// --------------------------------------------------------------- context
+extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_ctx **out) {
+    if (!m || !out || max_batch <= 0 || max_ctx <= 0) return fail(QASR_ERR_ARG, "bad context arguments");
+    *out = nullptr;
+    HIPCHK(hipSetDevice(m->device));
+    std::unique_ptr<qasr_ctx> c(new qasr_ctx());
+    c->m = m;
+    c->max_batch = max_batch;
+    c->max_ctx = max_ctx;
+    HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
+    const Hparams &hp = m->hp;
+    const size_t kv = (size_t)hp.dec_layers * max_batch * hp.n_kv_head * max_ctx * 128;
+    int rc = 0;
+    if ((rc = dev_alloc(c.get(), (void **)&c->kc, kv * 2)) || (rc = dev_alloc(c.get(), (void **)&c->vc, kv * 2))) return rc;
+    std::vector<float> rope;
+    rope_table(rope, max_ctx, 128, hp.rope_theta);
+    if ((rc = dev_alloc(c.get(), (void **)&c->rope, rope.size() * 4))) return rc;
+    HIPCHK(hipMemcpy(c->rope, rope.data(), rope.size() * 4, hipMemcpyHostToDevice));
+    const int B = max_batch, QD = hp.n_head * 128, KD = hp.n_kv_head * 128;
+    c->max_splits = (max_ctx + c->split_len - 1) / c->split_len;
+    c->hist_cap = max_ctx;
+    if ((rc = dev_alloc(c.get(), (void **)&c->d_tok, B * 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_hist, (size_t)B * max_ctx * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_pos, B * 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_nkv, B * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_slot, B * 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_step, 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_x, (size_t)B * hp.hidden * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_xh, (size_t)B * hp.hidden * 2)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_qkv, (size_t)B * (QD + 2 * KD) * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_q, (size_t)B * QD * 2)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_att, (size_t)B * QD * 2)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_act, (size_t)B * hp.dec_ffn * 2)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_part_o, (size_t)B * hp.n_head * c->max_splits * 128 * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_part_ml, (size_t)B * hp.n_head * c->max_splits * 2 * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_logits, (size_t)B * hp.vocab * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_amax, (size_t)B * 8)))
+        return rc;
+    std::vector<int> slots(B);
+    for (int b = 0; b < B; b++) slots[b] = b;
+    HIPCHK(hipMemcpy(c->d_slot, slots.data(), B * 4, hipMemcpyHostToDevice));
+    *out = c.release();
+    return 0;
+}
+
+extern "C" void qasr_ctx_free(qasr_ctx *c) { delete c; }
+
+// ------------------------------------------------------------ size helpers
+extern "C" int qasr_mel_frames(int n) { return mel_frames(n); }
+extern "C" int qasr_encoder_frames(int T) { return encoder_frames(T); }
+extern "C" int qasr_prompt_len(int n) { return n + 15; }
+extern "C" int qasr_build_prompt(const qasr_model *m, int n_audio, int32_t *ids, int *audio_pos) {
+    Hparams hp = m ? m->hp : Hparams();
+    std::vector<int32_t> p = build_prompt(hp, n_audio, {}, audio_pos);
+    if (ids) memcpy(ids, p.data(), p.size() * 4);
+    return (int)p.size();
+}
+
+// =================================================================== stages
+// mel for B clips whose PCM is already in c->pcm (offsets/lengths given);
+// result in c->mel as B blocks [128][T_b].
+static int run_mel(qasr_ctx *c, const std::vector<long> &off, const std::vector<int> &n, std::vector<long> &mel_off,
+                   std::vector<int> &T) {
+    qasr_model *m = c->m;
+    const int B = (int)n.size();
+    std::vector<MelClip> clips(B);
+    std::vector<int2> blocks;
+    long tmp_total = 0, out_total = 0;
+    T.resize(B);
+    mel_off.resize(B);
+    const int fpb = mel_frames_per_block();
+    for (int b = 0; b < B; b++) {
+        const int TF = n[b] / 160 + 1;
+        clips[b] = MelClip{off[b], n[b], TF, tmp_total, out_total};
+        T[b] = TF - 1;
+        mel_off[b] = out_total;
+        tmp_total += 128L * TF;
+        out_total += 128L * (TF - 1);
+        for (int f = 0; f < TF; f += fpb) blocks.push_back(make_int2(b, f));
+    }
+    int rc;
+    if ((rc = upload(c, c->melclips, clips)) || (rc = upload(c, c->melblocks, blocks)) ||
+        (rc = ensure(c, c->meltmp, tmp_total * 8)) || (rc = ensure(c, c->mel, std::max<long>(out_total, 1) * 4)) ||
+        (rc = ensure(c, c->melmax, B * 8)))
+        return rc;
+    HIPCHK(hipMemsetAsync(c->melmax.p, 0, B * 8, c->st));
+    launch_mel(c->pcm.as<float>(), c->melclips.as<MelClip>(), B, blocks.empty() ? nullptr : c->melblocks.as<int2>(),
+               (int)blocks.size(), m->tw, m->hann, m->filters, c->meltmp.as<double>(), c->melmax.as<unsigned long long>(),
+               c->mel.as<float>(), c->st);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// encoder over B clips whose mel sits at d_mel + mel_off[b] ([128][T_b]).
+// conv_only: stop after conv_out + PE (output [sum N][d_model] in c->ex).
+static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> &mel_off, const std::vector<int> &T,
+                       bool conv_only, std::vector<int> &Nb) {
+    qasr_model *m = c->m;
+    const Hparams &hp = m->hp;
+    const int B = (int)T.size(), C = hp.conv_ch, D = hp.d_model, FF = hp.enc_ffn;
+    std::vector<ChunkDesc> ch;
+    std::vector<int> s1, s2, s3, pepos;
+    int r1 = 0, r2 = 0, r3 = 0, er = 0;
+    Nb.assign(B, 0);
+    for (int b = 0; b < B; b++) {
+        for (int s = 0; s < T[b]; s += 100) {
+            ChunkDesc d;
+            d.mel_off = mel_off[b] + s;
+            d.T = T[b];
+            d.L = std::min(100, T[b] - s);
+            d.W1 = (d.L - 1) / 2 + 1;
+            d.W2 = (d.W1 - 1) / 2 + 1;
+            d.W3 = (d.W2 - 1) / 2 + 1;
+            d.row1 = r1; d.row2 = r2; d.row3 = r3; d.enc_row = er;
+            s1.push_back(r1); s2.push_back(r2); s3.push_back(r3);
+            r1 += 64 * d.W1; r2 += 32 * d.W2; r3 += 16 * d.W3; er += d.W3;
+            for (int w = 0; w < d.W3; w++) pepos.push_back(w);
+            Nb[b] += d.W3;
+            ch.push_back(d);
+        }
+    }
+    const int NC = (int)ch.size(), N = er;
+    if (N == 0) return 0;
+    int rc;
+    if ((rc = upload(c, c->chunks, ch)) || (rc = upload(c, c->rs1, s1)) || (rc = upload(c, c->rs2, s2)) ||
+        (rc = upload(c, c->rs3, s3)) || (rc = upload(c, c->pepos, pepos)) ||
+        (rc = ensure(c, c->act1, (size_t)r1 * C * 2)) || (rc = ensure(c, c->act2, (size_t)r2 * C * 2)) ||
+        (rc = ensure(c, c->act3, (size_t)r3 * C * 2)) || (rc = ensure(c, c->ex, (size_t)N * D * 4)) ||
+        (rc = ensure(c, c->exh, (size_t)N * std::max(D, FF) * 2)) || (rc = ensure(c, c->eqkv, (size_t)N * 3 * D * 4)) ||
+        (rc = ensure(c, c->eatt, (size_t)N * D * 2)) || (rc = ensure(c, c->eff, (size_t)N * FF * 2)) ||
+        (rc = ensure(c, c->feats, (size_t)N * hp.hidden * 4)))
+        return rc;
+    hipStream_t s = c->st;
+    launch_conv1(d_mel, c->chunks.as<ChunkDesc>(), c->rs1.as<int>(), NC, r1, m->conv1_w, m->conv1_b, m->gelu, C,
+                 c->act1.as<uint16_t>(), s);
+    GemmArgs g{};
+    g.chunks = c->chunks.as<ChunkDesc>();
+    g.n_chunks = NC;
+    g.C = C;
+    g.gelu = m->gelu;
+    // conv2: act1 (NHWC, H=64) -> act2 (NHWC, H=32)
+    g.A = c->act1.as<uint16_t>(); g.W = m->conv2_w; g.ldw = 9 * C; g.M = r2; g.N = C; g.K = 9 * C;
+    g.row_start = c->rs2.as<int>(); g.bias = m->conv2_b; g.out_f16 = c->act2.as<uint16_t>(); g.ldo16 = C;
+    launch_gemm(AM_CONV2, EPI_GELU_F16, g, s);
+    // conv3: act2 -> act3 rows ordered (chunk, w, h) so conv_out's A is dense
+    g.A = c->act2.as<uint16_t>(); g.W = m->conv3_w; g.M = r3; g.row_start = c->rs3.as<int>(); g.bias = m->conv3_b;
+    g.out_f16 = c->act3.as<uint16_t>();
+    launch_gemm(AM_CONV3, EPI_GELU_F16, g, s);
+    // conv_out (no bias) + per-chunk sinusoidal PE (src/audio_encoder.cpp:147-149, :400-404)
+    GemmArgs o{};
+    o.A = c->act3.as<uint16_t>(); o.lda = 16 * C; o.W = m->conv_out_w; o.ldw = 16 * C; o.M = N; o.N = D; o.K = 16 * C;
+    o.out_f32 = c->ex.as<float>(); o.ldo = D; o.pe = m->pe; o.pe_pos = c->pepos.as<int>();
+    launch_gemm(AM_DENSE, EPI_F32, o, s);
+    HIPCHK(hipGetLastError());
+    if (conv_only) return 0;
+
+    std::vector<int> segs(2 * B);
+    int acc = 0, maxn = 0;
+    for (int b = 0; b < B; b++) { segs[b] = acc; segs[B + b] = Nb[b]; acc += Nb[b]; maxn = std::max(maxn, Nb[b]); }
+    if ((rc = upload(c, c->segs, segs))) return rc;
+    float *x = c->ex.as<float>();
+    uint16_t *xh = c->exh.as<uint16_t>();
+    for (int l = 0; l < hp.enc_layers; l++) {
+        const EncLayer &L = m->enc[l];
+        launch_layernorm_f16(x, N, D, L.ln1_w, L.ln1_b, hp.enc_eps, xh, s);
+        GemmArgs q{};
+        q.A = xh; q.lda = D; q.W = L.wqkv; q.ldw = D; q.M = N; q.N = 3 * D; q.K = D; q.bias = L.bqkv;
+        q.out_f32 = c->eqkv.as<float>(); q.ldo = 3 * D;
+        launch_gemm(AM_DENSE, EPI_F32, q, s);
+        launch_enc_attention(c->eqkv.as<float>(), c->segs.as<int>(), c->segs.as<int>() + B, B, maxn, D, hp.enc_heads,
+                             c->eatt.as<uint16_t>(), s);
+        GemmArgs op{};
+        op.A = c->eatt.as<uint16_t>(); op.lda = D; op.W = L.wo; op.ldw = D; op.M = N; op.N = D; op.K = D; op.bias = L.bo;
+        op.res = x; op.ldr = D; op.out_f32 = x; op.ldo = D;
+        launch_gemm(AM_DENSE, EPI_F32, op, s);
+        launch_layernorm_f16(x, N, D, L.ln2_w, L.ln2_b, hp.enc_eps, xh, s);
+        GemmArgs f1{};
+        f1.A = xh; f1.lda = D; f1.W = L.w1; f1.ldw = D; f1.M = N; f1.N = FF; f1.K = D; f1.bias = L.b1; f1.gelu = m->gelu;
+        f1.out_f16 = c->eff.as<uint16_t>(); f1.ldo16 = FF;
+        launch_gemm(AM_DENSE, EPI_GELU_F16, f1, s);
+        GemmArgs f2{};
+        f2.A = c->eff.as<uint16_t>(); f2.lda = FF; f2.W = L.w2; f2.ldw = FF; f2.M = N; f2.N = D; f2.K = FF; f2.bias = L.b2;
+        f2.res = x; f2.ldr = D; f2.out_f32 = x; f2.ldo = D;
+        launch_gemm(AM_DENSE, EPI_F32, f2, s);
+    }
+    launch_layernorm_f16(x, N, D, m->ln_post_w, m->ln_post_b, hp.enc_eps, xh, s);
+    GemmArgs p1{};
+    p1.A = xh; p1.lda = D; p1.W = m->proj1_w; p1.ldw = D; p1.M = N; p1.N = D; p1.K = D; p1.bias = m->proj1_b; p1.gelu = m->gelu;
+    p1.out_f16 = c->eatt.as<uint16_t>(); p1.ldo16 = D;
+    launch_gemm(AM_DENSE, EPI_GELU_F16, p1, s);
+    GemmArgs p2{};
+    p2.A = c->eatt.as<uint16_t>(); p2.lda = D; p2.W = m->proj2_w; p2.ldw = D; p2.M = N; p2.N = hp.hidden; p2.K = D;
+    p2.bias = m->proj2_b; p2.out_f32 = c->feats.as<float>(); p2.ldo = hp.hidden;
+    launch_gemm(AM_DENSE, EPI_F32, p2, s);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// decoder layer stack over `rows` rows of x (prefill).  Row tables live in
+// c->prow: [row_seq | row_pos | row_audio] (3*rows ints).
+static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::vector<int> &P, const float *d_feats,
+                       const std::vector<int> &audio_pos, const std::vector<int> &N, bool want_logits) {
+    qasr_model *m = c->m;
+    const Hparams &hp = m->hp;
+    const int B = (int)P.size(), H = hp.hidden, QD = hp.n_head * 128, KD = hp.n_kv_head * 128, F = hp.dec_ffn;
+    if (B > c->max_batch) return fail(QASR_ERR_ARG, "batch exceeds context max_batch");
+    int rows = 0, maxp = 0;
+    for (int b = 0; b < B; b++) {
+        if (P[b] <= 0) return fail(QASR_ERR_ARG, "empty prompt");
+        if (P[b] > c->max_ctx) return fail(QASR_ERR_ARG, "Context length exceeded");
+        rows += P[b];
+        maxp = std::max(maxp, P[b]);
+    }
+    std::vector<int> tab(3 * rows + 3 * B), lastrow(B);
+    int r = 0, fr = 0;
+    for (int b = 0; b < B; b++) {
+        const bool splice = d_feats && N[b] > 0 && audio_pos[b] >= 0 && audio_pos[b] + N[b] <= P[b];
+        for (int t = 0; t < P[b]; t++, r++) {
+            tab[r] = b;
+            tab[rows + r] = t;
+            tab[2 * rows + r] = (splice && t >= audio_pos[b] && t < audio_pos[b] + N[b]) ? fr + (t - audio_pos[b]) : -1;
+        }
+        fr += N[b];
+        lastrow[b] = r - 1;
+    }
+    int acc = 0;
+    for (int b = 0; b < B; b++) {   // seq_row0 | seq_len | seq_slot
+        tab[3 * rows + b] = acc;
+        tab[3 * rows + B + b] = P[b];
+        tab[3 * rows + 2 * B + b] = b;
+        acc += P[b];
+    }
+    int rc;
+    if ((rc = upload(c, c->prow, tab)) || (rc = upload(c, c->plast, lastrow)) || (rc = upload(c, c->pids, ids)) ||
+        (rc = ensure(c, c->px, (size_t)rows * H * 4)) || (rc = ensure(c, c->pxh, (size_t)rows * std::max(H, F) * 2)) ||
+        (rc = ensure(c, c->pqkv, (size_t)rows * (QD + 2 * KD) * 4)) || (rc = ensure(c, c->pq, (size_t)rows * QD * 2)) ||
+        (rc = ensure(c, c->patt, (size_t)rows * QD * 2)) || (rc = ensure(c, c->pact, (size_t)rows * F * 2)))
+        return rc;
+    hipStream_t s = c->st;
+    const int *d_seq = c->prow.as<int>(), *d_pos = d_seq + rows, *d_aud = d_seq + 2 * rows;
+    const int *d_srow0 = d_seq + 3 * rows, *d_slen = d_srow0 + B, *d_sslot = d_slen + B;
+    float *x = c->px.as<float>();
+    uint16_t *xh = c->pxh.as<uint16_t>();
+    launch_embed(c->pids.as<int32_t>(), rows, m->embd, H, d_feats, d_aud, x, s);
+    const size_t layer_kv = (size_t)c->max_batch * hp.n_kv_head * c->max_ctx * 128;
+    for (int l = 0; l < hp.dec_layers; l++) {
+        const DecLayer &L = m->dec[l];
+        launch_rmsnorm_f16(x, H, nullptr, rows, H, L.attn_norm, hp.rms_eps, xh, s);
+        GemmArgs q{};
+        q.A = xh; q.lda = H; q.W = L.wqkv; q.ldw = H; q.M = rows; q.N = QD + 2 * KD; q.K = H;
+        q.out_f32 = c->pqkv.as<float>(); q.ldo = QD + 2 * KD;
+        launch_gemm(AM_DENSE, EPI_F32, q, s);
+        QkvPostArgs qa{};
+        qa.qkv = c->pqkv.as<float>(); qa.rows = rows; qa.row_seq = d_seq; qa.row_pos = d_pos;
+        qa.q_norm = L.q_norm; qa.k_norm = L.k_norm; qa.eps = hp.rms_eps; qa.rope = c->rope;
+        qa.n_head = hp.n_head; qa.n_kv_head = hp.n_kv_head; qa.q_out = c->pq.as<uint16_t>();
+        qa.kc = c->kc + l * layer_kv; qa.vc = c->vc + l * layer_kv; qa.max_ctx = c->max_ctx;
+        launch_qkv_post(qa, s);
+        PrefillAttnArgs pa{};
+        pa.q = c->pq.as<uint16_t>(); pa.kc = qa.kc; pa.vc = qa.vc; pa.seq_row0 = d_srow0; pa.seq_len = d_slen;
+        pa.seq_slot = d_sslot; pa.n_seq = B; pa.max_len = maxp; pa.n_head = hp.n_head; pa.n_kv_head = hp.n_kv_head;
+        pa.max_ctx = c->max_ctx; pa.scale = 1.0f / sqrtf(128.0f); pa.out = c->patt.as<uint16_t>();
+        launch_prefill_attention(pa, s);
+        GemmArgs o{};
+        o.A = c->patt.as<uint16_t>(); o.lda = QD; o.W = L.wo; o.ldw = QD; o.M = rows; o.N = H; o.K = QD;
+        o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
+        launch_gemm(AM_DENSE, EPI_F32, o, s);
+        launch_rmsnorm_f16(x, H, nullptr, rows, H, L.ffn_norm, hp.rms_eps, xh, s);
+        GemmArgs gu{};
+        gu.A = xh; gu.lda = H; gu.W = L.wgu; gu.ldw = H; gu.M = rows; gu.N = 2 * F; gu.K = H;
+        gu.out_f16 = c->pact.as<uint16_t>(); gu.ldo16 = F;
+        launch_gemm(AM_DENSE, EPI_SWIGLU_F16, gu, s);
+        GemmArgs dn{};
+        dn.A = c->pact.as<uint16_t>(); dn.lda = F; dn.W = L.wd; dn.ldw = F; dn.M = rows; dn.N = H; dn.K = F;
+        dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
+        launch_gemm(AM_DENSE, EPI_F32, dn, s);
+    }
+    // last row of each sequence -> RMSNorm -> tied LM head + argmax (src/text_decoder.cpp:564-572)
+    uint16_t *xl = c->d_xh;
+    launch_rmsnorm_f16(x, H, c->plast.as<int>(), B, H, m->out_norm, hp.rms_eps, xl, s);
+    launch_fill_u64(c->d_amax, B, 0ull, s);
+    if (B <= 8) {
+        GemvArgs gv{};
+        gv.xh = xl; gv.ldxh = H; gv.W = m->embd; gv.K = H; gv.N = hp.vocab; gv.M = B;
+        gv.out_f32 = want_logits ? c->d_logits : nullptr; gv.ldo = hp.vocab; gv.amax = c->d_amax;
+        launch_gemv(EPI_ARGMAX, gv, s);
+    } else {
+        GemmArgs lm{};
+        lm.A = xl; lm.lda = H; lm.W = m->embd; lm.ldw = H; lm.M = B; lm.N = hp.vocab; lm.K = H;
+        lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
+        launch_gemm(AM_DENSE, EPI_ARGMAX, lm, s);
+    }
+    HIPCHK(hipMemsetAsync(c->d_step, 0, 4, s));
+    launch_argmax_finish(c->d_amax, B, c->d_tok, c->d_hist, c->hist_cap, c->d_step, s);
+    // decode state: next position = P_b, n_kv = P_b + 1 (the fed token's own key included)
+    std::vector<int> pos(B), nkv(B);
+    for (int b = 0; b < B; b++) { pos[b] = P[b]; nkv[b] = P[b] + 1; }
+    HIPCHK(hipMemcpyAsync(c->d_pos, pos.data(), B * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->d_nkv, nkv.data(), B * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));   // pos/nkv host vectors go out of scope
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// one decode step for B sequences: token d_tok at position d_pos
+static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits) {
+    qasr_model *m = c->m;
+    const Hparams &hp = m->hp;
+    const int H = hp.hidden, QD = hp.n_head * 128, KD = hp.n_kv_head * 128, F = hp.dec_ffn;
+    hipStream_t s = c->st;
+    float *x = c->d_x;
+    launch_embed(c->d_tok, B, m->embd, H, nullptr, nullptr, x, s);
+    const size_t layer_kv = (size_t)c->max_batch * hp.n_kv_head * c->max_ctx * 128;
+    const bool skinny = B <= 8;
+    for (int l = 0; l < hp.dec_layers; l++) {
+        const DecLayer &L = m->dec[l];
+        if (skinny) {
+            GemvArgs q{};
+            q.x = x; q.ldx = H; q.norm_w = L.attn_norm; q.eps = hp.rms_eps; q.W = L.wqkv; q.K = H; q.N = QD + 2 * KD; q.M = B;
+            q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
+            launch_gemv(EPI_F32, q, s);
+        } else {
+            launch_rmsnorm_f16(x, H, nullptr, B, H, L.attn_norm, hp.rms_eps, c->d_xh, s);
+            GemmArgs q{};
+            q.A = c->d_xh; q.lda = H; q.W = L.wqkv; q.ldw = H; q.M = B; q.N = QD + 2 * KD; q.K = H;
+            q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
+            launch_gemm(AM_DENSE, EPI_F32, q, s);
+        }
+        QkvPostArgs qa{};
+        qa.qkv = c->d_qkv; qa.rows = B; qa.row_seq = c->d_slot; qa.row_pos = c->d_pos;
+        qa.q_norm = L.q_norm; qa.k_norm = L.k_norm; qa.eps = hp.rms_eps; qa.rope = c->rope;
+        qa.n_head = hp.n_head; qa.n_kv_head = hp.n_kv_head; qa.q_out = c->d_q;
+        qa.kc = c->kc + l * layer_kv; qa.vc = c->vc + l * layer_kv; qa.max_ctx = c->max_ctx;
+        launch_qkv_post(qa, s);
+        DecodeAttnArgs da{};
+        da.q = c->d_q; da.kc = qa.kc; da.vc = qa.vc; da.n_kv = c->d_nkv; da.seq_slot = c->d_slot; da.B = B;
+        da.n_head = hp.n_head; da.n_kv_head = hp.n_kv_head; da.max_ctx = c->max_ctx; da.max_splits = c->max_splits;
+        da.split_len = c->split_len; da.scale = 1.0f / sqrtf(128.0f); da.part_o = c->d_part_o; da.part_ml = c->d_part_ml;
+        da.out = c->d_att;
+        launch_decode_attention(da, s);
+        if (skinny) {
+            GemvArgs o{};
+            o.xh = c->d_att; o.ldxh = QD; o.W = L.wo; o.K = QD; o.N = H; o.M = B; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
+            launch_gemv(EPI_F32, o, s);
+            GemvArgs gu{};
+            gu.x = x; gu.ldx = H; gu.norm_w = L.ffn_norm; gu.eps = hp.rms_eps; gu.W = L.wgu; gu.K = H; gu.N = F; gu.M = B;
+            gu.out_f16 = c->d_act; gu.ldo16 = F;
+            launch_gemv(EPI_SWIGLU_F16, gu, s);
+            GemvArgs dn{};
+            dn.xh = c->d_act; dn.ldxh = F; dn.W = L.wd; dn.K = F; dn.N = H; dn.M = B; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
+            launch_gemv(EPI_F32, dn, s);
+        } else {
+            GemmArgs o{};
+            o.A = c->d_att; o.lda = QD; o.W = L.wo; o.ldw = QD; o.M = B; o.N = H; o.K = QD; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
+            launch_gemm(AM_DENSE, EPI_F32, o, s);
+            launch_rmsnorm_f16(x, H, nullptr, B, H, L.ffn_norm, hp.rms_eps, c->d_xh, s);
+            GemmArgs gu{};
+            gu.A = c->d_xh; gu.lda = H; gu.W = L.wgu; gu.ldw = H; gu.M = B; gu.N = 2 * F; gu.K = H; gu.out_f16 = c->d_act; gu.ldo16 = F;
+            launch_gemm(AM_DENSE, EPI_SWIGLU_F16, gu, s);
+            GemmArgs dn{};
+            dn.A = c->d_act; dn.lda = F; dn.W = L.wd; dn.ldw = F; dn.M = B; dn.N = H; dn.K = F; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
+            launch_gemm(AM_DENSE, EPI_F32, dn, s);
+        }
+    }
+    launch_fill_u64(c->d_amax, B, 0ull, s);
+    if (skinny) {
+        GemvArgs lm{};
+        lm.x = x; lm.ldx = H; lm.norm_w = m->out_norm; lm.eps = hp.rms_eps; lm.W = m->embd; lm.K = H; lm.N = hp.vocab; lm.M = B;
+        lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
+        launch_gemv(EPI_ARGMAX, lm, s);
+    } else {
+        launch_rmsnorm_f16(x, H, nullptr, B, H, m->out_norm, hp.rms_eps, c->d_xh, s);
+        GemmArgs lm{};
+        lm.A = c->d_xh; lm.lda = H; lm.W = m->embd; lm.ldw = H; lm.M = B; lm.N = hp.vocab; lm.K = H;
+        lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
+        launch_gemm(AM_DENSE, EPI_ARGMAX, lm, s);
+    }
+    launch_step_advance(c->d_pos, c->d_nkv, c->d_step, B, s);
+    launch_argmax_finish(c->d_amax, B, c->d_tok, c->d_hist, c->hist_cap, c->d_step, s);
+}
+
+static int decode_graph(qasr_ctx *c, int B, bool want_logits) {
+    if (c->graph && c->graph_B == B && c->graph_logits == want_logits) return 0;
+    if (c->graph) {
+        HIPCHK(hipGraphExecDestroy(c->graph));
+        c->graph = nullptr;
+    }
+    hipGraph_t gr;
+    HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
+    decode_step_kernels(c, B, want_logits);
+    HIPCHK(hipStreamEndCapture(c->st, &gr));
+    HIPCHK(hipGraphInstantiate(&c->graph, gr, nullptr, nullptr, 0));
+    HIPCHK(hipGraphDestroy(gr));
+    c->graph_B = B;
+    c->graph_logits = want_logits;
+    return 0;
+}
+
+// ================================================================== C-ABI
+extern "C" int qasr_mel(qasr_ctx *c, const float *const *pcm, const int *n, int B, float *mel_out) {
+    if (!c || !pcm || !n || B <= 0 || !mel_out) return fail(QASR_ERR_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(c->m->device));
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->pin_used = 0;
+    std::vector<long> off(B);
+    std::vector<int> nn(n, n + B);
+    long tot = 0;
+    for (int b = 0; b < B; b++) { if (n[b] < 0) return fail(QASR_ERR_ARG, "negative length"); off[b] = tot; tot += n[b]; }
+    int rc = ensure(c, c->pcm, std::max<long>(tot, 1) * 4);
+    if (rc) return rc;
+    for (int b = 0; b < B; b++)
+        if (n[b]) HIPCHK(hipMemcpyAsync(c->pcm.as<float>() + off[b], pcm[b], (size_t)n[b] * 4, hipMemcpyHostToDevice, c->st));
+    std::vector<long> mo;
+    std::vector<int> T;
+    if ((rc = run_mel(c, off, nn, mo, T))) return rc;
+    long total = 0;
+    for (int b = 0; b < B; b++) total += 128L * T[b];
+    if (total) HIPCHK(hipMemcpyAsync(mel_out, c->mel.p, total * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+static int encode_common(qasr_ctx *c, const float *mel, const int *T, int B, float *outp, bool conv_only) {
+    if (!c || !mel || !T || B <= 0 || !outp) return fail(QASR_ERR_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(c->m->device));
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->pin_used = 0;
+    std::vector<int> Tv(T, T + B);
+    std::vector<long> mo(B);
+    long tot = 0;
+    for (int b = 0; b < B; b++) { if (T[b] < 0) return fail(QASR_ERR_ARG, "negative length"); mo[b] = tot; tot += 128L * T[b]; }
+    int rc = ensure(c, c->mel, std::max<long>(tot, 1) * 4);
+    if (rc) return rc;
+    if (tot) HIPCHK(hipMemcpyAsync(c->mel.p, mel, tot * 4, hipMemcpyHostToDevice, c->st));
+    std::vector<int> Nb;
+    if ((rc = run_encoder(c, c->mel.as<float>(), mo, Tv, conv_only, Nb))) return rc;
+    long N = 0;
+    for (int v : Nb) N += v;
+    const int width = conv_only ? c->m->hp.d_model : c->m->hp.hidden;
+    if (N) HIPCHK(hipMemcpyAsync(outp, conv_only ? c->ex.p : c->feats.p, (size_t)N * width * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+extern "C" int qasr_encode(qasr_ctx *c, const float *mel, const int *T, int B, float *feats) {
+    return encode_common(c, mel, T, B, feats, false);
+}
+extern "C" int qasr_encode_conv(qasr_ctx *c, const float *mel, const int *T, int B, float *out) {
+    return encode_common(c, mel, T, B, out, true);
+}
+
+extern "C" int qasr_prefill(qasr_ctx *c, const int32_t *ids, const int *P, const float *feats, const int *audio_pos,
+                            const int *N, int B, float *logits_last, int32_t *argmax) {
+    if (!c || !ids || !P || B <= 0) return fail(QASR_ERR_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(c->m->device));
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->pin_used = 0;
+    const int H = c->m->hp.hidden;
+    std::vector<int> Pv(P, P + B), Nv(B, 0), ap(B, -1);
+    long nid = 0, nf = 0;
+    for (int b = 0; b < B; b++) {
+        nid += P[b];
+        if (feats && N) { Nv[b] = N[b]; nf += N[b]; }
+        if (audio_pos) ap[b] = audio_pos[b];
+    }
+    for (long i = 0; i < nid; i++)
+        if (ids[i] < 0 || ids[i] >= c->m->hp.vocab) return fail(QASR_ERR_ARG, "token id out of range");
+    std::vector<int32_t> idv(ids, ids + nid);
+    int rc;
+    if (nf) {
+        if ((rc = ensure(c, c->feats, (size_t)nf * H * 4))) return rc;
+        HIPCHK(hipMemcpyAsync(c->feats.p, feats, (size_t)nf * H * 4, hipMemcpyHostToDevice, c->st));
+    }
+    if ((rc = run_prefill(c, idv, Pv, nf ? c->feats.as<float>() : nullptr, ap, Nv, logits_last != nullptr))) return rc;
+    if (logits_last) HIPCHK(hipMemcpyAsync(logits_last, c->d_logits, (size_t)B * c->m->hp.vocab * 4, hipMemcpyDeviceToHost, c->st));
+    if (argmax) HIPCHK(hipMemcpyAsync(argmax, c->d_tok, B * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_past, int B, float *logits, int32_t *argmax) {
+    if (!c || !tok || !n_past || B <= 0 || B > c->max_batch) return fail(QASR_ERR_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(c->m->device));
+    std::vector<int> pos(B), nkv(B);
+    for (int b = 0; b < B; b++) {
+        if (n_past[b] < 0 || n_past[b] + 1 > c->max_ctx) return fail(QASR_ERR_ARG, "Context length exceeded");
+        if (tok[b] < 0 || tok[b] >= c->m->hp.vocab) return fail(QASR_ERR_ARG, "token id out of range");
+        pos[b] = n_past[b];
+        nkv[b] = n_past[b] + 1;
+    }
+    HIPCHK(hipMemcpyAsync(c->d_tok, tok, B * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(c->d_pos, pos.data(), B * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(c->d_nkv, nkv.data(), B * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemsetAsync(c->d_step, 0, 4, c->st));
+    decode_step_kernels(c, B, logits != nullptr);
+    HIPCHK(hipGetLastError());
+    if (logits) HIPCHK(hipMemcpyAsync(logits, c->d_logits, (size_t)B * c->m->hp.vocab * 4, hipMemcpyDeviceToHost, c->st));
+    if (argmax) HIPCHK(hipMemcpyAsync(argmax, c->d_tok, B * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+extern "C" int qasr_stage_audio(qasr_ctx *c, const float *const *pcm, const int *n, int B) {
+    if (!c || !pcm || !n || B <= 0) return fail(QASR_ERR_ARG, "bad arguments");
+    if (B > c->max_batch) return fail(QASR_ERR_ARG, "batch exceeds context max_batch");
+    HIPCHK(hipSetDevice(c->m->device));
+    c->staged_n.assign(n, n + B);
+    c->staged_off.assign(B, 0);
+    long tot = 0;
+    for (int b = 0; b < B; b++) { if (n[b] < 0) return fail(QASR_ERR_ARG, "negative length"); c->staged_off[b] = tot; tot += n[b]; }
+    int rc = ensure(c, c->pcm, std::max<long>(tot, 1) * 4);
+    if (rc) return rc;
+    for (int b = 0; b < B; b++)
+        if (n[b]) HIPCHK(hipMemcpyAsync(c->pcm.as<float>() + c->staged_off[b], pcm[b], (size_t)n[b] * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *tokens, int *n_tokens, qasr_timings *t) {
+    if (!c || max_tokens <= 0 || !tokens || !n_tokens) return fail(QASR_ERR_ARG, "bad arguments");
+    const int B = (int)c->staged_n.size();
+    if (B == 0) return fail(QASR_ERR_STATE, "no staged audio");
+    HIPCHK(hipSetDevice(c->m->device));
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->pin_used = 0;
+    qasr_model *m = c->m;
+    const Hparams &hp = m->hp;
+    hipStream_t s = c->st;
+    HIPCHK(hipEventRecord(c->ev[0], s));
+    std::vector<long> mo;
+    std::vector<int> T;
+    int rc;
+    if ((rc = run_mel(c, c->staged_off, c->staged_n, mo, T))) return rc;
+    HIPCHK(hipEventRecord(c->ev[1], s));
+    std::vector<int> Nb;
+    if ((rc = run_encoder(c, c->mel.as<float>(), mo, T, false, Nb))) return rc;
+    HIPCHK(hipEventRecord(c->ev[2], s));
+    std::vector<int32_t> ids;
+    std::vector<int> P(B), ap(B);
+    for (int b = 0; b < B; b++) {
+        std::vector<int32_t> p = build_prompt(hp, Nb[b], c->sys_ids, &ap[b]);
+        if (ap[b] < 0) return fail(QASR_ERR_ARG, "No audio_pad token found in input sequence");
+        P[b] = (int)p.size();
+        if (P[b] + max_tokens > c->max_ctx) return fail(QASR_ERR_ARG, "Context length exceeded (prompt + max_tokens > max_ctx)");
+        ids.insert(ids.end(), p.begin(), p.end());
+    }
+    if ((rc = run_prefill(c, ids, P, c->feats.as<float>(), ap, Nb, false))) return rc;
+    HIPCHK(hipEventRecord(c->ev[3], s));
+    // greedy loop (src/qwen3_asr.cpp:270-296): step k feeds token k at position P+k-1
+    if ((rc = decode_graph(c, B, false))) return rc;
+    std::vector<int32_t> hist((size_t)B * c->hist_cap);
+    int steps = 0;
+    if (ignore_eos) {
+        for (int k = 1; k < max_tokens; k++) HIPCHK(hipGraphLaunch(c->graph, s));
+        steps = max_tokens - 1;
+        HIPCHK(hipMemcpyAsync(hist.data(), c->d_hist, hist.size() * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    } else {
+        const int chunk = 8;
+        auto all_done = [&](int done) -> int {   // 1 = every sequence has emitted EOS
+            if (hipMemcpyAsync(hist.data(), c->d_hist, hist.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return -1;
+            for (int b = 0; b < B; b++) {
+                bool fin = false;
+                for (int k = 0; k <= done && !fin; k++) fin = hist[(size_t)b * c->hist_cap + k] == hp.eos_id;
+                if (!fin) return 0;
+            }
+            return 1;
+        };
+        int done = 0, st = 0;
+        while (done + 1 < max_tokens && (st = all_done(done)) == 0) {
+            const int todo = std::min(chunk, max_tokens - 1 - done);
+            for (int k = 0; k < todo; k++) HIPCHK(hipGraphLaunch(c->graph, s));
+            done += todo;
+        }
+        if (st < 0) return fail(QASR_ERR_DEVICE, "device copy failed in decode loop");
+        HIPCHK(hipMemcpyAsync(hist.data(), c->d_hist, hist.size() * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        steps = done;
+    }
+    HIPCHK(hipEventRecord(c->ev[4], s));
+    HIPCHK(hipEventSynchronize(c->ev[4]));
+    for (int b = 0; b < B; b++) {
+        int nt = 0;
+        for (int k = 0; k <= steps && k < max_tokens; k++) {
+            const int32_t tk = hist[(size_t)b * c->hist_cap + k];
+            tokens[(size_t)b * max_tokens + nt++] = tk;
+            if (!ignore_eos && tk == hp.eos_id) break;
+        }
+        if (!ignore_eos && nt > 0 && tokens[(size_t)b * max_tokens + nt - 1] == hp.eos_id) nt--;
+        n_tokens[b] = nt;
+    }
+    if (t) {
+        float a, b2, c2, d;
+        (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
+        (void)hipEventElapsedTime(&b2, c->ev[1], c->ev[2]);
+        (void)hipEventElapsedTime(&c2, c->ev[2], c->ev[3]);
+        (void)hipEventElapsedTime(&d, c->ev[3], c->ev[4]);
+        t->t_mel_ms = a; t->t_encode_ms = b2; t->t_prefill_ms = c2; t->t_decode_ms = d;
+        t->t_total_ms = (double)a + b2 + c2 + d;
+        t->n_decode_steps = steps;
+    }
+    return 0;
+}
+
+extern "C" int qasr_set_system_prompt(qasr_ctx *c, const int32_t *ids, int n) {
+    if (!c || n < 0 || (n > 0 && !ids)) return fail(QASR_ERR_ARG, "bad arguments");
+    c->sys_ids.assign(ids, ids + n);
+    return 0;
+}
+
+extern "C" int qasr_transcribe_batch(qasr_ctx *c, const float *const *pcm, const int *n, int B, int max_tokens, int ignore_eos,
+                                     int32_t *tokens, int *n_tokens, qasr_timings *t) {
+    int rc = qasr_stage_audio(c, pcm, n, B);
+    if (rc) return rc;
+    return qasr_run(c, max_tokens, ignore_eos, tokens, n_tokens, t);
+}
+
+// ------------------------------------------------------------------- text
+extern "C" int qasr_detokenize(const qasr_model *m, const int32_t *ids, int n, char *out, int cap) {
+    if (!m || (!ids && n > 0)) return fail(QASR_ERR_ARG, "bad arguments");
+    std::string s = m->tok.decode(std::vector<int32_t>(ids, ids + n));
+    if (out && cap > 0) {
+        const int k = std::min<int>((int)s.size(), cap - 1);
+        memcpy(out, s.data(), k);
+        out[k] = 0;
+    }
+    return (int)s.size();
+}
+
+extern "C" int qasr_tokenize(const qasr_model *m, const char *text, int32_t *ids, int cap) {
+    if (!m || !text) return fail(QASR_ERR_ARG, "bad arguments");
+    std::vector<int32_t> v = m->tok.encode(text);
+    if (ids) for (int i = 0; i < (int)v.size() && i < cap; i++) ids[i] = v[i];
+    return (int)v.size();
+}
+
+// --------------------------------------------------------- host utilities
+extern "C" int qasr_load_wav(const char *path, float *out, int max_n, int *sample_rate) {
+    std::vector<float> s;
+    int sr = 0;
+    std::string err;
+    if (!path || !load_wav(path, s, sr, err)) { g_err = err.empty() ? "bad path" : err; return -1; }
+    if (sample_rate) *sample_rate = sr;
+    if (out) memcpy(out, s.data(), (size_t)std::min<int>((int)s.size(), max_n) * 4);
+    return (int)s.size();
+}
+
+extern "C" int qasr_write_wav(const char *path, const float *pcm, int n, int sample_rate) {
+    if (!path || (!pcm && n > 0) || !write_wav(path, pcm, n, sample_rate)) return fail(QASR_ERR_IO, "cannot write wav");
+    return 0;
+}
+
+extern "C" int qasr_synth_pcm(uint64_t seed, int n, float *out) {
+    if (!out || n < 0) return fail(QASR_ERR_ARG, "bad arguments");
+    synth_pcm(seed, n, out);
+    return 0;
+}
+
+extern "C" int qasr_write_synthetic_gguf(const char *path, const char *config, uint64_t seed, int wtype) {
+    std::string err;
+    if (!path || !config) return fail(QASR_ERR_ARG, "bad arguments");
+    if (!write_synthetic_gguf(path, config, seed, wtype, err)) return fail(QASR_ERR_IO, err);
+    return 0;
+}

@@ -1,0 +1,429 @@
+// gemm.hip -- fp16 MFMA GEMM (C = A W^T) with fused epilogues, plus the
+// weight-streaming skinny GEMV used by the decode step.
+//
+// Numerics = ggml_mul_mat with F16 weights (SURVEY.md §8(a) numerics i, iv):
+// activations rounded to fp16 (RNE), fp16 x fp16 products accumulated in
+// fp32.  v_mfma_f32_16x16x32_f16 has exactly these input semantics; only
+// the summation order differs from ggml's SIMD lanes.
+//
+// Tiling: 256 threads = 4 waves (2x2), wave tile (BM/2)x(BN/2) built from
+// 16x16x32 MFMAs; K staged through LDS in 32-wide slabs (KS slabs per
+// barrier) of 64-byte rows with the chunk swizzle c ^ ((row>>1)&3), which is
+// conflict-free for the ds_read_b128 fragment reads (checked exhaustively
+// over the four 16-lane groups).  Register-staged double buffering: the next
+// tile's global loads are issued before the current tile's MFMAs.
+//
+// A operand modes: dense row-major, or an implicit im2col gather over the
+// NHWC conv activations (3x3, stride 2, pad 1) so conv2/conv3 of the audio
+// encoder never materialise im2col buffers (src/audio_encoder.cpp:116-128).
+#include "dev_common.h"
+#include "kernels.h"
+
+namespace qasr {
+
+__device__ __forceinline__ int find_chunk(const int *__restrict__ starts, int n, int r) {
+    int lo = 0, hi = n - 1;   // largest c with starts[c] <= r
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (starts[mid] <= r) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ float silu_f(float g) { return g / (1.0f + expf(-g)); }
+
+template <int BM, int BN, int KS, int AMODE, int EPI>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+    constexpr int FM = BM / 32, FN = BN / 32;
+    constexpr int ROWS = BM + BN;
+    constexpr int SLAB = ROWS * 32;            // halves per slab (A rows then W rows)
+    constexpr int NCH = ROWS * KS * 4;         // 16-byte chunks per stage
+    constexpr int CPT = (NCH + 255) / 256;     // chunks per thread
+    __shared__ __attribute__((aligned(16))) uint16_t smem[2 * KS * SLAB];
+    __shared__ int4 rowinfo[AMODE == AM_DENSE ? 1 : BM];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid >> 1, wc = wid & 1;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int M = g.M, K = g.K;
+
+    if constexpr (AMODE != AM_DENSE) {
+        for (int r = tid; r < BM; r += 256) {
+            const int row = m0 + r;
+            int4 info = make_int4(-1, 0, 0, 0);
+            if (row < M) {
+                const int c = find_chunk(g.row_start, g.n_chunks, row);
+                const ChunkDesc cd = g.chunks[c];
+                const int local = row - g.row_start[c];
+                int oh, ow, base, Win;
+                if constexpr (AMODE == AM_CONV2) {
+                    ow = local % cd.W2; oh = local / cd.W2; base = cd.row1; Win = cd.W1;
+                } else {
+                    oh = local % 16; ow = local / 16; base = cd.row2; Win = cd.W2;
+                }
+                info = make_int4(base, 2 * oh - 1, 2 * ow - 1, Win);
+            }
+            rowinfo[r] = info;
+        }
+        __syncthreads();
+    }
+
+    floatx4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    u32x4 stage[CPT];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int t = 0; t < CPT; t++) {
+            const int c = tid + t * 256;
+            u32x4 v = u32x4{0u, 0u, 0u, 0u};
+            if (c < NCH) {
+                const int q = c & 3, rs = c >> 2;
+                const int s = rs / ROWS, r = rs - s * ROWS;
+                const int k = k0 + s * 32 + q * 8;
+                if (r < BM) {
+                    const int row = m0 + r;
+                    if constexpr (AMODE == AM_DENSE) {
+                        if (row < M) v = *(const u32x4 *)(g.A + (long)row * g.lda + k);
+                    } else {
+                        const int4 ri = rowinfo[r];
+                        if (ri.x >= 0) {
+                            const int tap = k / g.C, ic = k - tap * g.C;
+                            const int kh = tap / 3, kw = tap - kh * 3;
+                            const int ih = ri.y + kh, iw = ri.z + kw;
+                            const int Hin = AMODE == AM_CONV2 ? 64 : 32;
+                            if (ih >= 0 && ih < Hin && iw >= 0 && iw < ri.w)
+                                v = *(const u32x4 *)(g.A + ((long)(ri.x + ih * ri.w + iw) * g.C + ic));
+                        }
+                    }
+                } else {
+                    const int n = n0 + r - BM;
+                    v = *(const u32x4 *)(g.W + (long)n * g.ldw + k);
+                }
+            }
+            stage[t] = v;
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int t = 0; t < CPT; t++) {
+            const int c = tid + t * 256;
+            if (c < NCH) {
+                const int q = c & 3, rs = c >> 2;
+                const int s = rs / ROWS, r = rs - s * ROWS;
+                uint16_t *dst = smem + (buf * KS + s) * SLAB + r * 32 + ((q ^ ((r >> 1) & 3)) << 3);
+                *(u32x4 *)dst = stage[t];
+            }
+        }
+    };
+
+    const int nk = K / (32 * KS);
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt++) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) gload((kt + 1) * 32 * KS);
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+            const uint16_t *sl = smem + (cur * KS + s) * SLAB;
+            half8 af[FM], bf[FN];
+            const int q = lane >> 4;
+#pragma unroll
+            for (int i = 0; i < FM; i++) {
+                const int r = wr * (BM / 2) + i * 16 + (lane & 15);
+                af[i] = *(const half8 *)(sl + r * 32 + ((q ^ ((r >> 1) & 3)) << 3));
+            }
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                const int r = BM + wc * (BN / 2) + j * 16 + (lane & 15);
+                bf[j] = *(const half8 *)(sl + r * 32 + ((q ^ ((r >> 1) & 3)) << 3));
+            }
+#pragma unroll
+            for (int i = 0; i < FM; i++)
+#pragma unroll
+                for (int j = 0; j < FN; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) sstore(cur ^ 1);
+        __syncthreads();
+    }
+
+    // ------------------------------------------------------------ epilogue
+    const int rbase = m0 + wr * (BM / 2) + 4 * (lane >> 4);
+    const int cbase = n0 + wc * (BN / 2) + (lane & 15);
+    if constexpr (EPI == EPI_SWIGLU_F16) {
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int p = 0; p < FN / 2; p++) {
+                const int ocol = (n0 + wc * (BN / 2)) / 2 + p * 16 + (lane & 15);
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int row = rbase + i * 16 + r;
+                    if (row < M) {
+                        const float gt = acc[i][2 * p][r], up = acc[i][2 * p + 1][r];
+                        const float v = silu_f(gt) * up;
+                        g.out_f16[(long)row * g.ldo16 + ocol] = f_to_u16(v);
+                    }
+                }
+            }
+    } else if constexpr (EPI == EPI_ARGMAX) {
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = rbase + i * 16 + r;
+                unsigned long long best = 0ull;
+#pragma unroll
+                for (int j = 0; j < FN; j++) {
+                    const int col = cbase + j * 16;
+                    const float v = acc[i][j][r];
+                    if (row < M && g.out_f32) g.out_f32[(long)row * g.ldo + col] = v;
+                    const unsigned long long key = argmax_key(v, col);
+                    best = key > best ? key : best;
+                }
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    const unsigned long long other = __shfl_xor(best, o, 64);
+                    best = other > best ? other : best;
+                }
+                if (row < M && (lane & 15) == 0) atomicMax(g.amax + row, best);
+            }
+    } else {
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                const int col = cbase + j * 16;
+                const float bcol = g.bias ? g.bias[col] : 0.0f;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int row = rbase + i * 16 + r;
+                    if (row >= M) continue;
+                    float v = acc[i][j][r];
+                    if (g.bias) v = fadd_rn(v, bcol);
+                    if constexpr (EPI == EPI_GELU_F16) {
+                        g.out_f16[(long)row * g.ldo16 + col] = f_to_u16(gelu_lut(v, g.gelu));
+                    } else if constexpr (EPI == EPI_F16) {
+                        g.out_f16[(long)row * g.ldo16 + col] = f_to_u16(v);
+                    } else {
+                        if (g.pe) v = fadd_rn(v, g.pe[(long)g.pe_pos[row] * g.N + col]);
+                        if (g.res) v = fadd_rn(v, g.res[(long)row * g.ldr + col]);
+                        g.out_f32[(long)row * g.ldo + col] = v;
+                    }
+                }
+            }
+    }
+}
+
+template <int BM, int BN, int KS, int AMODE, int EPI>
+static void run_gemm(const GemmArgs &g, hipStream_t s) {
+    dim3 grid(g.N / BN, (g.M + BM - 1) / BM);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, KS, AMODE, EPI>), grid, dim3(256), 0, s, g);
+}
+
+template <int AMODE, int EPI>
+static void dispatch_tiles(const GemmArgs &g, hipStream_t s) {
+    if constexpr (AMODE != AM_DENSE) {
+        // conv: K = 9*C, slab group must stay inside one tap -> C % (32*KS) == 0
+        if (g.N % 96 == 0 && g.C % 96 == 0) {
+            if (g.M >= 4096) run_gemm<128, 96, 3, AMODE, EPI>(g, s);
+            else run_gemm<64, 96, 3, AMODE, EPI>(g, s);
+        } else {
+            run_gemm<64, 64, 1, AMODE, EPI>(g, s);
+        }
+    } else {
+        const bool big = g.M >= 2048 && g.N % 128 == 0;
+        if (g.K % 64 == 0) {
+            if (big) run_gemm<128, 128, 2, AMODE, EPI>(g, s);
+            else run_gemm<64, 64, 2, AMODE, EPI>(g, s);
+        } else {
+            run_gemm<64, 64, 1, AMODE, EPI>(g, s);
+        }
+    }
+}
+
+void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s) {
+    if (g.M <= 0) return;
+    switch (amode * 8 + epi) {
+        case AM_DENSE * 8 + EPI_F32: dispatch_tiles<AM_DENSE, EPI_F32>(g, s); break;
+        case AM_DENSE * 8 + EPI_GELU_F16: dispatch_tiles<AM_DENSE, EPI_GELU_F16>(g, s); break;
+        case AM_DENSE * 8 + EPI_SWIGLU_F16: dispatch_tiles<AM_DENSE, EPI_SWIGLU_F16>(g, s); break;
+        case AM_DENSE * 8 + EPI_ARGMAX: dispatch_tiles<AM_DENSE, EPI_ARGMAX>(g, s); break;
+        case AM_DENSE * 8 + EPI_F16: dispatch_tiles<AM_DENSE, EPI_F16>(g, s); break;
+        case AM_CONV2 * 8 + EPI_GELU_F16: dispatch_tiles<AM_CONV2, EPI_GELU_F16>(g, s); break;
+        case AM_CONV3 * 8 + EPI_GELU_F16: dispatch_tiles<AM_CONV3, EPI_GELU_F16>(g, s); break;
+        default: break;
+    }
+}
+
+// ===================================================================== GEMV
+// One wave per CPW output columns; every lane streams 16-byte pieces of the
+// weight rows straight from HBM into VGPRs (no LDS round trip for W, cdna
+// guide: "GEMV / M <= 16 decode weights"), x rows live in LDS as fp16.
+template <int EPI, int CPW, int MR>
+__global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];   // [MR][K]
+    __shared__ double red[4][MR];
+    __shared__ unsigned long long bestk[4][MR];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int K = g.K;
+    // ---- prologue: x rows -> fp16 in LDS (optionally RMS-normalised)
+    if (g.norm_w) {
+        double ss[MR];
+#pragma unroll
+        for (int m = 0; m < MR; m++) ss[m] = 0.0;
+        for (int k = tid; k < K; k += 256)
+#pragma unroll
+            for (int m = 0; m < MR; m++) {
+                if (m < g.M) {
+                    const float v = g.x[(long)m * g.ldx + k];
+                    ss[m] += (double)(v * v);
+                }
+            }
+#pragma unroll
+        for (int m = 0; m < MR; m++) {
+            const double t = wave_sum_d(ss[m]);
+            if (lane == 0) red[wid][m] = t;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < MR; m++) {
+            const double tot = red[0][m] + red[1][m] + red[2][m] + red[3][m];
+            const float mean = (float)(tot / K);
+            const float scale = 1.0f / sqrtf(mean + g.eps);
+            for (int k = tid; k < K; k += 256) {
+                float v = 0.0f;
+                if (m < g.M) v = fmul_rn(fmul_rn(g.x[(long)m * g.ldx + k], scale), g.norm_w[k]);
+                xs[m * K + k] = f_to_u16(v);
+            }
+        }
+    } else if (g.xh) {
+        for (int k = tid * 8; k < K; k += 256 * 8)
+#pragma unroll
+            for (int m = 0; m < MR; m++)
+                *(u32x4 *)(xs + m * K + k) = m < g.M ? *(const u32x4 *)(g.xh + (long)m * g.ldxh + k) : u32x4{0u, 0u, 0u, 0u};
+    } else {
+        for (int k = tid; k < K; k += 256)
+#pragma unroll
+            for (int m = 0; m < MR; m++) xs[m * K + k] = m < g.M ? f_to_u16(g.x[(long)m * g.ldx + k]) : (uint16_t)0;
+    }
+    __syncthreads();
+
+    constexpr int NR = EPI == EPI_SWIGLU_F16 ? 2 : 1;   // weight rows per output
+    const int col0 = (blockIdx.x * 4 + wid) * CPW;
+    float acc[CPW][NR][MR];
+#pragma unroll
+    for (int c = 0; c < CPW; c++)
+#pragma unroll
+        for (int r = 0; r < NR; r++)
+#pragma unroll
+            for (int m = 0; m < MR; m++) acc[c][r][m] = 0.0f;
+    for (int k = lane * 8; k < K; k += 512) {   // K % 8 == 0; lanes past K idle on the last sweep
+        half8 wv[CPW][NR];
+#pragma unroll
+        for (int c = 0; c < CPW; c++)
+#pragma unroll
+            for (int r = 0; r < NR; r++) {
+                const int o = col0 + c;
+                long wrow = o;
+                if constexpr (EPI == EPI_SWIGLU_F16) wrow = 32L * (o >> 4) + (o & 15) + 16 * r;
+                wv[c][r] = o < g.N ? *(const half8 *)(g.W + wrow * K + k) : half8{};
+            }
+#pragma unroll
+        for (int m = 0; m < MR; m++) {
+            const half8 xv = *(const half8 *)(xs + m * K + k);
+#pragma unroll
+            for (int c = 0; c < CPW; c++)
+#pragma unroll
+                for (int r = 0; r < NR; r++)
+#pragma unroll
+                    for (int e = 0; e < 8; e++) acc[c][r][m] = fmaf((float)wv[c][r][e], (float)xv[e], acc[c][r][m]);
+        }
+    }
+    unsigned long long best[MR];
+#pragma unroll
+    for (int m = 0; m < MR; m++) best[m] = 0ull;
+#pragma unroll
+    for (int c = 0; c < CPW; c++) {
+        const int o = col0 + c;
+#pragma unroll
+        for (int m = 0; m < MR; m++) {
+            float v[NR];
+#pragma unroll
+            for (int r = 0; r < NR; r++) v[r] = wave_sum(acc[c][r][m]);
+            if (o >= g.N || m >= g.M) continue;
+            if constexpr (EPI == EPI_ARGMAX) {
+                if (lane == 0 && g.out_f32) g.out_f32[(long)m * g.ldo + o] = v[0];
+                const unsigned long long key = argmax_key(v[0], o);
+                best[m] = key > best[m] ? key : best[m];
+            } else if (lane == 0) {
+                if constexpr (EPI == EPI_SWIGLU_F16) {
+                    g.out_f16[(long)m * g.ldo16 + o] = f_to_u16(silu_f(v[0]) * v[1]);
+                } else {
+                    float y = v[0];
+                    if (g.bias) y = fadd_rn(y, g.bias[o]);
+                    if constexpr (EPI == EPI_GELU_F16) {
+                        (void)y;
+                    } else if constexpr (EPI == EPI_F16) {
+                        g.out_f16[(long)m * g.ldo16 + o] = f_to_u16(y);
+                    } else {
+                        if (g.res) y = fadd_rn(y, g.res[(long)m * g.ldr + o]);
+                        g.out_f32[(long)m * g.ldo + o] = y;
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (EPI == EPI_ARGMAX) {
+        if (lane == 0)
+#pragma unroll
+            for (int m = 0; m < MR; m++) bestk[wid][m] = best[m];
+        __syncthreads();
+        if (tid < MR && tid < g.M) {
+            unsigned long long b = bestk[0][tid];
+            for (int w = 1; w < 4; w++) b = bestk[w][tid] > b ? bestk[w][tid] : b;
+            atomicMax(g.amax + tid, b);
+        }
+    }
+}
+
+template <int EPI, int CPW, int MR>
+static void run_gemv(const GemvArgs &g, hipStream_t s) {
+    const int per_block = 4 * CPW;
+    const int blocks = (g.N + per_block - 1) / per_block;
+    const size_t lds = (size_t)MR * g.K * 2;
+    hipLaunchKernelGGL((gemv_kernel<EPI, CPW, MR>), dim3(blocks), dim3(256), lds, s, g);
+}
+
+template <int EPI, int MR>
+static void gemv_cpw(const GemvArgs &g, hipStream_t s) {
+    // keep >= ~512 waves in flight: fewer columns per wave for narrow outputs
+    if (g.N >= 8192) run_gemv<EPI, 4, MR>(g, s);
+    else if (g.N >= 2048) run_gemv<EPI, 2, MR>(g, s);
+    else run_gemv<EPI, 1, MR>(g, s);
+}
+
+template <int EPI>
+static void gemv_mr(const GemvArgs &g, hipStream_t s) {
+    if (g.M <= 1) gemv_cpw<EPI, 1>(g, s);
+    else if (g.M <= 2) gemv_cpw<EPI, 2>(g, s);
+    else if (g.M <= 4) gemv_cpw<EPI, 4>(g, s);
+    else gemv_cpw<EPI, 8>(g, s);
+}
+
+void launch_gemv(int epi, const GemvArgs &g, hipStream_t s) {
+    if (g.M <= 0) return;
+    switch (epi) {
+        case EPI_F32: gemv_mr<EPI_F32>(g, s); break;
+        case EPI_SWIGLU_F16: gemv_mr<EPI_SWIGLU_F16>(g, s); break;
+        case EPI_ARGMAX: gemv_mr<EPI_ARGMAX>(g, s); break;
+        case EPI_F16: gemv_mr<EPI_F16>(g, s); break;
+        default: break;
+    }
+}
+
+}  // namespace qasr

@@ -1,0 +1,146 @@
+// kernels.h -- launch interface of the gfx950 kernels (host-callable).
+// All pointers are device pointers; all launches go on the given stream and
+// are graph-capturable (no allocation, no synchronisation).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qasr {
+
+// ---------------------------------------------------------------- mel
+struct MelClip {
+    long pcm_off;   // first sample of the clip in the packed PCM buffer
+    int n;          // samples
+    int TF;         // computed frames = n/160 + 1 (last one dropped, src/mel_spectrogram.cpp:517-522)
+    long tmp_off;   // offset of [128][TF] fp64 scratch
+    long out_off;   // offset of [128][TF-1] fp32 output
+};
+void launch_mel(const float *pcm, const MelClip *clips, int n_clips, const int2 *blocks, int n_blocks,
+                const double2 *tw, const double *hann, const float *filt, double *tmp, unsigned long long *cmax,
+                float *out, hipStream_t s);
+int mel_frames_per_block();
+
+// ---------------------------------------------------------------- conv front-end
+// One entry per 100-frame mel chunk (src/audio_encoder.cpp:331-409).
+struct ChunkDesc {
+    long mel_off;   // element offset of mel[clip][0][chunk_start]
+    int T;          // mel row stride (frames of the clip)
+    int L;          // chunk frames (last chunk of a clip may be short; never padded)
+    int W1, W2, W3; // conv output widths
+    int row1, row2, row3;   // first row of this chunk in the conv1/2/3 output tables
+    int enc_row;    // first encoder frame (= row3 / 16)
+};
+
+// conv1 (1 -> C, 3x3, s2, p1) + bias + GELU(LUT) -> act1 NHWC fp16 [rows1][C]
+void launch_conv1(const float *mel, const ChunkDesc *chunks, const int *row1_start, int n_chunks, int rows1,
+                  const uint16_t *w /*[C][9]*/, const float *b, const uint16_t *gelu, int C, uint16_t *act1, hipStream_t s);
+
+// ---------------------------------------------------------------- GEMM
+enum GemmEpi {
+    EPI_F32 = 0,        // out_f32 = acc (+bias) (+res) (+pe[pe_pos[row]])
+    EPI_GELU_F16 = 1,   // out_f16 = gelu(acc + bias)
+    EPI_SWIGLU_F16 = 2, // interleaved gate/up rows -> out_f16 = silu(g) * u
+    EPI_ARGMAX = 3,     // optional out_f32 logits + per-row packed argmax (atomicMax)
+    EPI_F16 = 4,        // out_f16 = acc (+bias)
+};
+enum GemmAMode {
+    AM_DENSE = 0,       // A [M][lda] fp16 row-major
+    AM_CONV2 = 1,       // implicit im2col of act1 (NHWC, H=64), rows ordered (chunk, oh, ow)
+    AM_CONV3 = 2,       // implicit im2col of act2 (NHWC, H=32), rows ordered (chunk, ow, oh)
+};
+struct GemmArgs {
+    const uint16_t *A; int lda;
+    const uint16_t *W; int ldw;     // [N][K] fp16 (PyTorch [out][in])
+    int M, N, K;
+    // conv gather
+    const ChunkDesc *chunks; const int *row_start; int n_chunks; int C;
+    // epilogue
+    const float *bias;
+    const float *res; int ldr;
+    float *out_f32; int ldo;
+    uint16_t *out_f16; int ldo16;
+    const uint16_t *gelu;
+    const float *pe; const int *pe_pos;   // conv_out: + PE[pos][n]
+    unsigned long long *amax;             // [M] packed argmax keys
+};
+void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s);
+
+// skinny (decode) path: M <= 8 rows, weights streamed once from HBM.
+// x is fp32 [M][K]; if norm_w != nullptr the rows are RMS-normalised first
+// (ggml_rms_norm + ggml_mul), then rounded to fp16 as ggml's mul_mat does.
+struct GemvArgs {
+    const float *x; int ldx;
+    const uint16_t *xh; int ldxh;        // alternative fp16 input (no norm)
+    const float *norm_w; float eps;
+    const uint16_t *W; int K, N, M;      // N = output columns (for SWIGLU: F outputs)
+    const float *bias;
+    const float *res; int ldr;
+    float *out_f32; int ldo;
+    uint16_t *out_f16; int ldo16;
+    unsigned long long *amax;
+};
+void launch_gemv(int epi, const GemvArgs &g, hipStream_t s);
+
+// ---------------------------------------------------------------- norms
+// LayerNorm (ggml_norm + mul + add) fp32 [M][D] -> fp16
+void launch_layernorm_f16(const float *x, int M, int D, const float *w, const float *b, float eps, uint16_t *y, hipStream_t s);
+// RMSNorm (ggml_rms_norm + mul) fp32 -> fp16; rows gathered by optional row_idx
+void launch_rmsnorm_f16(const float *x, int ldx, const int *row_idx, int M, int D, const float *w, float eps,
+                        uint16_t *y, hipStream_t s);
+
+// ---------------------------------------------------------------- attention
+// encoder: full bidirectional fp32 attention per clip segment, head_dim 64.
+// qkv fp32 [rows][3*D]; out fp16 [rows][D]
+void launch_enc_attention(const float *qkv, const int *seg_start, const int *seg_len, int n_seg, int max_len,
+                          int D, int H, uint16_t *out, hipStream_t s);
+
+// decoder q/k RMSNorm + NEOX RoPE + fp16 KV-cache write (+ q fp16 out)
+struct QkvPostArgs {
+    const float *qkv; int rows;          // [rows][QD + 2*KD] fp32 from the fused QKV GEMM
+    const int *row_seq; const int *row_pos;   // per row: sequence slot, absolute position
+    const float *q_norm, *k_norm; float eps;
+    const float *rope;                   // [max_pos][64][2]
+    int n_head, n_kv_head;               // head_dim fixed at 128
+    uint16_t *q_out;                     // [rows][n_head*128] fp16
+    uint16_t *kc, *vc;                   // this layer's cache base: [seq][kvh][max_ctx][128]
+    int max_ctx;
+};
+void launch_qkv_post(const QkvPostArgs &a, hipStream_t s);
+
+// decoder causal prefill attention (fp16 Q/K/V, fp32 softmax), GQA 2:1, hd 128
+struct PrefillAttnArgs {
+    const uint16_t *q;                   // [rows][n_head*128]
+    const uint16_t *kc, *vc;             // layer cache base
+    const int *seq_row0; const int *seq_len; const int *seq_slot; int n_seq; int max_len;
+    int n_head, n_kv_head, max_ctx;
+    float scale;
+    uint16_t *out;                       // [rows][n_head*128] fp16
+};
+void launch_prefill_attention(const PrefillAttnArgs &a, hipStream_t s);
+
+// decoder single-token attention, split over the KV length + combine
+struct DecodeAttnArgs {
+    const uint16_t *q;                   // [B][n_head*128] fp16
+    const uint16_t *kc, *vc;
+    const int *n_kv;                     // [B] keys per sequence (n_past + 1)
+    const int *seq_slot;
+    int B, n_head, n_kv_head, max_ctx, max_splits, split_len;
+    float scale;
+    float *part_o; float *part_ml;       // scratch [B][n_head][max_splits][128], [B][n_head][max_splits][2]
+    uint16_t *out;                       // [B][n_head*128] fp16
+};
+void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
+
+// ---------------------------------------------------------------- decoder misc
+// embedding gather (fp16 -> fp32) + audio splice (src/text_decoder.cpp:429-459)
+void launch_embed(const int32_t *ids, int rows, const uint16_t *embd, int hidden, const float *audio,
+                  const int *row_audio /* -1 or audio row */, float *x, hipStream_t s);
+// final argmax decode of packed keys -> ids; optionally scatter into a token history
+void launch_argmax_finish(const unsigned long long *amax, int B, int32_t *ids, int32_t *hist, int hist_stride,
+                          const int *step, hipStream_t s);
+void launch_fill_u64(unsigned long long *p, int n, unsigned long long v, hipStream_t s);
+// decode-step bookkeeping on device: n_kv[b] += 1, row_pos[b] += 1, step += 1
+void launch_step_advance(int *row_pos, int *n_kv, int *step, int B, hipStream_t s);
+
+}  // namespace qasr

@@ -1,0 +1,166 @@
+// qwen3_asr.cpp -- Qwen3ASR (include/qwen3_asr.h) over the C-ABI.
+// Mirrors src/qwen3_asr.cpp:21-327: same error strings, same result fields;
+// mel / encode / prefill / greedy decode run on the GPU through qasr_run.
+#include "qwen3_asr.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+
+#include "qasr_host.h"
+
+namespace qwen3_asr {
+
+static int64_t now_ms() {
+    return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+Qwen3ASR::Qwen3ASR() = default;
+
+Qwen3ASR::~Qwen3ASR() {
+    if (ctx_) qasr_ctx_free(ctx_);
+    if (model_) qasr_model_free(model_);
+}
+
+bool Qwen3ASR::load_model(const std::string &model_path) {
+    const int64_t t0 = now_ms();
+    if (model_) { qasr_model_free(model_); model_ = nullptr; }
+    if (qasr_model_load(model_path.c_str(), device_, &model_) != 0) {
+        error_msg_ = std::string("Failed to load model: ") + qasr_last_error();
+        model_ = nullptr;
+        return false;
+    }
+    qasr_hparams hp;
+    qasr_model_hparams(model_, &hp);
+    config_.vocab_size = hp.vocab_size;
+    config_.hidden_size = hp.hidden_size;
+    config_.n_decoder_layers = hp.dec_layers;
+    config_.n_attention_heads = hp.n_heads;
+    config_.n_key_value_heads = hp.n_kv_heads;
+    config_.intermediate_size = hp.dec_ffn;
+    config_.head_dim = hp.head_dim;
+    config_.rms_norm_eps = hp.rms_eps;
+    config_.rope_theta = hp.rope_theta;
+    config_.eos_token_id = hp.eos_id;
+    config_.audio_start_token_id = hp.audio_start_id;
+    config_.audio_end_token_id = hp.audio_end_id;
+    config_.audio_pad_token_id = hp.audio_pad_id;
+    fprintf(stderr, "Model loaded in %lld ms\n", (long long)(now_ms() - t0));
+    return true;
+}
+
+bool Qwen3ASR::ensure_ctx(int batch, int n_ctx) {
+    if (ctx_ && ctx_batch_ >= batch && ctx_len_ >= n_ctx) return true;
+    if (ctx_) { qasr_ctx_free(ctx_); ctx_ = nullptr; }
+    const int nb = std::max(batch, ctx_batch_), nl = std::max(n_ctx, ctx_len_);
+    if (qasr_ctx_create(model_, nb, nl, &ctx_) != 0) {
+        error_msg_ = std::string("Failed to initialize KV cache: ") + qasr_last_error();
+        ctx_ = nullptr;
+        return false;
+    }
+    ctx_batch_ = nb;
+    ctx_len_ = nl;
+    return true;
+}
+
+transcribe_result Qwen3ASR::transcribe(const std::string &audio_path, const transcribe_params &params) {
+    transcribe_result result;
+    if (!model_) { result.error_msg = "Model not loaded"; return result; }
+    std::vector<float> samples;
+    int sr = 0;
+    if (!load_audio_file(audio_path, samples, sr)) {
+        result.error_msg = "Failed to load audio file: " + audio_path;
+        return result;
+    }
+    if (sr != 16000) {
+        result.error_msg = "Audio must be 16kHz, got " + std::to_string(sr) + " Hz";
+        return result;
+    }
+    return transcribe_internal(samples.data(), (int)samples.size(), params);
+}
+
+transcribe_result Qwen3ASR::transcribe(const float *samples, int n_samples, const transcribe_params &params) {
+    transcribe_result result;
+    if (!model_) { result.error_msg = "Model not loaded"; return result; }
+    return transcribe_internal(samples, n_samples, params);
+}
+
+std::vector<transcribe_result> Qwen3ASR::transcribe_batch(const std::vector<std::vector<float>> &clips,
+                                                          const transcribe_params &params) {
+    const int B = (int)clips.size();
+    std::vector<transcribe_result> out(B);
+    if (!model_) { for (auto &r : out) r.error_msg = "Model not loaded"; return out; }
+    int maxP = 0;
+    std::vector<const float *> ptr(B);
+    std::vector<int> n(B);
+    for (int b = 0; b < B; b++) {
+        ptr[b] = clips[b].data();
+        n[b] = (int)clips[b].size();
+        maxP = std::max(maxP, qasr_prompt_len(qasr_encoder_frames(qasr_mel_frames(n[b]))));
+    }
+    const int64_t t0 = now_ms();
+    std::vector<int32_t> sys;
+    if (!params.system_prompt.empty()) {
+        const int k = qasr_tokenize(model_, params.system_prompt.c_str(), nullptr, 0);
+        sys.resize(std::max(k, 0));
+        qasr_tokenize(model_, params.system_prompt.c_str(), sys.data(), k);
+    }
+    if (!ensure_ctx(B, maxP + (int)sys.size() + params.max_tokens)) {
+        for (auto &r : out) r.error_msg = error_msg_;
+        return out;
+    }
+    qasr_set_system_prompt(ctx_, sys.data(), (int)sys.size());
+    std::vector<int32_t> toks((size_t)B * params.max_tokens);
+    std::vector<int> nt(B);
+    qasr_timings tm{};
+    if (qasr_transcribe_batch(ctx_, ptr.data(), n.data(), B, params.max_tokens, 0, toks.data(), nt.data(), &tm) != 0) {
+        for (auto &r : out) r.error_msg = std::string("Decoding failed: ") + qasr_last_error();
+        return out;
+    }
+    const int64_t t1 = now_ms();
+    for (int b = 0; b < B; b++) {
+        transcribe_result &r = out[b];
+        r.tokens.assign(toks.begin() + (long)b * params.max_tokens, toks.begin() + (long)b * params.max_tokens + nt[b]);
+        const int len = qasr_detokenize(model_, r.tokens.data(), (int)r.tokens.size(), nullptr, 0);
+        std::string text(std::max(len, 0) + 1, '\0');
+        qasr_detokenize(model_, r.tokens.data(), (int)r.tokens.size(), &text[0], (int)text.size());
+        text.resize(std::max(len, 0));
+        r.text = text;
+        r.success = true;
+        r.t_mel_ms = (int64_t)tm.t_mel_ms;
+        r.t_encode_ms = (int64_t)tm.t_encode_ms;
+        r.t_decode_ms = (int64_t)(tm.t_prefill_ms + tm.t_decode_ms);
+        r.t_total_ms = t1 - t0;
+        if (progress_callback_)
+            for (int k = 1; k <= (int)r.tokens.size(); k++) progress_callback_(k, params.max_tokens);
+    }
+    return out;
+}
+
+transcribe_result Qwen3ASR::transcribe_internal(const float *samples, int n_samples, const transcribe_params &params) {
+    std::vector<std::vector<float>> one(1, std::vector<float>(samples, samples + n_samples));
+    transcribe_result r = transcribe_batch(one, params)[0];
+    if (r.success && params.print_progress) fprintf(stderr, "Tokens generated: %zu\n", r.tokens.size());
+    if (r.success && params.print_timing) {
+        fprintf(stderr, "\nTiming:\n");
+        fprintf(stderr, "  Mel spectrogram: %lld ms\n", (long long)r.t_mel_ms);
+        fprintf(stderr, "  Audio encoding:  %lld ms\n", (long long)r.t_encode_ms);
+        fprintf(stderr, "  Text decoding:   %lld ms\n", (long long)r.t_decode_ms);
+        fprintf(stderr, "  Total:           %lld ms\n", (long long)r.t_total_ms);
+        fprintf(stderr, "  Tokens generated: %zu\n", r.tokens.size());
+    }
+    return r;
+}
+
+void Qwen3ASR::set_progress_callback(progress_callback_t callback) { progress_callback_ = std::move(callback); }
+
+bool load_audio_file(const std::string &path, std::vector<float> &samples, int &sample_rate) {
+    std::string err;
+    if (!qasr::load_wav(path, samples, sample_rate, err)) {
+        fprintf(stderr, "Error: %s\n", err.c_str());
+        return false;
+    }
+    return true;
+}
+
+}  // namespace qwen3_asr

@@ -1,0 +1,303 @@
+"""qasr -- ctypes binding of libqasr.so (include/qasr_capi.h).
+
+Host-side mirror of the reference's Qwen3ASR / AudioEncoder / TextDecoder
+surface (src/qwen3_asr.h:55-116, src/audio_encoder.h:27-33,
+src/text_decoder.h:116-137) for tests, bench and scripting.  Every call goes
+through the C-ABI into hand-written HIP kernels; there is no CPU fallback:
+loading fails loudly if the in-tree libqasr.so is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libqasr.so")
+
+EXPORTS = [
+    "qasr_last_error", "qasr_version", "qasr_device_count",
+    "qasr_model_load", "qasr_model_free", "qasr_model_hparams", "qasr_model_device_bytes",
+    "qasr_ctx_create", "qasr_ctx_free",
+    "qasr_mel_frames", "qasr_encoder_frames", "qasr_prompt_len", "qasr_build_prompt",
+    "qasr_mel", "qasr_encode", "qasr_encode_conv", "qasr_prefill", "qasr_decode_step",
+    "qasr_stage_audio", "qasr_run", "qasr_set_system_prompt", "qasr_transcribe_batch",
+    "qasr_detokenize", "qasr_tokenize",
+    "qasr_load_wav", "qasr_write_wav", "qasr_synth_pcm", "qasr_write_synthetic_gguf",
+]
+
+
+class Hparams(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("enc_layers", "d_model", "enc_heads", "enc_ffn", "conv_channels", "n_mel")] + [
+        ("enc_eps", C.c_float)] + [(n, C.c_int32) for n in (
+            "vocab_size", "hidden_size", "dec_layers", "n_heads", "n_kv_heads", "head_dim", "dec_ffn")] + [
+        ("rms_eps", C.c_float), ("rope_theta", C.c_float)] + [(n, C.c_int32) for n in (
+            "eos_id", "pad_id", "audio_start_id", "audio_end_id", "audio_pad_id", "weight_type")]
+
+
+class Timings(C.Structure):
+    _fields_ = [("t_mel_ms", C.c_double), ("t_encode_ms", C.c_double), ("t_prefill_ms", C.c_double),
+                ("t_decode_ms", C.c_double), ("t_total_ms", C.c_double), ("n_decode_steps", C.c_int32)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load the in-tree libqasr.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libqasr.so not built at {LIB_PATH} (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        P, I, F = C.c_void_p, C.c_int, C.POINTER(C.c_float)
+        I32P, IP = C.POINTER(C.c_int32), C.POINTER(C.c_int)
+        sig = {
+            "qasr_last_error": ([], C.c_char_p), "qasr_version": ([], C.c_char_p),
+            "qasr_device_count": ([IP], I),
+            "qasr_model_load": ([C.c_char_p, I, C.POINTER(P)], I), "qasr_model_free": ([P], None),
+            "qasr_model_hparams": ([P, C.POINTER(Hparams)], I), "qasr_model_device_bytes": ([P], C.c_int64),
+            "qasr_ctx_create": ([P, I, I, C.POINTER(P)], I), "qasr_ctx_free": ([P], None),
+            "qasr_mel_frames": ([I], I), "qasr_encoder_frames": ([I], I), "qasr_prompt_len": ([I], I),
+            "qasr_build_prompt": ([P, I, I32P, IP], I),
+            "qasr_mel": ([P, C.POINTER(F), IP, I, F], I),
+            "qasr_encode": ([P, F, IP, I, F], I), "qasr_encode_conv": ([P, F, IP, I, F], I),
+            "qasr_prefill": ([P, I32P, IP, F, IP, IP, I, F, I32P], I),
+            "qasr_decode_step": ([P, I32P, IP, I, F, I32P], I),
+            "qasr_stage_audio": ([P, C.POINTER(F), IP, I], I),
+            "qasr_run": ([P, I, I, I32P, IP, C.POINTER(Timings)], I),
+            "qasr_set_system_prompt": ([P, I32P, I], I),
+            "qasr_transcribe_batch": ([P, C.POINTER(F), IP, I, I, I, I32P, IP, C.POINTER(Timings)], I),
+            "qasr_detokenize": ([P, I32P, I, C.c_char_p, I], I), "qasr_tokenize": ([P, C.c_char_p, I32P, I], I),
+            "qasr_load_wav": ([C.c_char_p, F, I, IP], I), "qasr_write_wav": ([C.c_char_p, F, I, I], I),
+            "qasr_synth_pcm": ([C.c_uint64, I, F], I),
+            "qasr_write_synthetic_gguf": ([C.c_char_p, C.c_char_p, C.c_uint64, I], I),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+class QasrError(RuntimeError):
+    pass
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise QasrError(f"{what}: {lib().qasr_last_error().decode(errors='replace')}")
+
+
+def _f(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _i32(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def _i(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_int))
+
+
+# ------------------------------------------------------------------ host utils
+def mel_frames(n: int) -> int:
+    return lib().qasr_mel_frames(n)
+
+
+def encoder_frames(T: int) -> int:
+    return lib().qasr_encoder_frames(T)
+
+
+def synth_pcm(seed: int, n: int) -> np.ndarray:
+    out = np.zeros(n, np.float32)
+    _check(lib().qasr_synth_pcm(seed, n, _f(out)), "synth_pcm")
+    return out
+
+
+def write_synthetic_gguf(path: str, config: str = "tiny", seed: int = 42, wtype: int = 1) -> None:
+    _check(lib().qasr_write_synthetic_gguf(path.encode(), config.encode(), seed, wtype), "write_synthetic_gguf")
+
+
+def load_wav(path: str):
+    sr = C.c_int(0)
+    n = lib().qasr_load_wav(path.encode(), None, 0, C.byref(sr))
+    if n < 0:
+        raise QasrError(f"load_wav: {lib().qasr_last_error().decode()}")
+    out = np.zeros(n, np.float32)
+    lib().qasr_load_wav(path.encode(), _f(out), n, C.byref(sr))
+    return out, sr.value
+
+
+def write_wav(path: str, pcm: np.ndarray, sr: int = 16000) -> None:
+    pcm = np.ascontiguousarray(pcm, np.float32)
+    _check(lib().qasr_write_wav(path.encode(), _f(pcm), len(pcm), sr), "write_wav")
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    lib().qasr_device_count(C.byref(n))
+    return n.value
+
+
+# ---------------------------------------------------------------------- model
+class Model:
+    """qasr_model: weights in one device arena (src/qwen3_asr.cpp:21-42)."""
+
+    def __init__(self, path: str, device: int = 0):
+        self.h = C.c_void_p()
+        _check(lib().qasr_model_load(path.encode(), device, C.byref(self.h)), "qasr_model_load")
+        hp = Hparams()
+        _check(lib().qasr_model_hparams(self.h, C.byref(hp)), "qasr_model_hparams")
+        self.hp = hp
+
+    def close(self):
+        if self.h:
+            lib().qasr_model_free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def device_bytes(self) -> int:
+        return lib().qasr_model_device_bytes(self.h)
+
+    def build_prompt(self, n_audio: int):
+        P = lib().qasr_prompt_len(n_audio)
+        ids = np.zeros(P, np.int32)
+        pos = C.c_int(0)
+        lib().qasr_build_prompt(self.h, n_audio, _i32(ids), C.byref(pos))
+        return ids, pos.value
+
+    def detokenize(self, ids: Sequence[int]) -> str:
+        a = np.ascontiguousarray(ids, np.int32)
+        n = lib().qasr_detokenize(self.h, _i32(a), len(a), None, 0)
+        buf = C.create_string_buffer(n + 1)
+        lib().qasr_detokenize(self.h, _i32(a), len(a), buf, n + 1)
+        return buf.raw[:n].decode("utf-8", errors="replace")
+
+    def tokenize(self, text: str) -> List[int]:
+        n = lib().qasr_tokenize(self.h, text.encode(), None, 0)
+        a = np.zeros(max(n, 1), np.int32)
+        lib().qasr_tokenize(self.h, text.encode(), _i32(a), n)
+        return a[:n].tolist()
+
+
+@dataclass
+class RunResult:
+    tokens: List[List[int]]
+    timings: Timings
+
+
+class Context:
+    """qasr_ctx: stream, KV cache, scratch (TextDecoder::init_kv_cache analogue)."""
+
+    def __init__(self, model: Model, max_batch: int = 1, max_ctx: int = 2048):
+        self.model = model
+        self.h = C.c_void_p()
+        _check(lib().qasr_ctx_create(model.h, max_batch, max_ctx, C.byref(self.h)), "qasr_ctx_create")
+        self.max_batch, self.max_ctx = max_batch, max_ctx
+
+    def close(self):
+        if self.h:
+            lib().qasr_ctx_free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- stages ------------------------------------------------------------
+    def mel(self, clips: Sequence[np.ndarray]) -> List[np.ndarray]:
+        clips = [np.ascontiguousarray(c, np.float32) for c in clips]
+        n = np.array([len(c) for c in clips], np.int32)
+        T = [mel_frames(int(k)) for k in n]
+        out = np.zeros(max(1, 128 * sum(T)), np.float32)
+        ptrs = (C.POINTER(C.c_float) * len(clips))(*[_f(c) for c in clips])
+        _check(lib().qasr_mel(self.h, ptrs, _i(n), len(clips), _f(out)), "qasr_mel")
+        res, o = [], 0
+        for t in T:
+            res.append(out[o:o + 128 * t].reshape(128, t))
+            o += 128 * t
+        return res
+
+    def _encode(self, mels: Sequence[np.ndarray], conv_only: bool) -> List[np.ndarray]:
+        T = np.array([m.shape[1] for m in mels], np.int32)
+        flat = np.ascontiguousarray(np.concatenate([np.ascontiguousarray(m, np.float32).ravel() for m in mels]))
+        N = [encoder_frames(int(t)) for t in T]
+        width = self.model.hp.d_model if conv_only else self.model.hp.hidden_size
+        out = np.zeros(max(1, sum(N) * width), np.float32)
+        fn = lib().qasr_encode_conv if conv_only else lib().qasr_encode
+        _check(fn(self.h, _f(flat), _i(T), len(mels), _f(out)), "qasr_encode")
+        res, o = [], 0
+        for k in N:
+            res.append(out[o * width:(o + k) * width].reshape(k, width))
+            o += k
+        return res
+
+    def encode(self, mels):
+        return self._encode(mels, False)
+
+    def encode_conv(self, mels):
+        return self._encode(mels, True)
+
+    def prefill(self, ids_list, feats_list=None, audio_pos=None, want_logits=True):
+        B = len(ids_list)
+        P = np.array([len(x) for x in ids_list], np.int32)
+        ids = np.ascontiguousarray(np.concatenate([np.asarray(x, np.int32) for x in ids_list]))
+        feats = None
+        N = np.zeros(B, np.int32)
+        ap = np.full(B, -1, np.int32) if audio_pos is None else np.asarray(audio_pos, np.int32)
+        if feats_list is not None:
+            N = np.array([f.shape[0] for f in feats_list], np.int32)
+            feats = np.ascontiguousarray(np.concatenate([np.asarray(f, np.float32) for f in feats_list]))
+        V = self.model.hp.vocab_size
+        logits = np.zeros((B, V), np.float32) if want_logits else None
+        am = np.zeros(B, np.int32)
+        _check(lib().qasr_prefill(self.h, _i32(ids), _i(P), _f(feats) if feats is not None else None, _i(ap), _i(N), B,
+                                  _f(logits) if want_logits else None, _i32(am)), "qasr_prefill")
+        return logits, am
+
+    def decode_step(self, tok, n_past, want_logits=True):
+        tok = np.ascontiguousarray(tok, np.int32)
+        npast = np.ascontiguousarray(n_past, np.int32)
+        B = len(tok)
+        logits = np.zeros((B, self.model.hp.vocab_size), np.float32) if want_logits else None
+        am = np.zeros(B, np.int32)
+        _check(lib().qasr_decode_step(self.h, _i32(tok), _i(npast), B, _f(logits) if want_logits else None, _i32(am)),
+               "qasr_decode_step")
+        return logits, am
+
+    # ---- whole path --------------------------------------------------------
+    def stage_audio(self, clips: Sequence[np.ndarray]) -> None:
+        self._staged = [np.ascontiguousarray(c, np.float32) for c in clips]
+        n = np.array([len(c) for c in self._staged], np.int32)
+        ptrs = (C.POINTER(C.c_float) * len(self._staged))(*[_f(c) for c in self._staged])
+        _check(lib().qasr_stage_audio(self.h, ptrs, _i(n), len(self._staged)), "qasr_stage_audio")
+
+    def run(self, max_tokens: int, ignore_eos: bool = False) -> RunResult:
+        B = len(self._staged)
+        toks = np.zeros((B, max_tokens), np.int32)
+        nt = np.zeros(B, np.int32)
+        t = Timings()
+        _check(lib().qasr_run(self.h, max_tokens, int(ignore_eos), _i32(toks), _i(nt), C.byref(t)), "qasr_run")
+        return RunResult([toks[b, :nt[b]].tolist() for b in range(B)], t)
+
+    def set_system_prompt(self, ids: Sequence[int]) -> None:
+        a = np.ascontiguousarray(ids, np.int32)
+        _check(lib().qasr_set_system_prompt(self.h, _i32(a) if len(a) else None, len(a)), "qasr_set_system_prompt")
+
+    def transcribe(self, clips, max_tokens=1024, ignore_eos=False) -> RunResult:
+        self.stage_audio(clips)
+        return self.run(max_tokens, ignore_eos)

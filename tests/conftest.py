@@ -1,0 +1,61 @@
+"""pytest configuration: markers, build of the libraries, shared fixtures.
+
+`-m "not gpu"`: oracle vs golden vectors, host logic, C-ABI exports (no GPU).
+`-m gpu`: parity of the HIP path (through the C-ABI) against the oracle.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "qwen3-asr.cpp_amd", "python"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+    config.addinivalue_line("markers", "slow: long-running (full-size model)")
+
+
+@pytest.fixture(scope="session")
+def built():
+    lib = os.path.join(ROOT, "qwen3-asr.cpp_amd", "libqasr.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "qwen3-asr.cpp_amd")], check=True)
+    orc = os.path.join(ROOT, "oracle", "liboracle.so")
+    if not os.path.exists(orc):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    return True
+
+
+@pytest.fixture(scope="session")
+def tiny_gguf(built, tmp_path_factory):
+    import qasr
+    p = str(tmp_path_factory.mktemp("models") / "tiny-f16.gguf")
+    qasr.write_synthetic_gguf(p, "tiny", 42, 1)
+    return p
+
+
+@pytest.fixture(scope="session")
+def tiny_oracle(tiny_gguf):
+    import oracle_py as op
+    op.set_threads(min(8, os.cpu_count() or 1))
+    return op.OracleModel(tiny_gguf)
+
+
+def gpu_available() -> bool:
+    try:
+        import qasr
+        return qasr.device_count() > 0
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def gpu(built):
+    if not gpu_available():
+        pytest.fail("GPU tests need a HIP device: the HIP path has no CPU fallback")
+    return True
