@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""bench.py -- RTFx + decode tok/s of the MI355X-native Qwen3-ASR hot path.
+
+Metric (BASELINE.json): RTFx (audio-sec / wall-sec) + decode tokens/s,
+Qwen3-ASR-0.6B f16.  A "step" = one full transcription (mel -> conv front-end
+-> encoder -> prompt splice -> prefill -> greedy decode) of the configs[1]
+workload per GPU: one 92 s / 16 kHz clip (the README benchmark clip length,
+README.md:129-138; synthetic audio since the Korean WAV is not shipped) with
+the fixed decode budget ceil(3.5 tok/s x 92 s) = 322 tokens, EOS ignored
+(SURVEY.md §8(d)).  Weights: synthetic Qwen3-ASR-0.6B-shaped f16 GGUF
+(random init, reference tensor names/shapes) unless $QASR_MODEL is set.
+PCM is staged in HBM before the timed region (qasr_stage_audio).
+
+Multi-GPU: one process per GPU (torchrun); each rank transcribes its own clips
+(weak scaling, no data-path collective); barrier + max-over-ranks timing via
+torch.distributed (RCCL); value = all ranks' audio-seconds / max wall time.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "qwen3-asr.cpp_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+
+import qasr  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+README_RTFX = 92.0 / 5.007   # 92 s clip in 5,007 ms on M2 Pro (README.md:136)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--seconds", type=float, default=92.0, help="clip length (configs[1]: 92 s)")
+    ap.add_argument("--batch", type=int, default=1, help="clips per GPU per step")
+    ap.add_argument("--tok-rate", type=float, default=3.5, help="decode budget tokens per audio second")
+    ap.add_argument("--model", default=os.environ.get("QASR_MODEL", ""))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=4, help="reference's effective ggml thread count")
+    ap.add_argument("--no-probe", action="store_true")
+    return ap.parse_args()
+
+
+def synthetic_model(rank: int) -> str:
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "qasr_synth_full_f16.gguf")
+    lock = path + ".done"
+    if rank == 0 and not os.path.exists(lock):
+        qasr.write_synthetic_gguf(path + ".tmp", "full", 42, 1)
+        os.replace(path + ".tmp", path)
+        open(lock, "w").close()
+    while not os.path.exists(lock):
+        time.sleep(0.5)
+    return path
+
+
+def cpu_baseline(model_path: str, secs: float, tok_rate: float, threads: int):
+    """Oracle (C restatement of the reference CPU path) on a bounded sample."""
+    import oracle_py as op
+    op.set_threads(threads)
+    om = op.OracleModel(model_path)
+    n = int(secs * 16000)
+    pcm = qasr.synth_pcm(1000, n)
+    ntok = int(math.ceil(tok_rate * secs))
+    t0 = time.perf_counter()
+    toks, t = om.transcribe(pcm, max_tokens=ntok, ignore_eos=True)
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(secs / dt, 4),
+        "unit": "audio-sec/wall-sec (RTFx)",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"one {secs:g} s synthetic clip, {ntok}-token greedy budget, full-size synthetic f16 model; "
+                  f"mel single-thread fp64 DFT as the reference, encoder/decoder {threads} threads "
+                  f"(mel {t[0]:.0f} ms, encode {t[1]:.0f} ms, decode {t[2]:.0f} ms)",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+        torch.cuda.set_device(local)
+        dist_mod.init_process_group("nccl")
+        dist = dist_mod
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    model_path = args.model or synthetic_model(rank)
+    m = qasr.Model(model_path, local)
+    n = int(args.seconds * 16000)
+    ntok = int(math.ceil(args.tok_rate * args.seconds))
+    T = qasr.mel_frames(n)
+    P = qasr.lib().qasr_prompt_len(qasr.encoder_frames(T))
+    ctx = qasr.Context(m, max_batch=args.batch, max_ctx=P + ntok + 8)
+    clips = [qasr.synth_pcm(1000 + rank * args.batch + i, n) for i in range(args.batch)]
+    ctx.stage_audio(clips)
+    for _ in range(args.warmup):
+        ctx.run(ntok, ignore_eos=True)
+    if not args.no_probe:
+        ctx.set_probe(1)
+    barrier()
+    t0 = time.perf_counter()
+    res = None
+    tm = {"mel": 0.0, "encode": 0.0, "prefill": 0.0, "decode": 0.0}
+    for _ in range(args.steps):
+        res = ctx.run(ntok, ignore_eos=True)   # synchronises its stream before returning
+        tm["mel"] += res.timings.t_mel_ms
+        tm["encode"] += res.timings.t_encode_ms
+        tm["prefill"] += res.timings.t_prefill_ms
+        tm["decode"] += res.timings.t_decode_ms
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    probe_ms, probe_n, probe_b = ctx.get_probe() if not args.no_probe else (0.0, 0, 0.0)
+    assert all(len(x) == ntok for x in res.tokens), "decode budget not met"
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    N = world
+    audio = N * args.batch * args.seconds * args.steps
+    value = audio / dt
+    out = {
+        "metric": "RTFx (audio-sec/wall-sec) + decode tokens/sec, Qwen3-ASR-0.6B f16",
+        "value": round(value, 3),
+        "unit": "audio-sec/wall-sec",
+        "n_gpus": N,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / README_RTFX, 3),
+        "dtype": "f16",
+        "data": "synthetic (seeded 16 kHz clip; random-init Qwen3-ASR-0.6B-shaped f16 GGUF)" if not args.model else
+                "synthetic audio; model " + os.path.basename(args.model),
+        "config": {"workload": f"configs[1]: one {args.seconds:g} s clip per GPU per step, greedy decode budget "
+                               f"{ntok} tokens (3.5 tok/s), EOS ignored", "clips_per_gpu": args.batch,
+                   "clip_seconds": args.seconds, "decode_tokens": ntok, "parallelism": f"dp{N} (utterance sharding)"},
+        "decode_tokens_per_s": round(N * args.batch * ntok * args.steps / dt, 2),
+        "stage_ms_per_step_rank0": {k: round(v / args.steps, 3) for k, v in tm.items()},
+    }
+    if probe_n:
+        avg_s = probe_ms / probe_n / 1e3
+        achieved = probe_b / avg_s / 1e9
+        out["roofline"] = {"kernel": "gemv_kernel<EPI_ARGMAX> (decode LM head, tied 151936x1024 f16 + fused argmax)",
+                           "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                           "bytes_per_launch": probe_b, "avg_launch_us": round(avg_s * 1e6, 2), "launches": probe_n}
+    if N == 1 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(model_path, args.cpu_sample_seconds, args.tok_rate, args.cpu_threads)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -132,6 +132,13 @@ int qasr_set_system_prompt(qasr_ctx *c, const int32_t *ids, int n);
 int qasr_transcribe_batch(qasr_ctx *c, const float *const *pcm, const int *n, int B, int max_tokens,
                           int ignore_eos, int32_t *tokens, int *n_tokens, qasr_timings *t);
 
+/* ---- measurement ---------------------------------------------------------- */
+/* Probe one kernel of the greedy decode step with HIP events on the context's
+ * stream during qasr_run (kernel 1 = LM-head GEMV + fused argmax).  Costs one
+ * extra graph launch per step while enabled; 0 disables and resets. */
+int qasr_set_probe(qasr_ctx *c, int kernel);
+int qasr_get_probe(qasr_ctx *c, double *total_ms, int64_t *launches, double *bytes_per_launch);
+
 /* ---- text (host) ---------------------------------------------------------- */
 /* UTF-8 text for ids (special <|..|> and [PAD..] tokens skipped); returns the
  * byte length (excluding NUL), writes at most cap-1 bytes + NUL. */

@@ -100,6 +100,12 @@ struct qasr_ctx {
     // staged audio
     std::vector<int> staged_n;
     std::vector<long> staged_off;
+    // kernel probe: HIP-event timing of one decode-step kernel inside qasr_run
+    int probe = 0;
+    double probe_ms = 0.0;
+    long probe_n = 0;
+    std::vector<hipEvent_t> pev;
+    hipGraphExec_t graph_pre = nullptr, graph_post = nullptr;
     // decode graph
     hipGraphExec_t graph = nullptr;
     int graph_B = -1;
@@ -107,6 +113,9 @@ struct qasr_ctx {
     ~qasr_ctx() {
         (void)hipSetDevice(m->device);
         if (graph) (void)hipGraphExecDestroy(graph);
+        if (graph_pre) (void)hipGraphExecDestroy(graph_pre);
+        if (graph_post) (void)hipGraphExecDestroy(graph_post);
+        for (auto &e : pev) (void)hipEventDestroy(e);
         for (auto &b : owned) (void)hipFree(b.p);
         for (auto &e : ev) if (e) (void)hipEventDestroy(e);
         if (pin) (void)hipHostFree(pin);
@@ -685,16 +694,17 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
 }
 
 // one decode step for B sequences: token d_tok at position d_pos
-static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits) {
+// part: 0 = whole step, 1 = embed + layers, 2 = LM head (+argmax), 3 = bookkeeping
+static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part = 0) {
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
     const int H = hp.hidden, QD = hp.n_head * 128, KD = hp.n_kv_head * 128, F = hp.dec_ffn;
     hipStream_t s = c->st;
     float *x = c->d_x;
-    launch_embed(c->d_tok, B, m->embd, H, nullptr, nullptr, x, s);
-    const size_t layer_kv = (size_t)c->max_batch * hp.n_kv_head * c->max_ctx * 128;
     const bool skinny = B <= 8;
-    for (int l = 0; l < hp.dec_layers; l++) {
+    const size_t layer_kv = (size_t)c->max_batch * hp.n_kv_head * c->max_ctx * 128;
+    if (part == 0 || part == 1) launch_embed(c->d_tok, B, m->embd, H, nullptr, nullptr, x, s);
+    for (int l = 0; (part == 0 || part == 1) && l < hp.dec_layers; l++) {
         const DecLayer &L = m->dec[l];
         if (skinny) {
             GemvArgs q{};
@@ -744,7 +754,9 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits) {
             launch_gemm(AM_DENSE, EPI_F32, dn, s);
         }
     }
-    launch_fill_u64(c->d_amax, B, 0ull, s);
+    if (part == 0 || part == 1) launch_fill_u64(c->d_amax, B, 0ull, s);
+    if (part == 3) goto bookkeeping;
+    if (part == 1) return;
     if (skinny) {
         GemvArgs lm{};
         lm.x = x; lm.ldx = H; lm.norm_w = m->out_norm; lm.eps = hp.rms_eps; lm.W = m->embd; lm.K = H; lm.N = hp.vocab; lm.M = B;
@@ -757,24 +769,87 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits) {
         lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
         launch_gemm(AM_DENSE, EPI_ARGMAX, lm, s);
     }
+    if (part == 2) return;
+bookkeeping:
     launch_step_advance(c->d_pos, c->d_nkv, c->d_step, B, s);
     launch_argmax_finish(c->d_amax, B, c->d_tok, c->d_hist, c->hist_cap, c->d_step, s);
 }
 
-static int decode_graph(qasr_ctx *c, int B, bool want_logits) {
-    if (c->graph && c->graph_B == B && c->graph_logits == want_logits) return 0;
-    if (c->graph) {
-        HIPCHK(hipGraphExecDestroy(c->graph));
-        c->graph = nullptr;
+// algorithmic HBM bytes of one launch of the probed kernel (decode LM head:
+// the tied 151936 x 1024 fp16 embedding streamed once + x rows + logits/keys)
+static double probe_bytes(qasr_ctx *c, int B) {
+    const Hparams &hp = c->m->hp;
+    return (double)hp.vocab * hp.hidden * 2 + (double)B * hp.hidden * 4 + (double)B * 8;
+}
+
+static int capture(qasr_ctx *c, int B, bool want_logits, int part, hipGraphExec_t *out) {
+    if (*out) {
+        HIPCHK(hipGraphExecDestroy(*out));
+        *out = nullptr;
     }
     hipGraph_t gr;
     HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
-    decode_step_kernels(c, B, want_logits);
+    decode_step_kernels(c, B, want_logits, part);
     HIPCHK(hipStreamEndCapture(c->st, &gr));
-    HIPCHK(hipGraphInstantiate(&c->graph, gr, nullptr, nullptr, 0));
+    HIPCHK(hipGraphInstantiate(out, gr, nullptr, nullptr, 0));
     HIPCHK(hipGraphDestroy(gr));
+    return 0;
+}
+
+static int decode_graph(qasr_ctx *c, int B, bool want_logits) {
+    if (c->graph && c->graph_B == B && c->graph_logits == want_logits) return 0;
+    int rc;
+    if ((rc = capture(c, B, want_logits, 0, &c->graph)) || (rc = capture(c, B, want_logits, 1, &c->graph_pre)) ||
+        (rc = capture(c, B, want_logits, 3, &c->graph_post)))
+        return rc;
     c->graph_B = B;
     c->graph_logits = want_logits;
+    return 0;
+}
+
+// one greedy step; under a probe the LM head runs eagerly between HIP events
+static int launch_step(qasr_ctx *c, int B, int k) {
+    if (!c->probe) {
+        HIPCHK(hipGraphLaunch(c->graph, c->st));
+        return 0;
+    }
+    while ((int)c->pev.size() < 2 * (k + 1)) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        c->pev.push_back(e);
+    }
+    HIPCHK(hipGraphLaunch(c->graph_pre, c->st));
+    HIPCHK(hipEventRecord(c->pev[2 * k], c->st));
+    decode_step_kernels(c, B, c->graph_logits, 2);
+    HIPCHK(hipEventRecord(c->pev[2 * k + 1], c->st));
+    HIPCHK(hipGraphLaunch(c->graph_post, c->st));
+    return 0;
+}
+
+static int probe_collect(qasr_ctx *c, int nsteps) {
+    if (!c->probe) return 0;
+    for (int k = 0; k < nsteps; k++) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, c->pev[2 * k], c->pev[2 * k + 1]));
+        c->probe_ms += ms;
+        c->probe_n++;
+    }
+    return 0;
+}
+
+extern "C" int qasr_set_probe(qasr_ctx *c, int kernel) {
+    if (!c || kernel < 0 || kernel > 1) return fail(QASR_ERR_ARG, "bad probe id");
+    c->probe = kernel;
+    c->probe_ms = 0.0;
+    c->probe_n = 0;
+    return 0;
+}
+
+extern "C" int qasr_get_probe(qasr_ctx *c, double *total_ms, int64_t *launches, double *bytes_per_launch) {
+    if (!c) return fail(QASR_ERR_ARG, "null context");
+    if (total_ms) *total_ms = c->probe_ms;
+    if (launches) *launches = c->probe_n;
+    if (bytes_per_launch) *bytes_per_launch = c->graph_B > 0 ? probe_bytes(c, c->graph_B) : 0.0;
     return 0;
 }
 
@@ -933,7 +1008,8 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
     std::vector<int32_t> hist((size_t)B * c->hist_cap);
     int steps = 0;
     if (ignore_eos) {
-        for (int k = 1; k < max_tokens; k++) HIPCHK(hipGraphLaunch(c->graph, s));
+        for (int k = 1; k < max_tokens; k++)
+            if ((rc = launch_step(c, B, k - 1))) return rc;
         steps = max_tokens - 1;
         HIPCHK(hipMemcpyAsync(hist.data(), c->d_hist, hist.size() * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -953,7 +1029,8 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
         int done = 0, st = 0;
         while (done + 1 < max_tokens && (st = all_done(done)) == 0) {
             const int todo = std::min(chunk, max_tokens - 1 - done);
-            for (int k = 0; k < todo; k++) HIPCHK(hipGraphLaunch(c->graph, s));
+            for (int k = 0; k < todo; k++)
+                if ((rc = launch_step(c, B, done + k))) return rc;
             done += todo;
         }
         if (st < 0) return fail(QASR_ERR_DEVICE, "device copy failed in decode loop");
@@ -963,6 +1040,7 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
     }
     HIPCHK(hipEventRecord(c->ev[4], s));
     HIPCHK(hipEventSynchronize(c->ev[4]));
+    if ((rc = probe_collect(c, steps))) return rc;
     for (int b = 0; b < B; b++) {
         int nt = 0;
         for (int k = 0; k <= steps && k < max_tokens; k++) {

@@ -25,6 +25,7 @@ EXPORTS = [
     "qasr_mel_frames", "qasr_encoder_frames", "qasr_prompt_len", "qasr_build_prompt",
     "qasr_mel", "qasr_encode", "qasr_encode_conv", "qasr_prefill", "qasr_decode_step",
     "qasr_stage_audio", "qasr_run", "qasr_set_system_prompt", "qasr_transcribe_batch",
+    "qasr_set_probe", "qasr_get_probe",
     "qasr_detokenize", "qasr_tokenize",
     "qasr_load_wav", "qasr_write_wav", "qasr_synth_pcm", "qasr_write_synthetic_gguf",
 ]
@@ -71,6 +72,8 @@ def lib() -> C.CDLL:
             "qasr_run": ([P, I, I, I32P, IP, C.POINTER(Timings)], I),
             "qasr_set_system_prompt": ([P, I32P, I], I),
             "qasr_transcribe_batch": ([P, C.POINTER(F), IP, I, I, I, I32P, IP, C.POINTER(Timings)], I),
+            "qasr_set_probe": ([P, I], I),
+            "qasr_get_probe": ([P, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_double)], I),
             "qasr_detokenize": ([P, I32P, I, C.c_char_p, I], I), "qasr_tokenize": ([P, C.c_char_p, I32P, I], I),
             "qasr_load_wav": ([C.c_char_p, F, I, IP], I), "qasr_write_wav": ([C.c_char_p, F, I, I], I),
             "qasr_synth_pcm": ([C.c_uint64, I, F], I),
@@ -297,6 +300,14 @@ class Context:
     def set_system_prompt(self, ids: Sequence[int]) -> None:
         a = np.ascontiguousarray(ids, np.int32)
         _check(lib().qasr_set_system_prompt(self.h, _i32(a) if len(a) else None, len(a)), "qasr_set_system_prompt")
+
+    def set_probe(self, kernel: int) -> None:
+        _check(lib().qasr_set_probe(self.h, kernel), "qasr_set_probe")
+
+    def get_probe(self):
+        ms, n, b = C.c_double(0), C.c_int64(0), C.c_double(0)
+        _check(lib().qasr_get_probe(self.h, C.byref(ms), C.byref(n), C.byref(b)), "qasr_get_probe")
+        return ms.value, n.value, b.value
 
     def transcribe(self, clips, max_tokens=1024, ignore_eos=False) -> RunResult:
         self.stage_audio(clips)

@@ -1,0 +1,90 @@
+"""GPU parity at the real Qwen3-ASR-0.6B dimensions (synthetic f16 weights,
+reference tensor names/shapes: 18 x 896 encoder, 28 x 1024 decoder,
+151936 vocab).  Sizes are kept where the CPU oracle finishes in seconds;
+the full 30 s / 92 s workloads are covered by size-independent properties
+(batch == single, determinism, decode budget) and by bench.py."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as op
+import qasr
+
+pytestmark = pytest.mark.gpu
+SR = 16000
+
+
+@pytest.fixture(scope="module")
+def full(gpu, tmp_path_factory):
+    p = os.environ.get("QASR_MODEL") or str(tmp_path_factory.mktemp("full") / "full-f16.gguf")
+    if not os.environ.get("QASR_MODEL"):
+        qasr.write_synthetic_gguf(p, "full", 42, 1)
+    m = qasr.Model(p)
+    c = qasr.Context(m, max_batch=4, max_ctx=1536)
+    op.set_threads(min(16, os.cpu_count() or 1))
+    om = op.OracleModel(p)
+    yield m, c, om
+    c.close()
+    m.close()
+
+
+def test_full_hparams(full):
+    m, _, _ = full
+    hp = m.hp
+    assert (hp.enc_layers, hp.d_model, hp.enc_heads, hp.enc_ffn, hp.conv_channels) == (18, 896, 14, 3584, 480)
+    assert (hp.vocab_size, hp.hidden_size, hp.dec_layers, hp.n_heads, hp.n_kv_heads, hp.head_dim, hp.dec_ffn) == (
+        151936, 1024, 28, 16, 8, 128, 3072)
+    assert m.device_bytes > 1.5e9
+
+
+@pytest.mark.parametrize("secs", [1.0, 3.1])
+def test_full_encode(full, secs):
+    _, c, om = full
+    mel = op.log_mel(qasr.synth_pcm(11000, int(secs * SR)))
+    g = c.encode([mel])[0]
+    o = om.encode(mel)
+    d = np.abs(g - o)
+    assert g.shape == o.shape == (qasr.encoder_frames(mel.shape[1]), 1024)
+    assert d.max() <= 2e-2 and d.mean() <= 1e-3, (d.max(), d.mean())
+
+
+def test_full_prefill_and_steps(full):
+    m, c, om = full
+    mel = op.log_mel(qasr.synth_pcm(12000, 2 * SR))
+    feats = om.encode(mel)
+    ids, pos = m.build_prompt(feats.shape[0])
+    lg, am = c.prefill([ids], [feats], [pos])
+    d = op.OracleDecoder(om, 256)
+    lo = d.forward(ids, 0, feats, pos)
+    scale = float(np.abs(lo).max())
+    assert np.abs(lg[0] - lo).max() <= 1e-2 * scale
+    rng = np.random.default_rng(3)
+    n_past = len(ids)
+    for _ in range(6):
+        tok = int(rng.integers(0, 151643))
+        lg, am = c.decode_step([tok], [n_past])
+        lo = d.forward([tok], n_past)
+        assert np.abs(lg[0] - lo).max() <= 1e-2 * float(np.abs(lo).max())
+        n_past += 1
+
+
+def test_full_transcribe_tokens(full):
+    _, c, om = full
+    pcm = qasr.synth_pcm(13000, 2 * SR)
+    r = c.transcribe([pcm], max_tokens=8, ignore_eos=True)
+    ora, _ = om.transcribe(pcm, max_tokens=8, ignore_eos=True)
+    assert r.tokens[0] == ora
+
+
+def test_full_30s_batch_properties(full):
+    """30 s clips (configs[0]/[2] length): batched == single, deterministic,
+    budget met, token ids in range."""
+    _, c, _ = full
+    clips = [qasr.synth_pcm(14000 + i, 30 * SR) for i in range(2)]
+    rb = c.transcribe(clips, max_tokens=24, ignore_eos=True)
+    rb2 = c.transcribe(clips, max_tokens=24, ignore_eos=True)
+    assert rb.tokens == rb2.tokens
+    for pcm, t in zip(clips, rb.tokens):
+        assert len(t) == 24 and all(0 <= x < 151936 for x in t)
+        assert c.transcribe([pcm], max_tokens=24, ignore_eos=True).tokens[0] == t
