@@ -80,6 +80,10 @@ const char *qasr_version(void);
 int qasr_device_count(int *n);
 
 /* ---- model ---------------------------------------------------------------- */
+/* device >= 0: upload weights to that HIP device.  device = QASR_HOST_ONLY:
+ * parse + validate the GGUF and load the tokenizer only (no GPU needed);
+ * such a model serves hparams/text calls but cannot create a context. */
+#define QASR_HOST_ONLY (-1)
 int qasr_model_load(const char *gguf_path, int device, qasr_model **out);
 void qasr_model_free(qasr_model *m);
 int qasr_model_hparams(const qasr_model *m, qasr_hparams *out);

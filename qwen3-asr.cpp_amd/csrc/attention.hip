@@ -306,82 +306,147 @@ void launch_prefill_attention(const PrefillAttnArgs &a, hipStream_t s) {
 }
 
 // ================================================== decoder single token
-// grid (max_splits, n_kv_head, B); block 256: 16 lanes per key (8 dims each),
-// 4 keys per wave instruction, both q heads of the kv group at once.
-__global__ __launch_bounds__(256) void decode_attn_split_kernel(DecodeAttnArgs a) {
-    __shared__ float sc[2][512];
-    __shared__ float red[2][4][2];
-    __shared__ float ored[4][2][128];
-    const int b = blockIdx.z, gk = blockIdx.y, sp = blockIdx.x;
-    const int nkv = a.n_kv[b];
-    const int k0 = sp * a.split_len;
-    if (k0 >= nkv) return;
-    const int k1 = min(nkv, k0 + a.split_len);
+// grid (max_splits, n_kv_head, B), block 512 (8 waves).  Split = 256 keys:
+// every K/V row of the split is requested at kernel entry (32 keys per wave,
+// 16 lanes x 16 B per key, 8+8 loads in flight per lane) before any
+// dependent work, so the split costs ~one HBM latency.  Every block re-derives
+// the two normalised + rotated q heads of its kv group (cheap); the block
+// owning the last split also normalises/rotates the new key, writes K/V into
+// the fp16 cache and uses them from LDS.  Partials are published
+// write-through (sc1) and counted with one agent-scope atomic; the last
+// arriver combines (MI355X_MICROARCH.md §visibility, table row 1) and resets
+// the counter for the next layer.
+#define DSPLIT 256
+#define DWAVES 8
+
+__device__ __forceinline__ void st_sc1(float *p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ float ld_sc1(const float *p) {
+    return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(512) void decode_attn_kernel(DecodeAttnArgs a) {
+    __shared__ float ys[2][128];
+    __shared__ __attribute__((aligned(16))) uint16_t qs[2][128];
+    __shared__ __attribute__((aligned(16))) uint16_t knew[128];
+    __shared__ __attribute__((aligned(16))) uint16_t vnew[128];
+    __shared__ float sc[2][DSPLIT];
+    __shared__ float wred[2][DWAVES][2];
+    __shared__ double red[DWAVES];
+    __shared__ float ored[DWAVES][2][128];
+    __shared__ float cml[2][2];
+    __shared__ int last_flag;
+    const int b = blockIdx.z, g = blockIdx.y, sp = blockIdx.x;
+    const int pos = a.pos[b];
+    const int nkv = pos + 1;
+    const int nsp = (nkv + DSPLIT - 1) / DSPLIT;
+    if (sp >= nsp) return;
+    const int k0 = sp * DSPLIT, k1 = min(nkv, k0 + DSPLIT);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
+    const float *raw = a.qkv + (long)b * (QD + 2 * KD);
+    const long cbase = ((long)a.seq_slot[b] * a.n_kv_head + g) * a.max_ctx;
+    uint16_t *kc = a.kc + cbase * 128, *vc = a.vc + cbase * 128;
+    const bool lastsp = sp == nsp - 1;
+    // ---- issue every cached K/V load of the split first (keys < pos)
     const int sub = lane >> 4, dl = (lane & 15) * 8;
-    const int QD = a.n_head * 128;
-    const long cbase = ((long)a.seq_slot[b] * a.n_kv_head + gk) * a.max_ctx;
-    const uint16_t *kc = a.kc + cbase * 128, *vc = a.vc + cbase * 128;
-    const half8 q0 = *(const half8 *)(a.q + (long)b * QD + (2 * gk) * 128 + dl);
-    const half8 q1 = *(const half8 *)(a.q + (long)b * QD + (2 * gk + 1) * 128 + dl);
-    // scores
-    for (int kb = k0 + wid * 4; kb < k1; kb += 16) {
-        const int key = kb + sub;
-        float s0 = 0.f, s1 = 0.f;
-        if (key < k1) {
-            const half8 kv = *(const half8 *)(kc + (long)key * 128 + dl);
+    constexpr int KPW = DSPLIT / DWAVES / 4;   // loads per lane = 8
+    half8 kv[KPW], vv[KPW];
 #pragma unroll
-            for (int e = 0; e < 8; e++) {
-                s0 = fmaf((float)kv[e], (float)q0[e], s0);
-                s1 = fmaf((float)kv[e], (float)q1[e], s1);
-            }
+    for (int i = 0; i < KPW; i++) {
+        const int key = k0 + wid * (DSPLIT / DWAVES) + i * 4 + sub;
+        kv[i] = half8{};
+        vv[i] = half8{};
+        if (key < k1 && key != pos) {
+            kv[i] = *(const half8 *)(kc + (long)key * 128 + dl);
+            vv[i] = *(const half8 *)(vc + (long)key * 128 + dl);
+        }
+    }
+    // ---- q heads 2g, 2g+1 (threads 0..255) and, in the last split, the new
+    //      k (threads 256..383) / v (384..511): ggml_rms_norm + mul + NEOX RoPE
+    const int part_id = tid >> 7, d = tid & 127;
+    float x = 0.f;
+    if (part_id < 2) x = raw[(2 * g + part_id) * 128 + d];
+    else if (lastsp) x = raw[QD + (part_id - 2) * KD + g * 128 + d];
+    {
+        const double ss = wave_sum_d((double)(x * x));
+        if (lane == 0) red[wid] = ss;
+    }
+    __syncthreads();
+    if (part_id < 2) {
+        const float scale = 1.0f / sqrtf((float)((red[2 * part_id] + red[2 * part_id + 1]) / 128.0) + a.eps);
+        ys[part_id][d] = fmul_rn(fmul_rn(x, scale), a.q_norm[d]);
+    } else if (lastsp && part_id == 2) {
+        const float scale = 1.0f / sqrtf((float)((red[4] + red[5]) / 128.0) + a.eps);
+        sc[0][d] = fmul_rn(fmul_rn(x, scale), a.k_norm[d]);   // sc[0] borrowed as scratch for the new k
+    } else if (lastsp) {
+        const uint16_t v = f_to_u16(x);   // ggml_cpy f32 -> f16
+        vnew[d] = v;
+        vc[(long)pos * 128 + d] = v;
+    }
+    __syncthreads();
+    if (part_id < 2 || (lastsp && part_id == 2)) {
+        const float2 cs = *(const float2 *)(a.rope + ((long)pos * 64 + (d & 63)) * 2);
+        const float *yy = part_id < 2 ? ys[part_id] : sc[0];
+        const float y0 = yy[d & 63], y1 = yy[(d & 63) + 64];
+        const uint16_t r = f_to_u16(d < 64 ? y0 * cs.x - y1 * cs.y : y0 * cs.y + y1 * cs.x);
+        if (part_id < 2) qs[part_id][d] = r;
+        else { knew[d] = r; kc[(long)pos * 128 + d] = r; }
+    }
+    __syncthreads();
+    // ---- scores
+    const half8 q0 = *(const half8 *)&qs[0][dl], q1 = *(const half8 *)&qs[1][dl];
+#pragma unroll
+    for (int i = 0; i < KPW; i++) {
+        const int j = wid * (DSPLIT / DWAVES) + i * 4 + sub;
+        if (k0 + j == pos) { kv[i] = *(const half8 *)&knew[dl]; vv[i] = *(const half8 *)&vnew[dl]; }
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            s0 = fmaf((float)kv[i][e], (float)q0[e], s0);
+            s1 = fmaf((float)kv[i][e], (float)q1[e], s1);
         }
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
             s0 += __shfl_xor(s0, o, 64);
             s1 += __shfl_xor(s1, o, 64);
         }
-        if ((lane & 15) == 0 && key < k1) {
-            sc[0][key - k0] = s0 * a.scale;
-            sc[1][key - k0] = s1 * a.scale;
+        if ((lane & 15) == 0) {
+            const bool ok = k0 + j < k1;
+            sc[0][j] = ok ? s0 * a.scale : -INFINITY;
+            sc[1][j] = ok ? s1 * a.scale : -INFINITY;
         }
     }
     __syncthreads();
-    const int n = k1 - k0;
-    float mx0 = -INFINITY, mx1 = -INFINITY;
-    for (int i = tid; i < n; i += 256) { mx0 = fmaxf(mx0, sc[0][i]); mx1 = fmaxf(mx1, sc[1][i]); }
-    mx0 = wave_max(mx0);
-    mx1 = wave_max(mx1);
-    if (lane == 0) { red[0][wid][0] = mx0; red[1][wid][0] = mx1; }
-    __syncthreads();
-    mx0 = fmaxf(fmaxf(red[0][0][0], red[0][1][0]), fmaxf(red[0][2][0], red[0][3][0]));
-    mx1 = fmaxf(fmaxf(red[1][0][0], red[1][1][0]), fmaxf(red[1][2][0], red[1][3][0]));
-    float l0 = 0.f, l1 = 0.f;
-    for (int i = tid; i < n; i += 256) {
-        const float p0 = expf(sc[0][i] - mx0), p1 = expf(sc[1][i] - mx1);
-        sc[0][i] = p0;
-        sc[1][i] = p1;
-        l0 += p0;
-        l1 += p1;
+    // ---- split-local softmax statistics: thread t handles key t&255 of head t>>8
+    {
+        const int hh = tid >> 8, j = tid & 255;
+        const float v = sc[hh][j];
+        const float mx = wave_max(v);
+        if (lane == 0) wred[hh][wid & 3][0] = mx;
+        __syncthreads();
+        const float M = fmaxf(fmaxf(wred[hh][0][0], wred[hh][1][0]), fmaxf(wred[hh][2][0], wred[hh][3][0]));
+        const float p = k0 + j < k1 ? expf(v - M) : 0.f;
+        sc[hh][j] = p;
+        const float l = wave_sum(p);
+        if (lane == 0) wred[hh][wid & 3][1] = l;
+        __syncthreads();
+        if (tid == 0 || tid == 256) {
+            cml[hh][0] = M;
+            cml[hh][1] = wred[hh][0][1] + wred[hh][1][1] + wred[hh][2][1] + wred[hh][3][1];
+        }
     }
-    l0 = wave_sum(l0);
-    l1 = wave_sum(l1);
-    if (lane == 0) { red[0][wid][1] = l0; red[1][wid][1] = l1; }
-    __syncthreads();
-    // P.V: lane owns 8 dims, 4 keys per wave instruction
+    // ---- P.V
     float acc0[8], acc1[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) { acc0[e] = 0.f; acc1[e] = 0.f; }
-    for (int kb = k0 + wid * 4; kb < k1; kb += 16) {
-        const int key = kb + sub;
-        if (key < k1) {
-            const half8 vv = *(const half8 *)(vc + (long)key * 128 + dl);
-            const float p0 = sc[0][key - k0], p1 = sc[1][key - k0];
 #pragma unroll
-            for (int e = 0; e < 8; e++) {
-                acc0[e] = fmaf((float)vv[e], p0, acc0[e]);
-                acc1[e] = fmaf((float)vv[e], p1, acc1[e]);
-            }
+    for (int i = 0; i < KPW; i++) {
+        const int j = wid * (DSPLIT / DWAVES) + i * 4 + sub;
+        const float p0 = sc[0][j], p1 = sc[1][j];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            acc0[e] = fmaf((float)vv[i][e], p0, acc0[e]);
+            acc1[e] = fmaf((float)vv[i][e], p1, acc1[e]);
         }
     }
 #pragma unroll
@@ -396,37 +461,66 @@ __global__ __launch_bounds__(256) void decode_attn_split_kernel(DecodeAttnArgs a
         for (int e = 0; e < 8; e++) { ored[wid][0][dl + e] = acc0[e]; ored[wid][1][dl + e] = acc1[e]; }
     }
     __syncthreads();
-    const int hh = tid >> 7, d = tid & 127;
-    const float ov = ored[0][hh][d] + ored[1][hh][d] + ored[2][hh][d] + ored[3][hh][d];
-    const int head = 2 * gk + hh;
-    const long pidx = ((long)b * a.n_head + head) * a.max_splits + sp;
-    a.part_o[pidx * 128 + d] = ov;
-    if (d == 0) {
-        a.part_ml[pidx * 2 + 0] = hh ? mx1 : mx0;
-        a.part_ml[pidx * 2 + 1] = red[hh][0][1] + red[hh][1][1] + red[hh][2][1] + red[hh][3][1];
+    const int h = (tid >> 7) & 1;
+    const bool active = tid < 256;   // threads 256..511 idle from here on (no early return: barriers follow)
+    float o = 0.f;
+#pragma unroll
+    for (int w = 0; w < DWAVES; w++) o += ored[w][h][d];
+    uint16_t *dst = a.out + (long)b * QD + (2 * g + h) * 128 + d;
+    if (nsp == 1) {
+        if (active) *dst = f_to_u16(cml[h][1] > 0.f ? o / cml[h][1] : 0.f);
+        return;
     }
-}
-
-// grid (n_head, B), block 128
-__global__ __launch_bounds__(128) void decode_attn_combine_kernel(DecodeAttnArgs a) {
-    const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
-    const int nsp = (a.n_kv[b] + a.split_len - 1) / a.split_len;
-    const long base = ((long)b * a.n_head + h) * a.max_splits;
+    // ---- publish partial (write-through), count arrivals
+    float *part = a.part + (((long)b * a.n_kv_head + g) * a.max_splits) * 2 * 132;
+    float *mine = part + ((long)sp * 2 + h) * 132;
+    if (active) {
+        st_sc1(mine + d, o);
+        if (d < 2) st_sc1(mine + 128 + d, cml[h][d]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(a.counter + (long)b * a.n_kv_head + g, 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        last_flag = prev == (unsigned)(nsp - 1);
+    }
+    __syncthreads();
+    if (!last_flag || !active) return;
+    // ---- last arriver: combine all splits of (b, g) with sc1 loads
+    float mv[32], lv[32];
     float M = -INFINITY;
-    for (int s = 0; s < nsp; s++) M = fmaxf(M, a.part_ml[(base + s) * 2]);
-    float l = 0.f, o = 0.f;
-    for (int s = 0; s < nsp; s++) {
-        const float w = expf(a.part_ml[(base + s) * 2] - M);
-        l += a.part_ml[(base + s) * 2 + 1] * w;
-        o += a.part_o[(base + s) * 128 + d] * w;
-    }
-    a.out[(long)b * a.n_head * 128 + h * 128 + d] = f_to_u16(l > 0.f ? o / l : 0.f);
+#pragma unroll
+    for (int s2 = 0; s2 < 32; s2++)
+        if (s2 < nsp) {
+            mv[s2] = ld_sc1(part + ((long)s2 * 2 + h) * 132 + 128);
+            lv[s2] = ld_sc1(part + ((long)s2 * 2 + h) * 132 + 129);
+        }
+    float ov[32];
+#pragma unroll
+    for (int s2 = 0; s2 < 32; s2++)
+        if (s2 < nsp) ov[s2] = ld_sc1(part + ((long)s2 * 2 + h) * 132 + d);
+#pragma unroll
+    for (int s2 = 0; s2 < 32; s2++)
+        if (s2 < nsp) M = fmaxf(M, mv[s2]);
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 32; s2++)
+        if (s2 < nsp) {
+            const float w = expf(mv[s2] - M);
+            L += lv[s2] * w;
+            O += ov[s2] * w;
+        }
+    *dst = f_to_u16(L > 0.f ? O / L : 0.f);
+    if (tid == 0) __hip_atomic_store(a.counter + (long)b * a.n_kv_head + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {
     if (a.B <= 0) return;
-    hipLaunchKernelGGL(decode_attn_split_kernel, dim3(a.max_splits, a.n_kv_head, a.B), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(a.n_head, a.B), dim3(128), 0, s, a);
+    hipLaunchKernelGGL(decode_attn_kernel, dim3(a.max_splits, a.n_kv_head, a.B), dim3(512), 0, s, a);
 }
+
+int decode_split_len() { return DSPLIT; }
+int decode_max_splits() { return 32; }
 
 }  // namespace qasr

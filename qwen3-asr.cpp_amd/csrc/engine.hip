@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -59,7 +60,7 @@ struct qasr_model {
     double2 *tw;
     double *hann;
     ~qasr_model() {
-        if (arena) {
+        if (arena && device >= 0) {
             (void)hipSetDevice(device);
             (void)hipFree(arena);
         }
@@ -89,10 +90,11 @@ struct qasr_ctx {
     // fixed decode state (sized by max_batch)
     int32_t *d_tok = nullptr, *d_hist = nullptr;
     int *d_pos = nullptr, *d_nkv = nullptr, *d_slot = nullptr, *d_step = nullptr;
-    float *d_x = nullptr, *d_qkv = nullptr, *d_part_o = nullptr, *d_part_ml = nullptr, *d_logits = nullptr;
+    float *d_x = nullptr, *d_qkv = nullptr, *d_part = nullptr, *d_logits = nullptr;
+    unsigned int *d_counter = nullptr;
     uint16_t *d_q = nullptr, *d_att = nullptr, *d_act = nullptr, *d_xh = nullptr;
     unsigned long long *d_amax = nullptr;
-    int max_splits = 0, split_len = 256, hist_cap = 0;
+    int max_splits = 0, hist_cap = 0;
     // pinned host staging for small per-call tables (reset at each top-level call)
     char *pin = nullptr;
     size_t pin_cap = 0, pin_used = 0;
@@ -100,6 +102,7 @@ struct qasr_ctx {
     // staged audio
     std::vector<int> staged_n;
     std::vector<long> staged_off;
+    bool eager = false;            // QASR_NO_GRAPH=1: launch the decode step eagerly (profilers)
     // kernel probe: HIP-event timing of one decode-step kernel inside qasr_run
     int probe = 0;
     double probe_ms = 0.0;
@@ -208,10 +211,13 @@ static bool check_shape(const gguf_tensor *t, std::vector<int64_t> ne, uint32_t 
 extern "C" int qasr_model_load(const char *path, int device, qasr_model **out) {
     if (!path || !out) return fail(QASR_ERR_ARG, "null argument");
     *out = nullptr;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(QASR_ERR_DEVICE, "no HIP device available");
-    if (device < 0 || device >= ndev) return fail(QASR_ERR_ARG, "bad device index");
-    HIPCHK(hipSetDevice(device));
+    const bool host_only = device == QASR_HOST_ONLY;
+    if (!host_only) {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(QASR_ERR_DEVICE, "no HIP device available");
+        if (device < 0 || device >= ndev) return fail(QASR_ERR_ARG, "bad device index");
+        HIPCHK(hipSetDevice(device));
+    }
     GGUFFile f;
     if (!f.open(path)) return fail(QASR_ERR_IO, f.error());
     std::unique_ptr<qasr_model> m(new qasr_model());
@@ -359,6 +365,10 @@ extern "C" int qasr_model_load(const char *path, int device, qasr_model **out) {
     ups.push_back({"tw", tw.size() * 8, (void **)&m->tw, [tw](uint8_t *o) { memcpy(o, tw.data(), tw.size() * 8); }});
     ups.push_back({"hann", hn.size() * 8, (void **)&m->hann, [hn](uint8_t *o) { memcpy(o, hn.data(), hn.size() * 8); }});
 
+    if (host_only) {   // hparams + tokenizer only: text helpers, validation, tests without a GPU
+        *out = m.release();
+        return 0;
+    }
     size_t total = 0;
     std::vector<size_t> offs(ups.size());
     for (size_t i = 0; i < ups.size(); i++) {
@@ -394,6 +404,7 @@ extern "C" int64_t qasr_model_device_bytes(const qasr_model *m) { return m ? (in
 // --------------------------------------------------------------- context
 extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_ctx **out) {
     if (!m || !out || max_batch <= 0 || max_ctx <= 0) return fail(QASR_ERR_ARG, "bad context arguments");
+    if (!m->arena) return fail(QASR_ERR_STATE, "model was loaded host-only (device QASR_HOST_ONLY)");
     *out = nullptr;
     HIPCHK(hipSetDevice(m->device));
     std::unique_ptr<qasr_ctx> c(new qasr_ctx());
@@ -411,7 +422,11 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     if ((rc = dev_alloc(c.get(), (void **)&c->rope, rope.size() * 4))) return rc;
     HIPCHK(hipMemcpy(c->rope, rope.data(), rope.size() * 4, hipMemcpyHostToDevice));
     const int B = max_batch, QD = hp.n_head * 128, KD = hp.n_kv_head * 128;
-    c->max_splits = (max_ctx + c->split_len - 1) / c->split_len;
+    c->max_splits = (max_ctx + decode_split_len() - 1) / decode_split_len();
+    if (c->max_splits > decode_max_splits())
+        return fail(QASR_ERR_ARG, "max_ctx exceeds " + std::to_string(decode_max_splits() * decode_split_len()));
+    const char *ng = getenv("QASR_NO_GRAPH");
+    c->eager = ng && ng[0] == '1';
     c->hist_cap = max_ctx;
     if ((rc = dev_alloc(c.get(), (void **)&c->d_tok, B * 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_hist, (size_t)B * max_ctx * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_pos, B * 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_nkv, B * 4)) ||
@@ -422,14 +437,15 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_q, (size_t)B * QD * 2)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_att, (size_t)B * QD * 2)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_act, (size_t)B * hp.dec_ffn * 2)) ||
-        (rc = dev_alloc(c.get(), (void **)&c->d_part_o, (size_t)B * hp.n_head * c->max_splits * 128 * 4)) ||
-        (rc = dev_alloc(c.get(), (void **)&c->d_part_ml, (size_t)B * hp.n_head * c->max_splits * 2 * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_part, (size_t)B * hp.n_kv_head * c->max_splits * 2 * 132 * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_counter, (size_t)B * hp.n_kv_head * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_logits, (size_t)B * hp.vocab * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_amax, (size_t)B * 8)))
         return rc;
     std::vector<int> slots(B);
     for (int b = 0; b < B; b++) slots[b] = b;
     HIPCHK(hipMemcpy(c->d_slot, slots.data(), B * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(c->d_counter, 0, (size_t)B * hp.n_kv_head * 4));
     *out = c.release();
     return 0;
 }
@@ -718,17 +734,11 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part =
             q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
             launch_gemm(AM_DENSE, EPI_F32, q, s);
         }
-        QkvPostArgs qa{};
-        qa.qkv = c->d_qkv; qa.rows = B; qa.row_seq = c->d_slot; qa.row_pos = c->d_pos;
-        qa.q_norm = L.q_norm; qa.k_norm = L.k_norm; qa.eps = hp.rms_eps; qa.rope = c->rope;
-        qa.n_head = hp.n_head; qa.n_kv_head = hp.n_kv_head; qa.q_out = c->d_q;
-        qa.kc = c->kc + l * layer_kv; qa.vc = c->vc + l * layer_kv; qa.max_ctx = c->max_ctx;
-        launch_qkv_post(qa, s);
         DecodeAttnArgs da{};
-        da.q = c->d_q; da.kc = qa.kc; da.vc = qa.vc; da.n_kv = c->d_nkv; da.seq_slot = c->d_slot; da.B = B;
+        da.qkv = c->d_qkv; da.q_norm = L.q_norm; da.k_norm = L.k_norm; da.eps = hp.rms_eps; da.rope = c->rope;
+        da.pos = c->d_pos; da.kc = c->kc + l * layer_kv; da.vc = c->vc + l * layer_kv; da.seq_slot = c->d_slot; da.B = B;
         da.n_head = hp.n_head; da.n_kv_head = hp.n_kv_head; da.max_ctx = c->max_ctx; da.max_splits = c->max_splits;
-        da.split_len = c->split_len; da.scale = 1.0f / sqrtf(128.0f); da.part_o = c->d_part_o; da.part_ml = c->d_part_ml;
-        da.out = c->d_att;
+        da.scale = 1.0f / sqrtf(128.0f); da.part = c->d_part; da.counter = c->d_counter; da.out = c->d_att;
         launch_decode_attention(da, s);
         if (skinny) {
             GemvArgs o{};
@@ -797,6 +807,11 @@ static int capture(qasr_ctx *c, int B, bool want_logits, int part, hipGraphExec_
 }
 
 static int decode_graph(qasr_ctx *c, int B, bool want_logits) {
+    if (c->eager) {
+        c->graph_B = B;
+        c->graph_logits = want_logits;
+        return 0;
+    }
     if (c->graph && c->graph_B == B && c->graph_logits == want_logits) return 0;
     int rc;
     if ((rc = capture(c, B, want_logits, 0, &c->graph)) || (rc = capture(c, B, want_logits, 1, &c->graph_pre)) ||
@@ -810,7 +825,8 @@ static int decode_graph(qasr_ctx *c, int B, bool want_logits) {
 // one greedy step; under a probe the LM head runs eagerly between HIP events
 static int launch_step(qasr_ctx *c, int B, int k) {
     if (!c->probe) {
-        HIPCHK(hipGraphLaunch(c->graph, c->st));
+        if (c->eager) decode_step_kernels(c, B, c->graph_logits, 0);
+        else HIPCHK(hipGraphLaunch(c->graph, c->st));
         return 0;
     }
     while ((int)c->pev.size() < 2 * (k + 1)) {
@@ -818,11 +834,13 @@ static int launch_step(qasr_ctx *c, int B, int k) {
         HIPCHK(hipEventCreate(&e));
         c->pev.push_back(e);
     }
-    HIPCHK(hipGraphLaunch(c->graph_pre, c->st));
+    if (c->eager) decode_step_kernels(c, B, c->graph_logits, 1);
+    else HIPCHK(hipGraphLaunch(c->graph_pre, c->st));
     HIPCHK(hipEventRecord(c->pev[2 * k], c->st));
     decode_step_kernels(c, B, c->graph_logits, 2);
     HIPCHK(hipEventRecord(c->pev[2 * k + 1], c->st));
-    HIPCHK(hipGraphLaunch(c->graph_post, c->st));
+    if (c->eager) decode_step_kernels(c, B, c->graph_logits, 3);
+    else HIPCHK(hipGraphLaunch(c->graph_post, c->st));
     return 0;
 }
 

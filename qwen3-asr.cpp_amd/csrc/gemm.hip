@@ -264,13 +264,34 @@ void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s) {
 // One wave per CPW output columns; every lane streams 16-byte pieces of the
 // weight rows straight from HBM into VGPRs (no LDS round trip for W, cdna
 // guide: "GEMV / M <= 16 decode weights"), x rows live in LDS as fp16.
-template <int EPI, int CPW, int MR>
+// NK = ceil(K/512) sweeps of a 64-lane x 8-half window.  The first column
+// group's weights are requested before the x prologue so the two HBM
+// latencies overlap; the grid strides over column groups beyond 1024 blocks.
+template <int EPI, int CPW, int MR, int NK>
 __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
     extern __shared__ __attribute__((aligned(16))) uint16_t xs[];   // [MR][K]
     __shared__ double red[4][MR];
     __shared__ unsigned long long bestk[4][MR];
+    constexpr int NR = EPI == EPI_SWIGLU_F16 ? 2 : 1;   // weight rows per output
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int K = g.K;
+    const int ncg = (g.N + CPW - 1) / CPW;
+    int cg = blockIdx.x * 4 + wid;
+    half8 wv[CPW][NR][NK];
+    auto wload = [&](int cgi) {
+#pragma unroll
+        for (int c = 0; c < CPW; c++)
+#pragma unroll
+            for (int r = 0; r < NR; r++)
+#pragma unroll
+                for (int t = 0; t < NK; t++) {
+                    const int o = cgi * CPW + c, k = t * 512 + lane * 8;
+                    long wrow = o;
+                    if constexpr (EPI == EPI_SWIGLU_F16) wrow = 32L * (o >> 4) + (o & 15) + 16 * r;
+                    wv[c][r][t] = (o < g.N && k < K) ? __builtin_nontemporal_load((const half8 *)(g.W + wrow * K + k)) : half8{};
+                }
+    };
+    if (cg < ncg) wload(cg);
     // ---- prologue: x rows -> fp16 in LDS (optionally RMS-normalised)
     if (g.norm_w) {
         double ss[MR];
@@ -313,66 +334,60 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
     }
     __syncthreads();
 
-    constexpr int NR = EPI == EPI_SWIGLU_F16 ? 2 : 1;   // weight rows per output
-    const int col0 = (blockIdx.x * 4 + wid) * CPW;
-    float acc[CPW][NR][MR];
-#pragma unroll
-    for (int c = 0; c < CPW; c++)
-#pragma unroll
-        for (int r = 0; r < NR; r++)
-#pragma unroll
-            for (int m = 0; m < MR; m++) acc[c][r][m] = 0.0f;
-    for (int k = lane * 8; k < K; k += 512) {   // K % 8 == 0; lanes past K idle on the last sweep
-        half8 wv[CPW][NR];
-#pragma unroll
-        for (int c = 0; c < CPW; c++)
-#pragma unroll
-            for (int r = 0; r < NR; r++) {
-                const int o = col0 + c;
-                long wrow = o;
-                if constexpr (EPI == EPI_SWIGLU_F16) wrow = 32L * (o >> 4) + (o & 15) + 16 * r;
-                wv[c][r] = o < g.N ? *(const half8 *)(g.W + wrow * K + k) : half8{};
-            }
-#pragma unroll
-        for (int m = 0; m < MR; m++) {
-            const half8 xv = *(const half8 *)(xs + m * K + k);
-#pragma unroll
-            for (int c = 0; c < CPW; c++)
-#pragma unroll
-                for (int r = 0; r < NR; r++)
-#pragma unroll
-                    for (int e = 0; e < 8; e++) acc[c][r][m] = fmaf((float)wv[c][r][e], (float)xv[e], acc[c][r][m]);
-        }
-    }
     unsigned long long best[MR];
 #pragma unroll
     for (int m = 0; m < MR; m++) best[m] = 0ull;
+    for (; cg < ncg; cg += gridDim.x * 4) {
+        const int col0 = cg * CPW;
+        float acc[CPW][NR][MR];
 #pragma unroll
-    for (int c = 0; c < CPW; c++) {
-        const int o = col0 + c;
+        for (int c = 0; c < CPW; c++)
 #pragma unroll
-        for (int m = 0; m < MR; m++) {
-            float v[NR];
+            for (int r = 0; r < NR; r++)
 #pragma unroll
-            for (int r = 0; r < NR; r++) v[r] = wave_sum(acc[c][r][m]);
-            if (o >= g.N || m >= g.M) continue;
-            if constexpr (EPI == EPI_ARGMAX) {
-                if (lane == 0 && g.out_f32) g.out_f32[(long)m * g.ldo + o] = v[0];
-                const unsigned long long key = argmax_key(v[0], o);
-                best[m] = key > best[m] ? key : best[m];
-            } else if (lane == 0) {
-                if constexpr (EPI == EPI_SWIGLU_F16) {
-                    g.out_f16[(long)m * g.ldo16 + o] = f_to_u16(silu_f(v[0]) * v[1]);
-                } else {
-                    float y = v[0];
-                    if (g.bias) y = fadd_rn(y, g.bias[o]);
-                    if constexpr (EPI == EPI_GELU_F16) {
-                        (void)y;
-                    } else if constexpr (EPI == EPI_F16) {
-                        g.out_f16[(long)m * g.ldo16 + o] = f_to_u16(y);
+                for (int m = 0; m < MR; m++) acc[c][r][m] = 0.0f;
+#pragma unroll
+        for (int t = 0; t < NK; t++) {
+            const int k = t * 512 + lane * 8;
+            if (k >= K) break;
+#pragma unroll
+            for (int m = 0; m < MR; m++) {
+                const half8 xv = *(const half8 *)(xs + m * K + k);
+#pragma unroll
+                for (int c = 0; c < CPW; c++)
+#pragma unroll
+                    for (int r = 0; r < NR; r++)
+#pragma unroll
+                        for (int e = 0; e < 8; e++) acc[c][r][m] = fmaf((float)wv[c][r][t][e], (float)xv[e], acc[c][r][m]);
+            }
+        }
+        const int nxt = cg + gridDim.x * 4;
+        if (nxt < ncg) wload(nxt);   // next group's weights in flight during the reductions
+#pragma unroll
+        for (int c = 0; c < CPW; c++) {
+            const int o = col0 + c;
+#pragma unroll
+            for (int m = 0; m < MR; m++) {
+                float v[NR];
+#pragma unroll
+                for (int r = 0; r < NR; r++) v[r] = wave_sum(acc[c][r][m]);
+                if (o >= g.N || m >= g.M) continue;
+                if constexpr (EPI == EPI_ARGMAX) {
+                    if (lane == 0 && g.out_f32) g.out_f32[(long)m * g.ldo + o] = v[0];
+                    const unsigned long long key = argmax_key(v[0], o);
+                    best[m] = key > best[m] ? key : best[m];
+                } else if (lane == 0) {
+                    if constexpr (EPI == EPI_SWIGLU_F16) {
+                        g.out_f16[(long)m * g.ldo16 + o] = f_to_u16(silu_f(v[0]) * v[1]);
                     } else {
-                        if (g.res) y = fadd_rn(y, g.res[(long)m * g.ldr + o]);
-                        g.out_f32[(long)m * g.ldo + o] = y;
+                        float y = v[0];
+                        if (g.bias) y = fadd_rn(y, g.bias[o]);
+                        if constexpr (EPI == EPI_F16) {
+                            g.out_f16[(long)m * g.ldo16 + o] = f_to_u16(y);
+                        } else {
+                            if (g.res) y = fadd_rn(y, g.res[(long)m * g.ldr + o]);
+                            g.out_f32[(long)m * g.ldo + o] = y;
+                        }
                     }
                 }
             }
@@ -391,20 +406,31 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
     }
 }
 
-template <int EPI, int CPW, int MR>
+template <int EPI, int CPW, int MR, int NK>
 static void run_gemv(const GemvArgs &g, hipStream_t s) {
     const int per_block = 4 * CPW;
-    const int blocks = (g.N + per_block - 1) / per_block;
+    int blocks = (g.N + per_block - 1) / per_block;
+    if (blocks > 1024) blocks = 1024;   // 256 CUs x 4 resident workgroups, grid-stride beyond
     const size_t lds = (size_t)MR * g.K * 2;
-    hipLaunchKernelGGL((gemv_kernel<EPI, CPW, MR>), dim3(blocks), dim3(256), lds, s, g);
+    hipLaunchKernelGGL((gemv_kernel<EPI, CPW, MR, NK>), dim3(blocks), dim3(256), lds, s, g);
+}
+
+template <int EPI, int CPW, int MR>
+static void gemv_nk(const GemvArgs &g, hipStream_t s) {
+    const int nk = (g.K + 511) / 512;
+    if (nk <= 1) run_gemv<EPI, CPW, MR, 1>(g, s);
+    else if (nk <= 2) run_gemv<EPI, CPW, MR, 2>(g, s);
+    else if (nk <= 4) run_gemv<EPI, CPW, MR, 4>(g, s);
+    else if (nk <= 6) run_gemv<EPI, CPW, MR, 6>(g, s);
+    else run_gemv<EPI, CPW, MR, 8>(g, s);
 }
 
 template <int EPI, int MR>
 static void gemv_cpw(const GemvArgs &g, hipStream_t s) {
     // keep >= ~512 waves in flight: fewer columns per wave for narrow outputs
-    if (g.N >= 8192) run_gemv<EPI, 4, MR>(g, s);
-    else if (g.N >= 2048) run_gemv<EPI, 2, MR>(g, s);
-    else run_gemv<EPI, 1, MR>(g, s);
+    if (g.N >= 8192) gemv_nk<EPI, 4, MR>(g, s);
+    else if (g.N >= 2048) gemv_nk<EPI, 2, MR>(g, s);
+    else gemv_nk<EPI, 1, MR>(g, s);
 }
 
 template <int EPI>

@@ -119,18 +119,25 @@ struct PrefillAttnArgs {
 };
 void launch_prefill_attention(const PrefillAttnArgs &a, hipStream_t s);
 
-// decoder single-token attention, split over the KV length + combine
+// decoder single-token attention, fused: q/k RMSNorm + RoPE, fp16 KV-cache
+// write of the new token, split-KV flash decoding and the cross-split combine
+// (last-arriving block per (sequence, kv head)), one launch per layer.
 struct DecodeAttnArgs {
-    const uint16_t *q;                   // [B][n_head*128] fp16
-    const uint16_t *kc, *vc;
-    const int *n_kv;                     // [B] keys per sequence (n_past + 1)
+    const float *qkv;                    // [B][QD + 2*KD] fp32 (raw QKV projection)
+    const float *q_norm, *k_norm; float eps;
+    const float *rope;                   // [max_pos][64][2]
+    const int *pos;                      // [B] position of the fed token (n_past)
+    uint16_t *kc, *vc;                   // this layer's cache base
     const int *seq_slot;
-    int B, n_head, n_kv_head, max_ctx, max_splits, split_len;
+    int B, n_head, n_kv_head, max_ctx, max_splits;
     float scale;
-    float *part_o; float *part_ml;       // scratch [B][n_head][max_splits][128], [B][n_head][max_splits][2]
+    float *part;                         // [B][n_kv_head][max_splits][2][132]
+    unsigned int *counter;               // [B][n_kv_head], zero at rest (self-resetting)
     uint16_t *out;                       // [B][n_head*128] fp16
 };
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
+int decode_split_len();
+int decode_max_splits();
 
 // ---------------------------------------------------------------- decoder misc
 // embedding gather (fp16 -> fp32) + audio splice (src/text_decoder.cpp:429-459)
