@@ -306,94 +306,132 @@ void launch_prefill_attention(const PrefillAttnArgs &a, hipStream_t s) {
 }
 
 // ================================================== decoder single token
-// grid (max_splits, n_kv_head, B), block 512 (8 waves).  Split = 256 keys:
-// every K/V row of the split is requested at kernel entry (32 keys per wave,
-// 16 lanes x 16 B per key, 8+8 loads in flight per lane) before any
-// dependent work, so the split costs ~one HBM latency.  Every block re-derives
-// the two normalised + rotated q heads of its kv group (cheap); the block
-// owning the last split also normalises/rotates the new key, writes K/V into
-// the fp16 cache and uses them from LDS.  Partials are published
-// write-through (sc1) and counted with one agent-scope atomic; the last
-// arriver combines (MI355X_MICROARCH.md §visibility, table row 1) and resets
-// the counter for the next layer.
-#define DSPLIT 256
-#define DWAVES 8
+// grid (grid_splits, n_kv_head, B), block 256 (4 waves).  Split = 64 keys, so a
+// 1.5k-token context spreads over ~190 workgroups (one CU streams only ~32 KB).
+// Every K/V row of the split -- and the raw q/k/v of the token -- is requested
+// at kernel entry, before the device-resident position is known: the split
+// costs about one HBM latency.  Each block normalises + rotates the two q heads
+// of its kv group (src/text_decoder.cpp:640-700: rms_norm, NEOX RoPE); the
+// block owning the last split also builds the new key, writes K/V into the fp16
+// cache and uses them from LDS.  Partials (unnormalised O, max, sum) are
+// published write-through (sc1 16-B stores, drained) and counted with one
+// agent-scope atomic per block; the last arriver of the kv group reads them back
+// with sc1 loads, combines (S_inv = 1/S as ggml's flash_attn_ext) and writes the
+// fp16 attention output (MI355X_MICROARCH.md, inter-workgroup hand-off table,
+// row 1).  Counters are zero at rest: the last arriver re-arms its own.
+#define DSPLIT 64
+#define DWAVES 4
 
-__device__ __forceinline__ void st_sc1(float *p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ float ld_sc1(const float *p) {
-    return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void st_sc1_x4(float *p, float4 f) {
+    const floatx4 v = {f.x, f.y, f.z, f.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+// nine 16-B sc1 loads (element tid + 256 j of src, clamped to n4 - 1) issued
+// back to back and drained in the same asm block, so no copy of an output can
+// be scheduled before the data has landed
+__device__ __forceinline__ void ld_sc1_x4_burst9(const floatx4 *src, int tid, int n4, floatx4 *v) {
+    const floatx4 *p[9];
+#pragma unroll
+    for (int j = 0; j < 9; j++) p[j] = src + min(tid + 256 * j, n4 - 1);
+    asm volatile(
+        "global_load_dwordx4 %0, %9, off sc1\n\t"
+        "global_load_dwordx4 %1, %10, off sc1\n\t"
+        "global_load_dwordx4 %2, %11, off sc1\n\t"
+        "global_load_dwordx4 %3, %12, off sc1\n\t"
+        "global_load_dwordx4 %4, %13, off sc1\n\t"
+        "global_load_dwordx4 %5, %14, off sc1\n\t"
+        "global_load_dwordx4 %6, %15, off sc1\n\t"
+        "global_load_dwordx4 %7, %16, off sc1\n\t"
+        "global_load_dwordx4 %8, %17, off sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8])
+        : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7]), "v"(p[8])
+        : "memory");
 }
 
-__global__ __launch_bounds__(512) void decode_attn_kernel(DecodeAttnArgs a) {
+__global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     __shared__ float ys[2][128];
+    __shared__ float kn[128];
     __shared__ __attribute__((aligned(16))) uint16_t qs[2][128];
     __shared__ __attribute__((aligned(16))) uint16_t knew[128];
     __shared__ __attribute__((aligned(16))) uint16_t vnew[128];
     __shared__ float sc[2][DSPLIT];
-    __shared__ float wred[2][DWAVES][2];
-    __shared__ double red[DWAVES];
+    __shared__ double red[DWAVES][2];
     __shared__ float ored[DWAVES][2][128];
     __shared__ float cml[2][2];
-    __shared__ int last_flag;
+    __shared__ int last;
+    __shared__ floatx4 stage[32 * 66];   // combine: up to 32 splits x 2 heads x 33 float4
     const int b = blockIdx.z, g = blockIdx.y, sp = blockIdx.x;
-    const int pos = a.pos[b];
-    const int nkv = pos + 1;
-    const int nsp = (nkv + DSPLIT - 1) / DSPLIT;
-    if (sp >= nsp) return;
-    const int k0 = sp * DSPLIT, k1 = min(nkv, k0 + DSPLIT);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
+    const int hh = tid >> 7, d = tid & 127;
+    trace_mark(a.trace, 0);
+    // ---- the token's raw q (heads 2g, 2g+1) and k / v of group g: tiny, L2-hot
     const float *raw = a.qkv + (long)b * (QD + 2 * KD);
-    const long cbase = ((long)a.seq_slot[b] * a.n_kv_head + g) * a.max_ctx;
+    const float xq = raw[(2 * g + hh) * 128 + d];
+    const float xkv = raw[QD + hh * KD + g * 128 + d];   // hh 0: k, 1: v
+    const float wqn = a.q_norm[d], wkn = a.k_norm[d];
+    // ---- every K/V row of the split (addresses depend on blockIdx only; decode
+    //      contexts use identity sequence slots).  Rows past the position are
+    //      masked below; the cache is zero-initialised so they are finite.
+    const long cbase = ((long)b * a.n_kv_head + g) * a.max_ctx;
     uint16_t *kc = a.kc + cbase * 128, *vc = a.vc + cbase * 128;
-    const bool lastsp = sp == nsp - 1;
-    // ---- issue every cached K/V load of the split first (keys < pos)
+    const int k0 = sp * DSPLIT;
     const int sub = lane >> 4, dl = (lane & 15) * 8;
-    constexpr int KPW = DSPLIT / DWAVES / 4;   // loads per lane = 8
+    constexpr int KPW = DSPLIT / DWAVES / 4;   // key rows per lane = 4
     half8 kv[KPW], vv[KPW];
 #pragma unroll
     for (int i = 0; i < KPW; i++) {
-        const int key = k0 + wid * (DSPLIT / DWAVES) + i * 4 + sub;
-        kv[i] = half8{};
-        vv[i] = half8{};
-        if (key < k1 && key != pos) {
-            kv[i] = *(const half8 *)(kc + (long)key * 128 + dl);
-            vv[i] = *(const half8 *)(vc + (long)key * 128 + dl);
+        const int key = min(k0 + wid * (DSPLIT / DWAVES) + i * 4 + sub, a.max_ctx - 1);
+        kv[i] = *(const half8 *)(kc + (long)key * 128 + dl);
+        vv[i] = *(const half8 *)(vc + (long)key * 128 + dl);
+    }
+    // No exit test on the position anywhere: with one, hipcc hoists the
+    // dependent pos load and the test in front of the K/V requests (two memory
+    // latencies in series).  The host sizes the grid to the context
+    // (grid_splits, a 256-key bucket); a split past this sequence's end is
+    // fully masked and publishes an empty partial (m = -inf, l = 0, O = 0).
+    const int pos = a.pos[b];
+    const int nkv = pos + 1;
+    const int nsp = gridDim.x;
+    const int k1 = min(nkv, k0 + DSPLIT);
+    const bool lastsp = sp == (nkv - 1) / DSPLIT;
+    // ---- ggml_rms_norm (double sums of fp32 squares) * weight, then NEOX RoPE
+    {
+        const double sq = wave_sum_d((double)(xq * xq));
+        const double sk = wave_sum_d((double)(xkv * xkv));
+        if (lane == 0) { red[wid][0] = sq; red[wid][1] = sk; }
+    }
+    __syncthreads();
+    {
+        const float scale = 1.0f / sqrtf((float)((red[2 * hh][0] + red[2 * hh + 1][0]) / 128.0) + a.eps);
+        ys[hh][d] = fmul_rn(fmul_rn(xq, scale), wqn);
+        if (lastsp) {
+            if (hh == 0) {
+                const float sk = 1.0f / sqrtf((float)((red[0][1] + red[1][1]) / 128.0) + a.eps);
+                kn[d] = fmul_rn(fmul_rn(xkv, sk), wkn);
+            } else {
+                const uint16_t v = f_to_u16(xkv);   // ggml_cpy f32 -> f16
+                vnew[d] = v;
+                vc[(long)pos * 128 + d] = v;
+            }
         }
     }
-    // ---- q heads 2g, 2g+1 (threads 0..255) and, in the last split, the new
-    //      k (threads 256..383) / v (384..511): ggml_rms_norm + mul + NEOX RoPE
-    const int part_id = tid >> 7, d = tid & 127;
-    float x = 0.f;
-    if (part_id < 2) x = raw[(2 * g + part_id) * 128 + d];
-    else if (lastsp) x = raw[QD + (part_id - 2) * KD + g * 128 + d];
+    __syncthreads();
     {
-        const double ss = wave_sum_d((double)(x * x));
-        if (lane == 0) red[wid] = ss;
-    }
-    __syncthreads();
-    if (part_id < 2) {
-        const float scale = 1.0f / sqrtf((float)((red[2 * part_id] + red[2 * part_id + 1]) / 128.0) + a.eps);
-        ys[part_id][d] = fmul_rn(fmul_rn(x, scale), a.q_norm[d]);
-    } else if (lastsp && part_id == 2) {
-        const float scale = 1.0f / sqrtf((float)((red[4] + red[5]) / 128.0) + a.eps);
-        sc[0][d] = fmul_rn(fmul_rn(x, scale), a.k_norm[d]);   // sc[0] borrowed as scratch for the new k
-    } else if (lastsp) {
-        const uint16_t v = f_to_u16(x);   // ggml_cpy f32 -> f16
-        vnew[d] = v;
-        vc[(long)pos * 128 + d] = v;
-    }
-    __syncthreads();
-    if (part_id < 2 || (lastsp && part_id == 2)) {
         const float2 cs = *(const float2 *)(a.rope + ((long)pos * 64 + (d & 63)) * 2);
-        const float *yy = part_id < 2 ? ys[part_id] : sc[0];
-        const float y0 = yy[d & 63], y1 = yy[(d & 63) + 64];
-        const uint16_t r = f_to_u16(d < 64 ? y0 * cs.x - y1 * cs.y : y0 * cs.y + y1 * cs.x);
-        if (part_id < 2) qs[part_id][d] = r;
-        else { knew[d] = r; kc[(long)pos * 128 + d] = r; }
+        const float y0 = ys[hh][d & 63], y1 = ys[hh][(d & 63) + 64];
+        qs[hh][d] = f_to_u16(d < 64 ? y0 * cs.x - y1 * cs.y : y0 * cs.y + y1 * cs.x);
+        if (lastsp && hh == 0) {
+            const float z0 = kn[d & 63], z1 = kn[(d & 63) + 64];
+            const uint16_t r = f_to_u16(d < 64 ? z0 * cs.x - z1 * cs.y : z0 * cs.y + z1 * cs.x);
+            knew[d] = r;
+            kc[(long)pos * 128 + d] = r;
+        }
     }
     __syncthreads();
-    // ---- scores
+    // ---- scores: 16 lanes per key row, 8 dims each
+    if (a.trace) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); trace_mark(a.trace, 1); }
     const half8 q0 = *(const half8 *)&qs[0][dl], q1 = *(const half8 *)&qs[1][dl];
 #pragma unroll
     for (int i = 0; i < KPW; i++) {
@@ -417,24 +455,16 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(DecodeAttnArgs a) {
         }
     }
     __syncthreads();
-    // ---- split-local softmax statistics: thread t handles key t&255 of head t>>8
-    {
-        const int hh = tid >> 8, j = tid & 255;
-        const float v = sc[hh][j];
-        const float mx = wave_max(v);
-        if (lane == 0) wred[hh][wid & 3][0] = mx;
-        __syncthreads();
-        const float M = fmaxf(fmaxf(wred[hh][0][0], wred[hh][1][0]), fmaxf(wred[hh][2][0], wred[hh][3][0]));
-        const float p = k0 + j < k1 ? expf(v - M) : 0.f;
-        sc[hh][j] = p;
+    // ---- split-local softmax statistics: wave h owns head h, lane = key
+    if (wid < 2) {
+        const float v = sc[wid][lane];
+        const float M = wave_max(v);
+        const float p = k0 + lane < k1 ? expf(v - M) : 0.f;
+        sc[wid][lane] = p;
         const float l = wave_sum(p);
-        if (lane == 0) wred[hh][wid & 3][1] = l;
-        __syncthreads();
-        if (tid == 0 || tid == 256) {
-            cml[hh][0] = M;
-            cml[hh][1] = wred[hh][0][1] + wred[hh][1][1] + wred[hh][2][1] + wred[hh][3][1];
-        }
+        if (lane == 0) { cml[wid][0] = M; cml[wid][1] = l; }
     }
+    __syncthreads();
     // ---- P.V
     float acc0[8], acc1[8];
 #pragma unroll
@@ -461,66 +491,70 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(DecodeAttnArgs a) {
         for (int e = 0; e < 8; e++) { ored[wid][0][dl + e] = acc0[e]; ored[wid][1][dl + e] = acc1[e]; }
     }
     __syncthreads();
-    const int h = (tid >> 7) & 1;
-    const bool active = tid < 256;   // threads 256..511 idle from here on (no early return: barriers follow)
-    float o = 0.f;
-#pragma unroll
-    for (int w = 0; w < DWAVES; w++) o += ored[w][h][d];
-    uint16_t *dst = a.out + (long)b * QD + (2 * g + h) * 128 + d;
-    if (nsp == 1) {
-        if (active) *dst = f_to_u16(cml[h][1] > 0.f ? o / cml[h][1] : 0.f);
-        return;
-    }
-    // ---- publish partial (write-through), count arrivals
-    float *part = a.part + (((long)b * a.n_kv_head + g) * a.max_splits) * 2 * 132;
-    float *mine = part + ((long)sp * 2 + h) * 132;
-    if (active) {
-        st_sc1(mine + d, o);
-        if (d < 2) st_sc1(mine + 128 + d, cml[h][d]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned prev = __hip_atomic_fetch_add(a.counter + (long)b * a.n_kv_head + g, 1u, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-        last_flag = prev == (unsigned)(nsp - 1);
-    }
-    __syncthreads();
-    if (!last_flag || !active) return;
-    // ---- last arriver: combine all splits of (b, g) with sc1 loads
-    float mv[32], lv[32];
-    float M = -INFINITY;
-#pragma unroll
-    for (int s2 = 0; s2 < 32; s2++)
-        if (s2 < nsp) {
-            mv[s2] = ld_sc1(part + ((long)s2 * 2 + h) * 132 + 128);
-            lv[s2] = ld_sc1(part + ((long)s2 * 2 + h) * 132 + 129);
+    // ---- publish this split's partial: [2 heads][O 128 | m, l, 0, 0], 16-B sc1 stores
+    float *gpart = a.part + (((long)b * a.n_kv_head + g) * a.max_splits) * 2 * 132;
+    if (tid < 66) {
+        const int h = tid / 33, q = tid - h * 33;
+        float4 v;
+        if (q < 32) {
+            v.x = ored[0][h][4 * q] + ored[1][h][4 * q] + ored[2][h][4 * q] + ored[3][h][4 * q];
+            v.y = ored[0][h][4 * q + 1] + ored[1][h][4 * q + 1] + ored[2][h][4 * q + 1] + ored[3][h][4 * q + 1];
+            v.z = ored[0][h][4 * q + 2] + ored[1][h][4 * q + 2] + ored[2][h][4 * q + 2] + ored[3][h][4 * q + 2];
+            v.w = ored[0][h][4 * q + 3] + ored[1][h][4 * q + 3] + ored[2][h][4 * q + 3] + ored[3][h][4 * q + 3];
+        } else {
+            v = make_float4(cml[h][0], cml[h][1], 0.f, 0.f);
         }
-    float ov[32];
+        st_sc1_x4(gpart + ((long)sp * 2 + h) * 132 + 4 * q, v);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned int *cnt = a.counter + (long)b * a.n_kv_head + g;
+    if (tid == 0) last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nsp - 1;
+    __syncthreads();
+    trace_mark(a.trace, 2);
+    if (!last) return;
+    // ---- last arriver: combine the partials of both heads (empty ones weigh 0).
+    //      Passes of up to 32 splits are staged through LDS with one burst of
+    //      16-B sc1 loads each (a per-split load loop would serialise ~nsp
+    //      memory latencies); passes merge with the usual online rescale.
+    if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float M = -INFINITY, L = 0.f, O = 0.f;
+    for (int s0 = 0; s0 < nsp; s0 += 32) {
+        const int ns = min(32, nsp - s0), n4 = ns * 66;
+        const floatx4 *src = (const floatx4 *)(gpart + (long)s0 * 264);
+        floatx4 v[9];
+        ld_sc1_x4_burst9(src, tid, n4, v);
+        __syncthreads();   // previous pass's readers are done with stage
 #pragma unroll
-    for (int s2 = 0; s2 < 32; s2++)
-        if (s2 < nsp) ov[s2] = ld_sc1(part + ((long)s2 * 2 + h) * 132 + d);
-#pragma unroll
-    for (int s2 = 0; s2 < 32; s2++)
-        if (s2 < nsp) M = fmaxf(M, mv[s2]);
-    float L = 0.f, O = 0.f;
-#pragma unroll
-    for (int s2 = 0; s2 < 32; s2++)
-        if (s2 < nsp) {
-            const float w = expf(mv[s2] - M);
-            L += lv[s2] * w;
-            O += ov[s2] * w;
+        for (int j = 0; j < 9; j++)
+            if (tid + 256 * j < n4) stage[tid + 256 * j] = v[j];
+        __syncthreads();
+        const float *sf = (const float *)stage;
+        float Mp = -INFINITY;
+        for (int s2 = 0; s2 < ns; s2++) Mp = fmaxf(Mp, sf[(s2 * 2 + hh) * 132 + 128]);
+        const float Mn = fmaxf(M, Mp);
+        const float r = expf(M - Mn);   // first pass: exp(-inf) = 0 on L = O = 0
+        L *= r;
+        O *= r;
+        for (int s2 = 0; s2 < ns; s2++) {
+            const float *row = sf + (s2 * 2 + hh) * 132;
+            const float w = expf(row[128] - Mn);
+            L += row[129] * w;
+            O += row[d] * w;
         }
-    *dst = f_to_u16(L > 0.f ? O / L : 0.f);
-    if (tid == 0) __hip_atomic_store(a.counter + (long)b * a.n_kv_head + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        M = Mn;
+    }
+    const float inv = L > 0.f ? 1.0f / L : 0.f;   // ggml: S_inv = 1/S, VKQ *= S_inv
+    a.out[(long)b * QD + (2 * g + hh) * 128 + d] = f_to_u16(O * inv);
+    trace_mark(a.trace, 3);
 }
 
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {
     if (a.B <= 0) return;
-    hipLaunchKernelGGL(decode_attn_kernel, dim3(a.max_splits, a.n_kv_head, a.B), dim3(512), 0, s, a);
+    hipLaunchKernelGGL(decode_attn_kernel, dim3(a.grid_splits, a.n_kv_head, a.B), dim3(256), 0, s, a);
 }
 
 int decode_split_len() { return DSPLIT; }
-int decode_max_splits() { return 32; }
+int decode_max_splits() { return 256; }
 
 }  // namespace qasr

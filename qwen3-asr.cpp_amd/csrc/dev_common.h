@@ -20,6 +20,12 @@ __device__ __forceinline__ f16 f2h(float f) { return (f16)f; }
 __device__ __forceinline__ float u16_to_f(uint16_t u) { return (float)__builtin_bit_cast(f16, u); }
 __device__ __forceinline__ uint16_t f_to_u16(float f) { return __builtin_bit_cast(uint16_t, (f16)f); }
 
+// 100 MHz constant clock shared by all CUs (dev trace timestamps)
+__device__ __forceinline__ unsigned long long rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void trace_mark(unsigned long long *tr, int slot) {
+    if (tr && threadIdx.x == 0) tr[(long)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 4 + slot] = rt_now();
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

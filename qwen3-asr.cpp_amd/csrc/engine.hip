@@ -13,6 +13,7 @@
 #include <functional>
 #include <memory>
 #include <string>
+#include <map>
 #include <vector>
 
 #include "../../include/qasr_capi.h"
@@ -91,7 +92,7 @@ struct qasr_ctx {
     int32_t *d_tok = nullptr, *d_hist = nullptr;
     int *d_pos = nullptr, *d_nkv = nullptr, *d_slot = nullptr, *d_step = nullptr;
     float *d_x = nullptr, *d_qkv = nullptr, *d_part = nullptr, *d_logits = nullptr;
-    unsigned int *d_counter = nullptr;
+    unsigned int *d_counter = nullptr, *d_done = nullptr;
     uint16_t *d_q = nullptr, *d_att = nullptr, *d_act = nullptr, *d_xh = nullptr;
     unsigned long long *d_amax = nullptr;
     int max_splits = 0, hist_cap = 0;
@@ -103,21 +104,35 @@ struct qasr_ctx {
     std::vector<int> staged_n;
     std::vector<long> staged_off;
     bool eager = false;            // QASR_NO_GRAPH=1: launch the decode step eagerly (profilers)
+    int dev_skip = 0;              // QASR_DEV_SKIP bitmask: profiling only, omits decode kernels
+    // QASR_DEV_TRACE=<file>: per-block timestamps of one decode layer's kernels
+    // (layer QASR_DEV_TRACE_LAYER, default 10) of the last step, dumped by qasr_run
+    std::string trace_path;
+    int trace_layer = 10;
+    unsigned long long *d_trace = nullptr;   // [6 kernels][4096 blocks][4]
     // kernel probe: HIP-event timing of one decode-step kernel inside qasr_run
     int probe = 0;
     double probe_ms = 0.0;
     long probe_n = 0;
     std::vector<hipEvent_t> pev;
-    hipGraphExec_t graph_pre = nullptr, graph_post = nullptr;
-    // decode graph
-    hipGraphExec_t graph = nullptr;
+    // decode graphs, one set per attention split-grid bucket (the grid must
+    // cover the longest sequence's context: it grows by 64 keys per split)
+    struct StepGraphs { hipGraphExec_t full = nullptr, pre = nullptr, post = nullptr; };
+    std::map<int, StepGraphs> graphs;
     int graph_B = -1;
     bool graph_logits = false;
+    int graph_base = 0;            // max prompt length of the current run: step k feeds position base + k
+    void drop_graphs() {
+        for (auto &kv : graphs) {
+            if (kv.second.full) (void)hipGraphExecDestroy(kv.second.full);
+            if (kv.second.pre) (void)hipGraphExecDestroy(kv.second.pre);
+            if (kv.second.post) (void)hipGraphExecDestroy(kv.second.post);
+        }
+        graphs.clear();
+    }
     ~qasr_ctx() {
         (void)hipSetDevice(m->device);
-        if (graph) (void)hipGraphExecDestroy(graph);
-        if (graph_pre) (void)hipGraphExecDestroy(graph_pre);
-        if (graph_post) (void)hipGraphExecDestroy(graph_post);
+        drop_graphs();
         for (auto &e : pev) (void)hipEventDestroy(e);
         for (auto &b : owned) (void)hipFree(b.p);
         for (auto &e : ev) if (e) (void)hipEventDestroy(e);
@@ -427,6 +442,14 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         return fail(QASR_ERR_ARG, "max_ctx exceeds " + std::to_string(decode_max_splits() * decode_split_len()));
     const char *ng = getenv("QASR_NO_GRAPH");
     c->eager = ng && ng[0] == '1';
+    const char *ds = getenv("QASR_DEV_SKIP");
+    if (ds) c->dev_skip = atoi(ds);
+    if (const char *tp = getenv("QASR_DEV_TRACE")) {
+        c->trace_path = tp;
+        if (const char *tl = getenv("QASR_DEV_TRACE_LAYER")) c->trace_layer = atoi(tl);
+        if ((rc = dev_alloc(c.get(), (void **)&c->d_trace, 6 * 4096 * 4 * 8))) return rc;
+        HIPCHK(hipMemset(c->d_trace, 0, 6 * 4096 * 4 * 8));
+    }
     c->hist_cap = max_ctx;
     if ((rc = dev_alloc(c.get(), (void **)&c->d_tok, B * 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_hist, (size_t)B * max_ctx * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_pos, B * 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_nkv, B * 4)) ||
@@ -439,6 +462,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_act, (size_t)B * hp.dec_ffn * 2)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_part, (size_t)B * hp.n_kv_head * c->max_splits * 2 * 132 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_counter, (size_t)B * hp.n_kv_head * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_logits, (size_t)B * hp.vocab * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_amax, (size_t)B * 8)))
         return rc;
@@ -446,6 +470,10 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     for (int b = 0; b < B; b++) slots[b] = b;
     HIPCHK(hipMemcpy(c->d_slot, slots.data(), B * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(c->d_counter, 0, (size_t)B * hp.n_kv_head * 4));
+    HIPCHK(hipMemset(c->d_done, 0, 4));
+    HIPCHK(hipMemset(c->kc, 0, kv * 2));   // decode attention reads whole splits and masks: keep every row finite
+    HIPCHK(hipMemset(c->vc, 0, kv * 2));
+    HIPCHK(hipMemset(c->d_amax, 0, (size_t)B * 8));
     *out = c.release();
     return 0;
 }
@@ -699,6 +727,7 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
     }
     HIPCHK(hipMemsetAsync(c->d_step, 0, 4, s));
     launch_argmax_finish(c->d_amax, B, c->d_tok, c->d_hist, c->hist_cap, c->d_step, s);
+    launch_fill_u64(c->d_amax, B, 0ull, s);   // zero at rest for the decode graph
     // decode state: next position = P_b, n_kv = P_b + 1 (the fed token's own key included)
     std::vector<int> pos(B), nkv(B);
     for (int b = 0; b < B; b++) { pos[b] = P[b]; nkv[b] = P[b] + 1; }
@@ -710,8 +739,9 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
 }
 
 // one decode step for B sequences: token d_tok at position d_pos
-// part: 0 = whole step, 1 = embed + layers, 2 = LM head (+argmax), 3 = bookkeeping
-static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part = 0) {
+// part: 0 = whole step, 1 = embed + layers, 2 = LM head (+argmax), 3 = bookkeeping;
+// splits: attention grid (64-key splits) covering the longest context of the step
+static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, int splits) {
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
     const int H = hp.hidden, QD = hp.n_head * 128, KD = hp.n_kv_head * 128, F = hp.dec_ffn;
@@ -719,14 +749,20 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part =
     float *x = c->d_x;
     const bool skinny = B <= 8;
     const size_t layer_kv = (size_t)c->max_batch * hp.n_kv_head * c->max_ctx * 128;
-    if (part == 0 || part == 1) launch_embed(c->d_tok, B, m->embd, H, nullptr, nullptr, x, s);
+    if ((part == 0 || part == 1) && !skinny) launch_embed(c->d_tok, B, m->embd, H, nullptr, nullptr, x, s);
+    const int skip = c->dev_skip;   // profiling only (QASR_DEV_SKIP): drop kernels to price them
     for (int l = 0; (part == 0 || part == 1) && l < hp.dec_layers; l++) {
         const DecLayer &L = m->dec[l];
+        auto tr = [&](int k) -> unsigned long long * {
+            return c->d_trace && l == c->trace_layer ? c->d_trace + (size_t)k * 4096 * 4 : nullptr;
+        };
         if (skinny) {
             GemvArgs q{};
             q.x = x; q.ldx = H; q.norm_w = L.attn_norm; q.eps = hp.rms_eps; q.W = L.wqkv; q.K = H; q.N = QD + 2 * KD; q.M = B;
             q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
-            launch_gemv(EPI_F32, q, s);
+            if (l == 0) { q.embd_ids = c->d_tok; q.embd = m->embd; q.x_store = x; }   // fused embedding gather
+            q.trace = tr(0);
+            if (!(skip & 1)) launch_gemv(EPI_F32, q, s);
         } else {
             launch_rmsnorm_f16(x, H, nullptr, B, H, L.attn_norm, hp.rms_eps, c->d_xh, s);
             GemmArgs q{};
@@ -737,20 +773,23 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part =
         DecodeAttnArgs da{};
         da.qkv = c->d_qkv; da.q_norm = L.q_norm; da.k_norm = L.k_norm; da.eps = hp.rms_eps; da.rope = c->rope;
         da.pos = c->d_pos; da.kc = c->kc + l * layer_kv; da.vc = c->vc + l * layer_kv; da.seq_slot = c->d_slot; da.B = B;
-        da.n_head = hp.n_head; da.n_kv_head = hp.n_kv_head; da.max_ctx = c->max_ctx; da.max_splits = c->max_splits;
+        da.n_head = hp.n_head; da.n_kv_head = hp.n_kv_head; da.max_ctx = c->max_ctx; da.max_splits = c->max_splits; da.grid_splits = splits;
         da.scale = 1.0f / sqrtf(128.0f); da.part = c->d_part; da.counter = c->d_counter; da.out = c->d_att;
-        launch_decode_attention(da, s);
+        da.trace = tr(1);
+        if (!(skip & 2)) launch_decode_attention(da, s);
         if (skinny) {
             GemvArgs o{};
-            o.xh = c->d_att; o.ldxh = QD; o.W = L.wo; o.K = QD; o.N = H; o.M = B; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
-            launch_gemv(EPI_F32, o, s);
+            o.xh = c->d_att; o.ldxh = QD; o.trace = tr(2);
+            o.W = L.wo; o.K = QD; o.N = H; o.M = B; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
+            if (!(skip & 4)) launch_gemv(EPI_F32, o, s);
             GemvArgs gu{};
             gu.x = x; gu.ldx = H; gu.norm_w = L.ffn_norm; gu.eps = hp.rms_eps; gu.W = L.wgu; gu.K = H; gu.N = F; gu.M = B;
-            gu.out_f16 = c->d_act; gu.ldo16 = F;
-            launch_gemv(EPI_SWIGLU_F16, gu, s);
+            gu.out_f16 = c->d_act; gu.ldo16 = F; gu.trace = tr(3);
+            if (!(skip & 8)) launch_gemv(EPI_SWIGLU_F16, gu, s);
             GemvArgs dn{};
             dn.xh = c->d_act; dn.ldxh = F; dn.W = L.wd; dn.K = F; dn.N = H; dn.M = B; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
-            launch_gemv(EPI_F32, dn, s);
+            dn.trace = tr(4);
+            if (!(skip & 16)) launch_gemv(EPI_F32, dn, s);
         } else {
             GemmArgs o{};
             o.A = c->d_att; o.lda = QD; o.W = L.wo; o.ldw = QD; o.M = B; o.N = H; o.K = QD; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
@@ -764,15 +803,19 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part =
             launch_gemm(AM_DENSE, EPI_F32, dn, s);
         }
     }
-    if (part == 0 || part == 1) launch_fill_u64(c->d_amax, B, 0ull, s);
+    if (part == 3 && skinny) return;   // bookkeeping is fused into the LM-head GEMV
     if (part == 3) goto bookkeeping;
     if (part == 1) return;
-    if (skinny) {
+    if (skinny) {   // amax / done are zero at rest: the LM head's last workgroup re-arms them
         GemvArgs lm{};
         lm.x = x; lm.ldx = H; lm.norm_w = m->out_norm; lm.eps = hp.rms_eps; lm.W = m->embd; lm.K = H; lm.N = hp.vocab; lm.M = B;
         lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
+        lm.done = c->d_done; lm.tok_out = c->d_tok; lm.hist = c->d_hist; lm.hist_stride = c->hist_cap; lm.step = c->d_step;
+        lm.pos = c->d_pos;
         launch_gemv(EPI_ARGMAX, lm, s);
+        return;
     } else {
+        launch_fill_u64(c->d_amax, B, 0ull, s);
         launch_rmsnorm_f16(x, H, nullptr, B, H, m->out_norm, hp.rms_eps, c->d_xh, s);
         GemmArgs lm{};
         lm.A = c->d_xh; lm.lda = H; lm.W = m->embd; lm.ldw = H; lm.M = B; lm.N = hp.vocab; lm.K = H;
@@ -783,6 +826,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part =
 bookkeeping:
     launch_step_advance(c->d_pos, c->d_nkv, c->d_step, B, s);
     launch_argmax_finish(c->d_amax, B, c->d_tok, c->d_hist, c->hist_cap, c->d_step, s);
+    launch_fill_u64(c->d_amax, B, 0ull, s);   // re-arm (zero at rest)
 }
 
 // algorithmic HBM bytes of one launch of the probed kernel (decode LM head:
@@ -792,41 +836,55 @@ static double probe_bytes(qasr_ctx *c, int B) {
     return (double)hp.vocab * hp.hidden * 2 + (double)B * hp.hidden * 4 + (double)B * 8;
 }
 
-static int capture(qasr_ctx *c, int B, bool want_logits, int part, hipGraphExec_t *out) {
-    if (*out) {
-        HIPCHK(hipGraphExecDestroy(*out));
-        *out = nullptr;
-    }
+static int capture(qasr_ctx *c, int B, bool want_logits, int part, int splits, hipGraphExec_t *out) {
     hipGraph_t gr;
     HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
-    decode_step_kernels(c, B, want_logits, part);
+    decode_step_kernels(c, B, want_logits, part, splits);
     HIPCHK(hipStreamEndCapture(c->st, &gr));
     HIPCHK(hipGraphInstantiate(out, gr, nullptr, nullptr, 0));
     HIPCHK(hipGraphDestroy(gr));
     return 0;
 }
 
-static int decode_graph(qasr_ctx *c, int B, bool want_logits) {
-    if (c->eager) {
-        c->graph_B = B;
-        c->graph_logits = want_logits;
-        return 0;
-    }
-    if (c->graph && c->graph_B == B && c->graph_logits == want_logits) return 0;
-    int rc;
-    if ((rc = capture(c, B, want_logits, 0, &c->graph)) || (rc = capture(c, B, want_logits, 1, &c->graph_pre)) ||
-        (rc = capture(c, B, want_logits, 3, &c->graph_post)))
-        return rc;
+// split-grid bucket for a step whose longest sequence feeds position `pos`
+// (rounded up to 4 splits = 256 keys, so a run re-captures every 256 steps)
+static int split_bucket(qasr_ctx *c, int pos) {
+    const int need = (pos + 1 + decode_split_len() - 1) / decode_split_len();
+    return std::min(c->max_splits, (need + 3) / 4 * 4);
+}
+
+// prepare decode graphs for batch B; base = longest prompt (step k feeds base + k)
+static int decode_graph(qasr_ctx *c, int B, bool want_logits, int base) {
+    if (c->graph_B != B || c->graph_logits != want_logits) c->drop_graphs();
     c->graph_B = B;
     c->graph_logits = want_logits;
+    c->graph_base = base;
     return 0;
 }
 
-// one greedy step; under a probe the LM head runs eagerly between HIP events
+static int step_graphs(qasr_ctx *c, int splits, qasr_ctx::StepGraphs **out) {
+    auto &gs = c->graphs[splits];
+    const int B = c->graph_B;
+    int rc;
+    if (!gs.full) {
+        if ((rc = capture(c, B, c->graph_logits, 0, splits, &gs.full)) || (rc = capture(c, B, c->graph_logits, 1, splits, &gs.pre)))
+            return rc;
+        if (B > 8 && (rc = capture(c, B, c->graph_logits, 3, splits, &gs.post))) return rc;   // skinny: fused into the LM head
+    }
+    *out = &gs;
+    return 0;
+}
+
+// one greedy step (k = 0-based step of the run); under a probe the LM head
+// runs eagerly between HIP events
 static int launch_step(qasr_ctx *c, int B, int k) {
+    const int splits = split_bucket(c, c->graph_base + k);
+    qasr_ctx::StepGraphs *gs = nullptr;
+    int rc;
+    if (!c->eager && (rc = step_graphs(c, splits, &gs))) return rc;
     if (!c->probe) {
-        if (c->eager) decode_step_kernels(c, B, c->graph_logits, 0);
-        else HIPCHK(hipGraphLaunch(c->graph, c->st));
+        if (c->eager) decode_step_kernels(c, B, c->graph_logits, 0, splits);
+        else HIPCHK(hipGraphLaunch(gs->full, c->st));
         return 0;
     }
     while ((int)c->pev.size() < 2 * (k + 1)) {
@@ -834,13 +892,13 @@ static int launch_step(qasr_ctx *c, int B, int k) {
         HIPCHK(hipEventCreate(&e));
         c->pev.push_back(e);
     }
-    if (c->eager) decode_step_kernels(c, B, c->graph_logits, 1);
-    else HIPCHK(hipGraphLaunch(c->graph_pre, c->st));
+    if (c->eager) decode_step_kernels(c, B, c->graph_logits, 1, splits);
+    else HIPCHK(hipGraphLaunch(gs->pre, c->st));
     HIPCHK(hipEventRecord(c->pev[2 * k], c->st));
-    decode_step_kernels(c, B, c->graph_logits, 2);
+    decode_step_kernels(c, B, c->graph_logits, 2, splits);
     HIPCHK(hipEventRecord(c->pev[2 * k + 1], c->st));
-    if (c->eager) decode_step_kernels(c, B, c->graph_logits, 3);
-    else HIPCHK(hipGraphLaunch(c->graph_post, c->st));
+    if (c->eager) decode_step_kernels(c, B, c->graph_logits, 3, splits);
+    else if (gs->post) HIPCHK(hipGraphLaunch(gs->post, c->st));
     return 0;
 }
 
@@ -967,7 +1025,7 @@ extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_pa
     HIPCHK(hipMemcpyAsync(c->d_pos, pos.data(), B * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemcpyAsync(c->d_nkv, nkv.data(), B * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemsetAsync(c->d_step, 0, 4, c->st));
-    decode_step_kernels(c, B, logits != nullptr);
+    decode_step_kernels(c, B, logits != nullptr, 0, split_bucket(c, *std::max_element(pos.begin(), pos.end())));
     HIPCHK(hipGetLastError());
     if (logits) HIPCHK(hipMemcpyAsync(logits, c->d_logits, (size_t)B * c->m->hp.vocab * 4, hipMemcpyDeviceToHost, c->st));
     if (argmax) HIPCHK(hipMemcpyAsync(argmax, c->d_tok, B * 4, hipMemcpyDeviceToHost, c->st));
@@ -1022,7 +1080,7 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
     if ((rc = run_prefill(c, ids, P, c->feats.as<float>(), ap, Nb, false))) return rc;
     HIPCHK(hipEventRecord(c->ev[3], s));
     // greedy loop (src/qwen3_asr.cpp:270-296): step k feeds token k at position P+k-1
-    if ((rc = decode_graph(c, B, false))) return rc;
+    if ((rc = decode_graph(c, B, false, *std::max_element(P.begin(), P.end())))) return rc;
     std::vector<int32_t> hist((size_t)B * c->hist_cap);
     int steps = 0;
     if (ignore_eos) {
@@ -1059,6 +1117,14 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
     HIPCHK(hipEventRecord(c->ev[4], s));
     HIPCHK(hipEventSynchronize(c->ev[4]));
     if ((rc = probe_collect(c, steps))) return rc;
+    if (c->d_trace) {   // dev trace dump: raw [6][4096][4] u64
+        std::vector<unsigned long long> tr((size_t)6 * 4096 * 4);
+        HIPCHK(hipMemcpy(tr.data(), c->d_trace, tr.size() * 8, hipMemcpyDeviceToHost));
+        if (FILE *f = fopen(c->trace_path.c_str(), "wb")) {
+            (void)fwrite(tr.data(), 8, tr.size(), f);
+            fclose(f);
+        }
+    }
     for (int b = 0; b < B; b++) {
         int nt = 0;
         for (int k = 0; k <= steps && k < max_tokens; k++) {

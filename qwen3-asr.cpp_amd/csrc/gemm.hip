@@ -274,10 +274,14 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
     __shared__ unsigned long long bestk[4][MR];
     constexpr int NR = EPI == EPI_SWIGLU_F16 ? 2 : 1;   // weight rows per output
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    trace_mark(g.trace, 0);
     const int K = g.K;
     const int ncg = (g.N + CPW - 1) / CPW;
     int cg = blockIdx.x * 4 + wid;
     half8 wv[CPW][NR][NK];
+    // unconditional loads (clamped addresses, masked after): a conditional
+    // load makes hipcc wait vmcnt(0) at the branch join, which would serialise
+    // the weight stream behind the x prologue
     auto wload = [&](int cgi) {
 #pragma unroll
         for (int c = 0; c < CPW; c++)
@@ -285,52 +289,77 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
             for (int r = 0; r < NR; r++)
 #pragma unroll
                 for (int t = 0; t < NK; t++) {
-                    const int o = cgi * CPW + c, k = t * 512 + lane * 8;
+                    const int o = min(cgi * CPW + c, g.N - 1), k = min(t * 512 + lane * 8, K - 8);
                     long wrow = o;
                     if constexpr (EPI == EPI_SWIGLU_F16) wrow = 32L * (o >> 4) + (o & 15) + 16 * r;
-                    wv[c][r][t] = (o < g.N && k < K) ? __builtin_nontemporal_load((const half8 *)(g.W + wrow * K + k)) : half8{};
+                    wv[c][r][t] = __builtin_nontemporal_load((const half8 *)(g.W + wrow * K + k));
                 }
     };
     if (cg < ncg) wload(cg);
-    // ---- prologue: x rows -> fp16 in LDS (optionally RMS-normalised)
-    if (g.norm_w) {
+    // ---- prologue: x rows -> fp16 in LDS (optionally RMS-normalised); each
+    //      thread owns 4 consecutive elements per 1024-wide pass, one vector load each
+    constexpr int KP = (NK * 512 + 1023) / 1024;
+    if (g.norm_w || g.x) {
+        float xr[MR][KP][4];
         double ss[MR];
 #pragma unroll
-        for (int m = 0; m < MR; m++) ss[m] = 0.0;
-        for (int k = tid; k < K; k += 256)
+        for (int m = 0; m < MR; m++) {
+            ss[m] = 0.0;
+#pragma unroll
+            for (int p = 0; p < KP; p++) {
+                const int k = p * 1024 + tid * 4;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (m < g.M && k < K) {
+                    if (g.embd_ids) {
+                        const uint2 hv = *(const uint2 *)(g.embd + (long)g.embd_ids[m] * K + k);
+                        v = make_float4(u16_to_f(hv.x & 0xffff), u16_to_f(hv.x >> 16), u16_to_f(hv.y & 0xffff), u16_to_f(hv.y >> 16));
+                        if (g.x_store && blockIdx.x == 0) *(float4 *)(g.x_store + (long)m * g.ldx + k) = v;
+                    } else {
+                        v = *(const float4 *)(g.x + (long)m * g.ldx + k);
+                    }
+                }
+                xr[m][p][0] = v.x; xr[m][p][1] = v.y; xr[m][p][2] = v.z; xr[m][p][3] = v.w;
+                ss[m] += (double)(v.x * v.x);
+                ss[m] += (double)(v.y * v.y);
+                ss[m] += (double)(v.z * v.z);
+                ss[m] += (double)(v.w * v.w);
+            }
+        }
+        if (g.norm_w) {
 #pragma unroll
             for (int m = 0; m < MR; m++) {
-                if (m < g.M) {
-                    const float v = g.x[(long)m * g.ldx + k];
-                    ss[m] += (double)(v * v);
+                const double t = wave_sum_d(ss[m]);
+                if (lane == 0) red[wid][m] = t;
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int m = 0; m < MR; m++) {
+            float scale = 1.0f;
+            if (g.norm_w) {
+                const double tot = red[0][m] + red[1][m] + red[2][m] + red[3][m];
+                scale = 1.0f / sqrtf((float)(tot / K) + g.eps);
+            }
+#pragma unroll
+            for (int p = 0; p < KP; p++) {
+                const int k = p * 1024 + tid * 4;
+                if (k < K) {
+                    uint16_t h4[4];
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        float v = xr[m][p][e];
+                        if (g.norm_w) v = fmul_rn(fmul_rn(v, scale), g.norm_w[k + e]);
+                        h4[e] = m < g.M ? f_to_u16(v) : (uint16_t)0;
+                    }
+                    *(uint2 *)(xs + m * K + k) = make_uint2(h4[0] | ((uint32_t)h4[1] << 16), h4[2] | ((uint32_t)h4[3] << 16));
                 }
             }
-#pragma unroll
-        for (int m = 0; m < MR; m++) {
-            const double t = wave_sum_d(ss[m]);
-            if (lane == 0) red[wid][m] = t;
         }
-        __syncthreads();
-#pragma unroll
-        for (int m = 0; m < MR; m++) {
-            const double tot = red[0][m] + red[1][m] + red[2][m] + red[3][m];
-            const float mean = (float)(tot / K);
-            const float scale = 1.0f / sqrtf(mean + g.eps);
-            for (int k = tid; k < K; k += 256) {
-                float v = 0.0f;
-                if (m < g.M) v = fmul_rn(fmul_rn(g.x[(long)m * g.ldx + k], scale), g.norm_w[k]);
-                xs[m * K + k] = f_to_u16(v);
-            }
-        }
-    } else if (g.xh) {
+    } else {
         for (int k = tid * 8; k < K; k += 256 * 8)
 #pragma unroll
             for (int m = 0; m < MR; m++)
                 *(u32x4 *)(xs + m * K + k) = m < g.M ? *(const u32x4 *)(g.xh + (long)m * g.ldxh + k) : u32x4{0u, 0u, 0u, 0u};
-    } else {
-        for (int k = tid; k < K; k += 256)
-#pragma unroll
-            for (int m = 0; m < MR; m++) xs[m * K + k] = m < g.M ? f_to_u16(g.x[(long)m * g.ldx + k]) : (uint16_t)0;
     }
     __syncthreads();
 
@@ -393,6 +422,9 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
             }
         }
     }
+    if constexpr (EPI != EPI_ARGMAX) {
+        if (g.trace) { __syncthreads(); trace_mark(g.trace, 1); }
+    }
     if constexpr (EPI == EPI_ARGMAX) {
         if (lane == 0)
 #pragma unroll
@@ -401,7 +433,31 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
         if (tid < MR && tid < g.M) {
             unsigned long long b = bestk[0][tid];
             for (int w = 1; w < 4; w++) b = bestk[w][tid] > b ? bestk[w][tid] : b;
-            atomicMax(g.amax + tid, b);
+            const unsigned long long old = atomicMax(g.amax + tid, b);
+            asm volatile("" ::"v"(old));   // returned value used: the add has been performed at L2
+        }
+        if (g.done) {
+            __shared__ int last, st;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) last = __hip_atomic_fetch_add(g.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+            __syncthreads();
+            if (last) {
+                if (tid == 0) st = *g.step;
+                __syncthreads();
+                if (tid < g.M) {
+                    const unsigned long long k = __hip_atomic_load(g.amax + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const int id = argmax_key_idx(k);
+                    g.tok_out[tid] = id;
+                    g.hist[(long)tid * g.hist_stride + st + 1] = id;
+                    g.pos[tid] += 1;
+                    __hip_atomic_store(g.amax + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (tid == 0) {
+                    *g.step = st + 1;
+                    __hip_atomic_store(g.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
         }
     }
 }

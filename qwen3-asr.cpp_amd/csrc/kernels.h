@@ -79,6 +79,14 @@ struct GemvArgs {
     float *out_f32; int ldo;
     uint16_t *out_f16; int ldo16;
     unsigned long long *amax;
+    // fused embedding gather (decode layer 0): x[m] = embd[ids[m]] (fp16 -> fp32),
+    // block 0 also stores it to x_store for the residual stream
+    const int32_t *embd_ids; const uint16_t *embd; float *x_store;
+    // fused greedy-step bookkeeping (EPI_ARGMAX): the last workgroup decodes the
+    // argmax keys into tok_out / hist[b][step+1], advances pos[b] and step,
+    // and re-arms amax and done (both zero at rest)
+    unsigned int *done; int32_t *tok_out; int32_t *hist; int hist_stride; int *step; int *pos;
+    unsigned long long *trace;           // dev trace: per block [start, end, -, -] (100 MHz clock) or null
 };
 void launch_gemv(int epi, const GemvArgs &g, hipStream_t s);
 
@@ -120,8 +128,8 @@ struct PrefillAttnArgs {
 void launch_prefill_attention(const PrefillAttnArgs &a, hipStream_t s);
 
 // decoder single-token attention, fused: q/k RMSNorm + RoPE, fp16 KV-cache
-// write of the new token, split-KV flash decoding and the cross-split combine
-// (last-arriving block per (sequence, kv head)), one launch per layer.
+// write of the new token and split-KV flash decoding (64-key splits); the last
+// arriving split of each kv group combines the partials and writes out.
 struct DecodeAttnArgs {
     const float *qkv;                    // [B][QD + 2*KD] fp32 (raw QKV projection)
     const float *q_norm, *k_norm; float eps;
@@ -130,10 +138,12 @@ struct DecodeAttnArgs {
     uint16_t *kc, *vc;                   // this layer's cache base
     const int *seq_slot;
     int B, n_head, n_kv_head, max_ctx, max_splits;
+    int grid_splits;                     // launched splits: >= ceil((max pos + 1) / 64) over the batch
     float scale;
-    float *part;                         // [B][n_kv_head][max_splits][2][132]
-    unsigned int *counter;               // [B][n_kv_head], zero at rest (self-resetting)
-    uint16_t *out;                       // [B][n_head*128] fp16
+    float *part;                         // [B][n_kv_head][max_splits][2][132]: O[128], m, l, 0, 0
+    unsigned int *counter;               // [B][n_kv_head] split arrivals, zero at rest
+    uint16_t *out;                       // [B][n_head*128] fp16 attention output
+    unsigned long long *trace;           // dev trace: per block [start, K/V landed, published, end] or null
 };
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
 int decode_split_len();

@@ -1,0 +1,37 @@
+"""Summarise a QASR_DEV_TRACE dump: per-block 100 MHz timestamps of one decode
+layer's kernels (QKV GEMV, attention, o-proj, gate/up, down).  Dev tool only."""
+import sys
+
+import numpy as np
+
+NAMES = ["qkv_gemv", "attention", "oproj_gemv", "gateup_gemv", "down_gemv"]
+
+
+def main(path):
+    t = np.fromfile(path, dtype=np.uint64).reshape(6, 4096, 4).astype(np.int64)
+    live = [t[k][t[k][:, 0] > 0] for k in range(5)]
+    t0 = min(int(x[:, 0].min()) for x in live if len(x))
+    us = lambda v: (v - t0) / 100.0
+    prev_end = None
+    for k, x in enumerate(live):
+        if not len(x):
+            continue
+        st = x[:, 0]
+        if k == 1:
+            kv, pub, end = x[:, 1], x[:, 2], x[x[:, 3] > 0][:, 3]
+            print(f"{NAMES[k]:12s} blocks {len(x):4d} start {us(st.min()):7.2f}..{us(st.max()):7.2f}  "
+                  f"kv-landed med {np.median(kv - st) / 100:5.2f} max {us(kv.max()):7.2f}  "
+                  f"published max {us(pub.max()):7.2f}  combine-end max {us(end.max()):7.2f}")
+            e = end.max()
+        else:
+            en = x[:, 1]
+            print(f"{NAMES[k]:12s} blocks {len(x):4d} start {us(st.min()):7.2f}..{us(st.max()):7.2f}  "
+                  f"end {us(en.min()):7.2f}..{us(en.max()):7.2f}  block-dur med {np.median(en - st) / 100:5.2f}")
+            e = en.max()
+        if prev_end is not None:
+            print(f"{'':12s} gap from previous kernel's last block end to first start: {(st.min() - prev_end) / 100:5.2f} us")
+        prev_end = e
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
