@@ -280,6 +280,72 @@ static float dot_f32(const float *x, const float *y, int n) {
     return (float)s;
 }
 
+/* ---- Q8_0 (ggml block_q8_0: fp16 d + 32 x int8, 34 B; type id 8) ------
+ * Activation side of ggml_mul_mat with Q8_0 weights (vec_dot_type Q8_0):
+ * quantize_row_q8_0, x86 AVX2 path of ggml-cpu/arch/x86/quants.c (the build
+ * the reference's Linux CPU path compiles): amax per 32 values, d = amax/127
+ * stored fp16, q = round-half-even(x * (127/amax)).  (The generic C path
+ * uses id = 1/d and roundf; ties differ only, documented in DESIGN.md.) */
+static void quantize_row_q8(const float *x, int K, int8_t *q, uint16_t *d) {
+    for (int b = 0; b < K / 32; b++) {
+        const float *xb = x + 32 * b;
+        float amax = 0.0f;
+        for (int i = 0; i < 32; i++) amax = fmaxf(amax, fabsf(xb[i]));
+        const float dd = amax / 127.f;
+        d[b] = qo_f32_to_f16(dd);
+        const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+        for (int i = 0; i < 32; i++) q[32 * b + i] = (int8_t)nearbyintf(xb[i] * id);
+    }
+}
+
+/* ggml_vec_dot_q8_0_q8_0, AVX2 path: per block the exact int products are
+ * summed in 8 lanes of 4 (mul_sum_i8_pairs_float), each lane fma'd with
+ * d_w * d_x into an fp32 accumulator, then hsum_float_8. */
+static float dot_q8(const uint8_t *wrow, const int8_t *qx, const uint16_t *dx, int K) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int b = 0; b < K / 32; b++) {
+        const uint8_t *blk = wrow + 34 * b;
+        const uint16_t dwh = (uint16_t)(blk[0] | (blk[1] << 8));
+        const int8_t *qw = (const int8_t *)(blk + 2);
+        const float d = qo_f16_to_f32(dwh) * qo_f16_to_f32(dx[b]);
+        for (int j = 0; j < 8; j++) {
+            int s = 0;
+            for (int i = 4 * j; i < 4 * j + 4; i++) s += (int)qw[i] * (int)qx[32 * b + i];
+            acc[j] = fmaf(d, (float)s, acc[j]);
+        }
+    }
+    const float r0 = acc[0] + acc[4], r1 = acc[1] + acc[5], r2 = acc[2] + acc[6], r3 = acc[3] + acc[7];
+    return (r0 + r2) + (r1 + r3);
+}
+
+static void mul_mat_q8(const float *x, int M, int K, const uint8_t *w, int N, const float *bias, float *y) {
+    const int nb = K / 32;
+    int8_t *xq = (int8_t *)malloc((size_t)M * K);
+    uint16_t *xd = (uint16_t *)malloc((size_t)M * nb * sizeof(uint16_t));
+    #pragma omp parallel for num_threads(g_threads)
+    for (int m = 0; m < M; m++) quantize_row_q8(x + (size_t)m * K, K, xq + (size_t)m * K, xd + (size_t)m * nb);
+    #pragma omp parallel for schedule(static) num_threads(g_threads)
+    for (int n = 0; n < N; n++) {
+        const uint8_t *wr = w + (size_t)n * nb * 34;
+        for (int m = 0; m < M; m++) {
+            float v = dot_q8(wr, xq + (size_t)m * K, xd + (size_t)m * nb, K);
+            if (bias) v = v + bias[n];
+            y[(size_t)m * N + n] = v;
+        }
+    }
+    free(xq);
+    free(xd);
+}
+
+static void mul_mat_f16(const float *x, int M, int K, const uint16_t *w, int N, const float *bias, float *y);
+
+/* a linear layer's weight in the model's linear weight type (F16 or Q8_0) */
+static void mul_mat_w(const qo_model *m, const float *x, int M, int K, const uint16_t *w, int N, const float *bias,
+                      float *y) {
+    if (m->wtype == QO_TYPE_Q8_0) mul_mat_q8(x, M, K, (const uint8_t *)w, N, bias, y);
+    else mul_mat_f16(x, M, K, w, N, bias, y);
+}
+
 /* ggml_mul_mat(W[N][K] f16, X[M][K] f32): X is converted to fp16 (RNE,
  * vec_dot_type of F16) and every output is an fp32-accumulated fp16 dot.
  * y[M][N] = X W^T (+ bias, a separate ggml_add -> one fp32 rounding). */
@@ -457,7 +523,7 @@ int qo_encode_conv(const qo_model *m, const float *mel, int T, float *out, int f
             for (int c = 0; c < C; c++)
                 for (int h = 0; h < H3; h++) feat[(size_t)t * F + c * H3 + h] = x3[((size_t)c * H3 + h) * W3 + t];
         float *y = out + (size_t)n_out * D;
-        mul_mat_f16(feat, W3, F, m->conv_out_w, D, NULL, y);
+        mul_mat_w(m, feat, W3, F, m->conv_out_w, D, NULL, y);
         float *pe = (float *)malloc((size_t)W3 * D * sizeof(float));
         sinusoidal_pe(pe, W3, D);
         for (int i = 0; i < W3 * D; i++) y[i] += pe[i];
@@ -527,22 +593,22 @@ int qo_encode(const qo_model *m, const float *mel, int T, float *out, int flags)
     for (int il = 0; il < m->enc_layers; il++) {
         const qo_enc_layer *L = &m->enc[il];
         layer_norm(x, N, D, L->attn_norm_w, L->attn_norm_b, m->enc_eps, cur);
-        mul_mat_f16(cur, N, D, L->attn_q_w, D, L->attn_q_b, q);
-        mul_mat_f16(cur, N, D, L->attn_k_w, D, L->attn_k_b, k);
-        mul_mat_f16(cur, N, D, L->attn_v_w, D, L->attn_v_b, v);
+        mul_mat_w(m, cur, N, D, L->attn_q_w, D, L->attn_q_b, q);
+        mul_mat_w(m, cur, N, D, L->attn_k_w, D, L->attn_k_b, k);
+        mul_mat_w(m, cur, N, D, L->attn_v_w, D, L->attn_v_b, v);
         enc_attention(q, k, v, N, D, H, att);
-        mul_mat_f16(att, N, D, L->attn_out_w, D, L->attn_out_b, cur);
+        mul_mat_w(m, att, N, D, L->attn_out_w, D, L->attn_out_b, cur);
         for (size_t i = 0; i < (size_t)N * D; i++) x[i] = cur[i] + x[i];
         layer_norm(x, N, D, L->ffn_norm_w, L->ffn_norm_b, m->enc_eps, cur);
-        mul_mat_f16(cur, N, D, L->ffn_up_w, FF, L->ffn_up_b, ff);
+        mul_mat_w(m, cur, N, D, L->ffn_up_w, FF, L->ffn_up_b, ff);
         for (size_t i = 0; i < (size_t)N * FF; i++) ff[i] = gelu(ff[i], flags);
-        mul_mat_f16(ff, N, FF, L->ffn_down_w, D, L->ffn_down_b, cur);
+        mul_mat_w(m, ff, N, FF, L->ffn_down_w, D, L->ffn_down_b, cur);
         for (size_t i = 0; i < (size_t)N * D; i++) x[i] = cur[i] + x[i];
     }
     layer_norm(x, N, D, m->ln_post_w, m->ln_post_b, m->enc_eps, cur);
-    mul_mat_f16(cur, N, D, m->proj1_w, D, m->proj1_b, q);
+    mul_mat_w(m, cur, N, D, m->proj1_w, D, m->proj1_b, q);
     for (size_t i = 0; i < (size_t)N * D; i++) q[i] = gelu(q[i], flags);
-    mul_mat_f16(q, N, D, m->proj2_w, HID, m->proj2_b, out);
+    mul_mat_w(m, q, N, D, m->proj2_w, HID, m->proj2_b, out);
     free(ff); free(att); free(v); free(k); free(q); free(cur); free(x);
     return N;
 }
@@ -626,9 +692,9 @@ int qo_dec_forward(qo_dec *dd, const int32_t *tokens, int n_tokens, const float 
         uint16_t *kc = dd->kc + (size_t)il * dd->n_ctx * KD;
         uint16_t *vc = dd->vc + (size_t)il * dd->n_ctx * KD;
         rms_norm(x, n_tokens, HS, L->attn_norm, m->rms_eps, cur);
-        mul_mat_f16(cur, n_tokens, HS, L->attn_q, QD, NULL, q);
-        mul_mat_f16(cur, n_tokens, HS, L->attn_k, KD, NULL, k);
-        mul_mat_f16(cur, n_tokens, HS, L->attn_v, KD, NULL, v);
+        mul_mat_w(m, cur, n_tokens, HS, L->attn_q, QD, NULL, q);
+        mul_mat_w(m, cur, n_tokens, HS, L->attn_k, KD, NULL, k);
+        mul_mat_w(m, cur, n_tokens, HS, L->attn_v, KD, NULL, v);
         for (int t = 0; t < n_tokens; t++) {
             for (int h = 0; h < NH; h++) {
                 float *qh = q + (size_t)t * QD + h * HD;
@@ -683,13 +749,13 @@ int qo_dec_forward(qo_dec *dd, const int32_t *tokens, int n_tokens, const float 
                 const float Sinv = S == 0.0f ? 0.0f : 1.0f / S;
                 for (int d = 0; d < HD; d++) att[(size_t)t * QD + h * HD + d] = acc32[d] * Sinv;
             }
-        mul_mat_f16(att, n_tokens, QD, L->attn_output, HS, NULL, cur);
+        mul_mat_w(m, att, n_tokens, QD, L->attn_output, HS, NULL, cur);
         for (size_t i = 0; i < (size_t)n_tokens * HS; i++) x[i] = cur[i] + x[i];
         rms_norm(x, n_tokens, HS, L->ffn_norm, m->rms_eps, cur);
-        mul_mat_f16(cur, n_tokens, HS, L->ffn_gate, FF, NULL, g);
-        mul_mat_f16(cur, n_tokens, HS, L->ffn_up, FF, NULL, u);
+        mul_mat_w(m, cur, n_tokens, HS, L->ffn_gate, FF, NULL, g);
+        mul_mat_w(m, cur, n_tokens, HS, L->ffn_up, FF, NULL, u);
         for (size_t i = 0; i < (size_t)n_tokens * FF; i++) g[i] = silu(g[i]) * u[i];
-        mul_mat_f16(g, n_tokens, FF, L->ffn_down, HS, NULL, cur);
+        mul_mat_w(m, g, n_tokens, FF, L->ffn_down, HS, NULL, cur);
         for (size_t i = 0; i < (size_t)n_tokens * HS; i++) x[i] = cur[i] + x[i];
     }
     /* last row only (text_decoder.cpp:564-566) -> RMSNorm -> tied LM head */

@@ -35,7 +35,8 @@ extern "C" {
 #define QO_HOP 160
 #define QO_N_BINS 201
 
-/* Weights as host arrays.  2-D weights are IEEE fp16 bit patterns laid out as
+/* Weights as host arrays.  2-D weights are IEEE fp16 bit patterns (or raw
+ * Q8_0 blocks for the linear weights, see wtype) laid out as
  * in the GGUF file (ggml ne[0] = in_features, i.e. PyTorch [out][in] rows);
  * 1-D tensors are fp32.  Shapes follow src/gguf_loader.cpp:130-190 and
  * src/text_decoder.cpp:175-229. */
@@ -62,6 +63,10 @@ typedef struct {
     int vocab, hidden, dec_layers, n_head, n_kv_head, head_dim, dec_ffn;
     float rms_eps, rope_theta;
     int eos_id, audio_start_id, audio_end_id, audio_pad_id;
+    /* ggml type of the linear 2-D weights (every non-conv matrix except
+     * token_embd, scripts/convert_hf_to_gguf.py:230-308): QO_TYPE_F16 or
+     * QO_TYPE_Q8_0 (raw block_q8_0 rows, 34 B per 32 values) */
+    int wtype;
 
     const uint16_t *conv1_w, *conv2_w, *conv3_w, *conv_out_w;
     const float *conv1_b, *conv2_b, *conv3_b;
@@ -74,6 +79,9 @@ typedef struct {
     const float *output_norm;
     qo_dec_layer *dec;
 } qo_model;
+
+#define QO_TYPE_F16  1
+#define QO_TYPE_Q8_0 8
 
 /* numerics switches ("switches for (iii) and (viii)") */
 #define QO_GELU_EXACT   1   /* tanh-GELU in fp32 instead of ggml's fp16 LUT   */

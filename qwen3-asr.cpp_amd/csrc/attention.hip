@@ -24,7 +24,8 @@ namespace qasr {
 #define EVS 68   // V tile row stride (floats): conflict-free permuted reads
 
 __global__ __launch_bounds__(256) void enc_attn_kernel(const float *__restrict__ qkv, const int *__restrict__ seg_start,
-                                                       const int *__restrict__ seg_len, int D, uint16_t *__restrict__ out) {
+                                                       const int *__restrict__ seg_len, int D, uint16_t *__restrict__ out,
+                                                       float *__restrict__ out32) {
     __shared__ __attribute__((aligned(16))) float Ks[64 * EKS];
     __shared__ __attribute__((aligned(16))) float Vs[64 * EVS];
     const int b = blockIdx.z, h = blockIdx.y;
@@ -116,19 +117,27 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const float *__restrict__
     }
     if (q < N) {
         const float inv = 1.0f / l_run;
-        uint16_t *dst = out + (long)(r0 + q) * D + h * 64;
+        if (out32) {
+            float *dst = out32 + (long)(r0 + q) * D + h * 64;
 #pragma unroll
-        for (int d = 0; d < 4; d++)
+            for (int d = 0; d < 4; d++)
 #pragma unroll
-            for (int i = 0; i < 4; i++) dst[d * 16 + 4 * g + i] = f_to_u16(o[d][i] * inv);
+                for (int i = 0; i < 4; i++) dst[d * 16 + 4 * g + i] = o[d][i] * inv;
+        } else {
+            uint16_t *dst = out + (long)(r0 + q) * D + h * 64;
+#pragma unroll
+            for (int d = 0; d < 4; d++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) dst[d * 16 + 4 * g + i] = f_to_u16(o[d][i] * inv);
+        }
     }
 }
 
 void launch_enc_attention(const float *qkv, const int *seg_start, const int *seg_len, int n_seg, int max_len, int D, int H,
-                          uint16_t *out, hipStream_t s) {
+                          uint16_t *out, hipStream_t s, float *out32) {
     if (n_seg <= 0 || max_len <= 0) return;
     dim3 grid((max_len + 63) / 64, H, n_seg);
-    hipLaunchKernelGGL(enc_attn_kernel, grid, dim3(256), 0, s, qkv, seg_start, seg_len, D, out);
+    hipLaunchKernelGGL(enc_attn_kernel, grid, dim3(256), 0, s, qkv, seg_start, seg_len, D, out, out32);
 }
 
 // ===================================================== decoder q/k norm + RoPE
@@ -270,14 +279,18 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(PrefillAttnArgs a) {
         m_run = m_new;
 #pragma unroll
         for (int d = 0; d < 8; d++) o[d] *= alpha;
-        // P^T as the B operand: k-step u covers key sub-tiles 2u (j<4) and 2u+1 (j>=4)
+        // P^T as the B operand: k-step u covers key sub-tiles 2u (j<4) and 2u+1 (j>=4).
+        // P is fp32 in ggml's FA; it enters the f16 MFMA as hi + lo fp16 parts
+        // (p = hi + lo to ~2^-22), so P.V keeps fp32-accurate weights.
 #pragma unroll
         for (int u = 0; u < 2; u++) {
-            half8 pf;
+            half8 pf, pl;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 pf[j] = (f16)st[2 * u][j];
                 pf[4 + j] = (f16)st[2 * u + 1][j];
+                pl[j] = (f16)(st[2 * u][j] - (float)pf[j]);
+                pl[4 + j] = (f16)(st[2 * u + 1][j] - (float)pf[4 + j]);
             }
 #pragma unroll
             for (int d = 0; d < 8; d++) {
@@ -286,16 +299,25 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(PrefillAttnArgs a) {
                 half4 hi = *(const half4 *)(vr + 16);
                 half8 vf = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                 o[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf, o[d], 0, 0, 0);
+                o[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pl, o[d], 0, 0, 0);
             }
         }
     }
     if (q < L) {
         const float inv = l_run > 0.0f ? 1.0f / l_run : 0.0f;
-        uint16_t *dst = a.out + (long)(row0 + q) * QD + head * 128;
+        if (a.out32) {
+            float *dst = a.out32 + (long)(row0 + q) * QD + head * 128;
 #pragma unroll
-        for (int d = 0; d < 8; d++)
+            for (int d = 0; d < 8; d++)
 #pragma unroll
-            for (int i = 0; i < 4; i++) dst[d * 16 + 4 * g + i] = f_to_u16(o[d][i] * inv);
+                for (int i = 0; i < 4; i++) dst[d * 16 + 4 * g + i] = o[d][i] * inv;
+        } else {
+            uint16_t *dst = a.out + (long)(row0 + q) * QD + head * 128;
+#pragma unroll
+            for (int d = 0; d < 8; d++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) dst[d * 16 + 4 * g + i] = f_to_u16(o[d][i] * inv);
+        }
     }
 }
 
@@ -350,27 +372,28 @@ __device__ __forceinline__ void ld_sc1_x4_burst9(const floatx4 *src, int tid, in
 }
 
 __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
-    __shared__ float ys[2][128];
-    __shared__ float kn[128];
     __shared__ __attribute__((aligned(16))) uint16_t qs[2][128];
     __shared__ __attribute__((aligned(16))) uint16_t knew[128];
     __shared__ __attribute__((aligned(16))) uint16_t vnew[128];
     __shared__ float sc[2][DSPLIT];
-    __shared__ double red[DWAVES][2];
-    __shared__ float ored[DWAVES][2][128];
+    __shared__ __attribute__((aligned(16))) float ored[DWAVES * 4][2][128];   // [wave x row][head][dim]
     __shared__ float cml[2][2];
+    __shared__ float wsp[2][32];         // combine: per-split weights of a pass
+    __shared__ float lsum[2];
     __shared__ int last;
     __shared__ floatx4 stage[32 * 66];   // combine: up to 32 splits x 2 heads x 33 float4
     const int b = blockIdx.z, g = blockIdx.y, sp = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
-    const int hh = tid >> 7, d = tid & 127;
     trace_mark(a.trace, 0);
-    // ---- the token's raw q (heads 2g, 2g+1) and k / v of group g: tiny, L2-hot
+    // ---- the token's raw vectors, one per wave: wave 0/1 = q heads 2g/2g+1,
+    //      wave 2 = k, wave 3 = v of group g; lane owns dims lane and lane + 64
+    //      (the NEOX RoPE pair), so norm and rotation need no LDS round trip
     const float *raw = a.qkv + (long)b * (QD + 2 * KD);
-    const float xq = raw[(2 * g + hh) * 128 + d];
-    const float xkv = raw[QD + hh * KD + g * 128 + d];   // hh 0: k, 1: v
-    const float wqn = a.q_norm[d], wkn = a.k_norm[d];
+    const float *src = wid < 2 ? raw + (2 * g + wid) * 128 : raw + QD + (wid - 2) * KD + g * 128;
+    const float x0 = src[lane], x1 = src[lane + 64];
+    const float *nw = wid < 2 ? a.q_norm : a.k_norm;
+    const float w0 = nw[lane], w1 = nw[lane + 64];
     // ---- every K/V row of the split (addresses depend on blockIdx only; decode
     //      contexts use identity sequence slots).  Rows past the position are
     //      masked below; the cache is zero-initialised so they are finite.
@@ -396,38 +419,27 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     const int nsp = gridDim.x;
     const int k1 = min(nkv, k0 + DSPLIT);
     const bool lastsp = sp == (nkv - 1) / DSPLIT;
-    // ---- ggml_rms_norm (double sums of fp32 squares) * weight, then NEOX RoPE
-    {
-        const double sq = wave_sum_d((double)(xq * xq));
-        const double sk = wave_sum_d((double)(xkv * xkv));
-        if (lane == 0) { red[wid][0] = sq; red[wid][1] = sk; }
-    }
-    __syncthreads();
-    {
-        const float scale = 1.0f / sqrtf((float)((red[2 * hh][0] + red[2 * hh + 1][0]) / 128.0) + a.eps);
-        ys[hh][d] = fmul_rn(fmul_rn(xq, scale), wqn);
-        if (lastsp) {
-            if (hh == 0) {
-                const float sk = 1.0f / sqrtf((float)((red[0][1] + red[1][1]) / 128.0) + a.eps);
-                kn[d] = fmul_rn(fmul_rn(xkv, sk), wkn);
-            } else {
-                const uint16_t v = f_to_u16(xkv);   // ggml_cpy f32 -> f16
-                vnew[d] = v;
-                vc[(long)pos * 128 + d] = v;
-            }
+    const float2 cs = *(const float2 *)(a.rope + ((long)pos * 64 + lane) * 2);
+    // ---- ggml_rms_norm (double sum of fp32 squares) * weight, NEOX RoPE
+    //      (src/text_decoder.cpp:640-700); v is only cast to fp16
+    if (wid < 3) {
+        const double ss = wave_sum_d((double)(x0 * x0) + (double)(x1 * x1));
+        const float scale = 1.0f / sqrtf((float)(ss / 128.0) + a.eps);
+        const float y0 = fmul_rn(fmul_rn(x0, scale), w0), y1 = fmul_rn(fmul_rn(x1, scale), w1);
+        const uint16_t r0 = f_to_u16(y0 * cs.x - y1 * cs.y), r1 = f_to_u16(y0 * cs.y + y1 * cs.x);
+        if (wid < 2) {
+            qs[wid][lane] = r0;
+            qs[wid][lane + 64] = r1;
+        } else if (lastsp) {
+            knew[lane] = r0; knew[lane + 64] = r1;
+            kc[(long)pos * 128 + lane] = r0;
+            kc[(long)pos * 128 + lane + 64] = r1;
         }
-    }
-    __syncthreads();
-    {
-        const float2 cs = *(const float2 *)(a.rope + ((long)pos * 64 + (d & 63)) * 2);
-        const float y0 = ys[hh][d & 63], y1 = ys[hh][(d & 63) + 64];
-        qs[hh][d] = f_to_u16(d < 64 ? y0 * cs.x - y1 * cs.y : y0 * cs.y + y1 * cs.x);
-        if (lastsp && hh == 0) {
-            const float z0 = kn[d & 63], z1 = kn[(d & 63) + 64];
-            const uint16_t r = f_to_u16(d < 64 ? z0 * cs.x - z1 * cs.y : z0 * cs.y + z1 * cs.x);
-            knew[d] = r;
-            kc[(long)pos * 128 + d] = r;
-        }
+    } else if (lastsp) {
+        const uint16_t v0 = f_to_u16(x0), v1 = f_to_u16(x1);   // ggml_cpy f32 -> f16
+        vnew[lane] = v0; vnew[lane + 64] = v1;
+        vc[(long)pos * 128 + lane] = v0;
+        vc[(long)pos * 128 + lane + 64] = v1;
     }
     __syncthreads();
     // ---- scores: 16 lanes per key row, 8 dims each
@@ -443,11 +455,8 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
             s0 = fmaf((float)kv[i][e], (float)q0[e], s0);
             s1 = fmaf((float)kv[i][e], (float)q1[e], s1);
         }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-            s0 += __shfl_xor(s0, o, 64);
-            s1 += __shfl_xor(s1, o, 64);
-        }
+        s0 = row16_sum(s0);   // the key's 16 lanes
+        s1 = row16_sum(s1);
         if ((lane & 15) == 0) {
             const bool ok = k0 + j < k1;
             sc[0][j] = ok ? s0 * a.scale : -INFINITY;
@@ -455,6 +464,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
         }
     }
     __syncthreads();
+    trace_mark(a.trace, 6);
     // ---- split-local softmax statistics: wave h owns head h, lane = key
     if (wid < 2) {
         const float v = sc[wid][lane];
@@ -465,6 +475,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
         if (lane == 0) { cml[wid][0] = M; cml[wid][1] = l; }
     }
     __syncthreads();
+    trace_mark(a.trace, 7);
     // ---- P.V
     float acc0[8], acc1[8];
 #pragma unroll
@@ -479,28 +490,23 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
             acc1[e] = fmaf((float)vv[i][e], p1, acc1[e]);
         }
     }
-#pragma unroll
-    for (int e = 0; e < 8; e++) {
-        acc0[e] += __shfl_xor(acc0[e], 16, 64);
-        acc0[e] += __shfl_xor(acc0[e], 32, 64);
-        acc1[e] += __shfl_xor(acc1[e], 16, 64);
-        acc1[e] += __shfl_xor(acc1[e], 32, 64);
-    }
-    if (sub == 0) {
-#pragma unroll
-        for (int e = 0; e < 8; e++) { ored[wid][0][dl + e] = acc0[e]; ored[wid][1][dl + e] = acc1[e]; }
-    }
+    // per-(wave, row) partial sums go to LDS; the 16-way sum happens once, below
+    *(floatx4 *)&ored[wid * 4 + sub][0][dl] = floatx4{acc0[0], acc0[1], acc0[2], acc0[3]};
+    *(floatx4 *)&ored[wid * 4 + sub][0][dl + 4] = floatx4{acc0[4], acc0[5], acc0[6], acc0[7]};
+    *(floatx4 *)&ored[wid * 4 + sub][1][dl] = floatx4{acc1[0], acc1[1], acc1[2], acc1[3]};
+    *(floatx4 *)&ored[wid * 4 + sub][1][dl + 4] = floatx4{acc1[4], acc1[5], acc1[6], acc1[7]};
     __syncthreads();
+    trace_mark(a.trace, 2);
     // ---- publish this split's partial: [2 heads][O 128 | m, l, 0, 0], 16-B sc1 stores
     float *gpart = a.part + (((long)b * a.n_kv_head + g) * a.max_splits) * 2 * 132;
     if (tid < 66) {
         const int h = tid / 33, q = tid - h * 33;
         float4 v;
         if (q < 32) {
-            v.x = ored[0][h][4 * q] + ored[1][h][4 * q] + ored[2][h][4 * q] + ored[3][h][4 * q];
-            v.y = ored[0][h][4 * q + 1] + ored[1][h][4 * q + 1] + ored[2][h][4 * q + 1] + ored[3][h][4 * q + 1];
-            v.z = ored[0][h][4 * q + 2] + ored[1][h][4 * q + 2] + ored[2][h][4 * q + 2] + ored[3][h][4 * q + 2];
-            v.w = ored[0][h][4 * q + 3] + ored[1][h][4 * q + 3] + ored[2][h][4 * q + 3] + ored[3][h][4 * q + 3];
+            floatx4 t = *(const floatx4 *)&ored[0][h][4 * q];
+#pragma unroll
+            for (int w = 1; w < DWAVES * 4; w++) t += *(const floatx4 *)&ored[w][h][4 * q];
+            v = make_float4(t[0], t[1], t[2], t[3]);
         } else {
             v = make_float4(cml[h][0], cml[h][1], 0.f, 0.f);
         }
@@ -511,42 +517,51 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     unsigned int *cnt = a.counter + (long)b * a.n_kv_head + g;
     if (tid == 0) last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nsp - 1;
     __syncthreads();
-    trace_mark(a.trace, 2);
+    trace_mark(a.trace, 3);
     if (!last) return;
     // ---- last arriver: combine the partials of both heads (empty ones weigh 0).
     //      Passes of up to 32 splits are staged through LDS with one burst of
     //      16-B sc1 loads each (a per-split load loop would serialise ~nsp
-    //      memory latencies); passes merge with the usual online rescale.
+    //      memory latencies).  Wave h derives head h's split weights once
+    //      (lane = split); passes merge with the usual online rescale.
     if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int hh = tid >> 7, d = tid & 127;
     float M = -INFINITY, L = 0.f, O = 0.f;
     for (int s0 = 0; s0 < nsp; s0 += 32) {
         const int ns = min(32, nsp - s0), n4 = ns * 66;
-        const floatx4 *src = (const floatx4 *)(gpart + (long)s0 * 264);
+        const floatx4 *srcp = (const floatx4 *)(gpart + (long)s0 * 264);
         floatx4 v[9];
-        ld_sc1_x4_burst9(src, tid, n4, v);
-        __syncthreads();   // previous pass's readers are done with stage
+        ld_sc1_x4_burst9(srcp, tid, n4, v);
+        if (s0 == 0) trace_mark(a.trace, 5);
+        __syncthreads();   // previous pass's readers are done with stage / wsp
 #pragma unroll
         for (int j = 0; j < 9; j++)
             if (tid + 256 * j < n4) stage[tid + 256 * j] = v[j];
         __syncthreads();
         const float *sf = (const float *)stage;
-        float Mp = -INFINITY;
-        for (int s2 = 0; s2 < ns; s2++) Mp = fmaxf(Mp, sf[(s2 * 2 + hh) * 132 + 128]);
-        const float Mn = fmaxf(M, Mp);
-        const float r = expf(M - Mn);   // first pass: exp(-inf) = 0 on L = O = 0
-        L *= r;
-        O *= r;
-        for (int s2 = 0; s2 < ns; s2++) {
-            const float *row = sf + (s2 * 2 + hh) * 132;
-            const float w = expf(row[128] - Mn);
-            L += row[129] * w;
-            O += row[d] * w;
+        if (wid < 2) {
+            const float ms = lane < ns ? sf[(lane * 2 + wid) * 132 + 128] : -INFINITY;
+            const float ls = lane < ns ? sf[(lane * 2 + wid) * 132 + 129] : 0.f;
+            const float Mprev = s0 == 0 ? -INFINITY : cml[wid][0];   // running max of head wid
+            const float Mn = fmaxf(Mprev, wave_max(ms));
+            const float w = lane < ns ? expf(ms - Mn) : 0.f;
+            if (lane < 32) wsp[wid][lane] = w;
+            const float lp = wave_sum(ls * w);
+            if (lane == 0) { lsum[wid] = lp; cml[wid][0] = Mn; }
         }
+        __syncthreads();
+        const float Mn = cml[hh][0];
+        const float r = expf(M - Mn);   // first pass: exp(-inf) = 0 on L = O = 0
+        L = L * r + lsum[hh];
+        float op = 0.f;
+        for (int s2 = 0; s2 < ns; s2++) op = fmaf(wsp[hh][s2], sf[(s2 * 2 + hh) * 132 + d], op);
+        O = O * r + op;
         M = Mn;
     }
     const float inv = L > 0.f ? 1.0f / L : 0.f;   // ggml: S_inv = 1/S, VKQ *= S_inv
-    a.out[(long)b * QD + (2 * g + hh) * 128 + d] = f_to_u16(O * inv);
-    trace_mark(a.trace, 3);
+    if (a.out32) a.out32[(long)b * QD + (2 * g + hh) * 128 + d] = O * inv;
+    else a.out[(long)b * QD + (2 * g + hh) * 128 + d] = f_to_u16(O * inv);
+    trace_mark(a.trace, 4);
 }
 
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {

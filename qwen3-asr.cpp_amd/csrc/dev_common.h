@@ -23,13 +23,38 @@ __device__ __forceinline__ uint16_t f_to_u16(float f) { return __builtin_bit_cas
 // 100 MHz constant clock shared by all CUs (dev trace timestamps)
 __device__ __forceinline__ unsigned long long rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ void trace_mark(unsigned long long *tr, int slot) {
-    if (tr && threadIdx.x == 0) tr[(long)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 4 + slot] = rt_now();
+    if (tr && threadIdx.x == 0) tr[(long)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 8 + slot] = rt_now();
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// DPP lane moves (VALU, no LDS round trip): quad_perm xor1 / xor2, row half
+// mirror (lane i <-> 7-i in 8), row mirror (lane i <-> 15-i in 16)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// every lane of each 16-lane row receives the row's sum / max
+__device__ __forceinline__ float row16_sum(float v) {
+    v += dpp_f<0xB1>(v);
+    v += dpp_f<0x4E>(v);
+    v += dpp_f<0x141>(v);
+    v += dpp_f<0x140>(v);
     return v;
+}
+__device__ __forceinline__ float row16_max(float v) {
+    v = fmaxf(v, dpp_f<0xB1>(v));
+    v = fmaxf(v, dpp_f<0x4E>(v));
+    v = fmaxf(v, dpp_f<0x141>(v));
+    v = fmaxf(v, dpp_f<0x140>(v));
+    return v;
+}
+__device__ __forceinline__ float lane_f(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+// wave64 reductions: rows by DPP, then the four row results by readlane
+// (uniform result in every lane)
+__device__ __forceinline__ float wave_sum(float v) {
+    v = row16_sum(v);
+    return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
 }
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
@@ -37,9 +62,8 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    v = row16_max(v);
+    return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
 }
 
 // total order on finite doubles as unsigned 64-bit keys (for atomicMax)

@@ -63,7 +63,8 @@ void launch_conv1(const float *mel, const ChunkDesc *chunks, const int *row1_sta
 // to fp16 (what the following ggml_mul_mat does to its input).
 template <int D>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict__ x, int M, const float *__restrict__ w,
-                                                        const float *__restrict__ b, float eps, uint16_t *__restrict__ y) {
+                                                        const float *__restrict__ b, float eps, uint16_t *__restrict__ y,
+                                                        float *__restrict__ y32) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= M) return;
@@ -98,26 +99,29 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict_
             float t = fmul_rn(v[i], scale);
             if (w) t = fmul_rn(t, w[k]);
             if (b) t = fadd_rn(t, b[k]);
-            y[(long)row * D + k] = f_to_u16(t);
+            if (y32) y32[(long)row * D + k] = t;
+            else y[(long)row * D + k] = f_to_u16(t);
         }
     }
 }
 
-void launch_layernorm_f16(const float *x, int M, int D, const float *w, const float *b, float eps, uint16_t *y, hipStream_t s) {
+void launch_layernorm_f16(const float *x, int M, int D, const float *w, const float *b, float eps, uint16_t *y, hipStream_t s,
+                          float *y32) {
     if (M <= 0) return;
     dim3 grid((M + 3) / 4);
     switch (D) {
-        case 896: hipLaunchKernelGGL(layernorm_kernel<896>, grid, dim3(256), 0, s, x, M, w, b, eps, y); break;
-        case 256: hipLaunchKernelGGL(layernorm_kernel<256>, grid, dim3(256), 0, s, x, M, w, b, eps, y); break;
-        case 1024: hipLaunchKernelGGL(layernorm_kernel<1024>, grid, dim3(256), 0, s, x, M, w, b, eps, y); break;
-        default: hipLaunchKernelGGL(layernorm_kernel<2048>, grid, dim3(256), 0, s, x, M, w, b, eps, y); break;
+        case 896: hipLaunchKernelGGL(layernorm_kernel<896>, grid, dim3(256), 0, s, x, M, w, b, eps, y, y32); break;
+        case 256: hipLaunchKernelGGL(layernorm_kernel<256>, grid, dim3(256), 0, s, x, M, w, b, eps, y, y32); break;
+        case 1024: hipLaunchKernelGGL(layernorm_kernel<1024>, grid, dim3(256), 0, s, x, M, w, b, eps, y, y32); break;
+        default: hipLaunchKernelGGL(layernorm_kernel<2048>, grid, dim3(256), 0, s, x, M, w, b, eps, y, y32); break;
     }
 }
 
 // ggml_rms_norm: sum of squares (fp32 products) in double; scale = 1/sqrtf(mean+eps)
 template <int D>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const float *__restrict__ x, int ldx, const int *__restrict__ row_idx, int M,
-                                                      const float *__restrict__ w, float eps, uint16_t *__restrict__ y) {
+                                                      const float *__restrict__ w, float eps, uint16_t *__restrict__ y,
+                                                      float *__restrict__ y32) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= M) return;
@@ -138,18 +142,22 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float *__restrict__ 
 #pragma unroll
     for (int i = 0; i < PER; i++) {
         const int k = lane + 64 * i;
-        if (k < D) y[(long)row * D + k] = f_to_u16(fmul_rn(fmul_rn(v[i], scale), w[k]));
+        if (k < D) {
+            const float t = fmul_rn(fmul_rn(v[i], scale), w[k]);
+            if (y32) y32[(long)row * D + k] = t;
+            else y[(long)row * D + k] = f_to_u16(t);
+        }
     }
 }
 
 void launch_rmsnorm_f16(const float *x, int ldx, const int *row_idx, int M, int D, const float *w, float eps, uint16_t *y,
-                        hipStream_t s) {
+                        hipStream_t s, float *y32) {
     if (M <= 0) return;
     dim3 grid((M + 3) / 4);
     switch (D) {
-        case 1024: hipLaunchKernelGGL(rmsnorm_kernel<1024>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y); break;
-        case 256: hipLaunchKernelGGL(rmsnorm_kernel<256>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y); break;
-        default: hipLaunchKernelGGL(rmsnorm_kernel<2048>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y); break;
+        case 1024: hipLaunchKernelGGL(rmsnorm_kernel<1024>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y, y32); break;
+        case 256: hipLaunchKernelGGL(rmsnorm_kernel<256>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y, y32); break;
+        default: hipLaunchKernelGGL(rmsnorm_kernel<2048>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y, y32); break;
     }
 }
 
@@ -212,6 +220,47 @@ __global__ void step_advance_kernel(int *row_pos, int *n_kv, int *step, int B) {
 
 void launch_step_advance(int *row_pos, int *n_kv, int *step, int B, hipStream_t s) {
     hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(256), 0, s, row_pos, n_kv, step, B);
+}
+
+// ------------------------------------------------------- Q8_0 activations
+// ggml quantize_row_q8_0, x86 AVX2 path (ggml-cpu/arch/x86/quants.c): per
+// 32 values amax, d = amax/127 (stored fp16), q = round-half-even(x * 127/amax).
+// One thread per block; the fp16-rounded d is kept as fp32 for the dot.
+__global__ __launch_bounds__(256) void quantize_q8_kernel(const float *__restrict__ x32, const uint16_t *__restrict__ x16, int ldx,
+                                                          int M, int K, int gC, int8_t *__restrict__ q, float *__restrict__ d) {
+    const int nb = K / 32;
+    const long t = (long)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (long)M * nb) return;
+    const int row = (int)(t / nb), b = (int)(t - (long)row * nb);
+    float v[32];
+    float amax = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        const int j = 32 * b + i;
+        const int col = gC > 0 ? (j & 15) * gC + (j >> 4) : j;
+        v[i] = x32 ? x32[(long)row * ldx + col] : u16_to_f(x16[(long)row * ldx + col]);
+        amax = fmaxf(amax, fabsf(v[i]));
+    }
+    d[(long)row * nb + b] = u16_to_f(f_to_u16(amax / 127.f));
+    const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint32_t u = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) u |= (uint32_t)(uint8_t)(int8_t)__builtin_rintf(fmul_rn(v[4 * i + e], id)) << (8 * e);
+        w[i] = u;
+    }
+    u32x4 *dst = (u32x4 *)(q + (long)row * K + 32 * b);
+    dst[0] = u32x4{w[0], w[1], w[2], w[3]};
+    dst[1] = u32x4{w[4], w[5], w[6], w[7]};
+}
+
+void launch_quantize_q8(const float *x32, const uint16_t *x16, int ldx, int M, int K, int gather_C, int8_t *q, float *d,
+                        hipStream_t s) {
+    const long n = (long)M * (K / 32);
+    if (n <= 0) return;
+    hipLaunchKernelGGL(quantize_q8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x32, x16, ldx, M, K, gather_C, q, d);
 }
 
 }  // namespace qasr

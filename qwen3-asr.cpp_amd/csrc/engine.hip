@@ -37,13 +37,17 @@ static int fail(int code, const std::string &msg) {
     } while (0)
 
 // ------------------------------------------------------------------ model
+// Linear weights are fp16 [N][K] (F16 files) or int8 [N][K] quants with fp16
+// block scales *_d [N][K/32] (Q8_0 files: block_q8_0 split in two arrays).
 struct EncLayer {
     uint16_t *wqkv, *wo, *w1, *w2;
+    uint16_t *wqkv_d = nullptr, *wo_d = nullptr, *w1_d = nullptr, *w2_d = nullptr;
     float *bqkv, *bo, *b1, *b2, *ln1_w, *ln1_b, *ln2_w, *ln2_b;
 };
 struct DecLayer {
     float *attn_norm, *q_norm, *k_norm, *ffn_norm;
     uint16_t *wqkv, *wo, *wgu, *wd;
+    uint16_t *wqkv_d = nullptr, *wo_d = nullptr, *wgu_d = nullptr, *wd_d = nullptr;
 };
 
 struct qasr_model {
@@ -53,6 +57,8 @@ struct qasr_model {
     char *arena = nullptr;
     size_t arena_bytes = 0;
     uint16_t *conv1_w, *conv2_w, *conv3_w, *conv_out_w, *proj1_w, *proj2_w, *embd;
+    uint16_t *conv_out_d = nullptr, *proj1_d = nullptr, *proj2_d = nullptr;
+    bool q8 = false;   // linear weights are Q8_0 (scripts/convert_hf_to_gguf.py:230-308)
     float *conv1_b, *conv2_b, *conv3_b, *ln_post_w, *ln_post_b, *proj1_b, *proj2_b, *out_norm;
     std::vector<EncLayer> enc;
     std::vector<DecLayer> dec;
@@ -88,6 +94,9 @@ struct qasr_ctx {
     DevBuf chunks, rs1, rs2, rs3, pepos, act1, act2, act3;
     DevBuf ex, exh, eqkv, eatt, eff, feats, segs;
     DevBuf px, pxh, pqkv, pq, patt, pact, prow, plast, pids, pxl;
+    DevBuf q8a, q8d, x32;          // Q8_0 models: quantised activations (int8 + scales), fp32 layer inputs
+    float *d_att32 = nullptr, *d_act32 = nullptr;   // Q8_0 decode: fp32 attention output / SwiGLU output
+    int8_t *d_q8a = nullptr; float *d_q8d = nullptr, *d_x32 = nullptr;   // Q8_0 batched (B > 8) decode, graph-fixed
     // fixed decode state (sized by max_batch)
     int32_t *d_tok = nullptr, *d_hist = nullptr;
     int *d_pos = nullptr, *d_nkv = nullptr, *d_slot = nullptr, *d_step = nullptr;
@@ -109,7 +118,7 @@ struct qasr_ctx {
     // (layer QASR_DEV_TRACE_LAYER, default 10) of the last step, dumped by qasr_run
     std::string trace_path;
     int trace_layer = 10;
-    unsigned long long *d_trace = nullptr;   // [6 kernels][4096 blocks][4]
+    unsigned long long *d_trace = nullptr;   // [6 kernels][4096 blocks][8]
     // kernel probe: HIP-event timing of one decode-step kernel inside qasr_run
     int probe = 0;
     double probe_ms = 0.0;
@@ -189,6 +198,26 @@ static int upload(qasr_ctx *c, DevBuf &b, const std::vector<T> &v) {
 }
 
 // ----------------------------------------------------------------- errors
+// A Q8_0 linear layer: quantise the activation rows (fp32 a32 or fp16 a16,
+// optional conv_out gather) into c->q8a / c->q8d, then the int8 block GEMM.
+// g carries M, N, K and the epilogue.
+static void gemm_q8(qasr_ctx *c, int epi, GemmArgs g, const float *a32, const uint16_t *a16, int lda, int gather_C,
+                    const uint16_t *W, const uint16_t *Wd, hipStream_t s, int8_t *qa = nullptr, float *qd = nullptr) {
+    if (!qa) { qa = c->q8a.as<int8_t>(); qd = c->q8d.as<float>(); }
+    launch_quantize_q8(a32, a16, lda, g.M, g.K, gather_C, qa, qd, s);
+    g.Aq = qa; g.lda = g.K; g.Ad = qd; g.ldad = g.K / 32;
+    g.Wq = (const int8_t *)W; g.ldw = g.K; g.Wd = Wd;
+    launch_gemm_q8(epi, g, s);
+}
+
+static int ensure_q8(qasr_ctx *c, size_t rows, size_t kmax, size_t x32_cols) {
+    int rc;
+    if ((rc = ensure(c, c->q8a, rows * kmax)) || (rc = ensure(c, c->q8d, rows * (kmax / 32) * 4)) ||
+        (rc = ensure(c, c->x32, rows * x32_cols * 4)))
+        return rc;
+    return 0;
+}
+
 extern "C" const char *qasr_last_error(void) { return g_err.c_str(); }
 extern "C" const char *qasr_version(void) { return "qasr-mi355x 0.1.0 (gfx950)"; }
 extern "C" int qasr_device_count(int *n) {
@@ -217,7 +246,8 @@ static bool check_shape(const gguf_tensor *t, std::vector<int64_t> ne, uint32_t 
     }
     if (t->type != want_type) {
         err = "tensor " + t->name + ": unsupported ggml type " + std::to_string(t->type) +
-              (want_type == DT_F16 ? " (this build supports F16 2-D weights)" : " (expected F32)");
+              (want_type == DT_F32 ? " (expected F32)" : want_type == DT_Q8_0 ? " (expected Q8_0 like the other linear weights)"
+                                                                              : " (expected F16)");
         return false;
     }
     return true;
@@ -290,9 +320,52 @@ extern "C" int qasr_model_load(const char *path, int device, qasr_model **out) {
     copy_f32("audio.encoder.conv2.bias", C, &m->conv2_b);
     conv_w("audio.encoder.conv3.weight", C, &m->conv3_w);
     copy_f32("audio.encoder.conv3.bias", C, &m->conv3_b);
-    {   // conv_out: input feature c*16+h (src/audio_encoder.cpp:133-142) -> h*C + c
-        const gguf_tensor *t = need("audio.encoder.conv_out.weight", {(int64_t)C * 16, D}, DT_F16);
-        if (t)
+    // linear weights: every non-conv matrix except token_embd shares one type
+    const gguf_tensor *probe = T("blk.0.attn_q.weight");
+    const uint32_t LT = probe && probe->type == DT_Q8_0 ? DT_Q8_0 : DT_F16;
+    m->q8 = LT == DT_Q8_0;
+    // a linear weight [N][K] stacked from source tensors; rmap(r) -> {tensor, source row}
+    auto lin = [&](const std::string &key, std::vector<const gguf_tensor *> src, int K, int N,
+                   std::function<std::pair<int, int>(int)> rmap, uint16_t **dst, uint16_t **dst_d) {
+        for (auto *t : src) if (!t) return;
+        if (LT == DT_F16) {
+            ups.push_back({key, (size_t)N * K * 2, (void **)dst, [src, K, N, rmap](uint8_t *o) {
+                               for (int r = 0; r < N; r++) {
+                                   const auto sr = rmap(r);
+                                   memcpy(o + (size_t)r * K * 2, (const uint8_t *)src[sr.first]->data + (size_t)sr.second * K * 2,
+                                          (size_t)K * 2);
+                               }
+                           }});
+        } else {
+            if (K % 32) { if (err.empty()) err = key + ": Q8_0 row length must be a multiple of 32"; return; }
+            const int nb = K / 32;
+            auto blocks = [src, nb, rmap](int r) {
+                const auto sr = rmap(r);
+                return (const uint8_t *)src[sr.first]->data + (size_t)sr.second * nb * 34;
+            };
+            ups.push_back({key, (size_t)N * K, (void **)dst, [blocks, K, N, nb](uint8_t *o) {
+                               for (int r = 0; r < N; r++) {
+                                   const uint8_t *b = blocks(r);
+                                   for (int j = 0; j < nb; j++) memcpy(o + (size_t)r * K + 32 * j, b + 34 * j + 2, 32);
+                               }
+                           }});
+            ups.push_back({key + ".d", (size_t)N * nb * 2, (void **)dst_d, [blocks, N, nb](uint8_t *o) {
+                               for (int r = 0; r < N; r++) {
+                                   const uint8_t *b = blocks(r);
+                                   for (int j = 0; j < nb; j++) memcpy(o + ((size_t)r * nb + j) * 2, b + 34 * j, 2);
+                               }
+                           }});
+        }
+    };
+    auto ident = [](int r) { return std::make_pair(0, r); };
+    auto one = [&](const std::string &n, int K, int N, uint16_t **dst, uint16_t **dst_d) {
+        lin(n, {need(n, {K, N}, LT)}, K, N, ident, dst, dst_d);
+    };
+    {   // conv_out: input feature c*16+h (src/audio_encoder.cpp:133-142).  F16: permuted
+        // to h*C + c at load so the GEMM's A is conv3's [h][c] rows; Q8_0 keeps the
+        // file order (blocks run along it) and the activation quantiser gathers.
+        const gguf_tensor *t = need("audio.encoder.conv_out.weight", {(int64_t)C * 16, D}, LT);
+        if (t && LT == DT_F16)
             ups.push_back({t->name, (size_t)D * C * 16 * 2, (void **)&m->conv_out_w, [t, C, D](uint8_t *o) {
                                const uint16_t *s = (const uint16_t *)t->data;
                                uint16_t *d = (uint16_t *)o;
@@ -300,40 +373,40 @@ extern "C" int qasr_model_load(const char *path, int device, qasr_model **out) {
                                    for (int c = 0; c < C; c++)
                                        for (int h = 0; h < 16; h++) d[(size_t)n * C * 16 + h * C + c] = s[(size_t)n * C * 16 + c * 16 + h];
                            }});
+        else if (t)
+            lin(t->name, {t}, 16 * C, D, ident, &m->conv_out_w, &m->conv_out_d);
     }
     for (int l = 0; l < hp.enc_layers; l++) {
         const std::string p = "audio.encoder.blk." + std::to_string(l) + ".";
         EncLayer &L = m->enc[l];
-        const gguf_tensor *q = need(p + "attn_q.weight", {D, D}, DT_F16), *k = need(p + "attn_k.weight", {D, D}, DT_F16),
-                          *v = need(p + "attn_v.weight", {D, D}, DT_F16);
+        const gguf_tensor *q = need(p + "attn_q.weight", {D, D}, LT), *k = need(p + "attn_k.weight", {D, D}, LT),
+                          *v = need(p + "attn_v.weight", {D, D}, LT);
         const gguf_tensor *qb = need(p + "attn_q.bias", {D}, DT_F32), *kb = need(p + "attn_k.bias", {D}, DT_F32),
                           *vb = need(p + "attn_v.bias", {D}, DT_F32);
-        if (q && k && v && qb && kb && vb) {
-            const size_t mb = (size_t)D * D * 2;
-            ups.push_back({p + "qkv", 3 * mb, (void **)&L.wqkv, [q, k, v, mb](uint8_t *o) {
-                               memcpy(o, q->data, mb); memcpy(o + mb, k->data, mb); memcpy(o + 2 * mb, v->data, mb); }});
+        lin(p + "qkv", {q, k, v}, D, 3 * D, [D](int r) { return std::make_pair(r / D, r % D); }, &L.wqkv, &L.wqkv_d);
+        if (qb && kb && vb) {
             const size_t bb = (size_t)D * 4;
             ups.push_back({p + "bqkv", 3 * bb, (void **)&L.bqkv, [qb, kb, vb, bb](uint8_t *o) {
                                memcpy(o, qb->data, bb); memcpy(o + bb, kb->data, bb); memcpy(o + 2 * bb, vb->data, bb); }});
         }
-        copy_f16(p + "attn_out.weight", {D, D}, &L.wo);
+        one(p + "attn_out.weight", D, D, &L.wo, &L.wo_d);
         copy_f32(p + "attn_out.bias", D, &L.bo);
         copy_f32(p + "attn_norm.weight", D, &L.ln1_w);
         copy_f32(p + "attn_norm.bias", D, &L.ln1_b);
-        copy_f16(p + "ffn_up.weight", {D, FF}, &L.w1);
+        one(p + "ffn_up.weight", D, FF, &L.w1, &L.w1_d);
         copy_f32(p + "ffn_up.bias", FF, &L.b1);
-        copy_f16(p + "ffn_down.weight", {FF, D}, &L.w2);
+        one(p + "ffn_down.weight", FF, D, &L.w2, &L.w2_d);
         copy_f32(p + "ffn_down.bias", D, &L.b2);
         copy_f32(p + "ffn_norm.weight", D, &L.ln2_w);
         copy_f32(p + "ffn_norm.bias", D, &L.ln2_b);
     }
     copy_f32("audio.encoder.ln_post.weight", D, &m->ln_post_w);
     copy_f32("audio.encoder.ln_post.bias", D, &m->ln_post_b);
-    copy_f16("audio.encoder.proj1.weight", {D, D}, &m->proj1_w);
+    one("audio.encoder.proj1.weight", D, D, &m->proj1_w, &m->proj1_d);
     copy_f32("audio.encoder.proj1.bias", D, &m->proj1_b);
-    copy_f16("audio.encoder.proj2.weight", {D, H}, &m->proj2_w);
+    one("audio.encoder.proj2.weight", D, H, &m->proj2_w, &m->proj2_d);
     copy_f32("audio.encoder.proj2.bias", H, &m->proj2_b);
-    copy_f16("token_embd.weight", {H, V}, &m->embd);   // tied LM head (src/text_decoder.cpp:264-265)
+    copy_f16("token_embd.weight", {H, V}, &m->embd);   // tied LM head (src/text_decoder.cpp:264-265), F16 in both file types
     copy_f32("output_norm.weight", H, &m->out_norm);
     for (int l = 0; l < hp.dec_layers; l++) {
         const std::string p = "blk." + std::to_string(l) + ".";
@@ -342,26 +415,17 @@ extern "C" int qasr_model_load(const char *path, int device, qasr_model **out) {
         copy_f32(p + "attn_q_norm.weight", 128, &L.q_norm);
         copy_f32(p + "attn_k_norm.weight", 128, &L.k_norm);
         copy_f32(p + "ffn_norm.weight", H, &L.ffn_norm);
-        const gguf_tensor *q = need(p + "attn_q.weight", {H, QD}, DT_F16), *k = need(p + "attn_k.weight", {H, KD}, DT_F16),
-                          *v = need(p + "attn_v.weight", {H, KD}, DT_F16);
-        if (q && k && v) {
-            const size_t qb = (size_t)QD * H * 2, kb = (size_t)KD * H * 2;
-            ups.push_back({p + "qkv", qb + 2 * kb, (void **)&L.wqkv, [q, k, v, qb, kb](uint8_t *o) {
-                               memcpy(o, q->data, qb); memcpy(o + qb, k->data, kb); memcpy(o + qb + kb, v->data, kb); }});
-        }
-        copy_f16(p + "attn_output.weight", {QD, H}, &L.wo);
-        const gguf_tensor *gt = need(p + "ffn_gate.weight", {H, F}, DT_F16), *ut = need(p + "ffn_up.weight", {H, F}, DT_F16);
-        if (gt && ut)   // interleave 16-row blocks: [gate 16q..16q+15 | up 16q..16q+15]
-            ups.push_back({p + "gu", (size_t)2 * F * H * 2, (void **)&L.wgu, [gt, ut, F, H](uint8_t *o) {
-                               const uint16_t *gs = (const uint16_t *)gt->data, *us = (const uint16_t *)ut->data;
-                               uint16_t *d = (uint16_t *)o;
-                               for (int r = 0; r < 2 * F; r++) {
-                                   const int q = r / 32, w = r % 32;
-                                   const uint16_t *src = w < 16 ? gs + (size_t)(16 * q + w) * H : us + (size_t)(16 * q + w - 16) * H;
-                                   memcpy(d + (size_t)r * H, src, (size_t)H * 2);
-                               }
-                           }});
-        copy_f16(p + "ffn_down.weight", {F, H}, &L.wd);
+        const gguf_tensor *q = need(p + "attn_q.weight", {H, QD}, LT), *k = need(p + "attn_k.weight", {H, KD}, LT),
+                          *v = need(p + "attn_v.weight", {H, KD}, LT);
+        lin(p + "qkv", {q, k, v}, H, QD + 2 * KD,
+            [QD, KD](int r) { return r < QD ? std::make_pair(0, r) : r < QD + KD ? std::make_pair(1, r - QD) : std::make_pair(2, r - QD - KD); },
+            &L.wqkv, &L.wqkv_d);
+        one(p + "attn_output.weight", QD, H, &L.wo, &L.wo_d);
+        const gguf_tensor *gt = need(p + "ffn_gate.weight", {H, F}, LT), *ut = need(p + "ffn_up.weight", {H, F}, LT);
+        // interleave 16-row blocks: [gate 16q..16q+15 | up 16q..16q+15] -> SwiGLU in one epilogue
+        lin(p + "gu", {gt, ut}, H, 2 * F, [](int r) { return std::make_pair((r % 32) < 16 ? 0 : 1, 16 * (r / 32) + (r % 16)); },
+            &L.wgu, &L.wgu_d);
+        one(p + "ffn_down.weight", F, H, &L.wd, &L.wd_d);
     }
     if (!err.empty()) return fail(QASR_ERR_FORMAT, err);
     // constant tables
@@ -447,8 +511,8 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     if (const char *tp = getenv("QASR_DEV_TRACE")) {
         c->trace_path = tp;
         if (const char *tl = getenv("QASR_DEV_TRACE_LAYER")) c->trace_layer = atoi(tl);
-        if ((rc = dev_alloc(c.get(), (void **)&c->d_trace, 6 * 4096 * 4 * 8))) return rc;
-        HIPCHK(hipMemset(c->d_trace, 0, 6 * 4096 * 4 * 8));
+        if ((rc = dev_alloc(c.get(), (void **)&c->d_trace, 6 * 4096 * 8 * 8))) return rc;
+        HIPCHK(hipMemset(c->d_trace, 0, 6 * 4096 * 8 * 8));
     }
     c->hist_cap = max_ctx;
     if ((rc = dev_alloc(c.get(), (void **)&c->d_tok, B * 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_hist, (size_t)B * max_ctx * 4)) ||
@@ -460,6 +524,11 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_q, (size_t)B * QD * 2)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_att, (size_t)B * QD * 2)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_act, (size_t)B * hp.dec_ffn * 2)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_att32, (size_t)B * QD * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_act32, (size_t)B * hp.dec_ffn * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_q8a, (size_t)B * std::max(QD, std::max(hp.hidden, hp.dec_ffn)))) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_q8d, (size_t)B * std::max(QD, std::max(hp.hidden, hp.dec_ffn)) / 32 * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_x32, (size_t)B * std::max(QD, std::max(hp.hidden, hp.dec_ffn)) * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_part, (size_t)B * hp.n_kv_head * c->max_splits * 2 * 132 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_counter, (size_t)B * hp.n_kv_head * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) ||
@@ -581,11 +650,18 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     g.A = c->act2.as<uint16_t>(); g.W = m->conv3_w; g.M = r3; g.row_start = c->rs3.as<int>(); g.bias = m->conv3_b;
     g.out_f16 = c->act3.as<uint16_t>();
     launch_gemm(AM_CONV3, EPI_GELU_F16, g, s);
+    const bool q8 = m->q8;
+    if (q8 && (rc = ensure_q8(c, N, std::max(16 * C, std::max(D, FF)), D))) return rc;
     // conv_out (no bias) + per-chunk sinusoidal PE (src/audio_encoder.cpp:147-149, :400-404)
     GemmArgs o{};
-    o.A = c->act3.as<uint16_t>(); o.lda = 16 * C; o.W = m->conv_out_w; o.ldw = 16 * C; o.M = N; o.N = D; o.K = 16 * C;
+    o.M = N; o.N = D; o.K = 16 * C;
     o.out_f32 = c->ex.as<float>(); o.ldo = D; o.pe = m->pe; o.pe_pos = c->pepos.as<int>();
-    launch_gemm(AM_DENSE, EPI_F32, o, s);
+    if (q8) {
+        gemm_q8(c, EPI_F32, o, nullptr, c->act3.as<uint16_t>(), 16 * C, C, m->conv_out_w, m->conv_out_d, s);
+    } else {
+        o.A = c->act3.as<uint16_t>(); o.lda = 16 * C; o.W = m->conv_out_w; o.ldw = 16 * C;
+        launch_gemm(AM_DENSE, EPI_F32, o, s);
+    }
     HIPCHK(hipGetLastError());
     if (conv_only) return 0;
 
@@ -595,38 +671,40 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     if ((rc = upload(c, c->segs, segs))) return rc;
     float *x = c->ex.as<float>();
     uint16_t *xh = c->exh.as<uint16_t>();
+    float *x32 = q8 ? c->x32.as<float>() : nullptr;
+    // y = act W^T with the model's weight type: F16 takes the fp16 activation
+    // (a16), Q8_0 quantises the fp32 (a32) or fp16 one
+    auto linear = [&](int epi, GemmArgs g, const float *a32, const uint16_t *a16, int lda, const uint16_t *W, const uint16_t *Wd) {
+        if (q8) { gemm_q8(c, epi, g, a32, a32 ? nullptr : a16, lda, 0, W, Wd, s); return; }
+        g.A = a16; g.lda = lda; g.W = W; g.ldw = g.K;
+        launch_gemm(AM_DENSE, epi, g, s);
+    };
     for (int l = 0; l < hp.enc_layers; l++) {
         const EncLayer &L = m->enc[l];
-        launch_layernorm_f16(x, N, D, L.ln1_w, L.ln1_b, hp.enc_eps, xh, s);
+        launch_layernorm_f16(x, N, D, L.ln1_w, L.ln1_b, hp.enc_eps, xh, s, x32);
         GemmArgs q{};
-        q.A = xh; q.lda = D; q.W = L.wqkv; q.ldw = D; q.M = N; q.N = 3 * D; q.K = D; q.bias = L.bqkv;
-        q.out_f32 = c->eqkv.as<float>(); q.ldo = 3 * D;
-        launch_gemm(AM_DENSE, EPI_F32, q, s);
+        q.M = N; q.N = 3 * D; q.K = D; q.bias = L.bqkv; q.out_f32 = c->eqkv.as<float>(); q.ldo = 3 * D;
+        linear(EPI_F32, q, x32, xh, D, L.wqkv, L.wqkv_d);
         launch_enc_attention(c->eqkv.as<float>(), c->segs.as<int>(), c->segs.as<int>() + B, B, maxn, D, hp.enc_heads,
-                             c->eatt.as<uint16_t>(), s);
+                             c->eatt.as<uint16_t>(), s, x32);
         GemmArgs op{};
-        op.A = c->eatt.as<uint16_t>(); op.lda = D; op.W = L.wo; op.ldw = D; op.M = N; op.N = D; op.K = D; op.bias = L.bo;
-        op.res = x; op.ldr = D; op.out_f32 = x; op.ldo = D;
-        launch_gemm(AM_DENSE, EPI_F32, op, s);
-        launch_layernorm_f16(x, N, D, L.ln2_w, L.ln2_b, hp.enc_eps, xh, s);
+        op.M = N; op.N = D; op.K = D; op.bias = L.bo; op.res = x; op.ldr = D; op.out_f32 = x; op.ldo = D;
+        linear(EPI_F32, op, x32, c->eatt.as<uint16_t>(), D, L.wo, L.wo_d);
+        launch_layernorm_f16(x, N, D, L.ln2_w, L.ln2_b, hp.enc_eps, xh, s, x32);
         GemmArgs f1{};
-        f1.A = xh; f1.lda = D; f1.W = L.w1; f1.ldw = D; f1.M = N; f1.N = FF; f1.K = D; f1.bias = L.b1; f1.gelu = m->gelu;
-        f1.out_f16 = c->eff.as<uint16_t>(); f1.ldo16 = FF;
-        launch_gemm(AM_DENSE, EPI_GELU_F16, f1, s);
-        GemmArgs f2{};
-        f2.A = c->eff.as<uint16_t>(); f2.lda = FF; f2.W = L.w2; f2.ldw = FF; f2.M = N; f2.N = D; f2.K = FF; f2.bias = L.b2;
-        f2.res = x; f2.ldr = D; f2.out_f32 = x; f2.ldo = D;
-        launch_gemm(AM_DENSE, EPI_F32, f2, s);
+        f1.M = N; f1.N = FF; f1.K = D; f1.bias = L.b1; f1.gelu = m->gelu; f1.out_f16 = c->eff.as<uint16_t>(); f1.ldo16 = FF;
+        linear(EPI_GELU_F16, f1, x32, xh, D, L.w1, L.w1_d);
+        GemmArgs f2{};   // GELU output is fp16-exact (LUT): the Q8_0 path quantises it as is
+        f2.M = N; f2.N = D; f2.K = FF; f2.bias = L.b2; f2.res = x; f2.ldr = D; f2.out_f32 = x; f2.ldo = D;
+        linear(EPI_F32, f2, nullptr, c->eff.as<uint16_t>(), FF, L.w2, L.w2_d);
     }
-    launch_layernorm_f16(x, N, D, m->ln_post_w, m->ln_post_b, hp.enc_eps, xh, s);
+    launch_layernorm_f16(x, N, D, m->ln_post_w, m->ln_post_b, hp.enc_eps, xh, s, x32);
     GemmArgs p1{};
-    p1.A = xh; p1.lda = D; p1.W = m->proj1_w; p1.ldw = D; p1.M = N; p1.N = D; p1.K = D; p1.bias = m->proj1_b; p1.gelu = m->gelu;
-    p1.out_f16 = c->eatt.as<uint16_t>(); p1.ldo16 = D;
-    launch_gemm(AM_DENSE, EPI_GELU_F16, p1, s);
+    p1.M = N; p1.N = D; p1.K = D; p1.bias = m->proj1_b; p1.gelu = m->gelu; p1.out_f16 = c->eatt.as<uint16_t>(); p1.ldo16 = D;
+    linear(EPI_GELU_F16, p1, x32, xh, D, m->proj1_w, m->proj1_d);
     GemmArgs p2{};
-    p2.A = c->eatt.as<uint16_t>(); p2.lda = D; p2.W = m->proj2_w; p2.ldw = D; p2.M = N; p2.N = hp.hidden; p2.K = D;
-    p2.bias = m->proj2_b; p2.out_f32 = c->feats.as<float>(); p2.ldo = hp.hidden;
-    launch_gemm(AM_DENSE, EPI_F32, p2, s);
+    p2.M = N; p2.N = hp.hidden; p2.K = D; p2.bias = m->proj2_b; p2.out_f32 = c->feats.as<float>(); p2.ldo = hp.hidden;
+    linear(EPI_F32, p2, nullptr, c->eatt.as<uint16_t>(), D, m->proj2_w, m->proj2_d);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -676,15 +754,18 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
     const int *d_srow0 = d_seq + 3 * rows, *d_slen = d_srow0 + B, *d_sslot = d_slen + B;
     float *x = c->px.as<float>();
     uint16_t *xh = c->pxh.as<uint16_t>();
+    const bool q8 = m->q8;
+    if (q8 && (rc = ensure_q8(c, rows, std::max(H, std::max(QD, F)), std::max(H, std::max(QD, F))))) return rc;
+    float *x32 = q8 ? c->x32.as<float>() : nullptr;
     launch_embed(c->pids.as<int32_t>(), rows, m->embd, H, d_feats, d_aud, x, s);
     const size_t layer_kv = (size_t)c->max_batch * hp.n_kv_head * c->max_ctx * 128;
     for (int l = 0; l < hp.dec_layers; l++) {
         const DecLayer &L = m->dec[l];
-        launch_rmsnorm_f16(x, H, nullptr, rows, H, L.attn_norm, hp.rms_eps, xh, s);
+        launch_rmsnorm_f16(x, H, nullptr, rows, H, L.attn_norm, hp.rms_eps, xh, s, x32);
         GemmArgs q{};
-        q.A = xh; q.lda = H; q.W = L.wqkv; q.ldw = H; q.M = rows; q.N = QD + 2 * KD; q.K = H;
-        q.out_f32 = c->pqkv.as<float>(); q.ldo = QD + 2 * KD;
-        launch_gemm(AM_DENSE, EPI_F32, q, s);
+        q.M = rows; q.N = QD + 2 * KD; q.K = H; q.out_f32 = c->pqkv.as<float>(); q.ldo = QD + 2 * KD;
+        if (q8) gemm_q8(c, EPI_F32, q, x32, nullptr, H, 0, L.wqkv, L.wqkv_d, s);
+        else { q.A = xh; q.lda = H; q.W = L.wqkv; q.ldw = H; launch_gemm(AM_DENSE, EPI_F32, q, s); }
         QkvPostArgs qa{};
         qa.qkv = c->pqkv.as<float>(); qa.rows = rows; qa.row_seq = d_seq; qa.row_pos = d_pos;
         qa.q_norm = L.q_norm; qa.k_norm = L.k_norm; qa.eps = hp.rms_eps; qa.rope = c->rope;
@@ -694,21 +775,26 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
         PrefillAttnArgs pa{};
         pa.q = c->pq.as<uint16_t>(); pa.kc = qa.kc; pa.vc = qa.vc; pa.seq_row0 = d_srow0; pa.seq_len = d_slen;
         pa.seq_slot = d_sslot; pa.n_seq = B; pa.max_len = maxp; pa.n_head = hp.n_head; pa.n_kv_head = hp.n_kv_head;
-        pa.max_ctx = c->max_ctx; pa.scale = 1.0f / sqrtf(128.0f); pa.out = c->patt.as<uint16_t>();
+        pa.max_ctx = c->max_ctx; pa.scale = 1.0f / sqrtf(128.0f); pa.out = c->patt.as<uint16_t>(); pa.out32 = x32;
         launch_prefill_attention(pa, s);
         GemmArgs o{};
-        o.A = c->patt.as<uint16_t>(); o.lda = QD; o.W = L.wo; o.ldw = QD; o.M = rows; o.N = H; o.K = QD;
-        o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
-        launch_gemm(AM_DENSE, EPI_F32, o, s);
-        launch_rmsnorm_f16(x, H, nullptr, rows, H, L.ffn_norm, hp.rms_eps, xh, s);
+        o.M = rows; o.N = H; o.K = QD; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
+        if (q8) gemm_q8(c, EPI_F32, o, x32, nullptr, QD, 0, L.wo, L.wo_d, s);
+        else { o.A = c->patt.as<uint16_t>(); o.lda = QD; o.W = L.wo; o.ldw = QD; launch_gemm(AM_DENSE, EPI_F32, o, s); }
+        launch_rmsnorm_f16(x, H, nullptr, rows, H, L.ffn_norm, hp.rms_eps, xh, s, x32);
         GemmArgs gu{};
-        gu.A = xh; gu.lda = H; gu.W = L.wgu; gu.ldw = H; gu.M = rows; gu.N = 2 * F; gu.K = H;
-        gu.out_f16 = c->pact.as<uint16_t>(); gu.ldo16 = F;
-        launch_gemm(AM_DENSE, EPI_SWIGLU_F16, gu, s);
+        gu.M = rows; gu.N = 2 * F; gu.K = H;
+        if (q8) {   // SwiGLU in fp32 (the down projection quantises it); x32 is free once quantised
+            gu.out_f32 = x32; gu.ldo = F;
+            gemm_q8(c, EPI_SWIGLU_F32, gu, x32, nullptr, H, 0, L.wgu, L.wgu_d, s);
+        } else {
+            gu.A = xh; gu.lda = H; gu.W = L.wgu; gu.ldw = H; gu.out_f16 = c->pact.as<uint16_t>(); gu.ldo16 = F;
+            launch_gemm(AM_DENSE, EPI_SWIGLU_F16, gu, s);
+        }
         GemmArgs dn{};
-        dn.A = c->pact.as<uint16_t>(); dn.lda = F; dn.W = L.wd; dn.ldw = F; dn.M = rows; dn.N = H; dn.K = F;
-        dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
-        launch_gemm(AM_DENSE, EPI_F32, dn, s);
+        dn.M = rows; dn.N = H; dn.K = F; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
+        if (q8) gemm_q8(c, EPI_F32, dn, x32, nullptr, F, 0, L.wd, L.wd_d, s);
+        else { dn.A = c->pact.as<uint16_t>(); dn.lda = F; dn.W = L.wd; dn.ldw = F; launch_gemm(AM_DENSE, EPI_F32, dn, s); }
     }
     // last row of each sequence -> RMSNorm -> tied LM head + argmax (src/text_decoder.cpp:564-572)
     uint16_t *xl = c->d_xh;
@@ -751,45 +837,65 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
     const size_t layer_kv = (size_t)c->max_batch * hp.n_kv_head * c->max_ctx * 128;
     if ((part == 0 || part == 1) && !skinny) launch_embed(c->d_tok, B, m->embd, H, nullptr, nullptr, x, s);
     const int skip = c->dev_skip;   // profiling only (QASR_DEV_SKIP): drop kernels to price them
+    if (c->d_trace && (part == 0 || part == 1)) (void)hipMemsetAsync(c->d_trace, 0, 6 * 4096 * 8 * 8, s);
     for (int l = 0; (part == 0 || part == 1) && l < hp.dec_layers; l++) {
         const DecLayer &L = m->dec[l];
         auto tr = [&](int k) -> unsigned long long * {
-            return c->d_trace && l == c->trace_layer ? c->d_trace + (size_t)k * 4096 * 4 : nullptr;
+            return c->d_trace && l == c->trace_layer ? c->d_trace + (size_t)k * 4096 * 8 : nullptr;
         };
+        const bool q8 = m->q8;
         if (skinny) {
             GemvArgs q{};
-            q.x = x; q.ldx = H; q.norm_w = L.attn_norm; q.eps = hp.rms_eps; q.W = L.wqkv; q.K = H; q.N = QD + 2 * KD; q.M = B;
-            q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
+            q.x = x; q.ldx = H; q.norm_w = L.attn_norm; q.eps = hp.rms_eps; q.W = L.wqkv; q.Wd = L.wqkv_d; q.K = H;
+            q.N = QD + 2 * KD; q.M = B; q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
             if (l == 0) { q.embd_ids = c->d_tok; q.embd = m->embd; q.x_store = x; }   // fused embedding gather
             q.trace = tr(0);
             if (!(skip & 1)) launch_gemv(EPI_F32, q, s);
         } else {
-            launch_rmsnorm_f16(x, H, nullptr, B, H, L.attn_norm, hp.rms_eps, c->d_xh, s);
+            launch_rmsnorm_f16(x, H, nullptr, B, H, L.attn_norm, hp.rms_eps, c->d_xh, s, q8 ? c->d_x32 : nullptr);
             GemmArgs q{};
-            q.A = c->d_xh; q.lda = H; q.W = L.wqkv; q.ldw = H; q.M = B; q.N = QD + 2 * KD; q.K = H;
-            q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
-            launch_gemm(AM_DENSE, EPI_F32, q, s);
+            q.M = B; q.N = QD + 2 * KD; q.K = H; q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
+            if (q8) gemm_q8(c, EPI_F32, q, c->d_x32, nullptr, H, 0, L.wqkv, L.wqkv_d, s, c->d_q8a, c->d_q8d);
+            else { q.A = c->d_xh; q.lda = H; q.W = L.wqkv; q.ldw = H; launch_gemm(AM_DENSE, EPI_F32, q, s); }
         }
         DecodeAttnArgs da{};
         da.qkv = c->d_qkv; da.q_norm = L.q_norm; da.k_norm = L.k_norm; da.eps = hp.rms_eps; da.rope = c->rope;
         da.pos = c->d_pos; da.kc = c->kc + l * layer_kv; da.vc = c->vc + l * layer_kv; da.seq_slot = c->d_slot; da.B = B;
         da.n_head = hp.n_head; da.n_kv_head = hp.n_kv_head; da.max_ctx = c->max_ctx; da.max_splits = c->max_splits; da.grid_splits = splits;
         da.scale = 1.0f / sqrtf(128.0f); da.part = c->d_part; da.counter = c->d_counter; da.out = c->d_att;
+        da.out32 = q8 ? (skinny ? c->d_att32 : c->d_x32) : nullptr;
         da.trace = tr(1);
         if (!(skip & 2)) launch_decode_attention(da, s);
         if (skinny) {
             GemvArgs o{};
-            o.xh = c->d_att; o.ldxh = QD; o.trace = tr(2);
+            if (q8) { o.x = c->d_att32; o.ldx = QD; o.Wd = L.wo_d; }
+            else { o.xh = c->d_att; o.ldxh = QD; }
+            o.trace = tr(2);
             o.W = L.wo; o.K = QD; o.N = H; o.M = B; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
             if (!(skip & 4)) launch_gemv(EPI_F32, o, s);
             GemvArgs gu{};
-            gu.x = x; gu.ldx = H; gu.norm_w = L.ffn_norm; gu.eps = hp.rms_eps; gu.W = L.wgu; gu.K = H; gu.N = F; gu.M = B;
-            gu.out_f16 = c->d_act; gu.ldo16 = F; gu.trace = tr(3);
-            if (!(skip & 8)) launch_gemv(EPI_SWIGLU_F16, gu, s);
+            gu.x = x; gu.ldx = H; gu.norm_w = L.ffn_norm; gu.eps = hp.rms_eps; gu.W = L.wgu; gu.Wd = L.wgu_d; gu.K = H; gu.N = F; gu.M = B;
+            if (q8) { gu.out_f32 = c->d_act32; gu.ldo = F; }
+            else { gu.out_f16 = c->d_act; gu.ldo16 = F; }
+            gu.trace = tr(3);
+            if (!(skip & 8)) launch_gemv(q8 ? EPI_SWIGLU_F32 : EPI_SWIGLU_F16, gu, s);
             GemvArgs dn{};
-            dn.xh = c->d_act; dn.ldxh = F; dn.W = L.wd; dn.K = F; dn.N = H; dn.M = B; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
+            if (q8) { dn.x = c->d_act32; dn.ldx = F; dn.Wd = L.wd_d; }
+            else { dn.xh = c->d_act; dn.ldxh = F; }
+            dn.W = L.wd; dn.K = F; dn.N = H; dn.M = B; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
             dn.trace = tr(4);
             if (!(skip & 16)) launch_gemv(EPI_F32, dn, s);
+        } else if (q8) {
+            GemmArgs o{};
+            o.M = B; o.N = H; o.K = QD; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
+            gemm_q8(c, EPI_F32, o, c->d_x32, nullptr, QD, 0, L.wo, L.wo_d, s, c->d_q8a, c->d_q8d);
+            launch_rmsnorm_f16(x, H, nullptr, B, H, L.ffn_norm, hp.rms_eps, c->d_xh, s, c->d_x32);
+            GemmArgs gu{};
+            gu.M = B; gu.N = 2 * F; gu.K = H; gu.out_f32 = c->d_x32; gu.ldo = F;
+            gemm_q8(c, EPI_SWIGLU_F32, gu, c->d_x32, nullptr, H, 0, L.wgu, L.wgu_d, s, c->d_q8a, c->d_q8d);
+            GemmArgs dn{};
+            dn.M = B; dn.N = H; dn.K = F; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
+            gemm_q8(c, EPI_F32, dn, c->d_x32, nullptr, F, 0, L.wd, L.wd_d, s, c->d_q8a, c->d_q8d);
         } else {
             GemmArgs o{};
             o.A = c->d_att; o.lda = QD; o.W = L.wo; o.ldw = QD; o.M = B; o.N = H; o.K = QD; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
@@ -1117,8 +1223,8 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
     HIPCHK(hipEventRecord(c->ev[4], s));
     HIPCHK(hipEventSynchronize(c->ev[4]));
     if ((rc = probe_collect(c, steps))) return rc;
-    if (c->d_trace) {   // dev trace dump: raw [6][4096][4] u64
-        std::vector<unsigned long long> tr((size_t)6 * 4096 * 4);
+    if (c->d_trace) {   // dev trace dump: raw [6][4096][8] u64
+        std::vector<unsigned long long> tr((size_t)6 * 4096 * 8);
         HIPCHK(hipMemcpy(tr.data(), c->d_trace, tr.size() * 8, hipMemcpyDeviceToHost));
         if (FILE *f = fopen(c->trace_path.c_str(), "wb")) {
             (void)fwrite(tr.data(), 8, tr.size(), f);

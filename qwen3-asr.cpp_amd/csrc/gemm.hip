@@ -32,6 +32,82 @@ __device__ __forceinline__ int find_chunk(const int *__restrict__ starts, int n,
 
 __device__ __forceinline__ float silu_f(float g) { return g / (1.0f + expf(-g)); }
 
+// ------------------------------------------------------------ epilogue
+// acc[i][j] holds rows m0 + wr*BM/2 + 16i + 4(lane>>4) + r, column
+// n0 + wc*BN/2 + 16j + (lane&15) (v_mfma_*_16x16x* C layout)
+template <int BM, int BN, int EPI>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs &g, floatx4 (&acc)[BM / 32][BN / 32], int m0, int n0, int wr,
+                                              int wc, int lane) {
+    constexpr int FM = BM / 32, FN = BN / 32;
+    const int M = g.M;
+    const int rbase = m0 + wr * (BM / 2) + 4 * (lane >> 4);
+    const int cbase = n0 + wc * (BN / 2) + (lane & 15);
+    if constexpr (EPI == EPI_SWIGLU_F16 || EPI == EPI_SWIGLU_F32) {
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int p = 0; p < FN / 2; p++) {
+                const int ocol = (n0 + wc * (BN / 2)) / 2 + p * 16 + (lane & 15);
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int row = rbase + i * 16 + r;
+                    if (row < M) {
+                        const float gt = acc[i][2 * p][r], up = acc[i][2 * p + 1][r];
+                        const float v = silu_f(gt) * up;
+                        if constexpr (EPI == EPI_SWIGLU_F32) g.out_f32[(long)row * g.ldo + ocol] = v;
+                        else g.out_f16[(long)row * g.ldo16 + ocol] = f_to_u16(v);
+                    }
+                }
+            }
+    } else if constexpr (EPI == EPI_ARGMAX) {
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = rbase + i * 16 + r;
+                unsigned long long best = 0ull;
+#pragma unroll
+                for (int j = 0; j < FN; j++) {
+                    const int col = cbase + j * 16;
+                    const float v = acc[i][j][r];
+                    if (row < M && g.out_f32) g.out_f32[(long)row * g.ldo + col] = v;
+                    const unsigned long long key = argmax_key(v, col);
+                    best = key > best ? key : best;
+                }
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    const unsigned long long other = __shfl_xor(best, o, 64);
+                    best = other > best ? other : best;
+                }
+                if (row < M && (lane & 15) == 0) atomicMax(g.amax + row, best);
+            }
+    } else {
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                const int col = cbase + j * 16;
+                const float bcol = g.bias ? g.bias[col] : 0.0f;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int row = rbase + i * 16 + r;
+                    if (row >= M) continue;
+                    float v = acc[i][j][r];
+                    if (g.bias) v = fadd_rn(v, bcol);
+                    if constexpr (EPI == EPI_GELU_F16) {
+                        g.out_f16[(long)row * g.ldo16 + col] = f_to_u16(gelu_lut(v, g.gelu));
+                    } else if constexpr (EPI == EPI_F16) {
+                        g.out_f16[(long)row * g.ldo16 + col] = f_to_u16(v);
+                    } else {
+                        if (g.pe) v = fadd_rn(v, g.pe[(long)g.pe_pos[row] * g.N + col]);
+                        if (g.res) v = fadd_rn(v, g.res[(long)row * g.ldr + col]);
+                        g.out_f32[(long)row * g.ldo + col] = v;
+                    }
+                }
+            }
+    }
+}
+
 template <int BM, int BN, int KS, int AMODE, int EPI>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     constexpr int FM = BM / 32, FN = BN / 32;
@@ -151,72 +227,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
         __syncthreads();
     }
 
-    // ------------------------------------------------------------ epilogue
-    const int rbase = m0 + wr * (BM / 2) + 4 * (lane >> 4);
-    const int cbase = n0 + wc * (BN / 2) + (lane & 15);
-    if constexpr (EPI == EPI_SWIGLU_F16) {
-#pragma unroll
-        for (int i = 0; i < FM; i++)
-#pragma unroll
-            for (int p = 0; p < FN / 2; p++) {
-                const int ocol = (n0 + wc * (BN / 2)) / 2 + p * 16 + (lane & 15);
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int row = rbase + i * 16 + r;
-                    if (row < M) {
-                        const float gt = acc[i][2 * p][r], up = acc[i][2 * p + 1][r];
-                        const float v = silu_f(gt) * up;
-                        g.out_f16[(long)row * g.ldo16 + ocol] = f_to_u16(v);
-                    }
-                }
-            }
-    } else if constexpr (EPI == EPI_ARGMAX) {
-#pragma unroll
-        for (int i = 0; i < FM; i++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int row = rbase + i * 16 + r;
-                unsigned long long best = 0ull;
-#pragma unroll
-                for (int j = 0; j < FN; j++) {
-                    const int col = cbase + j * 16;
-                    const float v = acc[i][j][r];
-                    if (row < M && g.out_f32) g.out_f32[(long)row * g.ldo + col] = v;
-                    const unsigned long long key = argmax_key(v, col);
-                    best = key > best ? key : best;
-                }
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    const unsigned long long other = __shfl_xor(best, o, 64);
-                    best = other > best ? other : best;
-                }
-                if (row < M && (lane & 15) == 0) atomicMax(g.amax + row, best);
-            }
-    } else {
-#pragma unroll
-        for (int i = 0; i < FM; i++)
-#pragma unroll
-            for (int j = 0; j < FN; j++) {
-                const int col = cbase + j * 16;
-                const float bcol = g.bias ? g.bias[col] : 0.0f;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int row = rbase + i * 16 + r;
-                    if (row >= M) continue;
-                    float v = acc[i][j][r];
-                    if (g.bias) v = fadd_rn(v, bcol);
-                    if constexpr (EPI == EPI_GELU_F16) {
-                        g.out_f16[(long)row * g.ldo16 + col] = f_to_u16(gelu_lut(v, g.gelu));
-                    } else if constexpr (EPI == EPI_F16) {
-                        g.out_f16[(long)row * g.ldo16 + col] = f_to_u16(v);
-                    } else {
-                        if (g.pe) v = fadd_rn(v, g.pe[(long)g.pe_pos[row] * g.N + col]);
-                        if (g.res) v = fadd_rn(v, g.res[(long)row * g.ldr + col]);
-                        g.out_f32[(long)row * g.ldo + col] = v;
-                    }
-                }
-            }
-    }
+    gemm_epilogue<BM, BN, EPI>(g, acc, m0, n0, wr, wc, lane);
 }
 
 template <int BM, int BN, int KS, int AMODE, int EPI>
@@ -254,8 +265,153 @@ void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s) {
         case AM_DENSE * 8 + EPI_SWIGLU_F16: dispatch_tiles<AM_DENSE, EPI_SWIGLU_F16>(g, s); break;
         case AM_DENSE * 8 + EPI_ARGMAX: dispatch_tiles<AM_DENSE, EPI_ARGMAX>(g, s); break;
         case AM_DENSE * 8 + EPI_F16: dispatch_tiles<AM_DENSE, EPI_F16>(g, s); break;
+        case AM_DENSE * 8 + EPI_SWIGLU_F32: dispatch_tiles<AM_DENSE, EPI_SWIGLU_F32>(g, s); break;
         case AM_CONV2 * 8 + EPI_GELU_F16: dispatch_tiles<AM_CONV2, EPI_GELU_F16>(g, s); break;
         case AM_CONV3 * 8 + EPI_GELU_F16: dispatch_tiles<AM_CONV3, EPI_GELU_F16>(g, s); break;
+        default: break;
+    }
+}
+
+// ================================================================ Q8_0 GEMM
+// ggml_mul_mat(W Q8_0, X) = per 32-wide K block: exact int8 dot (here one
+// v_mfma_i32_16x16x32_i8 with a zero accumulator), converted to fp32 and
+// fma'd with d_w * d_x into the fp32 accumulator (ggml_vec_dot_q8_0_q8_0:
+// sumf += (d_x * d_y) * sumi).  A and W are staged as int8 rows of KS blocks
+// (row stride KS*32+16 B: the 8-byte fragment reads of 16 lanes hit distinct
+// bank pairs), their block scales as fp32 beside them.
+typedef int intx4 __attribute__((ext_vector_type(4)));
+
+template <int BM, int BN, int KS, int EPI>
+__global__ __launch_bounds__(256) void gemm_q8_kernel(GemmArgs g) {
+    constexpr int FM = BM / 32, FN = BN / 32;
+    constexpr int ROWS = BM + BN;
+    constexpr int RB = KS * 32 + 16;           // LDS bytes per row per stage
+    constexpr int NCH = ROWS * KS * 2;         // 16-byte chunks per stage
+    constexpr int CPT = (NCH + 255) / 256;
+    static_assert(ROWS <= 256, "one scale row per thread");
+    __shared__ __attribute__((aligned(16))) int8_t sq[2][ROWS * RB];
+    __shared__ __attribute__((aligned(16))) float ssc[2][KS][ROWS];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid >> 1, wc = wid & 1;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int M = g.M, K = g.K, nbw = K / 32;
+
+    floatx4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    u32x4 stage[CPT];
+    float sreg[KS];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int t = 0; t < CPT; t++) {
+            const int c = tid + t * 256;
+            u32x4 v = u32x4{0u, 0u, 0u, 0u};
+            if (c < NCH) {
+                const int r = c / (KS * 2), q = c - r * (KS * 2);
+                const int k = k0 + q * 16;
+                if (r < BM) {
+                    const int row = m0 + r;
+                    if (row < M) v = *(const u32x4 *)(g.Aq + (long)row * g.lda + k);
+                } else {
+                    v = *(const u32x4 *)(g.Wq + (long)(n0 + r - BM) * g.ldw + k);
+                }
+            }
+            stage[t] = v;
+        }
+        if (tid < ROWS) {
+            const int kb = k0 / 32;
+            if (tid < BM) {
+                const int row = m0 + tid;
+#pragma unroll
+                for (int u = 0; u < KS; u++) sreg[u] = row < M ? g.Ad[(long)row * g.ldad + kb + u] : 0.0f;
+            } else {
+                const uint16_t *wd = g.Wd + (long)(n0 + tid - BM) * nbw + kb;
+#pragma unroll
+                for (int u = 0; u < KS; u++) sreg[u] = u16_to_f(wd[u]);
+            }
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int t = 0; t < CPT; t++) {
+            const int c = tid + t * 256;
+            if (c < NCH) {
+                const int r = c / (KS * 2), q = c - r * (KS * 2);
+                *(u32x4 *)(&sq[buf][r * RB + q * 16]) = stage[t];
+            }
+        }
+        if (tid < ROWS)
+#pragma unroll
+            for (int u = 0; u < KS; u++) ssc[buf][u][tid] = sreg[u];
+    };
+
+    const int nk = K / (32 * KS);
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    const int kg = lane >> 4;
+    for (int kt = 0; kt < nk; kt++) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) gload((kt + 1) * 32 * KS);
+#pragma unroll
+        for (int u = 0; u < KS; u++) {
+            long af[FM], bf[FN];
+            floatx4 sa[FM];
+            float sb[FN];
+#pragma unroll
+            for (int i = 0; i < FM; i++) {
+                const int r = wr * (BM / 2) + i * 16 + (lane & 15);
+                af[i] = *(const long *)(&sq[cur][r * RB + u * 32 + kg * 8]);
+                sa[i] = *(const floatx4 *)(&ssc[cur][u][wr * (BM / 2) + i * 16 + 4 * kg]);
+            }
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                const int r = BM + wc * (BN / 2) + j * 16 + (lane & 15);
+                bf[j] = *(const long *)(&sq[cur][r * RB + u * 32 + kg * 8]);
+                sb[j] = ssc[cur][u][r];
+            }
+#pragma unroll
+            for (int i = 0; i < FM; i++)
+#pragma unroll
+                for (int j = 0; j < FN; j++) {
+                    const intx4 ci = __builtin_amdgcn_mfma_i32_16x16x32_i8(af[i], bf[j], intx4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) acc[i][j][r] = fmaf(fmul_rn(sb[j], sa[i][r]), (float)ci[r], acc[i][j][r]);
+                }
+        }
+        if (kt + 1 < nk) sstore(cur ^ 1);
+        __syncthreads();
+    }
+    gemm_epilogue<BM, BN, EPI>(g, acc, m0, n0, wr, wc, lane);
+}
+
+template <int BM, int BN, int KS, int EPI>
+static void run_gemm_q8(const GemmArgs &g, hipStream_t s) {
+    dim3 grid(g.N / BN, (g.M + BM - 1) / BM);
+    hipLaunchKernelGGL((gemm_q8_kernel<BM, BN, KS, EPI>), grid, dim3(256), 0, s, g);
+}
+
+template <int EPI>
+static void dispatch_q8(const GemmArgs &g, hipStream_t s) {
+    const bool big = g.M >= 2048 && g.N % 128 == 0;
+    if (g.K % 128 == 0) {
+        if (big) run_gemm_q8<128, 128, 2, EPI>(g, s);
+        else run_gemm_q8<64, 64, 4, EPI>(g, s);
+    } else {
+        run_gemm_q8<64, 64, 1, EPI>(g, s);
+    }
+}
+
+void launch_gemm_q8(int epi, const GemmArgs &g, hipStream_t s) {
+    if (g.M <= 0) return;
+    switch (epi) {
+        case EPI_F32: dispatch_q8<EPI_F32>(g, s); break;
+        case EPI_GELU_F16: dispatch_q8<EPI_GELU_F16>(g, s); break;
+        case EPI_SWIGLU_F32: dispatch_q8<EPI_SWIGLU_F32>(g, s); break;
         default: break;
     }
 }
@@ -462,6 +618,203 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
     }
 }
 
+// ================================================================ Q8_0 GEMV
+// Decode projections with Q8_0 weights (int8 [N][K] + fp16 scales [N][K/32]).
+// Prologue: x rows (optionally RMS-normalised, optionally gathered from the
+// embedding) quantised per 32 values exactly like quantize_row_q8_0 into LDS
+// (int8 + fp32 scale); 8 threads own one block, amax by xor-shuffles.  Each
+// lane streams 16 int8 weights per sweep (NK sweeps of 1024); two lanes form a
+// block: v_dot4_i32_i8 x4, pair sum, then fma(d_w * d_x, sumi) (ggml order).
+template <int EPI, int CPW, int MR, int NK>
+__global__ __launch_bounds__(256) void gemv_q8_kernel(GemvArgs g) {
+    extern __shared__ __attribute__((aligned(16))) int8_t xq[];   // [MR][K] int8, then [MR][K/32] fp32 scales
+    __shared__ double red[4][MR];
+    constexpr int NR = EPI == EPI_SWIGLU_F32 ? 2 : 1;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    trace_mark(g.trace, 0);
+    const int K = g.K, nb = K / 32;
+    float *xd = (float *)(xq + MR * K);
+    const int ncg = (g.N + CPW - 1) / CPW;
+    int cg = blockIdx.x * 4 + wid;
+    const int8_t *Wq = (const int8_t *)g.W;
+    u32x4 wv[CPW][NR][NK];
+    uint16_t wdv[CPW][NR][NK];
+    auto wload = [&](int cgi) {
+#pragma unroll
+        for (int c = 0; c < CPW; c++)
+#pragma unroll
+            for (int r = 0; r < NR; r++)
+#pragma unroll
+                for (int t = 0; t < NK; t++) {
+                    const int o = min(cgi * CPW + c, g.N - 1), k = min(t * 1024 + lane * 16, K - 16);
+                    long wrow = o;
+                    if constexpr (EPI == EPI_SWIGLU_F32) wrow = 32L * (o >> 4) + (o & 15) + 16 * r;
+                    wv[c][r][t] = __builtin_nontemporal_load((const u32x4 *)(Wq + wrow * K + k));
+                    wdv[c][r][t] = g.Wd[wrow * nb + (k >> 5)];
+                }
+    };
+    if (cg < ncg) wload(cg);
+    // ---- prologue: each thread owns 4 consecutive elements per 1024-wide pass
+    constexpr int KP = NK;
+    {
+        float xr[MR][KP][4];
+        double ss[MR];
+#pragma unroll
+        for (int m = 0; m < MR; m++) {
+            ss[m] = 0.0;
+#pragma unroll
+            for (int p = 0; p < KP; p++) {
+                const int k = p * 1024 + tid * 4;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (m < g.M && k < K) {
+                    if (g.embd_ids) {
+                        const uint2 hv = *(const uint2 *)(g.embd + (long)g.embd_ids[m] * K + k);
+                        v = make_float4(u16_to_f(hv.x & 0xffff), u16_to_f(hv.x >> 16), u16_to_f(hv.y & 0xffff), u16_to_f(hv.y >> 16));
+                        if (g.x_store && blockIdx.x == 0) *(float4 *)(g.x_store + (long)m * g.ldx + k) = v;
+                    } else {
+                        v = *(const float4 *)(g.x + (long)m * g.ldx + k);
+                    }
+                }
+                xr[m][p][0] = v.x; xr[m][p][1] = v.y; xr[m][p][2] = v.z; xr[m][p][3] = v.w;
+                ss[m] += (double)(v.x * v.x);
+                ss[m] += (double)(v.y * v.y);
+                ss[m] += (double)(v.z * v.z);
+                ss[m] += (double)(v.w * v.w);
+            }
+        }
+        if (g.norm_w) {
+#pragma unroll
+            for (int m = 0; m < MR; m++) {
+                const double t = wave_sum_d(ss[m]);
+                if (lane == 0) red[wid][m] = t;
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int m = 0; m < MR; m++) {
+            float scale = 1.0f;
+            if (g.norm_w) {
+                const double tot = red[0][m] + red[1][m] + red[2][m] + red[3][m];
+                scale = 1.0f / sqrtf((float)(tot / K) + g.eps);
+            }
+#pragma unroll
+            for (int p = 0; p < KP; p++) {
+                const int k = p * 1024 + tid * 4;
+                float v[4], amax = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    v[e] = xr[m][p][e];
+                    if (g.norm_w && k < K) v[e] = fmul_rn(fmul_rn(v[e], scale), g.norm_w[k + e]);
+                    if (m >= g.M) v[e] = 0.0f;
+                    amax = fmaxf(amax, fabsf(v[e]));
+                }
+                // block of 32 = 8 consecutive lanes (quantize_row_q8_0)
+                amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+                amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+                amax = fmaxf(amax, __shfl_xor(amax, 4, 64));
+                if (k < K) {
+                    const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+                    uint32_t u = 0;
+#pragma unroll
+                    for (int e = 0; e < 4; e++) u |= (uint32_t)(uint8_t)(int8_t)__builtin_rintf(fmul_rn(v[e], id)) << (8 * e);
+                    *(uint32_t *)(xq + m * K + k) = u;
+                    if ((tid & 7) == 0) xd[m * nb + (k >> 5)] = u16_to_f(f_to_u16(amax / 127.f));
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    for (; cg < ncg; cg += gridDim.x * 4) {
+        const int col0 = cg * CPW;
+        float acc[CPW][NR][MR];
+#pragma unroll
+        for (int c = 0; c < CPW; c++)
+#pragma unroll
+            for (int r = 0; r < NR; r++)
+#pragma unroll
+                for (int m = 0; m < MR; m++) acc[c][r][m] = 0.0f;
+#pragma unroll
+        for (int t = 0; t < NK; t++) {
+            const int k = t * 1024 + lane * 16;
+            const bool ok = k < K;   // lane-uniform per pair: K % 32 == 0
+            const int kk = ok ? k : 0;
+#pragma unroll
+            for (int m = 0; m < MR; m++) {
+                const u32x4 xv = *(const u32x4 *)(xq + m * K + kk);
+                const float dx = xd[m * nb + (kk >> 5)];
+#pragma unroll
+                for (int c = 0; c < CPW; c++)
+#pragma unroll
+                    for (int r = 0; r < NR; r++) {
+                        int si = __builtin_amdgcn_sdot4((int)wv[c][r][t].x, (int)xv.x, 0, false);
+                        si = __builtin_amdgcn_sdot4((int)wv[c][r][t].y, (int)xv.y, si, false);
+                        si = __builtin_amdgcn_sdot4((int)wv[c][r][t].z, (int)xv.z, si, false);
+                        si = __builtin_amdgcn_sdot4((int)wv[c][r][t].w, (int)xv.w, si, false);
+                        si += __shfl_xor(si, 1, 64);   // the two halves of the 32-block
+                        const float dd = fmul_rn(u16_to_f(wdv[c][r][t]), dx);
+                        if (ok && !(lane & 1)) acc[c][r][m] = fmaf(dd, (float)si, acc[c][r][m]);
+                    }
+            }
+        }
+        const int nxt = cg + gridDim.x * 4;
+        if (nxt < ncg) wload(nxt);
+#pragma unroll
+        for (int c = 0; c < CPW; c++) {
+            const int o = col0 + c;
+#pragma unroll
+            for (int m = 0; m < MR; m++) {
+                float v[NR];
+#pragma unroll
+                for (int r = 0; r < NR; r++) v[r] = wave_sum(acc[c][r][m]);
+                if (o >= g.N || m >= g.M || lane != 0) continue;
+                if constexpr (EPI == EPI_SWIGLU_F32) {
+                    g.out_f32[(long)m * g.ldo + o] = silu_f(v[0]) * v[1];
+                } else {
+                    float y = v[0];
+                    if (g.bias) y = fadd_rn(y, g.bias[o]);
+                    if (g.res) y = fadd_rn(y, g.res[(long)m * g.ldr + o]);
+                    g.out_f32[(long)m * g.ldo + o] = y;
+                }
+            }
+        }
+    }
+    if (g.trace) { __syncthreads(); trace_mark(g.trace, 1); }
+}
+
+template <int EPI, int CPW, int MR, int NK>
+static void run_gemv_q8(const GemvArgs &g, hipStream_t s) {
+    const int per_block = 4 * CPW;
+    int blocks = (g.N + per_block - 1) / per_block;
+    if (blocks > 1024) blocks = 1024;
+    const size_t lds = (size_t)MR * g.K + (size_t)MR * (g.K / 32) * 4;
+    hipLaunchKernelGGL((gemv_q8_kernel<EPI, CPW, MR, NK>), dim3(blocks), dim3(256), lds, s, g);
+}
+
+template <int EPI, int CPW, int MR>
+static void gemv_q8_nk(const GemvArgs &g, hipStream_t s) {
+    const int nk = (g.K + 1023) / 1024;
+    if (nk <= 1) run_gemv_q8<EPI, CPW, MR, 1>(g, s);
+    else if (nk <= 2) run_gemv_q8<EPI, CPW, MR, 2>(g, s);
+    else if (nk <= 3) run_gemv_q8<EPI, CPW, MR, 3>(g, s);
+    else if (nk <= 4) run_gemv_q8<EPI, CPW, MR, 4>(g, s);
+    else run_gemv_q8<EPI, CPW, MR, 8>(g, s);
+}
+
+template <int EPI, int MR>
+static void gemv_q8_cpw(const GemvArgs &g, hipStream_t s) {
+    if (g.N >= 2048) gemv_q8_nk<EPI, 2, MR>(g, s);
+    else gemv_q8_nk<EPI, 1, MR>(g, s);
+}
+
+template <int EPI>
+static void gemv_q8_mr(const GemvArgs &g, hipStream_t s) {
+    if (g.M <= 1) gemv_q8_cpw<EPI, 1>(g, s);
+    else if (g.M <= 2) gemv_q8_cpw<EPI, 2>(g, s);
+    else if (g.M <= 4) gemv_q8_cpw<EPI, 4>(g, s);
+    else gemv_q8_cpw<EPI, 8>(g, s);
+}
+
 template <int EPI, int CPW, int MR, int NK>
 static void run_gemv(const GemvArgs &g, hipStream_t s) {
     const int per_block = 4 * CPW;
@@ -499,6 +852,14 @@ static void gemv_mr(const GemvArgs &g, hipStream_t s) {
 
 void launch_gemv(int epi, const GemvArgs &g, hipStream_t s) {
     if (g.M <= 0) return;
+    if (g.Wd) {   // Q8_0 weights: fp32 x only
+        switch (epi) {
+            case EPI_F32: gemv_q8_mr<EPI_F32>(g, s); break;
+            case EPI_SWIGLU_F32: gemv_q8_mr<EPI_SWIGLU_F32>(g, s); break;
+            default: break;
+        }
+        return;
+    }
     switch (epi) {
         case EPI_F32: gemv_mr<EPI_F32>(g, s); break;
         case EPI_SWIGLU_F16: gemv_mr<EPI_SWIGLU_F16>(g, s); break;

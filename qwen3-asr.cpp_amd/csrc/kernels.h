@@ -43,6 +43,7 @@ enum GemmEpi {
     EPI_SWIGLU_F16 = 2, // interleaved gate/up rows -> out_f16 = silu(g) * u
     EPI_ARGMAX = 3,     // optional out_f32 logits + per-row packed argmax (atomicMax)
     EPI_F16 = 4,        // out_f16 = acc (+bias)
+    EPI_SWIGLU_F32 = 5, // as EPI_SWIGLU_F16 with fp32 out_f32 (input of a Q8_0 layer)
 };
 enum GemmAMode {
     AM_DENSE = 0,       // A [M][lda] fp16 row-major
@@ -63,8 +64,24 @@ struct GemmArgs {
     const uint16_t *gelu;
     const float *pe; const int *pe_pos;   // conv_out: + PE[pos][n]
     unsigned long long *amax;             // [M] packed argmax keys
+    // Q8_0 operands (launch_gemm_q8): A int8 [M][lda] with fp32 block scales
+    // Ad [M][ldad] (one per 32 values), W int8 [N][ldw] with fp16 scales
+    // Wd [N][K/32] (ggml block_q8_0 split into quants and scales)
+    const int8_t *Aq; const float *Ad; int ldad;
+    const int8_t *Wq; const uint16_t *Wd;
 };
 void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s);
+// ggml_mul_mat with Q8_0 weights: exact int8 block dots (v_mfma_i32_16x16x32_i8
+// per 32-wide K block), each scaled by d_w * d_x into an fp32 accumulator.
+// Requires K % 128 == 0 (every Qwen3-ASR width) or K % 32 == 0 (slower tile).
+void launch_gemm_q8(int epi, const GemmArgs &g, hipStream_t s);
+// ggml quantize_row_q8_0 of fp32 (x32) or fp16 (x16) rows [M][K] (row stride
+// ldx elements) -> q int8 [M][K], d fp32 [M][K/32] (the fp16-rounded scale).
+// gather_C > 0: row element j = c*16 + h is read from column h*gather_C + c
+// (the conv_out feature order of src/audio_encoder.cpp:133-142 over the
+// [h][c] conv3 activations).
+void launch_quantize_q8(const float *x32, const uint16_t *x16, int ldx, int M, int K, int gather_C, int8_t *q, float *d,
+                        hipStream_t s);
 
 // skinny (decode) path: M <= 8 rows, weights streamed once from HBM.
 // x is fp32 [M][K]; if norm_w != nullptr the rows are RMS-normalised first
@@ -74,6 +91,8 @@ struct GemvArgs {
     const uint16_t *xh; int ldxh;        // alternative fp16 input (no norm)
     const float *norm_w; float eps;
     const uint16_t *W; int K, N, M;      // N = output columns (for SWIGLU: F outputs)
+    const uint16_t *Wd;                  // non-null: W is Q8_0 int8 [N][K] with fp16 scales Wd [N][K/32];
+                                         // x (fp32) is quantised per 32 in the prologue (ggml vec_dot_type Q8_0)
     const float *bias;
     const float *res; int ldr;
     float *out_f32; int ldo;
@@ -86,22 +105,24 @@ struct GemvArgs {
     // argmax keys into tok_out / hist[b][step+1], advances pos[b] and step,
     // and re-arms amax and done (both zero at rest)
     unsigned int *done; int32_t *tok_out; int32_t *hist; int hist_stride; int *step; int *pos;
-    unsigned long long *trace;           // dev trace: per block [start, end, -, -] (100 MHz clock) or null
+    unsigned long long *trace;           // dev trace: per block [start, end, ...] (8 slots, 100 MHz clock) or null
 };
 void launch_gemv(int epi, const GemvArgs &g, hipStream_t s);
 
 // ---------------------------------------------------------------- norms
-// LayerNorm (ggml_norm + mul + add) fp32 [M][D] -> fp16
-void launch_layernorm_f16(const float *x, int M, int D, const float *w, const float *b, float eps, uint16_t *y, hipStream_t s);
-// RMSNorm (ggml_rms_norm + mul) fp32 -> fp16; rows gathered by optional row_idx
+// LayerNorm (ggml_norm + mul + add) fp32 [M][D] -> fp16 y, or fp32 y32 when
+// non-null (input of a Q8_0 layer)
+void launch_layernorm_f16(const float *x, int M, int D, const float *w, const float *b, float eps, uint16_t *y, hipStream_t s,
+                          float *y32 = nullptr);
+// RMSNorm (ggml_rms_norm + mul) fp32 -> fp16 (or fp32 y32); rows gathered by optional row_idx
 void launch_rmsnorm_f16(const float *x, int ldx, const int *row_idx, int M, int D, const float *w, float eps,
-                        uint16_t *y, hipStream_t s);
+                        uint16_t *y, hipStream_t s, float *y32 = nullptr);
 
 // ---------------------------------------------------------------- attention
 // encoder: full bidirectional fp32 attention per clip segment, head_dim 64.
-// qkv fp32 [rows][3*D]; out fp16 [rows][D]
+// qkv fp32 [rows][3*D]; out fp16 [rows][D] (or fp32 out32 when non-null)
 void launch_enc_attention(const float *qkv, const int *seg_start, const int *seg_len, int n_seg, int max_len,
-                          int D, int H, uint16_t *out, hipStream_t s);
+                          int D, int H, uint16_t *out, hipStream_t s, float *out32 = nullptr);
 
 // decoder q/k RMSNorm + NEOX RoPE + fp16 KV-cache write (+ q fp16 out)
 struct QkvPostArgs {
@@ -124,6 +145,7 @@ struct PrefillAttnArgs {
     int n_head, n_kv_head, max_ctx;
     float scale;
     uint16_t *out;                       // [rows][n_head*128] fp16
+    float *out32;                        // non-null: fp32 output instead (input of a Q8_0 o-proj)
 };
 void launch_prefill_attention(const PrefillAttnArgs &a, hipStream_t s);
 
@@ -143,7 +165,8 @@ struct DecodeAttnArgs {
     float *part;                         // [B][n_kv_head][max_splits][2][132]: O[128], m, l, 0, 0
     unsigned int *counter;               // [B][n_kv_head] split arrivals, zero at rest
     uint16_t *out;                       // [B][n_head*128] fp16 attention output
-    unsigned long long *trace;           // dev trace: per block [start, K/V landed, published, end] or null
+    float *out32;                        // non-null: fp32 output instead (input of a Q8_0 o-proj)
+    unsigned long long *trace;           // dev trace: per block [start, K/V landed, partial ready, counted, end, burst landed]
 };
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
 int decode_split_len();

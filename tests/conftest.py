@@ -46,6 +46,22 @@ def tiny_oracle(tiny_gguf):
     return op.OracleModel(tiny_gguf)
 
 
+@pytest.fixture(scope="session")
+def tiny_q8_gguf(built, tmp_path_factory):
+    """Same seed as tiny_gguf, linear weights Q8_0 (convert_hf_to_gguf.py --type q8_0 policy)."""
+    import qasr
+    p = str(tmp_path_factory.mktemp("models") / "tiny-q8_0.gguf")
+    qasr.write_synthetic_gguf(p, "tiny", 42, 8)
+    return p
+
+
+@pytest.fixture(scope="session")
+def tiny_q8_oracle(tiny_q8_gguf):
+    import oracle_py as op
+    op.set_threads(min(8, os.cpu_count() or 1))
+    return op.OracleModel(tiny_q8_gguf)
+
+
 def gpu_available() -> bool:
     try:
         import qasr

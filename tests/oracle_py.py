@@ -119,7 +119,7 @@ class QoModel(C.Structure):
         ("enc_eps", C.c_float)] + [(n, C.c_int) for n in (
             "vocab", "hidden", "dec_layers", "n_head", "n_kv_head", "head_dim", "dec_ffn")] + [
         ("rms_eps", C.c_float), ("rope_theta", C.c_float)] + [(n, C.c_int) for n in (
-            "eos_id", "audio_start_id", "audio_end_id", "audio_pad_id")] + [(n, C.c_void_p) for n in (
+            "eos_id", "audio_start_id", "audio_end_id", "audio_pad_id", "wtype")] + [(n, C.c_void_p) for n in (
         "conv1_w", "conv2_w", "conv3_w", "conv_out_w", "conv1_b", "conv2_b", "conv3_b", "ln_post_w", "ln_post_b",
         "proj1_w", "proj2_w", "proj1_b", "proj2_b")] + [("enc", C.POINTER(EncLayer)), ("token_embd", C.c_void_p),
                                                         ("output_norm", C.c_void_p), ("dec", C.POINTER(DecLayer))]
@@ -216,11 +216,17 @@ class OracleModel:
         m.audio_end_id = int(kv.get("qwen3-asr.audio.end_token_id", 151670))
         m.audio_pad_id = int(kv.get("qwen3-asr.audio.pad_token_id", 151676))
         self._keep = []
+        # linear 2-D weights share one type: F16 (1) or Q8_0 (8); convs and
+        # token_embd stay F16 (scripts/convert_hf_to_gguf.py:230-308)
+        m.wtype = g.tensors["blk.0.attn_q.weight"][0]
+        self.wtype = m.wtype
 
-        def ptr(name):
+        def ptr(name, linear=False):
             ty, ne, arr = g.tensors[name]
-            if ty == 8:
-                raise ValueError("oracle takes F16 2-D weights")
+            if linear and ty != m.wtype:
+                raise ValueError(f"{name}: mixed linear weight types")
+            if not linear and ty == 8:
+                raise ValueError(f"{name}: Q8_0 only for linear weights")
             a = np.ascontiguousarray(arr)
             self._keep.append(a)
             return a.ctypes.data
@@ -228,10 +234,10 @@ class OracleModel:
         e = "audio.encoder."
         m.conv1_w, m.conv2_w, m.conv3_w = ptr(e + "conv1.weight"), ptr(e + "conv2.weight"), ptr(e + "conv3.weight")
         m.conv1_b, m.conv2_b, m.conv3_b = ptr(e + "conv1.bias"), ptr(e + "conv2.bias"), ptr(e + "conv3.bias")
-        m.conv_out_w = ptr(e + "conv_out.weight")
+        m.conv_out_w = ptr(e + "conv_out.weight", True)
         m.ln_post_w, m.ln_post_b = ptr(e + "ln_post.weight"), ptr(e + "ln_post.bias")
-        m.proj1_w, m.proj1_b = ptr(e + "proj1.weight"), ptr(e + "proj1.bias")
-        m.proj2_w, m.proj2_b = ptr(e + "proj2.weight"), ptr(e + "proj2.bias")
+        m.proj1_w, m.proj1_b = ptr(e + "proj1.weight", True), ptr(e + "proj1.bias")
+        m.proj2_w, m.proj2_b = ptr(e + "proj2.weight", True), ptr(e + "proj2.bias")
         self.enc = (EncLayer * m.enc_layers)()
         for i in range(m.enc_layers):
             p = f"{e}blk.{i}."
@@ -242,7 +248,7 @@ class OracleModel:
                          ("attn_norm_b", "attn_norm.bias"), ("ffn_up_w", "ffn_up.weight"), ("ffn_down_w", "ffn_down.weight"),
                          ("ffn_up_b", "ffn_up.bias"), ("ffn_down_b", "ffn_down.bias"), ("ffn_norm_w", "ffn_norm.weight"),
                          ("ffn_norm_b", "ffn_norm.bias")):
-                setattr(L, f, ptr(p + n))
+                setattr(L, f, ptr(p + n, f in ("attn_q_w", "attn_k_w", "attn_v_w", "attn_out_w", "ffn_up_w", "ffn_down_w")))
         m.enc = self.enc
         m.token_embd = ptr("token_embd.weight")
         m.output_norm = ptr("output_norm.weight")
@@ -252,7 +258,8 @@ class OracleModel:
             L = self.dec[i]
             for f in ("attn_norm", "attn_q_norm", "attn_k_norm", "ffn_norm", "attn_q", "attn_k", "attn_v", "attn_output",
                       "ffn_gate", "ffn_up", "ffn_down"):
-                setattr(L, f, ptr(p + f + ".weight"))
+                setattr(L, f, ptr(p + f + ".weight", f in ("attn_q", "attn_k", "attn_v", "attn_output", "ffn_gate", "ffn_up",
+                                                           "ffn_down")))
         m.dec = self.dec
         self.m = m
         self.vocab = m.vocab

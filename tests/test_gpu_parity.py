@@ -136,7 +136,7 @@ def test_decode_steps_teacher_forced(tiny, tiny_oracle):
     assert worst <= 1e-2, worst
 
 
-def _margin_aware_equal(gpu_toks, ora_toks, om, pcm, max_tokens):
+def _margin_aware_equal(gpu_toks, ora_toks, om, pcm, max_tokens, flags=0):
     """Token-exact unless the oracle's own top-1/top-2 margin at the first
     divergence is within the fp noise floor; returns (first_div, margin)."""
     n = min(len(gpu_toks), len(ora_toks))
@@ -148,7 +148,7 @@ def _margin_aware_equal(gpu_toks, ora_toks, om, pcm, max_tokens):
     mel = op.log_mel(pcm)
     feats = om.encode(mel)
     ids = om.prompt(feats.shape[0])
-    d = op.OracleDecoder(om, len(ids) + max_tokens + 1)
+    d = op.OracleDecoder(om, len(ids) + max_tokens + 1, flags)
     lo = d.forward(ids, 0, feats, 9)
     for i in range(first):
         lo = d.forward([ora_toks[i]], len(ids) + i)

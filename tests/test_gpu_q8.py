@@ -1,0 +1,139 @@
+"""GPU parity of the Q8_0 model path (BASELINE config 3 weights) against the
+oracle's Q8_0 restatement of ggml (activations quantised per 32 values,
+exact int8 block dots scaled by d_w * d_x).
+
+Tolerance: the F16 bounds (tests/test_gpu_parity.py header), widened to the
+Q8_0 computation's own noise floor where that is larger.  An activation whose
+fp32 value differs in its last bits (summation order) can round to the
+neighbouring int8 quantum (amax/127, ~1 % of the block), so the oracle itself
+moves by that much under a 1e-6 relative input perturbation; the floor is
+measured in the test (2.5x the oracle's self-sensitivity).
+
+The decoder comparisons use the oracle's QO_FA_V_F32 switch: ggml's CPU flash
+attention accumulates V.P in fp16, the HIP kernels in fp32; with
+F16 weights that difference is absorbed by the fp16 rounding of the o-proj
+input, with Q8_0 it reaches the activation quantiser, so the Q8_0 arithmetic
+is isolated by comparing against the fp32-accumulating oracle."""
+import numpy as np
+import pytest
+
+import oracle_py as op
+import qasr
+from test_gpu_parity import _margin_aware_equal, _stats
+
+pytestmark = pytest.mark.gpu
+FA32 = op.OracleModel.FA_V_F32
+
+SR = 16000
+
+
+@pytest.fixture(scope="module")
+def tq8(gpu, tiny_q8_gguf):
+    m = qasr.Model(tiny_q8_gguf)
+    c = qasr.Context(m, max_batch=12, max_ctx=640)
+    yield m, c
+    c.close()
+    m.close()
+
+
+@pytest.mark.parametrize("secs", [0.5, 2.37])
+def test_q8_encode_conv_matches_oracle(tq8, tiny_q8_oracle, secs):
+    _, c = tq8
+    mel = op.log_mel(qasr.synth_pcm(3000, int(secs * SR)))
+    g = c.encode_conv([mel])[0]
+    o = tiny_q8_oracle.encode_conv(mel)
+    mx, mean = _stats(g, o)
+    assert mx <= 2e-2 and mean <= 1e-3, (mx, mean)
+
+
+def _noise_floor(fn, mel):
+    """the oracle's own output change under a 1e-6 relative perturbation of mel"""
+    rng = np.random.default_rng(0)
+    mel2 = (mel * (1 + 1e-6 * rng.standard_normal(mel.shape))).astype(np.float32)
+    return _stats(fn(mel), fn(mel2))
+
+
+@pytest.mark.parametrize("secs", [1.0, 9.5])
+def test_q8_encode_matches_oracle(tq8, tiny_q8_oracle, secs):
+    _, c = tq8
+    mel = op.log_mel(qasr.synth_pcm(4000, int(secs * SR)))
+    g = c.encode([mel])[0]
+    o = tiny_q8_oracle.encode(mel)
+    mx, mean = _stats(g, o)
+    nmx, nmean = _noise_floor(tiny_q8_oracle.encode, mel)
+    assert mx <= max(2e-2, 2.5 * nmx) and mean <= max(1e-3, 2.5 * nmean), (mx, mean, nmx, nmean)
+
+
+def _perturb(a):
+    rng = np.random.default_rng(1)
+    return (a * (1 + 1e-6 * rng.standard_normal(a.shape))).astype(np.float32)
+
+
+def test_q8_prefill_and_decode_match_oracle(tq8, tiny_q8_oracle):
+    m, c = tq8
+    feats = tiny_q8_oracle.encode(op.log_mel(qasr.synth_pcm(6100, SR)))
+    ids, pos = m.build_prompt(feats.shape[0])
+    lg, _ = c.prefill([ids], [feats], [pos])
+    d = op.OracleDecoder(tiny_q8_oracle, 512, FA32)
+    dn = op.OracleDecoder(tiny_q8_oracle, 512, FA32)   # noise-floor twin: features perturbed by 1e-6
+    lo = d.forward(ids, 0, feats, pos)
+    ln = dn.forward(ids, 0, _perturb(feats), pos)
+    tol = max(1e-2 * float(np.abs(lo).max()), 2.5 * float(np.abs(lo - ln).max()))
+    assert np.abs(lg[0] - lo).max() <= tol, (np.abs(lg[0] - lo).max(), tol)
+    rng = np.random.default_rng(9)
+    n_past = len(ids)
+    errs, noise, scale = [], [], float(np.abs(lo).max())
+    for step in range(12):   # skinny GEMV path (B = 1)
+        tok = int(rng.integers(0, 151643))
+        lg, am = c.decode_step([tok], [n_past])
+        lo = d.forward([tok], n_past)
+        ln = dn.forward([tok], n_past)
+        errs.append(float(np.abs(lg[0] - lo).max()))
+        noise.append(float(np.abs(lo - ln).max()))
+        n_past += 1
+    # the noise floor is one sample of a heavy-tailed (rounding-flip) process:
+    # bound the worst step by 4x the worst twin step, the typical step by 1 %
+    assert max(errs) <= max(1e-2 * scale, 4 * max(noise)), (errs, noise)
+    assert float(np.median(errs)) <= 1e-2 * scale, (errs, scale)
+
+
+@pytest.mark.parametrize("path", ["f16", "q8"])
+def test_batched_decode_gemm_path(path, gpu, tiny_gguf, tiny_q8_gguf, tiny_oracle, tiny_q8_oracle):
+    """B = 10 > 8 takes the MFMA GEMM decode path: every row against the oracle
+    (Q8_0: with the noise-floor twin as above)."""
+    om = tiny_oracle if path == "f16" else tiny_q8_oracle
+    m = qasr.Model(tiny_gguf if path == "f16" else tiny_q8_gguf)
+    c = qasr.Context(m, max_batch=10, max_ctx=256)
+    try:
+        B = 10
+        feats = om.encode(op.log_mel(qasr.synth_pcm(6200, SR)))
+        ids, pos = m.build_prompt(feats.shape[0])
+        c.prefill([ids] * B, [feats] * B, [pos] * B, want_logits=False)
+        rng = np.random.default_rng(11)
+        n_past = len(ids)
+        toks = [int(t) for t in rng.integers(0, 151643, B)]
+        lg, _ = c.decode_step(toks, [n_past] * B)
+        for b in range(B):   # every row is one step after the same prefix: fork the oracle per row
+            fl = FA32 if path == "q8" else 0
+            db = op.OracleDecoder(om, 256, fl)
+            db.forward(ids, 0, feats, pos)
+            lo = db.forward([toks[b]], n_past)
+            dnb = op.OracleDecoder(om, 256, fl)
+            dnb.forward(ids, 0, _perturb(feats), pos)
+            ln = dnb.forward([toks[b]], n_past)
+            tol = 1e-2 * float(np.abs(lo).max())
+            if path == "q8":
+                tol = max(tol, 2.5 * float(np.abs(lo - ln).max()))
+            assert np.abs(lg[b] - lo).max() <= tol, (b, np.abs(lg[b] - lo).max(), tol)
+    finally:
+        c.close()
+        m.close()
+
+
+def test_q8_transcribe_matches_oracle(tq8, tiny_q8_oracle):
+    _, c = tq8
+    pcm = qasr.synth_pcm(7100, int(2.2 * SR))
+    r = c.transcribe([pcm], max_tokens=24, ignore_eos=True)
+    ora, _ = tiny_q8_oracle.transcribe(pcm, max_tokens=24, ignore_eos=True, flags=FA32)
+    assert len(r.tokens[0]) == 24
+    _margin_aware_equal(r.tokens[0], ora, tiny_q8_oracle, pcm, 24, flags=FA32)

@@ -8,7 +8,7 @@ NAMES = ["qkv_gemv", "attention", "oproj_gemv", "gateup_gemv", "down_gemv"]
 
 
 def main(path):
-    t = np.fromfile(path, dtype=np.uint64).reshape(6, 4096, 4).astype(np.int64)
+    t = np.fromfile(path, dtype=np.uint64).reshape(6, 4096, 8).astype(np.int64)
     live = [t[k][t[k][:, 0] > 0] for k in range(5)]
     t0 = min(int(x[:, 0].min()) for x in live if len(x))
     us = lambda v: (v - t0) / 100.0
@@ -18,11 +18,17 @@ def main(path):
             continue
         st = x[:, 0]
         if k == 1:
-            kv, pub, end = x[:, 1], x[:, 2], x[x[:, 3] > 0][:, 3]
+            kv, rdy, cnt = x[:, 1], x[:, 2], x[:, 3]
+            lastb = x[x[:, 4] > 0]
             print(f"{NAMES[k]:12s} blocks {len(x):4d} start {us(st.min()):7.2f}..{us(st.max()):7.2f}  "
-                  f"kv-landed med {np.median(kv - st) / 100:5.2f} max {us(kv.max()):7.2f}  "
-                  f"published max {us(pub.max()):7.2f}  combine-end max {us(end.max()):7.2f}")
-            e = end.max()
+                  f"kv-landed med +{np.median(kv - st) / 100:5.2f} max {us(kv.max()):7.2f}")
+            print(f"{'':12s} scores +{np.median(x[:, 6] - kv) / 100:5.2f} softmax +{np.median(x[:, 7] - x[:, 6]) / 100:5.2f} "
+                  f"pv +{np.median(rdy - x[:, 7]) / 100:5.2f}")
+            print(f"{'':12s} partial-ready med +{np.median(rdy - kv) / 100:5.2f} max {us(rdy.max()):7.2f}  "
+                  f"counted med +{np.median(cnt - rdy) / 100:5.2f} max {us(cnt.max()):7.2f}")
+            print(f"{'':12s} combiners {len(lastb)}: burst landed +{np.median(lastb[:, 5] - lastb[:, 3]) / 100:5.2f}  "
+                  f"end +{np.median(lastb[:, 4] - lastb[:, 5]) / 100:5.2f}  end max {us(lastb[:, 4].max()):7.2f}")
+            e = lastb[:, 4].max()
         else:
             en = x[:, 1]
             print(f"{NAMES[k]:12s} blocks {len(x):4d} start {us(st.min()):7.2f}..{us(st.max()):7.2f}  "
