@@ -84,6 +84,22 @@ def cpu_baseline(model_path: str, secs: float, tok_rate: float, threads: int):
     }
 
 
+def pmc_traffic(kernel_prefix: str):
+    """HBM bytes per launch of the roofline kernel from the newest committed
+    rocprofv3 PMC summary (profiles/<round>/summary.json, tools/job_prof.sh:
+    separate FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH x2 correction)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for k in d.get("kernels", []):
+            if k["name"].startswith(kernel_prefix) and "hbm_read_bytes" in k:
+                return k["hbm_read_bytes"] + k.get("hbm_write_bytes", 0), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -163,9 +179,11 @@ def main():
     if probe_n:
         avg_s = probe_ms / probe_n / 1e3
         achieved = probe_b / avg_s / 1e9
+        mr = next(r for r in (1, 2, 4, 8, args.batch) if r >= args.batch)   # gemv_mr row bucket
+        traffic, src = pmc_traffic(f"void qasr::gemv_kernel<3, 4, {mr},")
         out["roofline"] = {"kernel": "gemv_kernel<EPI_ARGMAX> (decode LM head, tied 151936x1024 f16 + fused argmax)",
                            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
                            "bytes_per_launch": probe_b, "avg_launch_us": round(avg_s * 1e6, 2), "launches": probe_n}
     if N == 1 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(model_path, args.cpu_sample_seconds, args.tok_rate, args.cpu_threads)
