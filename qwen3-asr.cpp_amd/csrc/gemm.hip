@@ -416,6 +416,12 @@ void launch_gemm_q8(int epi, const GemmArgs &g, hipStream_t s) {
     }
 }
 
+// QASR_GEMV1=0 keeps the multi-row kernel for one-row calls (A/B timing)
+static bool getenv_gemv1() {
+    static const int on = [] { const char *e = getenv("QASR_GEMV1"); return e && e[0] == '0' ? 0 : 1; }();
+    return on;
+}
+
 // ===================================================================== GEMV
 // One wave per CPW output columns; every lane streams 16-byte pieces of the
 // weight rows straight from HBM into VGPRs (no LDS round trip for W, cdna
@@ -852,6 +858,7 @@ static void gemv_mr(const GemvArgs &g, hipStream_t s) {
 
 void launch_gemv(int epi, const GemvArgs &g, hipStream_t s) {
     if (g.M <= 0) return;
+    if (getenv_gemv1() && launch_gemv1(epi, g, s)) return;
     if (g.Wd) {   // Q8_0 weights: fp32 x only
         switch (epi) {
             case EPI_F32: gemv_q8_mr<EPI_F32>(g, s); break;

@@ -108,6 +108,8 @@ struct GemvArgs {
     unsigned long long *trace;           // dev trace: per block [start, end, ...] (8 slots, 100 MHz clock) or null
 };
 void launch_gemv(int epi, const GemvArgs &g, hipStream_t s);
+// gemv.hip: one-row f16 fast path of launch_gemv (false = not covered)
+bool launch_gemv1(int epi, const GemvArgs &g, hipStream_t s);
 
 // ---------------------------------------------------------------- norms
 // LayerNorm (ggml_norm + mul + add) fp32 [M][D] -> fp16 y, or fp32 y32 when
