@@ -27,6 +27,13 @@
  *          + decode_greedy                src/qwen3_asr.cpp:216-303
  *   qasr_detokenize / qasr_tokenize
  *       <- TextDecoder::decode_tokens / tokenize src/text_decoder.cpp:1069-1103
+ *   qasr_align, qasr_align_json          (ForcedAligner model files)
+ *       <- ForcedAligner::align           src/forced_aligner.cpp:1636-1720
+ *          (encode_audio :591-924, forward_decoder :1088-1169,
+ *           extract_timestamp_classes :1280-1306)
+ *   qasr_align_tokenize <- ForcedAligner::tokenize_with_timestamps :1564-1609
+ *   qasr_model_load_korean_dict <- ForcedAligner::load_korean_dict :1543-1562
+ *   qasr_fix_timestamps <- ForcedAligner::fix_timestamp_classes :1183-1265
  *
  * Conventions (mirroring the reference's):
  *   - return value: 0 = OK, nonzero = error; message via qasr_last_error().
@@ -67,6 +74,8 @@ typedef struct {
     float rms_eps, rope_theta;
     int32_t eos_id, pad_id, audio_start_id, audio_end_id, audio_pad_id;
     int32_t weight_type; /* ggml type of the 2-D linear weights: 1 = F16, 8 = Q8_0 */
+    /* Qwen3-ForcedAligner files (src/forced_aligner.h:36-73): classify_num > 0 */
+    int32_t classify_num, timestamp_token_id;
 } qasr_hparams;
 
 typedef struct {
@@ -142,6 +151,33 @@ int qasr_transcribe_batch(qasr_ctx *c, const float *const *pcm, const int *n, in
  * extra graph launch per step while enabled; 0 disables and resets. */
 int qasr_set_probe(qasr_ctx *c, int kernel);
 int qasr_get_probe(qasr_ctx *c, double *total_ms, int64_t *launches, double *bytes_per_launch);
+
+/* ---- forced alignment (Qwen3-ForcedAligner model files) ------------------- */
+/* Device part of ForcedAligner::align for one clip: text_ids are the words'
+ * BPE ids, each word followed by two timestamp tokens (qasr_align_tokenize);
+ * classes[i] = argmax class of the i-th timestamp token (x 80 ms), *n_ts =
+ * their number (writes at most cap).  The context needs max_ctx >=
+ * qasr_align_prompt_len.  t: t_mel_ms, t_encode_ms, t_prefill_ms (= decode). */
+int qasr_align(qasr_ctx *c, const float *pcm, int n_samples, const int32_t *text_ids, int n_text,
+               int32_t *classes, int cap, int *n_ts, qasr_timings *t);
+/* words -> ids with timestamps; language "korean" uses the loaded dictionary
+ * (qasr_model_load_korean_dict), else whitespace words.  Returns the number of
+ * ids (writes at most cap); *n_words = number of words. */
+int qasr_align_tokenize(const qasr_model *m, const char *text, const char *language, int32_t *ids, int cap,
+                        int *n_words);
+/* the words of that split, joined by '\n' (words never contain whitespace);
+ * returns the length, writes at most cap-1 bytes + NUL */
+int qasr_align_words(const qasr_model *m, const char *text, const char *language, char *out, int cap);
+int qasr_model_load_korean_dict(qasr_model *m, const char *path);
+/* LIS repair of raw classes (in -> out, n values) */
+int qasr_fix_timestamps(const int32_t *classes, int n, int32_t *out);
+/* prompt length of an alignment: n_text + 2 + pads(mel frames of n_samples) */
+int qasr_align_prompt_len(int n_samples, int n_text);
+/* The whole alignment -> the CLI's JSON document {"words": [{"word", "start",
+ * "end"}...]} (src/main.cpp:257-276).  Returns its length (or minus the error
+ * code on failure); writes at most cap-1 bytes + NUL. */
+int qasr_align_json(qasr_ctx *c, const float *pcm, int n_samples, const char *text, const char *language,
+                    char *out, int cap, qasr_timings *t);
 
 /* ---- text (host) ---------------------------------------------------------- */
 /* UTF-8 text for ids (special <|..|> and [PAD..] tokens skipped); returns the

@@ -506,10 +506,14 @@ int qo_encode_conv(const qo_model *m, const float *mel, int T, float *out, int f
     const int C = m->conv_ch, D = m->d_model, NM = m->n_mel;
     int n_out = 0;
     for (int s = 0; s < T; s += 100) {
-        const int L = (T - s) < 100 ? (T - s) : 100;
-        float *x0 = (float *)malloc((size_t)NM * L * sizeof(float));
+        /* ASR: the chunk on its own length.  Aligner: one batched graph over
+         * chunks zero-padded to 100 frames (src/forced_aligner.cpp:633-698);
+         * the short last chunk keeps chunk_out_len(true length) frames (:725-733). */
+        const int Lv = (T - s) < 100 ? (T - s) : 100;
+        const int L = m->aligner ? 100 : Lv;
+        float *x0 = (float *)calloc((size_t)NM * L, sizeof(float));
         for (int mm = 0; mm < NM; mm++)
-            for (int f = 0; f < L; f++) x0[mm * L + f] = mel[(size_t)mm * T + s + f];
+            for (int f = 0; f < Lv; f++) x0[mm * L + f] = mel[(size_t)mm * T + s + f];
         int H1, W1, H2, W2, H3, W3;
         float *x1 = (float *)malloc((size_t)C * 64 * 50 * sizeof(float));
         conv2d_s2(x0, 1, NM, L, m->conv1_w, m->conv1_b, C, x1, &H1, &W1, flags);
@@ -523,11 +527,12 @@ int qo_encode_conv(const qo_model *m, const float *mel, int T, float *out, int f
             for (int c = 0; c < C; c++)
                 for (int h = 0; h < H3; h++) feat[(size_t)t * F + c * H3 + h] = x3[((size_t)c * H3 + h) * W3 + t];
         float *y = out + (size_t)n_out * D;
-        mul_mat_w(m, feat, W3, F, m->conv_out_w, D, NULL, y);
+        const int Wk = chunk_out_len(Lv);   /* = W3 for the ASR */
+        mul_mat_w(m, feat, Wk, F, m->conv_out_w, D, NULL, y);
         float *pe = (float *)malloc((size_t)W3 * D * sizeof(float));
         sinusoidal_pe(pe, W3, D);
-        for (int i = 0; i < W3 * D; i++) y[i] += pe[i];
-        n_out += W3;
+        for (int i = 0; i < Wk * D; i++) y[i] += pe[i];
+        n_out += Wk;
         free(pe); free(feat); free(x3); free(x2); free(x1); free(x0);
     }
     return n_out;
@@ -535,8 +540,22 @@ int qo_encode_conv(const qo_model *m, const float *mel, int T, float *out, int f
 
 /* ggml_mul_mat(K, Q) (fp32), ggml_soft_max_ext(scale), ggml_mul_mat(V, P):
  * full bidirectional attention, no mask (src/audio_encoder.cpp:466-486). */
-static void enc_attention(const float *qkv_q, const float *qkv_k, const float *qkv_v, int N,
-                          int D, int H, float *out) {
+static void enc_attention_seg(const float *qkv_q, const float *qkv_k, const float *qkv_v, int N,
+                              int D, int H, float *out);
+/* The aligner's block-diagonal mask (-inf outside windows of 13 * 800/100 =
+ * 104 frames, src/forced_aligner.cpp:737-766) makes each window attend only
+ * to itself: softmax over a window == the full softmax with the -inf mask. */
+static void enc_attention(const qo_model *m, const float *q, const float *k, const float *v, int N, int D, int H,
+                          float *out) {
+    const int win = m->aligner ? 104 : N;
+    for (int s0 = 0; s0 < N; s0 += win) {
+        const int n = (N - s0) < win ? (N - s0) : win;
+        enc_attention_seg(q + (size_t)s0 * D, k + (size_t)s0 * D, v + (size_t)s0 * D, n, D, H, out + (size_t)s0 * D);
+    }
+}
+
+static void enc_attention_seg(const float *qkv_q, const float *qkv_k, const float *qkv_v, int N,
+                              int D, int H, float *out) {
     const int hd = D / H;
     const float scale = 1.0f / sqrtf((float)hd);
     #pragma omp parallel for collapse(2) schedule(dynamic, 8) num_threads(g_threads)
@@ -596,7 +615,7 @@ int qo_encode(const qo_model *m, const float *mel, int T, float *out, int flags)
         mul_mat_w(m, cur, N, D, L->attn_q_w, D, L->attn_q_b, q);
         mul_mat_w(m, cur, N, D, L->attn_k_w, D, L->attn_k_b, k);
         mul_mat_w(m, cur, N, D, L->attn_v_w, D, L->attn_v_b, v);
-        enc_attention(q, k, v, N, D, H, att);
+        enc_attention(m, q, k, v, N, D, H, att);
         mul_mat_w(m, att, N, D, L->attn_out_w, D, L->attn_out_b, cur);
         for (size_t i = 0; i < (size_t)N * D; i++) x[i] = cur[i] + x[i];
         layer_norm(x, N, D, L->ffn_norm_w, L->ffn_norm_b, m->enc_eps, cur);
@@ -661,13 +680,17 @@ static void rope_neox(float *x, int n_dims, int pos, float base) {
 }
 
 /* src/text_decoder.cpp:392-581 (build_graph) + :588-684 (forward_with_audio) */
-int qo_dec_forward(qo_dec *dd, const int32_t *tokens, int n_tokens, const float *audio,
-                   int n_audio, int audio_start_pos, int n_past, float *logits) {
+/* decoder layer stack; returns the final hidden rows x[n_tokens][hidden]
+ * (caller frees).  al_fa: the aligner's attention (ggml_flash_attn_ext on
+ * K kept in fp32 -> Q in fp32 and fp32 dots, V cast to fp16,
+ * src/forced_aligner.cpp:1041-1046) instead of the fp16 KV cache. */
+static float *dec_stack(qo_dec *dd, const int32_t *tokens, int n_tokens, const float *audio,
+                        int n_audio, int audio_start_pos, int n_past, int al_fa) {
     const qo_model *m = dd->m;
     const int HS = m->hidden, NH = m->n_head, NKV = m->n_kv_head, HD = m->head_dim, FF = m->dec_ffn;
     const int QD = NH * HD, KD = NKV * HD;
     const int n_kv = n_past + n_tokens;
-    if (n_kv > dd->n_ctx || n_tokens <= 0) return -1;
+    if (n_kv > dd->n_ctx || n_tokens <= 0) return NULL;
     const float scale = 1.0f / sqrtf((float)HD);
 
     float *x = (float *)malloc((size_t)n_tokens * HS * sizeof(float));
@@ -727,12 +750,21 @@ int qo_dec_forward(qo_dec *dd, const int32_t *tokens, int n_tokens, const float 
                 uint16_t acc16[512];
                 for (int d = 0; d < HD; d++) { acc32[d] = 0.0f; acc16[d] = 0; }
                 const int limit = n_past + t;
+                uint16_t vtmp[512];
                 for (int ic = 0; ic <= limit; ic++) {
-                    float s = dot_f16(kc + (size_t)ic * KD + hk * HD, qh, HD);
+                    float s;
+                    const uint16_t *vr;
+                    if (al_fa) {   /* n_past = 0: key/value rows of this call */
+                        s = dot_f32(k + (size_t)ic * KD + hk * HD, q + (size_t)t * QD + h * HD, HD);
+                        for (int d = 0; d < HD; d++) vtmp[d] = qo_f32_to_f16(v[(size_t)ic * KD + hk * HD + d]);
+                        vr = vtmp;
+                    } else {
+                        s = dot_f16(kc + (size_t)ic * KD + hk * HD, qh, HD);
+                        vr = vc + (size_t)ic * KD + hk * HD;
+                    }
                     s = s * scale;
                     const float Mold = M;
                     float ms = 1.0f, vs = 1.0f;
-                    const uint16_t *vr = vc + (size_t)ic * KD + hk * HD;
                     if (s > M) {
                         M = s;
                         ms = expf(Mold - M);
@@ -758,13 +790,42 @@ int qo_dec_forward(qo_dec *dd, const int32_t *tokens, int n_tokens, const float 
         mul_mat_w(m, g, n_tokens, FF, L->ffn_down, HS, NULL, cur);
         for (size_t i = 0; i < (size_t)n_tokens * HS; i++) x[i] = cur[i] + x[i];
     }
-    /* last row only (text_decoder.cpp:564-566) -> RMSNorm -> tied LM head */
-    float *last = x + (size_t)(n_tokens - 1) * HS;
-    rms_norm(last, 1, HS, m->output_norm, m->rms_eps, cur);
+    free(u); free(g); free(att); free(v); free(k); free(q); free(cur);
+    return x;
+}
+
+/* src/text_decoder.cpp:392-581 (build_graph) + :588-684 (forward_with_audio):
+ * last row only (:564-566) -> RMSNorm -> tied LM head */
+int qo_dec_forward(qo_dec *dd, const int32_t *tokens, int n_tokens, const float *audio,
+                   int n_audio, int audio_start_pos, int n_past, float *logits) {
+    const qo_model *m = dd->m;
+    const int HS = m->hidden;
+    float *x = dec_stack(dd, tokens, n_tokens, audio, n_audio, audio_start_pos, n_past, 0);
+    if (!x) return -1;
+    float *cur = (float *)malloc((size_t)HS * sizeof(float));
+    rms_norm(x + (size_t)(n_tokens - 1) * HS, 1, HS, m->output_norm, m->rms_eps, cur);
     mul_mat_f16(cur, 1, HS, m->token_embd, m->vocab, NULL, logits);
-    free(u); free(g); free(att); free(v); free(k); free(q); free(cur); free(x);
+    free(cur); free(x);
     return 0;
 }
+
+int qo_align_forward(const qo_model *m, const int32_t *tokens, int n_tokens, const float *audio, int n_audio,
+                     int audio_start_pos, const int *rows, int n_rows, float *logits, int flags) {
+    if (!m->aligner || !m->classify_w) return -1;
+    const int HS = m->hidden;
+    qo_dec *dd = qo_dec_new(m, n_tokens, flags);
+    float *x = dec_stack(dd, tokens, n_tokens, audio, n_audio, audio_start_pos, 0, 1);
+    qo_dec_free(dd);
+    if (!x) return -1;
+    float *sel = (float *)malloc((size_t)(n_rows > 0 ? n_rows : 1) * HS * sizeof(float));
+    for (int i = 0; i < n_rows; i++)   /* output_norm, then the classify head (no bias) */
+        rms_norm(x + (size_t)rows[i] * HS, 1, HS, m->output_norm, m->rms_eps, sel + (size_t)i * HS);
+    if (n_rows > 0) mul_mat_f16(sel, n_rows, HS, m->classify_w, m->classify_num, NULL, logits);
+    free(sel); free(x);
+    return 0;
+}
+
+
 
 /* src/qwen3_asr.cpp:305-317 */
 int32_t qo_argmax(const float *logits, int n) {

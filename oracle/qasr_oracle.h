@@ -78,6 +78,14 @@ typedef struct {
     const uint16_t *token_embd;   /* [vocab][hidden] fp16, also the tied LM head */
     const float *output_norm;
     qo_dec_layer *dec;
+
+    /* Qwen3-ForcedAligner (src/forced_aligner.h:36-73): aligner != 0 selects
+     * its encoder (chunks zero-padded to 100 frames, 104-frame attention
+     * windows, src/forced_aligner.cpp:591-924) and decoder attention (K kept
+     * fp32, V cast to fp16, :1041-1046); classify_w = output.weight rows
+     * [classify_num][hidden] fp16 (:1073-1076). */
+    int aligner, classify_num;
+    const uint16_t *classify_w;
 } qo_model;
 
 #define QO_TYPE_F16  1
@@ -119,6 +127,13 @@ int     qo_dec_forward(qo_dec *d, const int32_t *tokens, int n_tokens,
                        int n_past, float *logits);
 /* src/qwen3_asr.cpp:305-317: argmax, strict '>' so the lowest index wins ties */
 int32_t qo_argmax(const float *logits, int n);
+
+/* ForcedAligner::forward_decoder (src/forced_aligner.cpp:926-1169): one causal
+ * prefill of tokens (positions 0..n-1, audio rows spliced at audio_start_pos),
+ * then for each of rows[0..n_rows): output RMSNorm -> classify head ->
+ * logits[i][classify_num].  Requires m->aligner. */
+int qo_align_forward(const qo_model *m, const int32_t *tokens, int n_tokens, const float *audio, int n_audio,
+                     int audio_start_pos, const int *rows, int n_rows, float *logits, int flags);
 
 /* src/qwen3_asr.cpp:151-214 (no system prompt): returns P, ids may be NULL */
 int  qo_build_prompt(const qo_model *m, int n_audio, int32_t *ids);

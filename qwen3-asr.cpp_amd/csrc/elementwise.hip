@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void conv1_kernel(const float *__restrict__ me
         for (int kw = 0; kw < 3; kw++) {
             const int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;   // ih: mel bin, iw: frame in chunk
             float v = 0.0f;
-            if (ih >= 0 && ih < 128 && iw >= 0 && iw < cd.L) v = mel[cd.mel_off + (long)ih * cd.T + iw];
+            if (ih >= 0 && ih < 128 && iw >= 0 && iw < cd.Lv) v = mel[cd.mel_off + (long)ih * cd.T + iw];
             in[kh * 3 + kw] = h2f(f2h(v));
         }
     for (int oc = lane; oc < C; oc += 64) {

@@ -59,6 +59,9 @@ struct qasr_model {
     uint16_t *conv1_w, *conv2_w, *conv3_w, *conv_out_w, *proj1_w, *proj2_w, *embd;
     uint16_t *conv_out_d = nullptr, *proj1_d = nullptr, *proj2_d = nullptr;
     bool q8 = false;   // linear weights are Q8_0 (scripts/convert_hf_to_gguf.py:230-308)
+    uint16_t *cls_w = nullptr;   // aligner: classify head [cls_rows][hidden] fp16, rows >= classify_num zero
+    int cls_rows = 0;
+    std::unordered_map<std::string, int> ko_dict;   // aligner: Korean word list (src/forced_aligner.cpp:1543-1562)
     float *conv1_b, *conv2_b, *conv3_b, *ln_post_w, *ln_post_b, *proj1_b, *proj2_b, *out_norm;
     std::vector<EncLayer> enc;
     std::vector<DecLayer> dec;
@@ -94,6 +97,7 @@ struct qasr_ctx {
     DevBuf chunks, rs1, rs2, rs3, pepos, act1, act2, act3;
     DevBuf ex, exh, eqkv, eatt, eff, feats, segs;
     DevBuf px, pxh, pqkv, pq, patt, pact, prow, plast, pids, pxl;
+    DevBuf ats, atx, aam;          // aligner: timestamp-row indices, their normed rows, argmax keys
     DevBuf q8a, q8d, x32;          // Q8_0 models: quantised activations (int8 + scales), fp32 layer inputs
     float *d_att32 = nullptr, *d_act32 = nullptr;   // Q8_0 decode: fp32 attention output / SwiGLU output
     int8_t *d_q8a = nullptr; float *d_q8d = nullptr, *d_x32 = nullptr;   // Q8_0 batched (B > 8) decode, graph-fixed
@@ -407,6 +411,20 @@ extern "C" int qasr_model_load(const char *path, int device, qasr_model **out) {
     one("audio.encoder.proj2.weight", D, H, &m->proj2_w, &m->proj2_d);
     copy_f32("audio.encoder.proj2.bias", H, &m->proj2_b);
     copy_f16("token_embd.weight", {H, V}, &m->embd);   // tied LM head (src/text_decoder.cpp:264-265), F16 in both file types
+    if (hp.aligner) {   // classify head: output.weight as [hidden][classify_num] (src/forced_aligner.cpp:274-277, 1073)
+        const gguf_tensor *t = T("output.weight");
+        const int NC = hp.classify_num;
+        if (!t || t->type != DT_F16 || t->ne.size() != 2 || t->ne[0] != H || t->ne[1] < NC || NC <= 0) {
+            if (err.empty()) err = "aligner: output.weight must be F16 [hidden][>= classify_num]";
+        } else {
+            m->cls_rows = (NC + 63) / 64 * 64;   // the GEMM tiles 64 columns; padded rows never win the argmax
+            const size_t bytes = (size_t)m->cls_rows * H * 2;
+            ups.push_back({"output.weight", bytes, (void **)&m->cls_w, [t, NC, H, bytes](uint8_t *o) {
+                               memset(o, 0, bytes);
+                               memcpy(o, t->data, (size_t)NC * H * 2);
+                           }});
+        }
+    }
     copy_f32("output_norm.weight", H, &m->out_norm);
     for (int l = 0; l < hp.dec_layers; l++) {
         const std::string p = "blk." + std::to_string(l) + ".";
@@ -474,7 +492,8 @@ extern "C" int qasr_model_hparams(const qasr_model *m, qasr_hparams *o) {
     const Hparams &h = m->hp;
     *o = qasr_hparams{h.enc_layers, h.d_model, h.enc_heads, h.enc_ffn, h.conv_ch, h.n_mel, h.enc_eps,
                       h.vocab, h.hidden, h.dec_layers, h.n_head, h.n_kv_head, h.head_dim, h.dec_ffn, h.rms_eps, h.rope_theta,
-                      h.eos_id, h.pad_id, h.audio_start_id, h.audio_end_id, h.audio_pad_id, h.weight_type};
+                      h.eos_id, h.pad_id, h.audio_start_id, h.audio_end_id, h.audio_pad_id, h.weight_type,
+                      h.aligner ? h.classify_num : 0, h.timestamp_id};
     return 0;
 }
 
@@ -553,6 +572,9 @@ extern "C" void qasr_ctx_free(qasr_ctx *c) { delete c; }
 extern "C" int qasr_mel_frames(int n) { return mel_frames(n); }
 extern "C" int qasr_encoder_frames(int T) { return encoder_frames(T); }
 extern "C" int qasr_prompt_len(int n) { return n + 15; }
+extern "C" int qasr_align_prompt_len(int n_samples, int n_text) {
+    return n_text + 2 + feat_extract_output_lengths(mel_frames(n_samples));
+}
 extern "C" int qasr_build_prompt(const qasr_model *m, int n_audio, int32_t *ids, int *audio_pos) {
     Hparams hp = m ? m->hp : Hparams();
     std::vector<int32_t> p = build_prompt(hp, n_audio, {}, audio_pos);
@@ -606,20 +628,28 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     std::vector<int> s1, s2, s3, pepos;
     int r1 = 0, r2 = 0, r3 = 0, er = 0;
     Nb.assign(B, 0);
+    // ASR: each chunk on its own length (src/audio_encoder.cpp:331-409).  Aligner:
+    // every chunk zero-padded to 100 frames, the valid frames of the (short)
+    // last one kept (src/forced_aligner.cpp:601-735); one clip per call, so
+    // the valid conv_out rows are the leading rows.
+    const bool al = hp.aligner;
+    if (al && B != 1) return fail(QASR_ERR_ARG, "aligner encoder: one clip per call");
     for (int b = 0; b < B; b++) {
         for (int s = 0; s < T[b]; s += 100) {
             ChunkDesc d;
             d.mel_off = mel_off[b] + s;
             d.T = T[b];
-            d.L = std::min(100, T[b] - s);
+            d.Lv = std::min(100, T[b] - s);
+            d.L = al ? 100 : d.Lv;
             d.W1 = (d.L - 1) / 2 + 1;
             d.W2 = (d.W1 - 1) / 2 + 1;
             d.W3 = (d.W2 - 1) / 2 + 1;
             d.row1 = r1; d.row2 = r2; d.row3 = r3; d.enc_row = er;
             s1.push_back(r1); s2.push_back(r2); s3.push_back(r3);
-            r1 += 64 * d.W1; r2 += 32 * d.W2; r3 += 16 * d.W3; er += d.W3;
-            for (int w = 0; w < d.W3; w++) pepos.push_back(w);
-            Nb[b] += d.W3;
+            const int valid = chunk_out_len(d.Lv);
+            r1 += 64 * d.W1; r2 += 32 * d.W2; r3 += 16 * d.W3; er += valid;
+            for (int w = 0; w < valid; w++) pepos.push_back(w);
+            Nb[b] += valid;
             ch.push_back(d);
         }
     }
@@ -665,9 +695,23 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     HIPCHK(hipGetLastError());
     if (conv_only) return 0;
 
-    std::vector<int> segs(2 * B);
+    // attention segments: whole clips (ASR: full attention, src/audio_encoder.cpp:466-486)
+    // or the aligner's block-diagonal windows of 13 * (800 / 100) = 104 frames
+    // (src/forced_aligner.cpp:737-766)
+    std::vector<int> sst, sln;
     int acc = 0, maxn = 0;
-    for (int b = 0; b < B; b++) { segs[b] = acc; segs[B + b] = Nb[b]; acc += Nb[b]; maxn = std::max(maxn, Nb[b]); }
+    for (int b = 0; b < B; b++) {
+        const int win = al ? 104 : std::max(Nb[b], 1);
+        for (int o = 0; o < Nb[b]; o += win) {
+            sst.push_back(acc + o);
+            sln.push_back(std::min(win, Nb[b] - o));
+            maxn = std::max(maxn, sln.back());
+        }
+        acc += Nb[b];
+    }
+    const int NS = (int)sst.size();
+    std::vector<int> segs(sst);
+    segs.insert(segs.end(), sln.begin(), sln.end());
     if ((rc = upload(c, c->segs, segs))) return rc;
     float *x = c->ex.as<float>();
     uint16_t *xh = c->exh.as<uint16_t>();
@@ -685,7 +729,7 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
         GemmArgs q{};
         q.M = N; q.N = 3 * D; q.K = D; q.bias = L.bqkv; q.out_f32 = c->eqkv.as<float>(); q.ldo = 3 * D;
         linear(EPI_F32, q, x32, xh, D, L.wqkv, L.wqkv_d);
-        launch_enc_attention(c->eqkv.as<float>(), c->segs.as<int>(), c->segs.as<int>() + B, B, maxn, D, hp.enc_heads,
+        launch_enc_attention(c->eqkv.as<float>(), c->segs.as<int>(), c->segs.as<int>() + NS, NS, maxn, D, hp.enc_heads,
                              c->eatt.as<uint16_t>(), s, x32);
         GemmArgs op{};
         op.M = N; op.N = D; op.K = D; op.bias = L.bo; op.res = x; op.ldr = D; op.out_f32 = x; op.ldo = D;
@@ -709,10 +753,12 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     return 0;
 }
 
-// decoder layer stack over `rows` rows of x (prefill).  Row tables live in
-// c->prow: [row_seq | row_pos | row_audio] (3*rows ints).
-static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::vector<int> &P, const float *d_feats,
-                       const std::vector<int> &audio_pos, const std::vector<int> &N, bool want_logits) {
+// embedding gather + audio splice + decoder layer stack over the prompt rows of
+// B sequences (positions 0..P_b-1, KV cache of sequence b reset); leaves the
+// final hidden rows in c->px.  Row tables live in c->prow:
+// [row_seq | row_pos | row_audio] (3*rows ints) + [seq_row0 | seq_len | seq_slot].
+static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const std::vector<int> &P, const float *d_feats,
+                          const std::vector<int> &audio_pos, const std::vector<int> &N) {
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
     const int B = (int)P.size(), H = hp.hidden, QD = hp.n_head * 128, KD = hp.n_kv_head * 128, F = hp.dec_ffn;
@@ -796,7 +842,20 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
         if (q8) gemm_q8(c, EPI_F32, dn, x32, nullptr, F, 0, L.wd, L.wd_d, s);
         else { dn.A = c->pact.as<uint16_t>(); dn.lda = F; dn.W = L.wd; dn.ldw = F; launch_gemm(AM_DENSE, EPI_F32, dn, s); }
     }
-    // last row of each sequence -> RMSNorm -> tied LM head + argmax (src/text_decoder.cpp:564-572)
+    return 0;
+}
+
+// prefill (src/text_decoder.cpp:588-684): layers, then the LAST row of each
+// sequence -> RMSNorm -> tied LM head + argmax (:564-572)
+static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::vector<int> &P, const float *d_feats,
+                       const std::vector<int> &audio_pos, const std::vector<int> &N, bool want_logits) {
+    int rc;
+    if ((rc = prefill_layers(c, ids, P, d_feats, audio_pos, N))) return rc;
+    qasr_model *m = c->m;
+    const Hparams &hp = m->hp;
+    const int B = (int)P.size(), H = hp.hidden;
+    hipStream_t s = c->st;
+    float *x = c->px.as<float>();
     uint16_t *xl = c->d_xh;
     launch_rmsnorm_f16(x, H, c->plast.as<int>(), B, H, m->out_norm, hp.rms_eps, xl, s);
     launch_fill_u64(c->d_amax, B, 0ull, s);
@@ -1284,6 +1343,182 @@ extern "C" int qasr_tokenize(const qasr_model *m, const char *text, int32_t *ids
     std::vector<int32_t> v = m->tok.encode(text);
     if (ids) for (int i = 0; i < (int)v.size() && i < cap; i++) ids[i] = v[i];
     return (int)v.size();
+}
+
+// ------------------------------------------------------------ forced aligner
+// ForcedAligner::align (src/forced_aligner.cpp:1636-1720), device part: mel ->
+// aligner encoder (padded chunks, 104-frame windows) -> <|audio_start|> pad x n
+// <|audio_end|> text prompt (n from HF _get_feat_extract_output_lengths, the
+// encoder rows spliced from index 1) -> one causal prefill -> at every
+// timestamp-token row: RMSNorm -> classify head -> argmax (strict '>', :1280-1306).
+static int align_classes(qasr_ctx *c, const float *pcm, int n, const std::vector<int32_t> &text_ids,
+                         std::vector<int32_t> &classes, qasr_timings *t) {
+    qasr_model *m = c->m;
+    const Hparams &hp = m->hp;
+    if (!hp.aligner || !m->cls_w) return fail(QASR_ERR_STATE, "not a ForcedAligner model");
+    HIPCHK(hipSetDevice(m->device));
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->pin_used = 0;
+    hipStream_t s = c->st;
+    int rc;
+    if ((rc = ensure(c, c->pcm, (size_t)std::max(n, 1) * 4))) return rc;
+    HIPCHK(hipMemcpyAsync(c->pcm.p, pcm, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(c->ev[0], s));
+    std::vector<long> mo;
+    std::vector<int> T, Nb;
+    if ((rc = run_mel(c, {0L}, {n}, mo, T))) return rc;
+    HIPCHK(hipEventRecord(c->ev[1], s));
+    if ((rc = run_encoder(c, c->mel.as<float>(), mo, T, false, Nb))) return rc;
+    HIPCHK(hipEventRecord(c->ev[2], s));
+    const std::vector<int32_t> ids = build_align_tokens(hp, text_ids, feat_extract_output_lengths(T[0]));
+    const int P = (int)ids.size();
+    if (P > c->max_ctx) return fail(QASR_ERR_ARG, "Context length exceeded (aligner prompt > max_ctx)");
+    std::vector<int> rows;
+    for (int i = 0; i < P; i++) if (ids[i] == hp.timestamp_id) rows.push_back(i);
+    if ((rc = prefill_layers(c, ids, {P}, c->feats.as<float>(), {1}, {Nb[0]}))) return rc;
+    const int NT = (int)rows.size(), H = hp.hidden;
+    std::vector<unsigned long long> keys(NT);
+    if (NT > 0) {
+        if ((rc = upload(c, c->ats, rows)) || (rc = ensure(c, c->atx, (size_t)NT * H * 2)) || (rc = ensure(c, c->aam, (size_t)NT * 8)))
+            return rc;
+        HIPCHK(hipMemsetAsync(c->aam.p, 0, (size_t)NT * 8, s));
+        launch_rmsnorm_f16(c->px.as<float>(), H, c->ats.as<int>(), NT, H, m->out_norm, hp.rms_eps, c->atx.as<uint16_t>(), s);
+        GemmArgs g{};
+        g.A = c->atx.as<uint16_t>(); g.lda = H; g.W = m->cls_w; g.ldw = H; g.M = NT; g.N = m->cls_rows; g.K = H;
+        g.amax = c->aam.as<unsigned long long>(); g.n_valid = hp.classify_num;
+        launch_gemm(AM_DENSE, EPI_ARGMAX, g, s);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(keys.data(), c->aam.p, (size_t)NT * 8, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipEventRecord(c->ev[3], s));
+    HIPCHK(hipEventSynchronize(c->ev[3]));
+    classes.resize(NT);
+    for (int i = 0; i < NT; i++) classes[i] = (int32_t)(0xffffffffu - (uint32_t)(keys[i] & 0xffffffffu));
+    if (t) {
+        float a = 0, b = 0, d = 0, tot = 0;
+        HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+        HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+        HIPCHK(hipEventElapsedTime(&d, c->ev[2], c->ev[3]));
+        HIPCHK(hipEventElapsedTime(&tot, c->ev[0], c->ev[3]));
+        *t = qasr_timings{a, b, d, 0.0, tot, 0};
+    }
+    return 0;
+}
+
+extern "C" int qasr_align(qasr_ctx *c, const float *pcm, int n, const int32_t *text_ids, int n_text, int32_t *classes,
+                          int cap, int *n_ts, qasr_timings *t) {
+    if (!c || !pcm || n <= 0 || n_text < 0 || (n_text && !text_ids) || !n_ts) return fail(QASR_ERR_ARG, "bad arguments");
+    std::vector<int32_t> cls;
+    int rc = align_classes(c, pcm, n, std::vector<int32_t>(text_ids, text_ids + n_text), cls, t);
+    if (rc) return rc;
+    *n_ts = (int)cls.size();
+    if (classes) for (int i = 0; i < (int)cls.size() && i < cap; i++) classes[i] = cls[i];
+    return 0;
+}
+
+// ForcedAligner::tokenize_with_timestamps (src/forced_aligner.cpp:1564-1609)
+static std::vector<int32_t> align_tokens(const qasr_model *m, const std::string &text, const std::string &lang,
+                                         std::vector<std::string> &words) {
+    words = (lang == "korean" && !m->ko_dict.empty()) ? tokenize_korean(text, m->ko_dict) : split_words(text);
+    std::vector<int32_t> ids;
+    for (const std::string &w : words) {
+        std::vector<int32_t> t = m->tok.encode_word(w);
+        ids.insert(ids.end(), t.begin(), t.end());
+        ids.push_back(m->hp.timestamp_id);
+        ids.push_back(m->hp.timestamp_id);
+    }
+    return ids;
+}
+
+extern "C" int qasr_align_tokenize(const qasr_model *m, const char *text, const char *language, int32_t *ids, int cap,
+                                   int *n_words) {
+    if (!m || !text) return fail(QASR_ERR_ARG, "bad arguments");
+    std::vector<std::string> words;
+    std::vector<int32_t> v = align_tokens(m, text, language ? language : "", words);
+    if (ids) for (int i = 0; i < (int)v.size() && i < cap; i++) ids[i] = v[i];
+    if (n_words) *n_words = (int)words.size();
+    return (int)v.size();
+}
+
+extern "C" int qasr_align_words(const qasr_model *m, const char *text, const char *language, char *out, int cap) {
+    if (!m || !text) return -fail(QASR_ERR_ARG, "bad arguments");
+    std::vector<std::string> words;
+    align_tokens(m, text, language ? language : "", words);
+    std::string j;
+    for (size_t i = 0; i < words.size(); i++) { if (i) j += '\n'; j += words[i]; }
+    if (out && cap > 0) {
+        const size_t k = std::min(j.size(), (size_t)cap - 1);
+        memcpy(out, j.data(), k);
+        out[k] = 0;
+    }
+    return (int)j.size();
+}
+
+extern "C" int qasr_model_load_korean_dict(qasr_model *m, const char *path) {
+    if (!m || !path) return fail(QASR_ERR_ARG, "bad arguments");
+    if (!load_korean_dict(path, m->ko_dict)) return fail(QASR_ERR_IO, std::string("cannot read Korean dictionary: ") + path);
+    return 0;
+}
+
+extern "C" int qasr_fix_timestamps(const int32_t *classes, int n, int32_t *out) {
+    if (n < 0 || (n && (!classes || !out))) return fail(QASR_ERR_ARG, "bad arguments");
+    std::vector<int32_t> r = fix_timestamp_classes(std::vector<int32_t>(classes, classes + n));
+    if (n) memcpy(out, r.data(), (size_t)n * 4);
+    return 0;
+}
+
+static std::string json_escape(const std::string &s) {   // src/main.cpp:230-254
+    std::string r;
+    for (char ch : s) {
+        switch (ch) {
+            case '"': r += "\\\""; break;
+            case '\\': r += "\\\\"; break;
+            case '\b': r += "\\b"; break;
+            case '\f': r += "\\f"; break;
+            case '\n': r += "\\n"; break;
+            case '\r': r += "\\r"; break;
+            case '\t': r += "\\t"; break;
+            default:
+                if ((unsigned char)ch < 0x20) { char b[8]; snprintf(b, sizeof b, "\\u%04x", (unsigned char)ch); r += b; }
+                else r += ch;
+        }
+    }
+    return r;
+}
+
+// whole alignment -> the CLI's JSON document (src/main.cpp:257-276); returns
+// the JSON length (excluding NUL) or minus the error code; writes at most
+// cap-1 bytes + NUL
+extern "C" int qasr_align_json(qasr_ctx *c, const float *pcm, int n, const char *text, const char *language, char *out,
+                               int cap, qasr_timings *t) {
+    if (!c || !pcm || n <= 0 || !text) return -fail(QASR_ERR_ARG, "bad arguments");
+    const qasr_model *m = c->m;
+    std::vector<std::string> words;
+    const std::vector<int32_t> ids = align_tokens(m, text, language ? language : "", words);
+    std::vector<int32_t> cls;
+    int rc = align_classes(c, pcm, n, ids, cls, t);
+    if (rc) return -rc;
+    const std::vector<int32_t> fixed = fix_timestamp_classes(cls);
+    const float dur = (float)n / 16000.0f, seg = m->hp.ts_segment_ms / 1000.0f;
+    std::vector<float> ts(fixed.size());
+    for (size_t i = 0; i < fixed.size(); i++) ts[i] = std::min(fixed[i] * seg, dur);
+    std::string js = "{\n  \"words\": [\n";
+    for (size_t i = 0; i < words.size(); i++) {
+        const float st = 2 * i < ts.size() ? ts[2 * i] : 0.0f, en = 2 * i + 1 < ts.size() ? ts[2 * i + 1] : dur;
+        char b[64];
+        js += "    {\"word\": \"" + json_escape(words[i]) + "\", ";
+        snprintf(b, sizeof b, "\"start\": %.3f, \"end\": %.3f}", st, en);
+        js += b;
+        if (i + 1 < words.size()) js += ",";
+        js += "\n";
+    }
+    js += "  ]\n}";
+    if (out && cap > 0) {
+        const size_t k = std::min(js.size(), (size_t)cap - 1);
+        memcpy(out, js.data(), k);
+        out[k] = 0;
+    }
+    return (int)js.size();
 }
 
 // --------------------------------------------------------- host utilities

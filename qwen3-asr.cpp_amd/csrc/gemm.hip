@@ -71,7 +71,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs &g, floatx4 (&acc)[
                     const int col = cbase + j * 16;
                     const float v = acc[i][j][r];
                     if (row < M && g.out_f32) g.out_f32[(long)row * g.ldo + col] = v;
-                    const unsigned long long key = argmax_key(v, col);
+                    const unsigned long long key = (g.n_valid == 0 || col < g.n_valid) ? argmax_key(v, col) : 0ull;
                     best = key > best ? key : best;
                 }
 #pragma unroll

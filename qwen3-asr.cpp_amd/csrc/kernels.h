@@ -26,7 +26,9 @@ int mel_frames_per_block();
 struct ChunkDesc {
     long mel_off;   // element offset of mel[clip][0][chunk_start]
     int T;          // mel row stride (frames of the clip)
-    int L;          // chunk frames (last chunk of a clip may be short; never padded)
+    int L;          // chunk frames: ASR = the chunk's own length (last one short, not padded);
+                    // aligner = 100 always, zero-padded (src/forced_aligner.cpp:633-698)
+    int Lv;         // mel frames read (frames past Lv are zeros); ASR: Lv = L
     int W1, W2, W3; // conv output widths
     int row1, row2, row3;   // first row of this chunk in the conv1/2/3 output tables
     int enc_row;    // first encoder frame (= row3 / 16)
@@ -64,6 +66,7 @@ struct GemmArgs {
     const uint16_t *gelu;
     const float *pe; const int *pe_pos;   // conv_out: + PE[pos][n]
     unsigned long long *amax;             // [M] packed argmax keys
+    int n_valid;                          // EPI_ARGMAX: columns >= n_valid (zero-padded weight rows) never win; 0 = N
     // Q8_0 operands (launch_gemm_q8): A int8 [M][lda] with fp32 block scales
     // Ad [M][ldad] (one per 32 values), W int8 [N][ldw] with fp16 scales
     // Wd [N][K/32] (ggml block_q8_0 split into quants and scales)

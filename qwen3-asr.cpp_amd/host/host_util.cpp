@@ -82,6 +82,21 @@ Hparams read_hparams(const GGUFFile &f) {
     hp.audio_pad_id = (int)f.get_int("qwen3-asr.audio.pad_token_id", 151676);
     const gguf_tensor *t = f.tensor("blk.0.attn_q.weight");
     hp.weight_type = t ? (int)t->type : 1;
+    // ForcedAligner (src/forced_aligner.cpp:136-175): its loader reads the
+    // converter's keys only, with its own defaults (24 x 1024 encoder, vocab 152064)
+    const gguf_tensor *head = f.tensor("output.weight");
+    if (f.find("qwen3-asr.classify_num") || head) {
+        hp.aligner = true;
+        hp.enc_layers = (int)f.get_int("qwen3-asr.audio.encoder.layer_count", 24);
+        hp.d_model = (int)f.get_int("qwen3-asr.audio.encoder.embedding_length", 1024);
+        hp.enc_heads = (int)f.get_int("qwen3-asr.audio.encoder.attention.head_count", 16);
+        hp.enc_ffn = (int)f.get_int("qwen3-asr.audio.encoder.feed_forward_length", 4096);
+        hp.n_mel = (int)f.get_int("qwen3-asr.audio.num_mel_bins", 128);
+        hp.conv_ch = (int)f.get_int("qwen3-asr.audio.conv_channels", 480);
+        hp.vocab = (int)f.get_int("qwen3-asr.vocab_size", 152064);
+        hp.classify_num = (int)f.get_int("qwen3-asr.classify_num", 5000);
+        hp.timestamp_id = (int)f.get_int("qwen3-asr.timestamp_token_id", 151705);
+    }
     return hp;
 }
 
@@ -390,6 +405,164 @@ std::vector<int32_t> Tokenizer::encode(const std::string &text) const {
     return ids;
 }
 
+std::vector<int32_t> Tokenizer::encode_word(const std::string &word) const {
+    std::vector<int32_t> ids;
+    const auto &b2u = bytes_to_unicode();
+    std::string bpe;
+    for (unsigned char c : word) bpe += b2u[c];
+    std::vector<std::string> sym = utf8_chars(bpe);
+    while (sym.size() > 1) {
+        int best = INT_MAX;
+        size_t pos = 0;
+        for (size_t i = 0; i + 1 < sym.size(); i++) {
+            auto it = ranks_.find(sym[i] + " " + sym[i + 1]);
+            if (it != ranks_.end() && it->second < best) { best = it->second; pos = i; }
+        }
+        if (best == INT_MAX) break;
+        sym[pos] += sym[pos + 1];
+        sym.erase(sym.begin() + (long)pos + 1);
+    }
+    for (auto &sw : sym) {
+        auto it = tok2id_.find(sw);
+        if (it != tok2id_.end()) ids.push_back(it->second);
+        else fprintf(stderr, "BPE tokenizer: unknown subword token '%s'\n", sw.c_str());
+    }
+    return ids;
+}
+
+// ------------------------------------------------------- forced aligner
+static bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+std::vector<std::string> split_words(const std::string &text) {
+    std::vector<std::string> out;
+    size_t i = 0;
+    while (i < text.size()) {
+        while (i < text.size() && is_ws(text[i])) ++i;
+        if (i >= text.size()) break;
+        const size_t st = i;
+        while (i < text.size() && !is_ws(text[i])) ++i;
+        out.push_back(text.substr(st, i - st));
+    }
+    return out;
+}
+
+static size_t u8len(unsigned char c) {
+    if ((c & 0x80) == 0) return 1;
+    if ((c & 0xE0) == 0xC0) return 2;
+    if ((c & 0xF0) == 0xE0) return 3;
+    if ((c & 0xF8) == 0xF0) return 4;
+    return 1;
+}
+
+// first n characters / the rest, by UTF-8 lead bytes (clamped at the end)
+static void u8split(const std::string &s, size_t n, std::string &left, std::string &right) {
+    size_t b = 0;
+    for (size_t c = 0; c < n && b < s.size(); c++) b += u8len((unsigned char)s[b]);
+    if (b > s.size()) b = s.size();
+    left = s.substr(0, b);
+    right = s.substr(b);
+}
+
+std::vector<std::string> tokenize_korean(const std::string &text, const std::unordered_map<std::string, int> &dict) {
+    std::vector<std::string> out;
+    for (const std::string &w : split_words(text)) {
+        size_t len = 0;
+        for (size_t i = 0; i < w.size(); i += u8len((unsigned char)w[i])) len++;
+        if (len <= 2) { out.push_back(w); continue; }
+        // the longest dictionary prefix of >= 2 characters wins; with none, the
+        // whole word (score ties go to the longer left part)
+        float best = -1e9f;
+        size_t best_e = 0;
+        std::string bl, br;
+        for (size_t e = 2; e <= len; e++) {
+            std::string l, r;
+            u8split(w, e, l, r);
+            const float sc = dict.count(l) ? 1.0f : 0.0f;
+            if (sc > best || (sc == best && e > best_e)) { best = sc; best_e = e; bl = l; br = r; }
+        }
+        out.push_back(bl);
+        if (!br.empty()) out.push_back(br);
+    }
+    return out;
+}
+
+bool load_korean_dict(const std::string &path, std::unordered_map<std::string, int> &dict) {
+    FILE *fp = fopen(path.c_str(), "rb");
+    if (!fp) return false;
+    dict.clear();
+    std::string line;
+    int ch;
+    auto flush = [&] {
+        if (!line.empty() && line.back() == '\r') line.pop_back();   // std::getline keeps a CR; only the first field matters
+        if (!line.empty()) {
+            const size_t sp = line.find(' ');
+            const std::string word = sp == std::string::npos ? line : line.substr(0, sp);
+            if (!word.empty()) dict.emplace(word, 1);
+        }
+        line.clear();
+    };
+    while ((ch = fgetc(fp)) != EOF) {
+        if (ch == '\n') flush();
+        else line += (char)ch;
+    }
+    flush();
+    fclose(fp);
+    return true;
+}
+
+int feat_extract_output_lengths(int n) {
+    const int leave = n % 100;
+    const int feat = (leave - 1) / 2 + 1;
+    return ((feat - 1) / 2 + 1 - 1) / 2 + 1 + (n / 100) * 13;
+}
+
+std::vector<int32_t> fix_timestamp_classes(const std::vector<int32_t> &data) {
+    const int n = (int)data.size();
+    if (n == 0) return {};
+    std::vector<int> dp(n, 1), parent(n, -1);
+    for (int i = 1; i < n; i++)
+        for (int j = 0; j < i; j++)
+            if (data[j] <= data[i] && dp[j] + 1 > dp[i]) { dp[i] = dp[j] + 1; parent[i] = j; }
+    int max_len = 0, max_idx = 0;
+    for (int i = 0; i < n; i++)
+        if (dp[i] > max_len) { max_len = dp[i]; max_idx = i; }
+    std::vector<bool> normal(n, false);
+    for (int i = max_idx; i != -1; i = parent[i]) normal[i] = true;
+    std::vector<int32_t> r(data);
+    int i = 0;
+    while (i < n) {
+        if (normal[i]) { ++i; continue; }
+        int j = i;
+        while (j < n && !normal[j]) ++j;
+        const int cnt = j - i;
+        int32_t lv = -1, rv = -1;
+        for (int k = i - 1; k >= 0; --k) if (normal[k]) { lv = r[k]; break; }
+        for (int k = j; k < n; ++k) if (normal[k]) { rv = r[k]; break; }
+        if (cnt <= 2) {
+            for (int k = i; k < j; ++k) r[k] = lv < 0 ? rv : (rv < 0 ? lv : ((k - (i - 1)) <= (j - k) ? lv : rv));
+        } else if (lv >= 0 && rv >= 0) {
+            const float step = (float)(rv - lv) / (cnt + 1);
+            for (int k = i; k < j; ++k) r[k] = (int32_t)(lv + step * (k - i + 1));
+        } else if (lv >= 0) {
+            for (int k = i; k < j; ++k) r[k] = lv;
+        } else if (rv >= 0) {
+            for (int k = i; k < j; ++k) r[k] = rv;
+        }
+        i = j;
+    }
+    return r;
+}
+
+std::vector<int32_t> build_align_tokens(const Hparams &hp, const std::vector<int32_t> &text_tokens, int n_pads) {
+    std::vector<int32_t> t;
+    t.reserve(text_tokens.size() + n_pads + 2);
+    t.push_back(hp.audio_start_id);
+    for (int i = 0; i < n_pads; i++) t.push_back(hp.audio_pad_id);
+    t.push_back(hp.audio_end_id);
+    t.insert(t.end(), text_tokens.begin(), text_tokens.end());
+    return t;
+}
+
 // ---------------------------------------------------------------- prompt
 std::vector<int32_t> build_prompt(const Hparams &hp, int n_audio, const std::vector<int32_t> &sys, int *audio_pos) {
     const int32_t im_start = 151644, im_end = 151645, sys_tok = 8948, user = 872, asst = 77091, nl = 198;
@@ -420,18 +593,29 @@ struct SynTensor { std::string name; std::vector<int64_t> ne; int kind; float sc
 
 bool write_synthetic_gguf(const std::string &path, const std::string &config, uint64_t seed, int wtype, std::string &err) {
     Hparams hp;
-    bool tiny = config == "tiny";
+    // "full"/"tiny": Qwen3-ASR; "aligner"/"aligner-tiny": Qwen3-ForcedAligner
+    // (src/forced_aligner.h:36-73: 24 x 1024 encoder, 16 heads, ffn 4096,
+    // vocab 152064, 5000-class head)
+    const bool al = config == "aligner" || config == "aligner-tiny";
+    const bool tiny = config == "tiny" || config == "aligner-tiny";
+    if (!tiny && config != "full" && config != "aligner") {
+        err = "unknown synthetic config: " + config;
+        return false;
+    }
+    if (al) {
+        hp.aligner = true;
+        hp.classify_num = 5000;
+        if (!tiny) { hp.enc_layers = 24; hp.d_model = 1024; hp.enc_heads = 16; hp.enc_ffn = 4096; hp.vocab = 152064; }
+    }
     if (tiny) {
         hp.enc_layers = 2; hp.d_model = 256; hp.enc_heads = 4; hp.enc_ffn = 512; hp.conv_ch = 96;
         hp.hidden = 256; hp.dec_layers = 2; hp.n_head = 4; hp.n_kv_head = 2; hp.head_dim = 128; hp.dec_ffn = 512;
-    } else if (config != "full") {
-        err = "unknown synthetic config: " + config;
-        return false;
     }
     if (wtype != 1 && wtype != 8) { err = "wtype must be 1 (f16) or 8 (q8_0)"; return false; }
     GGUFWriter w;
     w.add_str("general.architecture", "qwen3-asr");
-    w.add_str("general.name", tiny ? "Qwen3-ASR-synthetic-tiny" : "Qwen3-ASR-0.6B-synthetic");
+    w.add_str("general.name", al ? (tiny ? "Qwen3-ForcedAligner-synthetic-tiny" : "Qwen3-ForcedAligner-0.6B-synthetic")
+                                 : (tiny ? "Qwen3-ASR-synthetic-tiny" : "Qwen3-ASR-0.6B-synthetic"));
     w.add_u32("general.alignment", 32);
     w.add_u32("qwen3-asr.block_count", hp.dec_layers);
     w.add_u32("qwen3-asr.embedding_length", hp.hidden);
@@ -452,7 +636,12 @@ bool write_synthetic_gguf(const std::string &path, const std::string &config, ui
     w.add_u32("qwen3-asr.audio.start_token_id", hp.audio_start_id);
     w.add_u32("qwen3-asr.audio.end_token_id", hp.audio_end_id);
     w.add_u32("qwen3-asr.audio.pad_token_id", hp.audio_pad_id);
-    if (tiny) {   // the reference's own encoder keys (src/gguf_loader.cpp:69-85)
+    if (al) {   // scripts/convert_hf_to_gguf.py:454-458
+        w.add_u32("qwen3-asr.classify_num", hp.classify_num);
+        w.add_u32("qwen3-asr.timestamp_token_id", hp.timestamp_id);
+        w.add_u32("qwen3-asr.timestamp_segment_time", hp.ts_segment_ms);
+    }
+    if (tiny && !al) {   // the reference's own encoder keys (src/gguf_loader.cpp:69-85)
         w.add_u32("audio.encoder_layers", hp.enc_layers);
         w.add_u32("audio.d_model", hp.d_model);
         w.add_u32("audio.attention_heads", hp.enc_heads);
@@ -489,6 +678,7 @@ bool write_synthetic_gguf(const std::string &path, const std::string &config, ui
     toks[hp.audio_end_id] = "<|audio_end|>";
     toks[hp.audio_pad_id] = "<|audio_pad|>";
     for (int i = 151677; i < hp.vocab; i++) toks[i] = "[PAD" + std::to_string(i) + "]";
+    if (al) toks[hp.timestamp_id] = "<timestamp>";
     w.add_str("tokenizer.ggml.model", "gpt2");
     w.add_str_array("tokenizer.ggml.tokens", toks);
     w.add_str_array("tokenizer.ggml.merges", merges);
@@ -532,6 +722,8 @@ bool write_synthetic_gguf(const std::string &path, const std::string &config, ui
     vec("audio.encoder.proj2.bias", H, 2);
     ts.push_back({"token_embd.weight", {H, hp.vocab}, 3, 4.0f / sqrtf((float)H)});
     vec("output_norm.weight", H, 1);
+    // aligner classification head: F16 in every file type (convert_hf_to_gguf.py:240-241)
+    if (al) ts.push_back({"output.weight", {H, hp.classify_num}, 3, 4.0f / sqrtf((float)H)});
     const int QD = hp.n_head * hp.head_dim, KD = hp.n_kv_head * hp.head_dim;
     for (int l = 0; l < hp.dec_layers; l++) {
         std::string p = "blk." + std::to_string(l) + ".";

@@ -1,8 +1,10 @@
-// main.cpp -- qwen3-asr-cli, transcription mode of src/main.cpp:14-161, 361-414
-// (same flags and output), plus MI355X additions: --device, batch file lists
-// (-f may repeat), --synthetic to write a synthetic GGUF for testing.
-// Forced alignment (--align / --transcribe-align) is the SURVEY §8(f) "next"
-// row and is rejected with a clear message in this build.
+// main.cpp -- qwen3-asr-cli: the three modes of src/main.cpp (transcription
+// :361-414, forced alignment --align :301-359, transcribe + align -a :416-500)
+// with the same flags and output, plus MI355X additions: --device, batch file
+// lists (-f may repeat, transcription mode), --synthetic to write a synthetic
+// GGUF (tiny|full|aligner|aligner-tiny) for testing.
+#include <algorithm>
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -10,14 +12,17 @@
 #include <string>
 #include <vector>
 
+#include "forced_aligner.h"
 #include "qwen3_asr.h"
 
 struct cli_params {
     std::string model_path = "models/qwen3-asr-0.6b-f16.gguf";
+    std::string aligner_model_path;
     std::vector<std::string> audio_paths;
-    std::string output_path, language, synthetic;
+    std::string output_path, language, synthetic, align_text;
     int32_t max_tokens = 1024, n_threads = 4, device = 0;
-    bool print_progress = false, print_timing = true, print_tokens = false, profile = false, align = false;
+    bool print_progress = false, print_timing = true, print_tokens = false, profile = false;
+    bool align_mode = false, transcribe_align_mode = false;
 };
 
 static void usage(const char *prog) {
@@ -25,7 +30,7 @@ static void usage(const char *prog) {
     fprintf(stderr, "  -m, --model <path>     Path to GGUF model (default: models/qwen3-asr-0.6b-f16.gguf)\n");
     fprintf(stderr, "  -f, --audio <path>     Path to audio file (WAV, 16kHz mono) [required; repeat for a batch]\n");
     fprintf(stderr, "  -o, --output <path>    Output file path (default: stdout)\n");
-    fprintf(stderr, "  -l, --language <code>  Language code (accepted, ignored by the ASR path)\n");
+    fprintf(stderr, "  -l, --language <code>  Language code (optional, e.g. 'korean' for Korean word splitting)\n");
     fprintf(stderr, "  -t, --threads <n>      Number of threads (accepted for compatibility)\n");
     fprintf(stderr, "  --max-tokens <n>       Maximum tokens to generate (default: 1024)\n");
     fprintf(stderr, "  --progress             Print progress during transcription\n");
@@ -33,8 +38,14 @@ static void usage(const char *prog) {
     fprintf(stderr, "  --tokens               Print token IDs\n");
     fprintf(stderr, "  --profile              Print timing profile\n");
     fprintf(stderr, "  --device <n>           HIP device index (default: 0)\n");
-    fprintf(stderr, "  --synthetic <cfg>      Write a synthetic GGUF (tiny|full) to --model and exit\n");
-    fprintf(stderr, "  -h, --help             Show this help message\n");
+    fprintf(stderr, "  --synthetic <cfg>      Write a synthetic GGUF (tiny|full|aligner|aligner-tiny) to --model and exit\n");
+    fprintf(stderr, "\nForced Alignment:\n");
+    fprintf(stderr, "  --align                Enable forced alignment mode\n");
+    fprintf(stderr, "  --text <text>          Reference transcript for alignment\n");
+    fprintf(stderr, "\nTranscribe + Align:\n");
+    fprintf(stderr, "  -a, --transcribe-align Run ASR then forced alignment\n");
+    fprintf(stderr, "  --aligner-model <path> Path to forced aligner GGUF model (required with --transcribe-align)\n");
+    fprintf(stderr, "\n  -h, --help             Show this help message\n");
 }
 
 static bool parse(int argc, char **argv, cli_params &p) {
@@ -58,29 +69,195 @@ static bool parse(int argc, char **argv, cli_params &p) {
         else if (!strcmp(a, "--no-timing")) p.print_timing = false;
         else if (!strcmp(a, "--tokens")) p.print_tokens = true;
         else if (!strcmp(a, "--profile")) p.profile = true;
-        else if (!strcmp(a, "--align") || !strcmp(a, "-a") || !strcmp(a, "--transcribe-align") || !strcmp(a, "--aligner-model") ||
-                 !strcmp(a, "--text")) {
-            p.align = true;
-            if (strcmp(a, "--align") && strcmp(a, "-a") && strcmp(a, "--transcribe-align") && i + 1 < argc) ++i;
-        } else if (!strcmp(a, "-h") || !strcmp(a, "--help")) { usage(argv[0]); exit(0); }
+        else if (!strcmp(a, "--align")) p.align_mode = true;
+        else if (!strcmp(a, "-a") || !strcmp(a, "--transcribe-align")) p.transcribe_align_mode = true;
+        else if (!strcmp(a, "--aligner-model")) { if (!val(p.aligner_model_path)) return false; }
+        else if (!strcmp(a, "--text")) { if (!val(p.align_text)) return false; }
+        else if (!strcmp(a, "-h") || !strcmp(a, "--help")) { usage(argv[0]); exit(0); }
         else { fprintf(stderr, "Error: Unknown argument: %s\n", a); return false; }
     }
-    if (p.align) { fprintf(stderr, "Error: forced alignment is not available in this build (ASR path only)\n"); return false; }
-    if (p.synthetic.empty() && p.audio_paths.empty()) { fprintf(stderr, "Error: Audio file path is required (-f/--audio)\n"); return false; }
+    if (!p.synthetic.empty()) return true;
+    if (p.audio_paths.empty()) { fprintf(stderr, "Error: Audio file path is required (-f/--audio)\n"); return false; }
+    // src/main.cpp:76-90
+    if (p.align_mode && p.align_text.empty()) {
+        fprintf(stderr, "Error: Reference text is required for alignment mode (--text)\n");
+        return false;
+    }
+    if (p.align_mode && p.transcribe_align_mode) {
+        fprintf(stderr, "Error: --align and --transcribe-align cannot be used together\n");
+        return false;
+    }
+    if (p.transcribe_align_mode && p.aligner_model_path.empty()) {
+        fprintf(stderr, "Error: --aligner-model is required for --transcribe-align\n");
+        return false;
+    }
+    if ((p.align_mode || p.transcribe_align_mode) && p.audio_paths.size() != 1) {
+        fprintf(stderr, "Error: alignment takes exactly one audio file\n");
+        return false;
+    }
     return true;
 }
 
-int main(int argc, char **argv) {
-    cli_params p;
-    if (!parse(argc, argv, p)) { fprintf(stderr, "\n"); usage(argv[0]); return 1; }
-    if (!p.synthetic.empty()) {
-        if (qasr_write_synthetic_gguf(p.model_path.c_str(), p.synthetic.c_str(), 42, 1) != 0) {
-            fprintf(stderr, "Error: %s\n", qasr_last_error());
-            return 1;
+// src/main.cpp:163-189: "language Xxxx..." prefix of the ASR text
+static std::string detect_language(const std::string &asr_text) {
+    const std::string prefix = "language ";
+    if (asr_text.size() < prefix.size() || asr_text.compare(0, prefix.size(), prefix) != 0) return "";
+    size_t pos = prefix.size();
+    if (pos >= asr_text.size() || !std::isupper((unsigned char)asr_text[pos])) return "";
+    ++pos;
+    while (pos < asr_text.size() && std::islower((unsigned char)asr_text[pos])) ++pos;
+    std::string lang = asr_text.substr(prefix.size(), pos - prefix.size());
+    std::transform(lang.begin(), lang.end(), lang.begin(), [](unsigned char c) { return (char)std::tolower(c); });
+    return lang;
+}
+
+// src/main.cpp:191-228
+static std::string extract_transcript(const std::string &asr_text) {
+    const std::string prefix = "language ";
+    if (asr_text.size() < prefix.size() || asr_text.compare(0, prefix.size(), prefix) != 0) return asr_text;
+    size_t pos = prefix.size();
+    if (pos >= asr_text.size()) return "";
+    if (!std::isupper((unsigned char)asr_text[pos])) return asr_text;
+    ++pos;
+    while (pos < asr_text.size() && std::islower((unsigned char)asr_text[pos])) ++pos;
+    while (pos < asr_text.size()) {
+        const unsigned char c = (unsigned char)asr_text[pos];
+        if (c >= 0x80 || !std::isspace(c)) break;
+        ++pos;
+    }
+    return asr_text.substr(pos);
+}
+
+// src/main.cpp:230-276
+static std::string escape_json_string(const std::string &s) {
+    std::string r;
+    for (char c : s) {
+        switch (c) {
+            case '"': r += "\\\""; break;
+            case '\\': r += "\\\\"; break;
+            case '\b': r += "\\b"; break;
+            case '\f': r += "\\f"; break;
+            case '\n': r += "\\n"; break;
+            case '\r': r += "\\r"; break;
+            case '\t': r += "\\t"; break;
+            default:
+                if ((unsigned char)c < 0x20) { char b[8]; snprintf(b, sizeof b, "\\u%04x", (unsigned char)c); r += b; }
+                else r += c;
         }
-        fprintf(stderr, "wrote synthetic %s model to %s\n", p.synthetic.c_str(), p.model_path.c_str());
+    }
+    return r;
+}
+
+static std::string alignment_to_json(const qwen3_asr::alignment_result &result) {
+    std::string json = "{\n  \"words\": [\n";
+    for (size_t i = 0; i < result.words.size(); ++i) {
+        const auto &w = result.words[i];
+        char buf[64];
+        snprintf(buf, sizeof buf, "\"start\": %.3f, \"end\": %.3f}", w.start, w.end);
+        json += "    {\"word\": \"" + escape_json_string(w.word) + "\", " + buf;
+        if (i + 1 < result.words.size()) json += ",";
+        json += "\n";
+    }
+    json += "  ]\n}";
+    return json;
+}
+
+// src/main.cpp:278-299
+static std::string find_korean_dict(const std::string &model_path) {
+    auto dir_of = [](const std::string &path) -> std::string {
+        const size_t pos = path.find_last_of("/\\");
+        return pos != std::string::npos ? path.substr(0, pos) : ".";
+    };
+    for (const std::string &p : {dir_of(model_path) + "/../assets/korean_dict_jieba.dict",
+                                 dir_of(model_path) + "/assets/korean_dict_jieba.dict", std::string("assets/korean_dict_jieba.dict")}) {
+        std::ifstream f(p);
+        if (f.good()) return p;
+    }
+    return "";
+}
+
+static int write_output(const cli_params &p, const std::string &text) {
+    if (p.output_path.empty()) {
+        printf("%s", text.c_str());
         return 0;
     }
+    std::ofstream out(p.output_path);
+    if (!out) { fprintf(stderr, "Error: Failed to open output file: %s\n", p.output_path.c_str()); return 1; }
+    out << text;
+    fprintf(stderr, "Output written to: %s\n", p.output_path.c_str());
+    return 0;
+}
+
+static bool load_aligner(qwen3_asr::ForcedAligner &al, const std::string &path, const std::string &lang, int device) {
+    al.set_device(device);
+    if (!al.load_model(path)) { fprintf(stderr, "Error (Aligner): %s\n", al.get_error().c_str()); return false; }
+    if (lang == "korean") {
+        const std::string dict = find_korean_dict(path);
+        if (dict.empty()) fprintf(stderr, "Warning: Korean dictionary not found. Falling back to whitespace splitting.\n");
+        else if (!al.load_korean_dict(dict)) fprintf(stderr, "Warning: Failed to load Korean dictionary from %s\n", dict.c_str());
+    }
+    return true;
+}
+
+static int run_alignment(const cli_params &p) {
+    fprintf(stderr, "qwen3-asr-cli (Forced Alignment Mode)\n  Model: %s\n  Audio: %s\n  Text: %s\n", p.model_path.c_str(),
+            p.audio_paths[0].c_str(), p.align_text.c_str());
+    if (!p.language.empty()) fprintf(stderr, "  Language: %s\n", p.language.c_str());
+    fprintf(stderr, "\n");
+    qwen3_asr::ForcedAligner al;
+    if (!load_aligner(al, p.model_path, p.language, p.device)) return 1;
+    fprintf(stderr, "Model loaded. Running alignment...\n");
+    auto r = al.align(p.audio_paths[0], p.align_text, p.language);
+    if (!r.success) { fprintf(stderr, "Error: %s\n", r.error_msg.c_str()); return 1; }
+    if (p.print_timing) {
+        fprintf(stderr, "\nTiming:\n");
+        fprintf(stderr, "  Mel spectrogram: %lld ms\n", (long long)r.t_mel_ms);
+        fprintf(stderr, "  Audio encoding:  %lld ms\n", (long long)r.t_encode_ms);
+        fprintf(stderr, "  Text decoding:   %lld ms\n", (long long)r.t_decode_ms);
+        fprintf(stderr, "  Total:           %lld ms\n", (long long)r.t_total_ms);
+        fprintf(stderr, "  Words aligned:   %zu\n", r.words.size());
+    }
+    return write_output(p, alignment_to_json(r) + "\n");
+}
+
+static int run_transcribe_and_align(const cli_params &p) {
+    fprintf(stderr, "qwen3-asr-cli (Transcribe + Align Mode)\n  ASR Model: %s\n  Aligner Model: %s\n  Audio: %s\n  Threads: %d\n\n",
+            p.model_path.c_str(), p.aligner_model_path.c_str(), p.audio_paths[0].c_str(), p.n_threads);
+    fprintf(stderr, "--- Phase 1: Transcription ---\n");
+    qwen3_asr::Qwen3ASR asr;
+    asr.set_device(p.device);
+    if (!asr.load_model(p.model_path)) { fprintf(stderr, "Error (ASR): %s\n", asr.get_error().c_str()); return 1; }
+    qwen3_asr::transcribe_params tp;
+    tp.max_tokens = p.max_tokens;
+    tp.language = p.language;
+    tp.n_threads = p.n_threads;
+    tp.print_progress = p.print_progress;
+    tp.print_timing = p.print_timing;
+    auto ar = asr.transcribe(p.audio_paths[0], tp);
+    if (!ar.success) { fprintf(stderr, "Error (ASR): %s\n", ar.error_msg.c_str()); return 1; }
+    const std::string detected = detect_language(ar.text);
+    const std::string lang = p.language.empty() ? detected : p.language;
+    const std::string transcript = extract_transcript(ar.text);
+    fprintf(stderr, "  Detected language: %s\n", detected.empty() ? "(none)" : detected.c_str());
+    if (!p.language.empty()) fprintf(stderr, "  Language override: %s\n", p.language.c_str());
+    fprintf(stderr, "  Alignment language: %s\n", lang.empty() ? "(none)" : lang.c_str());
+    fprintf(stderr, "  Transcript: %s\n", transcript.c_str());
+    fprintf(stderr, "\n--- Phase 2: Forced Alignment ---\n");
+    qwen3_asr::ForcedAligner al;
+    if (!load_aligner(al, p.aligner_model_path, lang, p.device)) return 1;
+    auto r = al.align(p.audio_paths[0], transcript, lang);
+    if (!r.success) { fprintf(stderr, "Error (Aligner): %s\n", r.error_msg.c_str()); return 1; }
+    if (p.print_timing) {
+        fprintf(stderr, "\nCombined Timing:\n");
+        fprintf(stderr, "  ASR:           %lld ms\n", (long long)ar.t_total_ms);
+        fprintf(stderr, "  Alignment:     %lld ms\n", (long long)r.t_total_ms);
+        fprintf(stderr, "  Total:         %lld ms\n", (long long)(ar.t_total_ms + r.t_total_ms));
+        fprintf(stderr, "  Words aligned: %zu\n", r.words.size());
+    }
+    return write_output(p, alignment_to_json(r) + "\n");
+}
+
+static int run_transcription(const cli_params &p) {
     fprintf(stderr, "qwen3-asr-cli\n  Model: %s\n", p.model_path.c_str());
     for (auto &a : p.audio_paths) fprintf(stderr, "  Audio: %s\n", a.c_str());
     fprintf(stderr, "  Threads: %d\n\n", p.n_threads);
@@ -107,8 +284,7 @@ int main(int argc, char **argv) {
         results = asr.transcribe_batch(clips, tp);
     }
     std::string all;
-    for (size_t i = 0; i < results.size(); i++) {
-        const auto &r = results[i];
+    for (const auto &r : results) {
         if (!r.success) { fprintf(stderr, "Error: %s\n", r.error_msg.c_str()); return 1; }
         if (p.print_tokens) {
             fprintf(stderr, "\nTokens (%zu):\n", r.tokens.size());
@@ -117,13 +293,21 @@ int main(int argc, char **argv) {
         }
         all += r.text + "\n";
     }
-    if (p.output_path.empty()) {
-        printf("%s", all.c_str());
-    } else {
-        std::ofstream out(p.output_path);
-        if (!out) { fprintf(stderr, "Error: Failed to open output file: %s\n", p.output_path.c_str()); return 1; }
-        out << all;
-        fprintf(stderr, "Output written to: %s\n", p.output_path.c_str());
+    return write_output(p, all);
+}
+
+int main(int argc, char **argv) {
+    cli_params p;
+    if (!parse(argc, argv, p)) { fprintf(stderr, "\n"); usage(argv[0]); return 1; }
+    if (!p.synthetic.empty()) {
+        if (qasr_write_synthetic_gguf(p.model_path.c_str(), p.synthetic.c_str(), 42, 1) != 0) {
+            fprintf(stderr, "Error: %s\n", qasr_last_error());
+            return 1;
+        }
+        fprintf(stderr, "wrote synthetic %s model to %s\n", p.synthetic.c_str(), p.model_path.c_str());
+        return 0;
     }
-    return 0;
+    if (p.transcribe_align_mode) return run_transcribe_and_align(p);
+    if (p.align_mode) return run_alignment(p);
+    return run_transcription(p);
 }

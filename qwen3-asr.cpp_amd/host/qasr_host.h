@@ -20,6 +20,10 @@ struct Hparams {
     float rms_eps = 1e-6f, rope_theta = 1000000.0f;
     int eos_id = 151645, pad_id = 151643, audio_start_id = 151669, audio_end_id = 151670, audio_pad_id = 151676;
     int weight_type = 1;
+    // ForcedAligner files (src/forced_aligner.h:36-73; keys convert_hf_to_gguf.py:454-458):
+    // classification head output.weight [hidden][classify_num], no chat template
+    bool aligner = false;
+    int classify_num = 0, timestamp_id = 151705, ts_segment_ms = 80;
 };
 
 // Reads hparams with the reference's keys and defaults.  Encoder keys: the
@@ -60,6 +64,9 @@ public:
     std::string decode(const std::vector<int32_t> &ids) const;
     std::string decode_token(int32_t id) const;
     std::vector<int32_t> encode(const std::string &text) const;
+    // one word, no leading-space marker; unknown subwords are skipped with a
+    // warning (src/forced_aligner.cpp:1589-1603)
+    std::vector<int32_t> encode_word(const std::string &word) const;
     size_t size() const { return vocab_.size(); }
 
 private:
@@ -70,6 +77,19 @@ private:
 
 // ---- prompt: src/qwen3_asr.cpp:151-214 ----
 std::vector<int32_t> build_prompt(const Hparams &hp, int n_audio, const std::vector<int32_t> &sys_ids, int *audio_pos);
+
+// ---- forced aligner host logic (src/forced_aligner.cpp) ----
+// whitespace words (' ', '\t', '\n', '\r'), :1577-1586
+std::vector<std::string> split_words(const std::string &text);
+// LTokenizer-style Korean split with the jieba word list, :1485-1541
+std::vector<std::string> tokenize_korean(const std::string &text, const std::unordered_map<std::string, int> &dict);
+bool load_korean_dict(const std::string &path, std::unordered_map<std::string, int> &dict);
+// HF _get_feat_extract_output_lengths: number of <|audio_pad|> tokens, :1173-1178
+int feat_extract_output_lengths(int mel_frames);
+// LIS-based timestamp repair (HF fix_timestamp), :1183-1265
+std::vector<int32_t> fix_timestamp_classes(const std::vector<int32_t> &data);
+// <|audio_start|> pad x n <|audio_end|> text..., :1308-1329; audio starts at index 1
+std::vector<int32_t> build_align_tokens(const Hparams &hp, const std::vector<int32_t> &text_tokens, int n_pads);
 
 // ---- synthetic model ----
 bool write_synthetic_gguf(const std::string &path, const std::string &config, uint64_t seed, int wtype, std::string &err);

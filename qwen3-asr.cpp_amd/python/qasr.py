@@ -28,6 +28,8 @@ EXPORTS = [
     "qasr_set_probe", "qasr_get_probe",
     "qasr_detokenize", "qasr_tokenize",
     "qasr_load_wav", "qasr_write_wav", "qasr_synth_pcm", "qasr_write_synthetic_gguf",
+    "qasr_align", "qasr_align_tokenize", "qasr_model_load_korean_dict", "qasr_fix_timestamps",
+    "qasr_align_prompt_len", "qasr_align_json", "qasr_align_words",
 ]
 
 
@@ -36,7 +38,8 @@ class Hparams(C.Structure):
         ("enc_eps", C.c_float)] + [(n, C.c_int32) for n in (
             "vocab_size", "hidden_size", "dec_layers", "n_heads", "n_kv_heads", "head_dim", "dec_ffn")] + [
         ("rms_eps", C.c_float), ("rope_theta", C.c_float)] + [(n, C.c_int32) for n in (
-            "eos_id", "pad_id", "audio_start_id", "audio_end_id", "audio_pad_id", "weight_type")]
+            "eos_id", "pad_id", "audio_start_id", "audio_end_id", "audio_pad_id", "weight_type",
+            "classify_num", "timestamp_token_id")]
 
 
 class Timings(C.Structure):
@@ -78,6 +81,13 @@ def lib() -> C.CDLL:
             "qasr_load_wav": ([C.c_char_p, F, I, IP], I), "qasr_write_wav": ([C.c_char_p, F, I, I], I),
             "qasr_synth_pcm": ([C.c_uint64, I, F], I),
             "qasr_write_synthetic_gguf": ([C.c_char_p, C.c_char_p, C.c_uint64, I], I),
+            "qasr_align": ([P, F, I, I32P, I, I32P, I, IP, C.POINTER(Timings)], I),
+            "qasr_align_tokenize": ([P, C.c_char_p, C.c_char_p, I32P, I, IP], I),
+            "qasr_model_load_korean_dict": ([P, C.c_char_p], I),
+            "qasr_fix_timestamps": ([I32P, I, I32P], I),
+            "qasr_align_prompt_len": ([I, I], I),
+            "qasr_align_words": ([P, C.c_char_p, C.c_char_p, C.c_char_p, I], I),
+            "qasr_align_json": ([P, F, I, C.c_char_p, C.c_char_p, C.c_char_p, I, C.POINTER(Timings)], I),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -142,6 +152,18 @@ def write_wav(path: str, pcm: np.ndarray, sr: int = 16000) -> None:
     _check(lib().qasr_write_wav(path.encode(), _f(pcm), len(pcm), sr), "write_wav")
 
 
+def fix_timestamps(classes: Sequence[int]) -> List[int]:
+    """LIS repair of raw timestamp classes (src/forced_aligner.cpp:1183-1265)."""
+    a = np.ascontiguousarray(classes, np.int32)
+    out = np.zeros(max(len(a), 1), np.int32)
+    _check(lib().qasr_fix_timestamps(_i32(a) if len(a) else None, len(a), _i32(out) if len(a) else None), "fix_timestamps")
+    return out[:len(a)].tolist()
+
+
+def align_prompt_len(n_samples: int, n_text: int) -> int:
+    return lib().qasr_align_prompt_len(n_samples, n_text)
+
+
 def device_count() -> int:
     n = C.c_int(0)
     lib().qasr_device_count(C.byref(n))
@@ -193,6 +215,30 @@ class Model:
         a = np.zeros(max(n, 1), np.int32)
         lib().qasr_tokenize(self.h, text.encode(), _i32(a), n)
         return a[:n].tolist()
+
+
+    # ---- forced aligner (Qwen3-ForcedAligner files) -------------------------
+    @property
+    def is_aligner(self) -> bool:
+        return self.hp.classify_num > 0
+
+    def align_tokenize(self, text: str, language: str = ""):
+        """ForcedAligner::tokenize_with_timestamps -> (ids, n_words)."""
+        nw = C.c_int(0)
+        n = lib().qasr_align_tokenize(self.h, text.encode(), language.encode(), None, 0, C.byref(nw))
+        a = np.zeros(max(n, 1), np.int32)
+        lib().qasr_align_tokenize(self.h, text.encode(), language.encode(), _i32(a), n, C.byref(nw))
+        return a[:n].tolist(), nw.value
+
+    def align_words(self, text: str, language: str = "") -> List[str]:
+        n = lib().qasr_align_words(self.h, text.encode(), language.encode(), None, 0)
+        buf = C.create_string_buffer(n + 1)
+        lib().qasr_align_words(self.h, text.encode(), language.encode(), buf, n + 1)
+        s = buf.raw[:n].decode("utf-8")
+        return s.split("\n") if s else []
+
+    def load_korean_dict(self, path: str) -> None:
+        _check(lib().qasr_model_load_korean_dict(self.h, path.encode()), "qasr_model_load_korean_dict")
 
 
 @dataclass
@@ -308,6 +354,32 @@ class Context:
         ms, n, b = C.c_double(0), C.c_int64(0), C.c_double(0)
         _check(lib().qasr_get_probe(self.h, C.byref(ms), C.byref(n), C.byref(b)), "qasr_get_probe")
         return ms.value, n.value, b.value
+
+    # ---- forced aligner ------------------------------------------------------
+    def align(self, pcm: np.ndarray, text_ids: Sequence[int]):
+        """Raw timestamp classes of one clip (qasr_align) -> (classes, timings)."""
+        pcm = np.ascontiguousarray(pcm, np.float32)
+        ids = np.ascontiguousarray(text_ids, np.int32)
+        cap = max(int(np.sum(ids == self.model.hp.timestamp_token_id)), 1)
+        out = np.zeros(cap, np.int32)
+        nts = C.c_int(0)
+        t = Timings()
+        _check(lib().qasr_align(self.h, _f(pcm), len(pcm), _i32(ids) if len(ids) else None, len(ids), _i32(out), cap,
+                                C.byref(nts), C.byref(t)), "qasr_align")
+        return out[:nts.value].tolist(), t
+
+    def align_json(self, pcm: np.ndarray, text: str, language: str = ""):
+        """ForcedAligner::align -> the CLI JSON document (parsed) and timings.
+        qasr_align_json returns the document length, or minus an error code."""
+        import json
+        pcm = np.ascontiguousarray(pcm, np.float32)
+        t = Timings()
+        n = lib().qasr_align_json(self.h, _f(pcm), len(pcm), text.encode(), language.encode(), None, 0, C.byref(t))
+        if n < 0:
+            raise QasrError(f"qasr_align_json: {lib().qasr_last_error().decode(errors='replace')}")
+        buf = C.create_string_buffer(n + 1)
+        lib().qasr_align_json(self.h, _f(pcm), len(pcm), text.encode(), language.encode(), buf, n + 1, C.byref(t))
+        return json.loads(buf.raw[:n].decode("utf-8")), t
 
     def transcribe(self, clips, max_tokens=1024, ignore_eos=False) -> RunResult:
         self.stage_audio(clips)

@@ -122,7 +122,9 @@ class QoModel(C.Structure):
             "eos_id", "audio_start_id", "audio_end_id", "audio_pad_id", "wtype")] + [(n, C.c_void_p) for n in (
         "conv1_w", "conv2_w", "conv3_w", "conv_out_w", "conv1_b", "conv2_b", "conv3_b", "ln_post_w", "ln_post_b",
         "proj1_w", "proj2_w", "proj1_b", "proj2_b")] + [("enc", C.POINTER(EncLayer)), ("token_embd", C.c_void_p),
-                                                        ("output_norm", C.c_void_p), ("dec", C.POINTER(DecLayer))]
+                                                        ("output_norm", C.c_void_p), ("dec", C.POINTER(DecLayer)),
+                                                        ("aligner", C.c_int), ("classify_num", C.c_int),
+                                                        ("classify_w", C.c_void_p)]
 
 
 _olib = None
@@ -151,6 +153,7 @@ def olib():
         L.qo_build_prompt.argtypes = [C.POINTER(QoModel), I, C.POINTER(C.c_int32)]
         L.qo_transcribe.argtypes = [C.POINTER(QoModel), F, I, I, I, I, C.POINTER(C.c_int32), C.POINTER(C.c_double)]
         L.qo_set_threads.argtypes = [I]
+        L.qo_align_forward.argtypes = [C.POINTER(QoModel), C.POINTER(C.c_int32), I, F, I, I, C.POINTER(I), I, F, I]
         L.qo_f32_to_f16.argtypes = [C.c_float]
         L.qo_f32_to_f16.restype = C.c_uint16
         _olib = L
@@ -195,14 +198,25 @@ class OracleModel:
             return int(kv[a]) if a in kv else int(kv.get(b, d))
 
         m = QoModel()
-        m.enc_layers = k2("audio.encoder_layers", "qwen3-asr.audio.encoder.layer_count", 18)
-        m.d_model = k2("audio.d_model", "qwen3-asr.audio.encoder.embedding_length", 896)
-        m.enc_heads = k2("audio.attention_heads", "qwen3-asr.audio.encoder.attention.head_count", 14)
-        m.enc_ffn = k2("audio.ffn_dim", "qwen3-asr.audio.encoder.feed_forward_length", 3584)
-        m.conv_ch = k2("audio.conv_channels", "qwen3-asr.audio.conv_channels", 480)
+        # ForcedAligner files (src/forced_aligner.cpp:136-175): converter keys
+        # only, aligner defaults; classify head output.weight
+        self.aligner = "qwen3-asr.classify_num" in kv or "output.weight" in g.tensors
+        if self.aligner:
+            m.aligner = 1
+            m.enc_layers = int(kv.get("qwen3-asr.audio.encoder.layer_count", 24))
+            m.d_model = int(kv.get("qwen3-asr.audio.encoder.embedding_length", 1024))
+            m.enc_heads = int(kv.get("qwen3-asr.audio.encoder.attention.head_count", 16))
+            m.enc_ffn = int(kv.get("qwen3-asr.audio.encoder.feed_forward_length", 4096))
+            m.conv_ch = int(kv.get("qwen3-asr.audio.conv_channels", 480))
+        else:
+            m.enc_layers = k2("audio.encoder_layers", "qwen3-asr.audio.encoder.layer_count", 18)
+            m.d_model = k2("audio.d_model", "qwen3-asr.audio.encoder.embedding_length", 896)
+            m.enc_heads = k2("audio.attention_heads", "qwen3-asr.audio.encoder.attention.head_count", 14)
+            m.enc_ffn = k2("audio.ffn_dim", "qwen3-asr.audio.encoder.feed_forward_length", 3584)
+            m.conv_ch = k2("audio.conv_channels", "qwen3-asr.audio.conv_channels", 480)
         m.n_mel = 128
         m.enc_eps = 1e-5
-        m.vocab = int(kv.get("qwen3-asr.vocab_size", 151936))
+        m.vocab = int(kv.get("qwen3-asr.vocab_size", 152064 if self.aligner else 151936))
         m.hidden = int(kv.get("qwen3-asr.embedding_length", 1024))
         m.dec_layers = int(kv.get("qwen3-asr.block_count", 28))
         m.n_head = int(kv.get("qwen3-asr.attention.head_count", 16))
@@ -261,6 +275,14 @@ class OracleModel:
                 setattr(L, f, ptr(p + f + ".weight", f in ("attn_q", "attn_k", "attn_v", "attn_output", "ffn_gate", "ffn_up",
                                                            "ffn_down")))
         m.dec = self.dec
+        if self.aligner:
+            m.classify_num = int(kv.get("qwen3-asr.classify_num", 5000))
+            self.timestamp_id = int(kv.get("qwen3-asr.timestamp_token_id", 151705))
+            ty, ne, arr = g.tensors["output.weight"]
+            assert ty == 1 and ne[0] == m.hidden and ne[1] >= m.classify_num
+            a = np.ascontiguousarray(arr[:m.classify_num * m.hidden])   # first classify_num rows (:274-277)
+            self._keep.append(a)
+            m.classify_w = a.ctypes.data
         self.m = m
         self.vocab = m.vocab
         self.hidden = m.hidden
@@ -295,6 +317,34 @@ class OracleModel:
         n = olib().qo_transcribe(C.byref(self.m), _f(pcm), len(pcm), max_tokens, int(ignore_eos), flags,
                                  toks.ctypes.data_as(C.POINTER(C.c_int32)), t.ctypes.data_as(C.POINTER(C.c_double)))
         return toks[:max(n, 0)].tolist(), t
+
+
+    # ------------------------------------------------------------ aligner
+    def align_forward(self, tokens, audio, audio_pos, rows, flags=0):
+        """ForcedAligner::forward_decoder + classify head at `rows` -> logits[len(rows)][classify_num]."""
+        toks = np.ascontiguousarray(tokens, np.int32)
+        a = np.ascontiguousarray(audio, np.float32)
+        r = np.ascontiguousarray(rows, np.int32)
+        out = np.zeros((max(len(r), 1), self.m.classify_num), np.float32)
+        rc = olib().qo_align_forward(C.byref(self.m), toks.ctypes.data_as(C.POINTER(C.c_int32)), len(toks), _f(a),
+                                     a.shape[0], audio_pos, r.ctypes.data_as(C.POINTER(C.c_int)), len(r), _f(out), flags)
+        assert rc == 0
+        return out[:len(r)]
+
+    def align_classes(self, pcm, text_ids, flags=0):
+        """ForcedAligner::align up to extract_timestamp_classes (src/forced_aligner.cpp:1636-1690):
+        returns (classes, logits at the timestamp rows, tokens)."""
+        mel = log_mel(pcm)
+        feats = self.encode(mel, flags)
+        T = mel.shape[1]
+        leave = T % 100
+        feat = (leave - 1) // 2 + 1 if leave > 0 else 1      # C integer division of (0-1)/2 = 0
+        pads = ((feat - 1) // 2 + 1 - 1) // 2 + 1 + (T // 100) * 13
+        toks = [self.m.audio_start_id] + [self.m.audio_pad_id] * pads + [self.m.audio_end_id] + list(text_ids)
+        rows = [i for i, t in enumerate(toks) if t == self.timestamp_id]
+        lg = self.align_forward(toks, feats, 1, rows, flags)
+        cls = [int(olib().qo_argmax(_f(np.ascontiguousarray(l)), len(l))) for l in lg]
+        return cls, lg, toks
 
 
 class OracleDecoder:
