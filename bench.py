@@ -32,6 +32,7 @@ import qasr  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 README_RTFX = 92.0 / 5.007   # 92 s clip in 5,007 ms on M2 Pro (README.md:136)
+README_ALIGN_RTFX = 92.0 / 18.005   # transcribe + align of the same clip (README.md:138)
 
 
 def parse():
@@ -47,14 +48,17 @@ def parse():
     ap.add_argument("--cpu-sample-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=4, help="reference's effective ggml thread count")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--q8", action="store_true", help="Q8_0 synthetic model (configs[2] weights)")
+    ap.add_argument("--pipeline", choices=("asr", "align"), default="asr",
+                    help="align: configs[4] transcribe + ForcedAligner on every clip (src/main.cpp:416-500)")
     return ap.parse_args()
 
 
-def synthetic_model(rank: int) -> str:
-    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "qasr_synth_full_f16.gguf")
+def synthetic_model(rank: int, config: str = "full", wtype: int = 1) -> str:
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"qasr_synth_{config}_{'q8_0' if wtype == 8 else 'f16'}.gguf")
     lock = path + ".done"
     if rank == 0 and not os.path.exists(lock):
-        qasr.write_synthetic_gguf(path + ".tmp", "full", 42, 1)
+        qasr.write_synthetic_gguf(path + ".tmp", config, 42, wtype)
         os.replace(path + ".tmp", path)
         open(lock, "w").close()
     while not os.path.exists(lock):
@@ -100,6 +104,20 @@ def pmc_traffic(kernel_prefix: str):
     return None, None
 
 
+def workload(args, ntok: int, align: bool) -> str:
+    """the BASELINE.json config this run is (configs[1] by default)"""
+    if align:
+        name = "configs[4]: transcribe + ForcedAligner"
+    elif args.q8 and args.batch > 1:
+        name = "configs[2]: q8_0 batch"
+    elif args.batch == 1 and not args.q8 and args.seconds == 92.0:
+        name = "configs[1]"
+    else:
+        name = "custom"
+    return (f"{name}: {args.batch} x {args.seconds:g} s clip(s) per GPU per step, greedy decode budget {ntok} tokens "
+            f"(3.5 tok/s), EOS ignored")
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -117,7 +135,8 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    model_path = args.model or synthetic_model(rank)
+    wtype = 8 if args.q8 else 1
+    model_path = args.model or synthetic_model(rank, "full", wtype)
     m = qasr.Model(model_path, local)
     n = int(args.seconds * 16000)
     ntok = int(math.ceil(args.tok_rate * args.seconds))
@@ -126,8 +145,21 @@ def main():
     ctx = qasr.Context(m, max_batch=args.batch, max_ctx=P + ntok + 8)
     clips = [qasr.synth_pcm(1000 + rank * args.batch + i, n) for i in range(args.batch)]
     ctx.stage_audio(clips)
+    actx, texts = None, []
+    if args.pipeline == "align":   # the ForcedAligner leg: transcript of each clip -> word timestamps
+        am = qasr.Model(synthetic_model(rank, "aligner", wtype), local)
+        r0 = ctx.run(ntok, ignore_eos=True)
+        texts = [m.detokenize(t) for t in r0.tokens]
+        need = max(qasr.align_prompt_len(n, len(am.align_tokenize(t)[0])) for t in texts)
+        actx = qasr.Context(am, max_batch=1, max_ctx=need + 8)
+
+    def align_all():
+        for pcm, t in zip(clips, texts):
+            actx.align_json(pcm, t)
     for _ in range(args.warmup):
         ctx.run(ntok, ignore_eos=True)
+        if actx:
+            align_all()
     if not args.no_probe:
         ctx.set_probe(1)
     barrier()
@@ -140,6 +172,10 @@ def main():
         tm["encode"] += res.timings.t_encode_ms
         tm["prefill"] += res.timings.t_prefill_ms
         tm["decode"] += res.timings.t_decode_ms
+        if actx:
+            ta = time.perf_counter()
+            align_all()
+            tm["align"] = tm.get("align", 0.0) + (time.perf_counter() - ta) * 1e3
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -157,7 +193,8 @@ def main():
     audio = N * args.batch * args.seconds * args.steps
     value = audio / dt
     out = {
-        "metric": "RTFx (audio-sec/wall-sec) + decode tokens/sec, Qwen3-ASR-0.6B f16",
+        "metric": "RTFx (audio-sec/wall-sec) + decode tokens/sec, Qwen3-ASR-0.6B " + ("q8_0" if args.q8 else "f16") +
+                  (" + ForcedAligner-0.6B (transcribe-align)" if actx else ""),
         "value": round(value, 3),
         "unit": "audio-sec/wall-sec",
         "n_gpus": N,
@@ -166,12 +203,13 @@ def main():
         "ms_per_step": round(dt / args.steps * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(value / README_RTFX, 3),
-        "dtype": "f16",
-        "data": "synthetic (seeded 16 kHz clip; random-init Qwen3-ASR-0.6B-shaped f16 GGUF)" if not args.model else
+        # published numbers exist only for the f16 clip (ASR, and ASR + align); none for q8_0
+        "vs_baseline": None if args.q8 else round(value / (README_ALIGN_RTFX if actx else README_RTFX), 3),
+        "dtype": "q8_0 weights, int8 x int8 -> fp32" if args.q8 else "f16",
+        "data": f"synthetic (seeded 16 kHz clip; random-init Qwen3-ASR-0.6B-shaped {'q8_0' if args.q8 else 'f16'} GGUF"
+                + (", ForcedAligner-0.6B-shaped aligner GGUF)" if actx else ")") if not args.model else
                 "synthetic audio; model " + os.path.basename(args.model),
-        "config": {"workload": f"configs[1]: one {args.seconds:g} s clip per GPU per step, greedy decode budget "
-                               f"{ntok} tokens (3.5 tok/s), EOS ignored", "clips_per_gpu": args.batch,
+        "config": {"workload": workload(args, ntok, bool(actx)), "clips_per_gpu": args.batch,
                    "clip_seconds": args.seconds, "decode_tokens": ntok, "parallelism": f"dp{N} (utterance sharding)"},
         "decode_tokens_per_s": round(N * args.batch * ntok * args.steps / dt, 2),
         "stage_ms_per_step_rank0": {k: round(v / args.steps, 3) for k, v in tm.items()},
