@@ -14,6 +14,8 @@
 //
 // Decoder single token: split-K flash decoding (VALU; 2 q heads per kv head)
 // + a combine kernel.
+#include <cstdlib>
+
 #include "dev_common.h"
 #include "kernels.h"
 
@@ -341,7 +343,7 @@ void launch_prefill_attention(const PrefillAttnArgs &a, hipStream_t s) {
 // with sc1 loads, combines (S_inv = 1/S as ggml's flash_attn_ext) and writes the
 // fp16 attention output (MI355X_MICROARCH.md, inter-workgroup hand-off table,
 // row 1).  Counters are zero at rest: the last arriver re-arms its own.
-#define DSPLIT 64
+#define DSPLIT 64   // split of the batch-1..8 grid; larger batches use 256-key splits
 #define DWAVES 4
 
 __device__ __forceinline__ void st_sc1_x4(float *p, float4 f) {
@@ -371,11 +373,12 @@ __device__ __forceinline__ void ld_sc1_x4_burst9(const floatx4 *src, int tid, in
         : "memory");
 }
 
+template <int SPL>
 __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     __shared__ __attribute__((aligned(16))) uint16_t qs[2][128];
     __shared__ __attribute__((aligned(16))) uint16_t knew[128];
     __shared__ __attribute__((aligned(16))) uint16_t vnew[128];
-    __shared__ float sc[2][DSPLIT];
+    __shared__ float sc[2][SPL];
     __shared__ __attribute__((aligned(16))) float ored[DWAVES * 4][2][128];   // [wave x row][head][dim]
     __shared__ float cml[2][2];
     __shared__ float wsp[2][32];         // combine: per-split weights of a pass
@@ -399,13 +402,13 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     //      masked below; the cache is zero-initialised so they are finite.
     const long cbase = ((long)b * a.n_kv_head + g) * a.max_ctx;
     uint16_t *kc = a.kc + cbase * 128, *vc = a.vc + cbase * 128;
-    const int k0 = sp * DSPLIT;
+    const int k0 = sp * SPL;
     const int sub = lane >> 4, dl = (lane & 15) * 8;
-    constexpr int KPW = DSPLIT / DWAVES / 4;   // key rows per lane = 4
+    constexpr int KPW = SPL / DWAVES / 4;   // key rows per lane (4 or 16)
     half8 kv[KPW], vv[KPW];
 #pragma unroll
     for (int i = 0; i < KPW; i++) {
-        const int key = min(k0 + wid * (DSPLIT / DWAVES) + i * 4 + sub, a.max_ctx - 1);
+        const int key = min(k0 + wid * (SPL / DWAVES) + i * 4 + sub, a.max_ctx - 1);
         kv[i] = *(const half8 *)(kc + (long)key * 128 + dl);
         vv[i] = *(const half8 *)(vc + (long)key * 128 + dl);
     }
@@ -417,8 +420,8 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     const int pos = a.pos[b];
     const int nkv = pos + 1;
     const int nsp = gridDim.x;
-    const int k1 = min(nkv, k0 + DSPLIT);
-    const bool lastsp = sp == (nkv - 1) / DSPLIT;
+    const int k1 = min(nkv, k0 + SPL);
+    const bool lastsp = sp == (nkv - 1) / SPL;
     const float2 cs = *(const float2 *)(a.rope + ((long)pos * 64 + lane) * 2);
     // ---- ggml_rms_norm (double sum of fp32 squares) * weight, NEOX RoPE
     //      (src/text_decoder.cpp:640-700); v is only cast to fp16
@@ -447,7 +450,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     const half8 q0 = *(const half8 *)&qs[0][dl], q1 = *(const half8 *)&qs[1][dl];
 #pragma unroll
     for (int i = 0; i < KPW; i++) {
-        const int j = wid * (DSPLIT / DWAVES) + i * 4 + sub;
+        const int j = wid * (SPL / DWAVES) + i * 4 + sub;
         if (k0 + j == pos) { kv[i] = *(const half8 *)&knew[dl]; vv[i] = *(const half8 *)&vnew[dl]; }
         float s0 = 0.f, s1 = 0.f;
 #pragma unroll
@@ -465,13 +468,21 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     }
     __syncthreads();
     trace_mark(a.trace, 6);
-    // ---- split-local softmax statistics: wave h owns head h, lane = key
+    // ---- split-local softmax statistics: wave h owns head h, lane = key (mod 64)
     if (wid < 2) {
-        const float v = sc[wid][lane];
-        const float M = wave_max(v);
-        const float p = k0 + lane < k1 ? expf(v - M) : 0.f;
-        sc[wid][lane] = p;
-        const float l = wave_sum(p);
+        constexpr int KL = SPL / 64;
+        float v[KL], mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < KL; i++) { v[i] = sc[wid][lane + 64 * i]; mx = fmaxf(mx, v[i]); }
+        const float M = wave_max(mx);
+        float ps = 0.f;
+#pragma unroll
+        for (int i = 0; i < KL; i++) {
+            const float p = k0 + lane + 64 * i < k1 ? expf(v[i] - M) : 0.f;
+            sc[wid][lane + 64 * i] = p;
+            ps += p;
+        }
+        const float l = wave_sum(ps);
         if (lane == 0) { cml[wid][0] = M; cml[wid][1] = l; }
     }
     __syncthreads();
@@ -482,7 +493,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     for (int e = 0; e < 8; e++) { acc0[e] = 0.f; acc1[e] = 0.f; }
 #pragma unroll
     for (int i = 0; i < KPW; i++) {
-        const int j = wid * (DSPLIT / DWAVES) + i * 4 + sub;
+        const int j = wid * (SPL / DWAVES) + i * 4 + sub;
         const float p0 = sc[0][j], p1 = sc[1][j];
 #pragma unroll
         for (int e = 0; e < 8; e++) {
@@ -566,7 +577,18 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
 
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {
     if (a.B <= 0) return;
-    hipLaunchKernelGGL(decode_attn_kernel, dim3(a.grid_splits, a.n_kv_head, a.B), dim3(256), 0, s, a);
+    if (a.B <= 8) {
+        hipLaunchKernelGGL(decode_attn_kernel<DSPLIT>, dim3(a.grid_splits, a.n_kv_head, a.B), dim3(256), 0, s, a);
+    } else {   // batches: longer splits (fewer workgroups and partials per sequence)
+        static const int spl = [] { const char *e = getenv("QASR_ATT_SPL"); return e ? atoi(e) : 256; }();
+        if (spl == 128) {
+            const int g2 = (a.grid_splits * DSPLIT + 127) / 128;
+            hipLaunchKernelGGL(decode_attn_kernel<128>, dim3(g2, a.n_kv_head, a.B), dim3(256), 0, s, a);
+        } else {
+            const int g4 = (a.grid_splits * DSPLIT + 255) / 256;
+            hipLaunchKernelGGL(decode_attn_kernel<256>, dim3(g4, a.n_kv_head, a.B), dim3(256), 0, s, a);
+        }
+    }
 }
 
 int decode_split_len() { return DSPLIT; }

@@ -122,30 +122,38 @@ template <int D>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const float *__restrict__ x, int ldx, const int *__restrict__ row_idx, int M,
                                                       const float *__restrict__ w, float eps, uint16_t *__restrict__ y,
                                                       float *__restrict__ y32) {
+    // one wave per row; lane owns columns 4*lane + 256*i (16-B loads/stores)
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= M) return;
-    constexpr int PER = (D + 63) / 64;
+    static_assert(D % 256 == 0, "D must be a multiple of 256");
+    constexpr int PER = D / 256;
     const int src = row_idx ? row_idx[row] : row;
     const float *xr = x + (long)src * ldx;
-    float v[PER];
-    double s = 0.0;
+    float4 v[PER], wv[PER];
 #pragma unroll
     for (int i = 0; i < PER; i++) {
-        const int k = lane + 64 * i;
-        v[i] = k < D ? xr[k] : 0.0f;
-        s += (double)fmul_rn(v[i], v[i]);
+        v[i] = *(const float4 *)(xr + 4 * lane + 256 * i);
+        wv[i] = *(const float4 *)(w + 4 * lane + 256 * i);
     }
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < PER; i++)
+        s += ((double)fmul_rn(v[i].x, v[i].x) + (double)fmul_rn(v[i].y, v[i].y)) +
+             ((double)fmul_rn(v[i].z, v[i].z) + (double)fmul_rn(v[i].w, v[i].w));
     s = wave_sum_d(s);
     const float mean = (float)(s / D);
     const float scale = 1.0f / sqrtf(mean + eps);
 #pragma unroll
     for (int i = 0; i < PER; i++) {
-        const int k = lane + 64 * i;
-        if (k < D) {
-            const float t = fmul_rn(fmul_rn(v[i], scale), w[k]);
-            if (y32) y32[(long)row * D + k] = t;
-            else y[(long)row * D + k] = f_to_u16(t);
+        const float4 t = make_float4(fmul_rn(fmul_rn(v[i].x, scale), wv[i].x), fmul_rn(fmul_rn(v[i].y, scale), wv[i].y),
+                                     fmul_rn(fmul_rn(v[i].z, scale), wv[i].z), fmul_rn(fmul_rn(v[i].w, scale), wv[i].w));
+        const long o = (long)row * D + 4 * lane + 256 * i;
+        if (y32) {
+            *(float4 *)(y32 + o) = t;
+        } else {
+            const uint32_t lo = f_to_u16(t.x) | ((uint32_t)f_to_u16(t.y) << 16), hi = f_to_u16(t.z) | ((uint32_t)f_to_u16(t.w) << 16);
+            *(uint2 *)(y + o) = make_uint2(lo, hi);
         }
     }
 }

@@ -883,6 +883,12 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
     return 0;
 }
 
+// decode-batch projections: the weight-streaming skinny GEMM where it takes
+// the shape, the tiled GEMM otherwise
+static void dec_gemm(int epi, const GemmArgs &g, hipStream_t s) {
+    if (!launch_gemm_skinny(epi, g, s)) launch_gemm(AM_DENSE, epi, g, s);
+}
+
 // one decode step for B sequences: token d_tok at position d_pos
 // part: 0 = whole step, 1 = embed + layers, 2 = LM head (+argmax), 3 = bookkeeping;
 // splits: attention grid (64-key splits) covering the longest context of the step
@@ -915,7 +921,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
             GemmArgs q{};
             q.M = B; q.N = QD + 2 * KD; q.K = H; q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
             if (q8) gemm_q8(c, EPI_F32, q, c->d_x32, nullptr, H, 0, L.wqkv, L.wqkv_d, s, c->d_q8a, c->d_q8d);
-            else { q.A = c->d_xh; q.lda = H; q.W = L.wqkv; q.ldw = H; launch_gemm(AM_DENSE, EPI_F32, q, s); }
+            else { q.A = c->d_xh; q.lda = H; q.W = L.wqkv; q.ldw = H; dec_gemm(EPI_F32, q, s); }
         }
         DecodeAttnArgs da{};
         da.qkv = c->d_qkv; da.q_norm = L.q_norm; da.k_norm = L.k_norm; da.eps = hp.rms_eps; da.rope = c->rope;
@@ -958,14 +964,14 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
         } else {
             GemmArgs o{};
             o.A = c->d_att; o.lda = QD; o.W = L.wo; o.ldw = QD; o.M = B; o.N = H; o.K = QD; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
-            launch_gemm(AM_DENSE, EPI_F32, o, s);
+            dec_gemm(EPI_F32, o, s);
             launch_rmsnorm_f16(x, H, nullptr, B, H, L.ffn_norm, hp.rms_eps, c->d_xh, s);
             GemmArgs gu{};
             gu.A = c->d_xh; gu.lda = H; gu.W = L.wgu; gu.ldw = H; gu.M = B; gu.N = 2 * F; gu.K = H; gu.out_f16 = c->d_act; gu.ldo16 = F;
-            launch_gemm(AM_DENSE, EPI_SWIGLU_F16, gu, s);
+            dec_gemm(EPI_SWIGLU_F16, gu, s);
             GemmArgs dn{};
             dn.A = c->d_act; dn.lda = F; dn.W = L.wd; dn.ldw = F; dn.M = B; dn.N = H; dn.K = F; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
-            launch_gemm(AM_DENSE, EPI_F32, dn, s);
+            dec_gemm(EPI_F32, dn, s);
         }
     }
     if (part == 3 && skinny) return;   // bookkeeping is fused into the LM-head GEMV
@@ -985,7 +991,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
         GemmArgs lm{};
         lm.A = c->d_xh; lm.lda = H; lm.W = m->embd; lm.ldw = H; lm.M = B; lm.N = hp.vocab; lm.K = H;
         lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
-        launch_gemm(AM_DENSE, EPI_ARGMAX, lm, s);
+        dec_gemm(EPI_ARGMAX, lm, s);
     }
     if (part == 2) return;
 bookkeeping:

@@ -1,0 +1,215 @@
+// gemm_skinny.hip -- weight-streaming MFMA GEMM for decode batches
+// (9 <= M <= 128 rows: the batched decode step's projections and LM head).
+//
+// The tiled GEMM (gemm.hip) gives a 64-row batch only N/64 workgroups -- 64
+// for the 4096-wide QKV projection -- so a batch-64 decode step ran its
+// weight streams on a quarter of the CUs (32 us for 8 MB).  Here a workgroup
+// owns only 16*NT output columns and its KW waves split K, so the grid is
+// N/(16 NT) workgroups of up to 1024 waves in all; every weight byte is read
+// once (nontemporal), the activations (<= 64 x K fp16) come from L2.
+//
+// Operands go straight from global memory into MFMA fragments: per 128-wide
+// K chunk and sub-step s, lane (q = lane>>4, c = lane&15) loads k = 32s + 8q
+// .. +8 of row c, so one load instruction covers 64 contiguous bytes of each
+// of 16 rows (the natural v_mfma_f32_16x16x32_f16 layout; fp16 x fp16
+// products summed in fp32 = ggml_mul_mat F16 numerics, gemm.hip header).
+// The KW per-wave partial tiles are summed through LDS in wave order
+// (deterministic), then the epilogue runs the same per-element code as the
+// tiled GEMM: +bias, +residual, fp16 / SwiGLU / argmax outputs.
+#include "dev_common.h"
+#include "kernels.h"
+
+namespace qasr {
+
+__device__ __forceinline__ float silu_s(float g) { return g / (1.0f + expf(-g)); }
+
+// VAR: diagnostic knob for tools/skinny_bench.hip (1 = no activation loads,
+// 2 = no weight loads); the engine always launches VAR = 0
+template <int MT, int NT, int KW, int EPI, int VAR = 0>
+__global__ __launch_bounds__(64 * KW) void gemm_skinny_kernel(GemmArgs g) {
+    constexpr int NTILE = MT * NT;
+    __shared__ __attribute__((aligned(16))) floatx4 red[KW][NTILE][64];
+    __shared__ unsigned long long rmax[64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int n0 = blockIdx.x * 16 * NT, m0 = blockIdx.y * 16 * MT;
+    const int M = g.M;
+    const int q = lane >> 4, c16 = lane & 15;
+
+    const u32x4 *wrow[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) wrow[t] = (const u32x4 *)(g.W + (long)(n0 + t * 16 + c16) * g.ldw + q * 8);
+    const u32x4 *arow[MT];
+    bool aok[MT];
+#pragma unroll
+    for (int t = 0; t < MT; t++) {
+        const int m = m0 + t * 16 + c16;
+        aok[t] = m < M;
+        arow[t] = (const u32x4 *)(g.A + (long)(aok[t] ? m : 0) * g.lda + q * 8);
+    }
+
+    // epilogue element e -> (tile, row in tile, column in tile); the residual
+    // rows it adds are requested now, so their latency hides under the K loop
+    constexpr int EPT = (NTILE * 256 + 64 * KW - 1) / (64 * KW);
+    float resv[EPT];
+    if constexpr (EPI == EPI_F32) {
+#pragma unroll
+        for (int k = 0; k < EPT; k++) {
+            const int e = tid + k * 64 * KW;
+            const int t = e >> 8, rin = (e >> 4) & 15, cin = e & 15;
+            const int i = t / NT, j = t - i * NT;
+            const int row = m0 + i * 16 + rin, col = n0 + j * 16 + cin;
+            resv[k] = (e < NTILE * 256 && row < M && g.res) ? g.res[(long)row * g.ldr + col] : 0.f;
+        }
+    }
+
+    floatx4 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; i++)
+#pragma unroll
+        for (int j = 0; j < NT; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int nch = g.K >> 7;
+    u32x4 wb[2][NT][4], ab[2][MT][4];
+    auto load = [&](int buf, int c) {
+        const int off = c * 16;   // 128 halves = 16 u32x4
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+            for (int s = 0; s < 4; s++)
+                wb[buf][t][s] = (VAR & 2) ? u32x4{1u, 2u, 3u, (unsigned)c} : __builtin_nontemporal_load(wrow[t] + off + 4 * s);
+#pragma unroll
+        for (int t = 0; t < MT; t++)
+#pragma unroll
+            for (int s = 0; s < 4; s++)
+                ab[buf][t][s] = (VAR & 1) ? u32x4{4u, 5u, 6u, (unsigned)c} : aok[t] ? arow[t][off + 4 * s] : u32x4{0u, 0u, 0u, 0u};
+    };
+    auto mma = [&](int buf) {
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+#pragma unroll
+            for (int i = 0; i < MT; i++)
+#pragma unroll
+                for (int j = 0; j < NT; j++)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, ab[buf][i][s]),
+                                                                       __builtin_bit_cast(half8, wb[buf][j][s]), acc[i][j], 0, 0, 0);
+    };
+    int c = wid;
+    if (c < nch) load(0, c);
+    for (; c < nch; c += 2 * KW) {
+        if (c + KW < nch) load(1, c + KW);
+        mma(0);
+        if (c + KW >= nch) break;
+        if (c + 2 * KW < nch) load(0, c + 2 * KW);
+        mma(1);
+    }
+
+#pragma unroll
+    for (int i = 0; i < MT; i++)
+#pragma unroll
+        for (int j = 0; j < NT; j++) red[wid][i * NT + j][lane] = acc[i][j];
+    if constexpr (EPI == EPI_ARGMAX)
+        if (tid < 64) rmax[tid] = 0ull;
+    __syncthreads();
+
+    // element e -> (tile, row in tile, column in tile); the MFMA C layout puts
+    // (row, col) in lane ((row >> 2) << 4) | col, register row & 3
+    auto tile_val = [&](int t, int rin, int cin) {
+        const int l = ((rin >> 2) << 4) | cin, r = rin & 3;
+        float v = red[0][t][l][r];
+#pragma unroll
+        for (int w = 1; w < KW; w++) v += red[w][t][l][r];
+        return v;
+    };
+    if constexpr (EPI == EPI_SWIGLU_F16 || EPI == EPI_SWIGLU_F32) {
+        // interleaved 16-row [gate | up] weight blocks: tiles 2p / 2p+1
+        for (int e = tid; e < MT * (NT / 2) * 256; e += 64 * KW) {
+            const int tp = e >> 8, rin = (e >> 4) & 15, cin = e & 15;
+            const int i = tp / (NT / 2), p = tp - i * (NT / 2);
+            const int row = m0 + i * 16 + rin;
+            if (row >= M) continue;
+            const float gt = tile_val(i * NT + 2 * p, rin, cin), up = tile_val(i * NT + 2 * p + 1, rin, cin);
+            const float v = silu_s(gt) * up;
+            const int ocol = n0 / 2 + p * 16 + cin;
+            if constexpr (EPI == EPI_SWIGLU_F32) g.out_f32[(long)row * g.ldo + ocol] = v;
+            else g.out_f16[(long)row * g.ldo16 + ocol] = f_to_u16(v);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < EPT; k++) {
+            const int e = tid + k * 64 * KW;
+            if (e >= NTILE * 256) break;
+            const int t = e >> 8, rin = (e >> 4) & 15, cin = e & 15;
+            const int i = t / NT, j = t - i * NT;
+            const int rl = i * 16 + rin, row = m0 + rl;
+            const int col = n0 + j * 16 + cin;
+            float v = tile_val(t, rin, cin);
+            if (row >= M) continue;
+            if constexpr (EPI == EPI_ARGMAX) {
+                if (g.out_f32) g.out_f32[(long)row * g.ldo + col] = v;
+                if (g.n_valid == 0 || col < g.n_valid) atomicMax(&rmax[rl], argmax_key(v, col));
+            } else {
+                if (g.bias) v = fadd_rn(v, g.bias[col]);
+                if constexpr (EPI == EPI_F16) {
+                    g.out_f16[(long)row * g.ldo16 + col] = f_to_u16(v);
+                } else {
+                    if (g.res) v = fadd_rn(v, resv[k]);
+                    g.out_f32[(long)row * g.ldo + col] = v;
+                }
+            }
+        }
+        if constexpr (EPI == EPI_ARGMAX) {
+            __syncthreads();
+            if (tid < MT * 16 && m0 + tid < M) atomicMax(g.amax + m0 + tid, rmax[tid]);
+        }
+    }
+}
+
+// grid: (column tiles, row blocks of 16*MT rows).  Blocks of one column tile
+// are gridDim.x apart in dispatch order; with gridDim.x % 8 == 0 they share an
+// XCD under the observed round-robin placement, so the weight tile's re-reads
+// hit that XCD's L2 (speed only, never correctness).
+template <int MT, int NT, int KW, int EPI>
+static void run_skinny(const GemmArgs &g, hipStream_t s) {
+    dim3 grid(g.N / (16 * NT), (g.M + 16 * MT - 1) / (16 * MT));
+    hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, EPI>), grid, dim3(64 * KW), 0, s, g);
+}
+
+// MTMAX: rows per block cap (x16); smaller batches use the fewest tiles
+template <int MTMAX, int NT, int KW, int EPI>
+static void skinny_mt(const GemmArgs &g, hipStream_t s) {
+    const int mt = (g.M + 15) / 16;
+    if (mt <= 1 || MTMAX == 1) run_skinny<1, NT, KW, EPI>(g, s);
+    else if (mt <= 2 || MTMAX == 2) run_skinny<MTMAX >= 2 ? 2 : 1, NT, KW, EPI>(g, s);
+    else if (mt <= 3 || MTMAX == 3) run_skinny<MTMAX >= 3 ? 3 : 1, NT, KW, EPI>(g, s);
+    else run_skinny<MTMAX >= 4 ? 4 : 1, NT, KW, EPI>(g, s);
+}
+
+bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s) {
+    static const int off = [] { const char *e = getenv("QASR_SKINNY"); return e && e[0] == '0'; }();
+    if (off || g.M <= 0 || g.M > 128 || g.K % 128 != 0 || g.lda % 8 != 0 || g.ldw % 8 != 0) return false;
+    switch (epi) {
+        case EPI_F32:
+        case EPI_F16:
+            if (g.N % 16 != 0) return false;
+            // tilings picked with tools/skinny_bench.hip at M = 64
+            if (g.N >= 4096) {   // QKV: 256 column tiles, all rows per block, K over 8 waves
+                if (epi == EPI_F32) skinny_mt<4, 1, 8, EPI_F32>(g, s); else skinny_mt<4, 1, 8, EPI_F16>(g, s);
+            } else {             // o / down projections: 64 column tiles x 16-row blocks, K over 8 waves
+                if (epi == EPI_F32) skinny_mt<1, 1, 8, EPI_F32>(g, s); else skinny_mt<1, 1, 8, EPI_F16>(g, s);
+            }
+            return true;
+        case EPI_SWIGLU_F16:
+        case EPI_SWIGLU_F32:
+            if (g.N % 32 != 0) return false;
+            if (epi == EPI_SWIGLU_F16) skinny_mt<2, 2, 4, EPI_SWIGLU_F16>(g, s); else skinny_mt<2, 2, 4, EPI_SWIGLU_F32>(g, s);
+            return true;
+        case EPI_ARGMAX:
+            if (g.N % 64 != 0) return false;
+            skinny_mt<4, 4, 2, EPI_ARGMAX>(g, s);
+            return true;
+        default:
+            return false;
+    }
+}
+
+}  // namespace qasr

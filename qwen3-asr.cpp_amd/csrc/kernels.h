@@ -74,6 +74,9 @@ struct GemmArgs {
     const int8_t *Wq; const uint16_t *Wd;
 };
 void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s);
+// decode-batch GEMM (gemm_skinny.hip): dense A, M <= 128, K % 128 == 0; returns
+// false (nothing launched) for shapes it does not take.  QASR_SKINNY=0 disables.
+bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s);
 // ggml_mul_mat with Q8_0 weights: exact int8 block dots (v_mfma_i32_16x16x32_i8
 // per 32-wide K block), each scaled by d_w * d_x into an fp32 accumulator.
 // Requires K % 128 == 0 (every Qwen3-ASR width) or K % 32 == 0 (slower tile).

@@ -1,0 +1,91 @@
+// skinny_bench.hip -- microbenchmark of the decode-batch GEMM tilings
+// (csrc/gemm_skinny.hip, included directly so every template is reachable).
+// Per shape: hipGraph of NREP dependent launches over NL weight copies
+// (> 256 MiB Infinity Cache, so weights stream from HBM as in a decode step);
+// prints us per launch for tilings (MT, NT, KW) and the diagnostic variants
+// VAR 1 (no activation loads) / 2 (no weight loads).
+#include "../qwen3-asr.cpp_amd/csrc/gemm_skinny.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+using namespace qasr;
+
+struct Shape { const char *name; int N, K, epi; };
+
+template <int MT, int NT, int KW, int EPI, int VAR>
+static double time_cfg(GemmArgs g, const std::vector<uint16_t *> &ws, hipStream_t s, const char *tag) {
+    const int NREP = 64;
+    dim3 grid(g.N / (16 * NT), (g.M + 16 * MT - 1) / (16 * MT));
+    hipGraph_t graph; hipGraphExec_t ex;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+    for (int r = 0; r < NREP; r++) {
+        g.W = ws[r % ws.size()];
+        hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, EPI, VAR>), grid, dim3(64 * KW), 0, s, g);
+    }
+    CK(hipStreamEndCapture(s, &graph));
+    CK(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
+    hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    CK(hipGraphLaunch(ex, s)); CK(hipStreamSynchronize(s));
+    float best = 1e30f;
+    for (int it = 0; it < 5; it++) {
+        CK(hipEventRecord(a, s)); CK(hipGraphLaunch(ex, s)); CK(hipEventRecord(b, s)); CK(hipEventSynchronize(b));
+        float ms; CK(hipEventElapsedTime(&ms, a, b)); best = ms < best ? ms : best;
+    }
+    const double us = best * 1e3 / NREP;
+    const double bytes = (double)g.N * g.K * 2;
+    printf("  %-28s MT%d NT%d KW%d VAR%d  %7.2f us  %6.0f GB/s  grid %4dx%d\n", tag, MT, NT, KW, VAR, us, bytes / us * 1e-3, grid.x, grid.y);
+    CK(hipGraphExecDestroy(ex)); CK(hipGraphDestroy(graph));
+    return us;
+}
+
+int main(int argc, char **argv) {
+    const int M = argc > 1 ? atoi(argv[1]) : 64;
+    hipStream_t s; CK(hipStreamCreate(&s));
+    Shape shapes[] = {{"qkv 4096x1024", 4096, 1024, EPI_F32}, {"o 1024x2048", 1024, 2048, EPI_F32},
+                      {"gu 6144x1024 swiglu", 6144, 1024, EPI_SWIGLU_F16}, {"down 1024x3072", 1024, 3072, EPI_F32}};
+    uint16_t *A; float *out, *res; uint16_t *out16;
+    CK(hipMalloc(&A, (size_t)128 * 4096 * 2)); CK(hipMemset(A, 0x11, (size_t)128 * 4096 * 2));
+    CK(hipMalloc(&out, (size_t)128 * 8192 * 4)); CK(hipMalloc(&res, (size_t)128 * 8192 * 4)); CK(hipMalloc(&out16, (size_t)128 * 8192 * 2));
+    CK(hipMemset(res, 0, (size_t)128 * 8192 * 4));
+    printf("M = %d\n", M);
+    for (const Shape &sh : shapes) {
+        const size_t wb = (size_t)sh.N * sh.K * 2;
+        const int NL = (int)((600ull << 20) / wb) + 1;
+        std::vector<uint16_t *> ws(NL);
+        for (auto &w : ws) { CK(hipMalloc(&w, wb)); CK(hipMemset(w, 0x22, wb)); }
+        GemmArgs g{};
+        g.A = A; g.lda = sh.K; g.ldw = sh.K; g.M = M; g.N = sh.N; g.K = sh.K;
+        g.out_f32 = out; g.ldo = sh.N; g.res = res; g.ldr = sh.N; g.out_f16 = out16; g.ldo16 = sh.N;
+        printf("%s (%zu MB, %d copies)\n", sh.name, wb >> 20, NL);
+        if (sh.epi == EPI_F32) {
+            time_cfg<4, 1, 4, EPI_F32, 0>(g, ws, s, "full");
+            time_cfg<4, 1, 4, EPI_F32, 1>(g, ws, s, "no A");
+            time_cfg<4, 1, 4, EPI_F32, 2>(g, ws, s, "no W");
+            time_cfg<4, 1, 4, EPI_F32, 3>(g, ws, s, "no loads");
+            time_cfg<2, 1, 4, EPI_F32, 0>(g, ws, s, "full");
+            time_cfg<1, 1, 4, EPI_F32, 0>(g, ws, s, "full");
+            time_cfg<1, 1, 8, EPI_F32, 0>(g, ws, s, "full");
+            time_cfg<1, 1, 8, EPI_F32, 1>(g, ws, s, "no A");
+            time_cfg<1, 1, 16, EPI_F32, 0>(g, ws, s, "full");
+            time_cfg<2, 1, 8, EPI_F32, 0>(g, ws, s, "full");
+            time_cfg<4, 1, 8, EPI_F32, 0>(g, ws, s, "full");
+            time_cfg<4, 1, 2, EPI_F32, 0>(g, ws, s, "full");
+            time_cfg<4, 2, 4, EPI_F32, 0>(g, ws, s, "full");
+        } else {
+            time_cfg<4, 2, 4, EPI_SWIGLU_F16, 0>(g, ws, s, "full");
+            time_cfg<4, 2, 4, EPI_SWIGLU_F16, 1>(g, ws, s, "no A");
+            time_cfg<4, 2, 4, EPI_SWIGLU_F16, 2>(g, ws, s, "no W");
+            time_cfg<2, 2, 4, EPI_SWIGLU_F16, 0>(g, ws, s, "full");
+            time_cfg<1, 2, 4, EPI_SWIGLU_F16, 0>(g, ws, s, "full");
+            time_cfg<1, 2, 8, EPI_SWIGLU_F16, 0>(g, ws, s, "full");
+            time_cfg<4, 2, 8, EPI_SWIGLU_F16, 0>(g, ws, s, "full");
+            time_cfg<4, 2, 2, EPI_SWIGLU_F16, 0>(g, ws, s, "full");
+        }
+        for (auto &w : ws) CK(hipFree(w));
+    }
+    return 0;
+}
