@@ -570,7 +570,15 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
         M = Mn;
     }
     const float inv = L > 0.f ? 1.0f / L : 0.f;   // ggml: S_inv = 1/S, VKQ *= S_inv
-    if (a.out32) a.out32[(long)b * QD + (2 * g + hh) * 128 + d] = O * inv;
+    if (a.outq) {   // quantised for the Q8_0 o-proj: a 32-block = 32 lanes of one wave
+        const float v = O * inv;
+        float am = fabsf(v);
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+        const long e = (long)b * QD + (2 * g + hh) * 128 + d;
+        a.outq[e] = q8_quant(v, am);
+        if ((d & 31) == 0) a.outd[e >> 5] = q8_scale(am);
+    } else if (a.out32) a.out32[(long)b * QD + (2 * g + hh) * 128 + d] = O * inv;
     else a.out[(long)b * QD + (2 * g + hh) * 128 + d] = f_to_u16(O * inv);
     trace_mark(a.trace, 4);
 }

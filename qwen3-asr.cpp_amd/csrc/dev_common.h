@@ -94,3 +94,12 @@ __device__ __forceinline__ float gelu_lut(float x, const uint16_t *__restrict__ 
     if (x >= 10.0f) return x;
     return u16_to_f(lut[f_to_u16(x)]);
 }
+
+// ggml quantize_row_q8_0 (x86 path) for one value of a 32-block whose |max| is
+// amax: d = fp16(amax / 127), q = round-half-even(v * 127 / amax)
+// (quantize_q8_kernel, elementwise.hip, is the reference restatement)
+__device__ __forceinline__ float q8_scale(float amax) { return u16_to_f(f_to_u16(amax / 127.f)); }
+__device__ __forceinline__ int8_t q8_quant(float v, float amax) {
+    const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+    return (int8_t)__builtin_rintf(fmul_rn(v, id));
+}

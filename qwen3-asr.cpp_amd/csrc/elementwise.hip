@@ -121,12 +121,14 @@ void launch_layernorm_f16(const float *x, int M, int D, const float *w, const fl
 template <int D>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const float *__restrict__ x, int ldx, const int *__restrict__ row_idx, int M,
                                                       const float *__restrict__ w, float eps, uint16_t *__restrict__ y,
-                                                      float *__restrict__ y32) {
-    // one wave per row; lane owns columns 4*lane + 256*i (16-B loads/stores)
+                                                      float *__restrict__ y32, int8_t *__restrict__ yq, float *__restrict__ yd) {
+    // one wave per row; lane owns columns 4*lane + 256*i (16-B loads/stores).
+    // yq/yd: Q8_0 output (int8 + fp32 block scales) of the same fp32 values,
+    // a 32-block = 8 lanes
+    static_assert(D % 256 == 0, "D must be a multiple of 256");
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= M) return;
-    static_assert(D % 256 == 0, "D must be a multiple of 256");
     constexpr int PER = D / 256;
     const int src = row_idx ? row_idx[row] : row;
     const float *xr = x + (long)src * ldx;
@@ -149,7 +151,16 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float *__restrict__ 
         const float4 t = make_float4(fmul_rn(fmul_rn(v[i].x, scale), wv[i].x), fmul_rn(fmul_rn(v[i].y, scale), wv[i].y),
                                      fmul_rn(fmul_rn(v[i].z, scale), wv[i].z), fmul_rn(fmul_rn(v[i].w, scale), wv[i].w));
         const long o = (long)row * D + 4 * lane + 256 * i;
-        if (y32) {
+        if (yq) {
+            float am = fmaxf(fmaxf(fabsf(t.x), fabsf(t.y)), fmaxf(fabsf(t.z), fabsf(t.w)));
+            am = fmaxf(am, __shfl_xor(am, 1, 64));
+            am = fmaxf(am, __shfl_xor(am, 2, 64));
+            am = fmaxf(am, __shfl_xor(am, 4, 64));
+            const uint32_t u = (uint32_t)(uint8_t)q8_quant(t.x, am) | (uint32_t)(uint8_t)q8_quant(t.y, am) << 8 |
+                               (uint32_t)(uint8_t)q8_quant(t.z, am) << 16 | (uint32_t)(uint8_t)q8_quant(t.w, am) << 24;
+            *(uint32_t *)(yq + o) = u;
+            if ((lane & 7) == 0) yd[(long)row * (D / 32) + lane / 8 + 8 * i] = q8_scale(am);
+        } else if (y32) {
             *(float4 *)(y32 + o) = t;
         } else {
             const uint32_t lo = f_to_u16(t.x) | ((uint32_t)f_to_u16(t.y) << 16), hi = f_to_u16(t.z) | ((uint32_t)f_to_u16(t.w) << 16);
@@ -158,15 +169,24 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float *__restrict__ 
     }
 }
 
-void launch_rmsnorm_f16(const float *x, int ldx, const int *row_idx, int M, int D, const float *w, float eps, uint16_t *y,
-                        hipStream_t s, float *y32) {
+static void rmsnorm_any(const float *x, int ldx, const int *row_idx, int M, int D, const float *w, float eps, uint16_t *y,
+                        float *y32, int8_t *yq, float *yd, hipStream_t s) {
     if (M <= 0) return;
     dim3 grid((M + 3) / 4);
     switch (D) {
-        case 1024: hipLaunchKernelGGL(rmsnorm_kernel<1024>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y, y32); break;
-        case 256: hipLaunchKernelGGL(rmsnorm_kernel<256>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y, y32); break;
-        default: hipLaunchKernelGGL(rmsnorm_kernel<2048>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y, y32); break;
+        case 1024: hipLaunchKernelGGL(rmsnorm_kernel<1024>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y, y32, yq, yd); break;
+        case 256: hipLaunchKernelGGL(rmsnorm_kernel<256>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y, y32, yq, yd); break;
+        default: hipLaunchKernelGGL(rmsnorm_kernel<2048>, grid, dim3(256), 0, s, x, ldx, row_idx, M, w, eps, y, y32, yq, yd); break;
     }
+}
+
+void launch_rmsnorm_f16(const float *x, int ldx, const int *row_idx, int M, int D, const float *w, float eps, uint16_t *y,
+                        hipStream_t s, float *y32) {
+    rmsnorm_any(x, ldx, row_idx, M, D, w, eps, y, y32, nullptr, nullptr, s);
+}
+
+void launch_rmsnorm_q8(const float *x, int ldx, int M, int D, const float *w, float eps, int8_t *yq, float *yd, hipStream_t s) {
+    rmsnorm_any(x, ldx, nullptr, M, D, w, eps, nullptr, nullptr, yq, yd, s);
 }
 
 // --------------------------------------------------------- embedding/splice

@@ -206,12 +206,22 @@ static int upload(qasr_ctx *c, DevBuf &b, const std::vector<T> &v) {
 // optional conv_out gather) into c->q8a / c->q8d, then the int8 block GEMM.
 // g carries M, N, K and the epilogue.
 static void gemm_q8(qasr_ctx *c, int epi, GemmArgs g, const float *a32, const uint16_t *a16, int lda, int gather_C,
-                    const uint16_t *W, const uint16_t *Wd, hipStream_t s, int8_t *qa = nullptr, float *qd = nullptr) {
+                    const uint16_t *W, const uint16_t *Wd, hipStream_t s, int8_t *qa = nullptr, float *qd = nullptr,
+                    bool decode = false) {
     if (!qa) { qa = c->q8a.as<int8_t>(); qd = c->q8d.as<float>(); }
     launch_quantize_q8(a32, a16, lda, g.M, g.K, gather_C, qa, qd, s);
     g.Aq = qa; g.lda = g.K; g.Ad = qd; g.ldad = g.K / 32;
     g.Wq = (const int8_t *)W; g.ldw = g.K; g.Wd = Wd;
+    if (decode && launch_gemm_skinny_q8(epi, g, s)) return;
     launch_gemm_q8(epi, g, s);
+}
+
+// decode batches: activations already quantised into d_q8a / d_q8d by the
+// producing kernel (rmsnorm_q8, the attention combiner)
+static void gemm_q8_pre(qasr_ctx *c, int epi, GemmArgs g, const uint16_t *W, const uint16_t *Wd, hipStream_t s) {
+    g.Aq = c->d_q8a; g.lda = g.K; g.Ad = c->d_q8d; g.ldad = g.K / 32;
+    g.Wq = (const int8_t *)W; g.ldw = g.K; g.Wd = Wd;
+    if (!launch_gemm_skinny_q8(epi, g, s)) launch_gemm_q8(epi, g, s);
 }
 
 static int ensure_q8(qasr_ctx *c, size_t rows, size_t kmax, size_t x32_cols) {
@@ -917,18 +927,23 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
             q.trace = tr(0);
             if (!(skip & 1)) launch_gemv(EPI_F32, q, s);
         } else {
-            launch_rmsnorm_f16(x, H, nullptr, B, H, L.attn_norm, hp.rms_eps, c->d_xh, s, q8 ? c->d_x32 : nullptr);
             GemmArgs q{};
             q.M = B; q.N = QD + 2 * KD; q.K = H; q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
-            if (q8) gemm_q8(c, EPI_F32, q, c->d_x32, nullptr, H, 0, L.wqkv, L.wqkv_d, s, c->d_q8a, c->d_q8d);
-            else { q.A = c->d_xh; q.lda = H; q.W = L.wqkv; q.ldw = H; dec_gemm(EPI_F32, q, s); }
+            if (q8) {
+                launch_rmsnorm_q8(x, H, B, H, L.attn_norm, hp.rms_eps, c->d_q8a, c->d_q8d, s);
+                gemm_q8_pre(c, EPI_F32, q, L.wqkv, L.wqkv_d, s);
+            } else {
+                launch_rmsnorm_f16(x, H, nullptr, B, H, L.attn_norm, hp.rms_eps, c->d_xh, s);
+                q.A = c->d_xh; q.lda = H; q.W = L.wqkv; q.ldw = H; dec_gemm(EPI_F32, q, s);
+            }
         }
         DecodeAttnArgs da{};
         da.qkv = c->d_qkv; da.q_norm = L.q_norm; da.k_norm = L.k_norm; da.eps = hp.rms_eps; da.rope = c->rope;
         da.pos = c->d_pos; da.kc = c->kc + l * layer_kv; da.vc = c->vc + l * layer_kv; da.seq_slot = c->d_slot; da.B = B;
         da.n_head = hp.n_head; da.n_kv_head = hp.n_kv_head; da.max_ctx = c->max_ctx; da.max_splits = c->max_splits; da.grid_splits = splits;
         da.scale = 1.0f / sqrtf(128.0f); da.part = c->d_part; da.counter = c->d_counter; da.out = c->d_att;
-        da.out32 = q8 ? (skinny ? c->d_att32 : c->d_x32) : nullptr;
+        da.out32 = q8 && skinny ? c->d_att32 : nullptr;
+        if (q8 && !skinny) { da.outq = c->d_q8a; da.outd = c->d_q8d; }
         da.trace = tr(1);
         if (!(skip & 2)) launch_decode_attention(da, s);
         if (skinny) {
@@ -953,14 +968,14 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
         } else if (q8) {
             GemmArgs o{};
             o.M = B; o.N = H; o.K = QD; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
-            gemm_q8(c, EPI_F32, o, c->d_x32, nullptr, QD, 0, L.wo, L.wo_d, s, c->d_q8a, c->d_q8d);
-            launch_rmsnorm_f16(x, H, nullptr, B, H, L.ffn_norm, hp.rms_eps, c->d_xh, s, c->d_x32);
+            gemm_q8_pre(c, EPI_F32, o, L.wo, L.wo_d, s);
+            launch_rmsnorm_q8(x, H, B, H, L.ffn_norm, hp.rms_eps, c->d_q8a, c->d_q8d, s);
             GemmArgs gu{};
             gu.M = B; gu.N = 2 * F; gu.K = H; gu.out_f32 = c->d_x32; gu.ldo = F;
-            gemm_q8(c, EPI_SWIGLU_F32, gu, c->d_x32, nullptr, H, 0, L.wgu, L.wgu_d, s, c->d_q8a, c->d_q8d);
+            gemm_q8_pre(c, EPI_SWIGLU_F32, gu, L.wgu, L.wgu_d, s);
             GemmArgs dn{};
             dn.M = B; dn.N = H; dn.K = F; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
-            gemm_q8(c, EPI_F32, dn, c->d_x32, nullptr, F, 0, L.wd, L.wd_d, s, c->d_q8a, c->d_q8d);
+            gemm_q8(c, EPI_F32, dn, c->d_x32, nullptr, F, 0, L.wd, L.wd_d, s, c->d_q8a, c->d_q8d, true);
         } else {
             GemmArgs o{};
             o.A = c->d_att; o.lda = QD; o.W = L.wo; o.ldw = QD; o.M = B; o.N = H; o.K = QD; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;

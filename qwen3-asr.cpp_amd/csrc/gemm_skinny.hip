@@ -22,6 +22,86 @@
 namespace qasr {
 
 __device__ __forceinline__ float silu_s(float g) { return g / (1.0f + expf(-g)); }
+typedef int intx4 __attribute__((ext_vector_type(4)));
+
+// Residual prefetch: epilogue element e -> (tile, row in tile, column in
+// tile); the residual values a thread adds are requested at kernel entry, so
+// their latency hides under the K loop.
+template <int MT, int NT, int KW, int EPI>
+struct SkinnyEpi {
+    static constexpr int NTILE = MT * NT;
+    static constexpr int EPT = (NTILE * 256 + 64 * KW - 1) / (64 * KW);
+    float resv[EPT];
+
+    __device__ __forceinline__ void prefetch(const GemmArgs &g, int m0, int n0, int tid) {
+        if constexpr (EPI == EPI_F32) {
+#pragma unroll
+            for (int k = 0; k < EPT; k++) {
+                const int e = tid + k * 64 * KW;
+                const int t = e >> 8, rin = (e >> 4) & 15, cin = e & 15;
+                const int i = t / NT, j = t - i * NT;
+                const int row = m0 + i * 16 + rin, col = n0 + j * 16 + cin;
+                resv[k] = (e < NTILE * 256 && row < g.M && g.res) ? g.res[(long)row * g.ldr + col] : 0.f;
+            }
+        }
+    }
+
+    // red: the KW waves' partial tiles in the MFMA C layout ((row, col) in lane
+    // ((row >> 2) << 4) | col, register row & 3), summed here in wave order
+    __device__ __forceinline__ void run(const GemmArgs &g, floatx4 (*red)[NTILE][64], unsigned long long *rmax, int m0,
+                                        int n0, int tid) {
+        const int M = g.M;
+        auto tile_val = [&](int t, int rin, int cin) {
+            const int l = ((rin >> 2) << 4) | cin, r = rin & 3;
+            float v = red[0][t][l][r];
+#pragma unroll
+            for (int w = 1; w < KW; w++) v += red[w][t][l][r];
+            return v;
+        };
+        if constexpr (EPI == EPI_SWIGLU_F16 || EPI == EPI_SWIGLU_F32) {
+            // interleaved 16-row [gate | up] weight blocks: tiles 2p / 2p+1
+            for (int e = tid; e < MT * (NT / 2) * 256; e += 64 * KW) {
+                const int tp = e >> 8, rin = (e >> 4) & 15, cin = e & 15;
+                const int i = tp / (NT / 2), p = tp - i * (NT / 2);
+                const int row = m0 + i * 16 + rin;
+                if (row >= M) continue;
+                const float gt = tile_val(i * NT + 2 * p, rin, cin), up = tile_val(i * NT + 2 * p + 1, rin, cin);
+                const float v = silu_s(gt) * up;
+                const int ocol = n0 / 2 + p * 16 + cin;
+                if constexpr (EPI == EPI_SWIGLU_F32) g.out_f32[(long)row * g.ldo + ocol] = v;
+                else g.out_f16[(long)row * g.ldo16 + ocol] = f_to_u16(v);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < EPT; k++) {
+                const int e = tid + k * 64 * KW;
+                if (e >= NTILE * 256) break;
+                const int t = e >> 8, rin = (e >> 4) & 15, cin = e & 15;
+                const int i = t / NT, j = t - i * NT;
+                const int rl = i * 16 + rin, row = m0 + rl;
+                const int col = n0 + j * 16 + cin;
+                float v = tile_val(t, rin, cin);
+                if (row >= M) continue;
+                if constexpr (EPI == EPI_ARGMAX) {
+                    if (g.out_f32) g.out_f32[(long)row * g.ldo + col] = v;
+                    if (g.n_valid == 0 || col < g.n_valid) atomicMax(&rmax[rl], argmax_key(v, col));
+                } else {
+                    if (g.bias) v = fadd_rn(v, g.bias[col]);
+                    if constexpr (EPI == EPI_F16) {
+                        g.out_f16[(long)row * g.ldo16 + col] = f_to_u16(v);
+                    } else {
+                        if (g.res) v = fadd_rn(v, resv[k]);
+                        g.out_f32[(long)row * g.ldo + col] = v;
+                    }
+                }
+            }
+            if constexpr (EPI == EPI_ARGMAX) {
+                __syncthreads();
+                if (tid < MT * 16 && m0 + tid < M) atomicMax(g.amax + m0 + tid, rmax[tid]);
+            }
+        }
+    }
+};
 
 // VAR: diagnostic knob for tools/skinny_bench.hip (1 = no activation loads,
 // 2 = no weight loads); the engine always launches VAR = 0
@@ -46,21 +126,8 @@ __global__ __launch_bounds__(64 * KW) void gemm_skinny_kernel(GemmArgs g) {
         aok[t] = m < M;
         arow[t] = (const u32x4 *)(g.A + (long)(aok[t] ? m : 0) * g.lda + q * 8);
     }
-
-    // epilogue element e -> (tile, row in tile, column in tile); the residual
-    // rows it adds are requested now, so their latency hides under the K loop
-    constexpr int EPT = (NTILE * 256 + 64 * KW - 1) / (64 * KW);
-    float resv[EPT];
-    if constexpr (EPI == EPI_F32) {
-#pragma unroll
-        for (int k = 0; k < EPT; k++) {
-            const int e = tid + k * 64 * KW;
-            const int t = e >> 8, rin = (e >> 4) & 15, cin = e & 15;
-            const int i = t / NT, j = t - i * NT;
-            const int row = m0 + i * 16 + rin, col = n0 + j * 16 + cin;
-            resv[k] = (e < NTILE * 256 && row < M && g.res) ? g.res[(long)row * g.ldr + col] : 0.f;
-        }
-    }
+    SkinnyEpi<MT, NT, KW, EPI> epi;
+    epi.prefetch(g, m0, n0, tid);
 
     floatx4 acc[MT][NT];
 #pragma unroll
@@ -110,58 +177,117 @@ __global__ __launch_bounds__(64 * KW) void gemm_skinny_kernel(GemmArgs g) {
     if constexpr (EPI == EPI_ARGMAX)
         if (tid < 64) rmax[tid] = 0ull;
     __syncthreads();
+    epi.run(g, red, rmax, m0, n0, tid);
+}
 
-    // element e -> (tile, row in tile, column in tile); the MFMA C layout puts
-    // (row, col) in lane ((row >> 2) << 4) | col, register row & 3
-    auto tile_val = [&](int t, int rin, int cin) {
-        const int l = ((rin >> 2) << 4) | cin, r = rin & 3;
-        float v = red[0][t][l][r];
+// ---------------------------------------------------------------- Q8_0
+// ggml_mul_mat(W Q8_0, X): activations already quantised to int8 + fp32
+// block scales (quantize_q8_kernel / the fused producers), weights int8 +
+// fp16 block scales.  Per 32-wide block one v_mfma_i32_16x16x32_i8 from a
+// zero accumulator gives the exact integer dot, then acc += (d_w * d_x) *
+// sumi in fp32 -- the numerics of gemm_q8_kernel (gemm.hip).  Operands are
+// 8-byte fragment loads (one instruction = 32 contiguous bytes of 16 rows).
+template <int MT, int NT, int KW, int EPI>
+__global__ __launch_bounds__(64 * KW) void gemm_skinny_q8_kernel(GemmArgs g) {
+    constexpr int NTILE = MT * NT;
+    __shared__ __attribute__((aligned(16))) floatx4 red[KW][NTILE][64];
+    __shared__ unsigned long long rmax[64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int n0 = blockIdx.x * 16 * NT, m0 = blockIdx.y * 16 * MT;
+    const int M = g.M, nbk = g.K >> 5;
+    const int q = lane >> 4, c16 = lane & 15;
+
+    const int8_t *wrow[NT];
+    const uint16_t *wdrow[NT];
 #pragma unroll
-        for (int w = 1; w < KW; w++) v += red[w][t][l][r];
-        return v;
-    };
-    if constexpr (EPI == EPI_SWIGLU_F16 || EPI == EPI_SWIGLU_F32) {
-        // interleaved 16-row [gate | up] weight blocks: tiles 2p / 2p+1
-        for (int e = tid; e < MT * (NT / 2) * 256; e += 64 * KW) {
-            const int tp = e >> 8, rin = (e >> 4) & 15, cin = e & 15;
-            const int i = tp / (NT / 2), p = tp - i * (NT / 2);
-            const int row = m0 + i * 16 + rin;
-            if (row >= M) continue;
-            const float gt = tile_val(i * NT + 2 * p, rin, cin), up = tile_val(i * NT + 2 * p + 1, rin, cin);
-            const float v = silu_s(gt) * up;
-            const int ocol = n0 / 2 + p * 16 + cin;
-            if constexpr (EPI == EPI_SWIGLU_F32) g.out_f32[(long)row * g.ldo + ocol] = v;
-            else g.out_f16[(long)row * g.ldo16 + ocol] = f_to_u16(v);
-        }
-    } else {
+    for (int t = 0; t < NT; t++) {
+        wrow[t] = g.Wq + (long)(n0 + t * 16 + c16) * g.ldw + q * 8;
+        wdrow[t] = g.Wd + (long)(n0 + t * 16 + c16) * nbk;
+    }
+    const int8_t *arow[MT];
+    bool aok[MT];
+    const float *adrow[MT][4];   // scales of the C-layout rows 4q + r of tile t
 #pragma unroll
-        for (int k = 0; k < EPT; k++) {
-            const int e = tid + k * 64 * KW;
-            if (e >= NTILE * 256) break;
-            const int t = e >> 8, rin = (e >> 4) & 15, cin = e & 15;
-            const int i = t / NT, j = t - i * NT;
-            const int rl = i * 16 + rin, row = m0 + rl;
-            const int col = n0 + j * 16 + cin;
-            float v = tile_val(t, rin, cin);
-            if (row >= M) continue;
-            if constexpr (EPI == EPI_ARGMAX) {
-                if (g.out_f32) g.out_f32[(long)row * g.ldo + col] = v;
-                if (g.n_valid == 0 || col < g.n_valid) atomicMax(&rmax[rl], argmax_key(v, col));
-            } else {
-                if (g.bias) v = fadd_rn(v, g.bias[col]);
-                if constexpr (EPI == EPI_F16) {
-                    g.out_f16[(long)row * g.ldo16 + col] = f_to_u16(v);
-                } else {
-                    if (g.res) v = fadd_rn(v, resv[k]);
-                    g.out_f32[(long)row * g.ldo + col] = v;
-                }
-            }
-        }
-        if constexpr (EPI == EPI_ARGMAX) {
-            __syncthreads();
-            if (tid < MT * 16 && m0 + tid < M) atomicMax(g.amax + m0 + tid, rmax[tid]);
+    for (int t = 0; t < MT; t++) {
+        const int m = m0 + t * 16 + c16;
+        aok[t] = m < M;
+        arow[t] = g.Aq + (long)(aok[t] ? m : 0) * g.lda + q * 8;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int mr = m0 + t * 16 + 4 * q + r;
+            adrow[t][r] = g.Ad + (long)(mr < M ? mr : 0) * g.ldad;
         }
     }
+    SkinnyEpi<MT, NT, KW, EPI> epi;
+    epi.prefetch(g, m0, n0, tid);
+
+    floatx4 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; i++)
+#pragma unroll
+        for (int j = 0; j < NT; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // one 128-wide K chunk = 4 blocks
+    const int nch = g.K >> 7;
+    long wb[2][NT][4], ab[2][MT][4];
+    uint2 wd[2][NT];          // 4 fp16 weight scales of the chunk
+    float4 ad[2][MT][4];      // [tile][r] 4 activation block scales of the chunk
+    auto load = [&](int buf, int c) {
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) wb[buf][t][u] = __builtin_nontemporal_load((const long *)(wrow[t] + c * 128 + u * 32));
+            wd[buf][t] = *(const uint2 *)(wdrow[t] + c * 4);
+        }
+#pragma unroll
+        for (int t = 0; t < MT; t++) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) ab[buf][t][u] = aok[t] ? *(const long *)(arow[t] + c * 128 + u * 32) : 0l;
+#pragma unroll
+            for (int r = 0; r < 4; r++) ad[buf][t][r] = *(const float4 *)(adrow[t][r] + c * 4);
+        }
+    };
+    auto mma = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            float sb[NT];
+#pragma unroll
+            for (int j = 0; j < NT; j++) {
+                const uint32_t h = u < 2 ? wd[buf][j].x : wd[buf][j].y;
+                sb[j] = u16_to_f((uint16_t)((u & 1) ? h >> 16 : h & 0xffffu));
+            }
+#pragma unroll
+            for (int i = 0; i < MT; i++)
+#pragma unroll
+                for (int j = 0; j < NT; j++) {
+                    const intx4 ci = __builtin_amdgcn_mfma_i32_16x16x32_i8(ab[buf][i][u], wb[buf][j][u], intx4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const float4 a4 = ad[buf][i][r];
+                        const float sa = u == 0 ? a4.x : u == 1 ? a4.y : u == 2 ? a4.z : a4.w;
+                        acc[i][j][r] = fmaf(fmul_rn(sb[j], sa), (float)ci[r], acc[i][j][r]);
+                    }
+                }
+        }
+    };
+    int c = wid;
+    if (c < nch) load(0, c);
+    for (; c < nch; c += 2 * KW) {
+        if (c + KW < nch) load(1, c + KW);
+        mma(0);
+        if (c + KW >= nch) break;
+        if (c + 2 * KW < nch) load(0, c + 2 * KW);
+        mma(1);
+    }
+
+#pragma unroll
+    for (int i = 0; i < MT; i++)
+#pragma unroll
+        for (int j = 0; j < NT; j++) red[wid][i * NT + j][lane] = acc[i][j];
+    if constexpr (EPI == EPI_ARGMAX)
+        if (tid < 64) rmax[tid] = 0ull;
+    __syncthreads();
+    epi.run(g, red, rmax, m0, n0, tid);
 }
 
 // grid: (column tiles, row blocks of 16*MT rows).  Blocks of one column tile
@@ -172,6 +298,21 @@ template <int MT, int NT, int KW, int EPI>
 static void run_skinny(const GemmArgs &g, hipStream_t s) {
     dim3 grid(g.N / (16 * NT), (g.M + 16 * MT - 1) / (16 * MT));
     hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, EPI>), grid, dim3(64 * KW), 0, s, g);
+}
+
+template <int MT, int NT, int KW, int EPI>
+static void run_skinny_q8(const GemmArgs &g, hipStream_t s) {
+    dim3 grid(g.N / (16 * NT), (g.M + 16 * MT - 1) / (16 * MT));
+    hipLaunchKernelGGL((gemm_skinny_q8_kernel<MT, NT, KW, EPI>), grid, dim3(64 * KW), 0, s, g);
+}
+
+template <int MTMAX, int NT, int KW, int EPI>
+static void skinny_q8_mt(const GemmArgs &g, hipStream_t s) {
+    const int mt = (g.M + 15) / 16;
+    if (mt <= 1 || MTMAX == 1) run_skinny_q8<1, NT, KW, EPI>(g, s);
+    else if (mt <= 2 || MTMAX == 2) run_skinny_q8<MTMAX >= 2 ? 2 : 1, NT, KW, EPI>(g, s);
+    else if (mt <= 3 || MTMAX == 3) run_skinny_q8<MTMAX >= 3 ? 3 : 1, NT, KW, EPI>(g, s);
+    else run_skinny_q8<MTMAX >= 4 ? 4 : 1, NT, KW, EPI>(g, s);
 }
 
 // MTMAX: rows per block cap (x16); smaller batches use the fewest tiles
@@ -206,6 +347,24 @@ bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s) {
         case EPI_ARGMAX:
             if (g.N % 64 != 0) return false;
             skinny_mt<4, 4, 2, EPI_ARGMAX>(g, s);
+            return true;
+        default:
+            return false;
+    }
+}
+
+bool launch_gemm_skinny_q8(int epi, const GemmArgs &g, hipStream_t s) {
+    static const int off = [] { const char *e = getenv("QASR_SKINNY"); return e && e[0] == '0'; }();
+    if (off || g.M <= 0 || g.M > 128 || g.K % 128 != 0 || g.lda % 16 != 0 || g.ldw % 16 != 0 || g.ldad % 4 != 0) return false;
+    switch (epi) {
+        case EPI_F32:
+            if (g.N % 16 != 0) return false;
+            if (g.N >= 4096) skinny_q8_mt<2, 1, 8, EPI_F32>(g, s);   // MT <= 2: the block scales cost 16 VGPRs per row tile
+            else skinny_q8_mt<1, 1, 8, EPI_F32>(g, s);
+            return true;
+        case EPI_SWIGLU_F32:
+            if (g.N % 32 != 0) return false;
+            skinny_q8_mt<2, 2, 4, EPI_SWIGLU_F32>(g, s);
             return true;
         default:
             return false;

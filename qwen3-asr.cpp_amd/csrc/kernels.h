@@ -77,6 +77,8 @@ void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s);
 // decode-batch GEMM (gemm_skinny.hip): dense A, M <= 128, K % 128 == 0; returns
 // false (nothing launched) for shapes it does not take.  QASR_SKINNY=0 disables.
 bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s);
+// the same for Q8_0 weights (Aq/Ad quantised activations, Wq/Wd): EPI_F32, EPI_SWIGLU_F32
+bool launch_gemm_skinny_q8(int epi, const GemmArgs &g, hipStream_t s);
 // ggml_mul_mat with Q8_0 weights: exact int8 block dots (v_mfma_i32_16x16x32_i8
 // per 32-wide K block), each scaled by d_w * d_x into an fp32 accumulator.
 // Requires K % 128 == 0 (every Qwen3-ASR width) or K % 32 == 0 (slower tile).
@@ -125,6 +127,9 @@ void launch_layernorm_f16(const float *x, int M, int D, const float *w, const fl
 // RMSNorm (ggml_rms_norm + mul) fp32 -> fp16 (or fp32 y32); rows gathered by optional row_idx
 void launch_rmsnorm_f16(const float *x, int ldx, const int *row_idx, int M, int D, const float *w, float eps,
                         uint16_t *y, hipStream_t s, float *y32 = nullptr);
+// the same norm quantised to Q8_0 in the kernel (decode batches of Q8_0 models):
+// yq int8 [M][D], yd fp32 [M][D/32] -- the values launch_quantize_q8 would give
+void launch_rmsnorm_q8(const float *x, int ldx, int M, int D, const float *w, float eps, int8_t *yq, float *yd, hipStream_t s);
 
 // ---------------------------------------------------------------- attention
 // encoder: full bidirectional fp32 attention per clip segment, head_dim 64.
@@ -154,6 +159,7 @@ struct PrefillAttnArgs {
     float scale;
     uint16_t *out;                       // [rows][n_head*128] fp16
     float *out32;                        // non-null: fp32 output instead (input of a Q8_0 o-proj)
+    int8_t *outq; float *outd;           // non-null: Q8_0 output [B][QD] int8 + [B][QD/32] scales
 };
 void launch_prefill_attention(const PrefillAttnArgs &a, hipStream_t s);
 
@@ -174,6 +180,7 @@ struct DecodeAttnArgs {
     unsigned int *counter;               // [B][n_kv_head] split arrivals, zero at rest
     uint16_t *out;                       // [B][n_head*128] fp16 attention output
     float *out32;                        // non-null: fp32 output instead (input of a Q8_0 o-proj)
+    int8_t *outq; float *outd;           // non-null: Q8_0 output [B][QD] int8 + [B][QD/32] scales
     unsigned long long *trace;           // dev trace: per block [start, K/V landed, partial ready, counted, end, burst landed]
 };
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
