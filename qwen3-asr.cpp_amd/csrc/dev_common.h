@@ -103,3 +103,18 @@ __device__ __forceinline__ int8_t q8_quant(float v, float amax) {
     const float id = amax != 0.0f ? 127.f / amax : 0.0f;
     return (int8_t)__builtin_rintf(fmul_rn(v, id));
 }
+
+typedef int intx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+
+// acc[r] += (d_w * d_x[r]) * sumi[r]: the scale products and the fma in
+// packed fp32 (v_pk_mul_f32 / v_pk_fma_f32, two rows per instruction; each
+// lane's arithmetic and rounding identical to the scalar fmul + fma)
+__device__ __forceinline__ void q8_scale_acc(floatx4 &acc, float dw, floatx4 dx, intx4 ci) {
+    const floatx2 w2 = {dw, dw};
+    const floatx2 s01 = w2 * floatx2{dx[0], dx[1]}, s23 = w2 * floatx2{dx[2], dx[3]};
+    const floatx2 c01 = {(float)ci[0], (float)ci[1]}, c23 = {(float)ci[2], (float)ci[3]};
+    const floatx2 a01 = __builtin_elementwise_fma(s01, c01, floatx2{acc[0], acc[1]});
+    const floatx2 a23 = __builtin_elementwise_fma(s23, c23, floatx2{acc[2], acc[3]});
+    acc = floatx4{a01[0], a01[1], a23[0], a23[1]};
+}

@@ -284,8 +284,38 @@ __global__ __launch_bounds__(256) void quantize_q8_kernel(const float *__restric
     dst[1] = u32x4{w[4], w[5], w[6], w[7]};
 }
 
+// the same quantisation for dense rows, coalesced: lane = 4 consecutive values
+// (one 16-B load), a 32-block = 8 lanes, a wave = 256 values of one row
+__global__ __launch_bounds__(256) void quantize_q8_rows_kernel(const float *__restrict__ x32, const uint16_t *__restrict__ x16,
+                                                               int ldx, int M, int K, int8_t *__restrict__ q, float *__restrict__ d) {
+    const int wpr = K / 256;   // waves per row
+    const long w = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= (long)M * wpr) return;
+    const int lane = threadIdx.x & 63;
+    const int row = (int)(w / wpr), col = (int)(w - (long)row * wpr) * 256 + 4 * lane;
+    float4 v;
+    if (x32) {
+        v = *(const float4 *)(x32 + (long)row * ldx + col);
+    } else {
+        const uint2 h = *(const uint2 *)(x16 + (long)row * ldx + col);
+        v = make_float4(u16_to_f(h.x & 0xffffu), u16_to_f(h.x >> 16), u16_to_f(h.y & 0xffffu), u16_to_f(h.y >> 16));
+    }
+    float am = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+    am = fmaxf(am, __shfl_xor(am, 1, 64));
+    am = fmaxf(am, __shfl_xor(am, 2, 64));
+    am = fmaxf(am, __shfl_xor(am, 4, 64));
+    *(uint32_t *)(q + (long)row * K + col) = (uint32_t)(uint8_t)q8_quant(v.x, am) | (uint32_t)(uint8_t)q8_quant(v.y, am) << 8 |
+                                            (uint32_t)(uint8_t)q8_quant(v.z, am) << 16 | (uint32_t)(uint8_t)q8_quant(v.w, am) << 24;
+    if ((lane & 7) == 0) d[(long)row * (K / 32) + col / 32] = q8_scale(am);
+}
+
 void launch_quantize_q8(const float *x32, const uint16_t *x16, int ldx, int M, int K, int gather_C, int8_t *q, float *d,
                         hipStream_t s) {
+    if (gather_C == 0 && K % 256 == 0 && ldx % 4 == 0 && M > 0) {
+        const long waves = (long)M * (K / 256);
+        hipLaunchKernelGGL(quantize_q8_rows_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, x32, x16, ldx, M, K, q, d);
+        return;
+    }
     const long n = (long)M * (K / 32);
     if (n <= 0) return;
     hipLaunchKernelGGL(quantize_q8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x32, x16, ldx, M, K, gather_C, q, d);

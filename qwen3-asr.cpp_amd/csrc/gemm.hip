@@ -279,7 +279,6 @@ void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s) {
 // sumf += (d_x * d_y) * sumi).  A and W are staged as int8 rows of KS blocks
 // (row stride KS*32+16 B: the 8-byte fragment reads of 16 lanes hit distinct
 // bank pairs), their block scales as fp32 beside them.
-typedef int intx4 __attribute__((ext_vector_type(4)));
 
 template <int BM, int BN, int KS, int EPI>
 __global__ __launch_bounds__(256) void gemm_q8_kernel(GemmArgs g) {
@@ -379,8 +378,7 @@ __global__ __launch_bounds__(256) void gemm_q8_kernel(GemmArgs g) {
 #pragma unroll
                 for (int j = 0; j < FN; j++) {
                     const intx4 ci = __builtin_amdgcn_mfma_i32_16x16x32_i8(af[i], bf[j], intx4{0, 0, 0, 0}, 0, 0, 0);
-#pragma unroll
-                    for (int r = 0; r < 4; r++) acc[i][j][r] = fmaf(fmul_rn(sb[j], sa[i][r]), (float)ci[r], acc[i][j][r]);
+                    q8_scale_acc(acc[i][j], sb[j], sa[i], ci);
                 }
         }
         if (kt + 1 < nk) sstore(cur ^ 1);

@@ -22,7 +22,6 @@
 namespace qasr {
 
 __device__ __forceinline__ float silu_s(float g) { return g / (1.0f + expf(-g)); }
-typedef int intx4 __attribute__((ext_vector_type(4)));
 
 // Residual prefetch: epilogue element e -> (tile, row in tile, column in
 // tile); the residual values a thread adds are requested at kernel entry, so
@@ -261,12 +260,13 @@ __global__ __launch_bounds__(64 * KW) void gemm_skinny_q8_kernel(GemmArgs g) {
 #pragma unroll
                 for (int j = 0; j < NT; j++) {
                     const intx4 ci = __builtin_amdgcn_mfma_i32_16x16x32_i8(ab[buf][i][u], wb[buf][j][u], intx4{0, 0, 0, 0}, 0, 0, 0);
+                    floatx4 sa;
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         const float4 a4 = ad[buf][i][r];
-                        const float sa = u == 0 ? a4.x : u == 1 ? a4.y : u == 2 ? a4.z : a4.w;
-                        acc[i][j][r] = fmaf(fmul_rn(sb[j], sa), (float)ci[r], acc[i][j][r]);
+                        sa[r] = u == 0 ? a4.x : u == 1 ? a4.y : u == 2 ? a4.z : a4.w;
                     }
+                    q8_scale_acc(acc[i][j], sb[j], sa, ci);
                 }
         }
     };
