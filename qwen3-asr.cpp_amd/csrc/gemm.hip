@@ -152,6 +152,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 
     u32x4 stage[CPT];
     auto gload = [&](int k0) {
+        // conv modes: a stage's KS*32 k values lie inside one 3x3 tap (the host
+        // guarantees C % (32*KS) == 0), so the tap and its (kh, kw) are uniform
+        // per stage -- no per-chunk division by C
+        int tap = 0, kh = 0, kw = 0;
+        if constexpr (AMODE != AM_DENSE) {
+            tap = k0 / g.C;
+            kh = tap / 3;
+            kw = tap - kh * 3;
+        }
 #pragma unroll
         for (int t = 0; t < CPT; t++) {
             const int c = tid + t * 256;
@@ -167,8 +176,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
                     } else {
                         const int4 ri = rowinfo[r];
                         if (ri.x >= 0) {
-                            const int tap = k / g.C, ic = k - tap * g.C;
-                            const int kh = tap / 3, kw = tap - kh * 3;
+                            const int ic = k - tap * g.C;
                             const int ih = ri.y + kh, iw = ri.z + kw;
                             const int Hin = AMODE == AM_CONV2 ? 64 : 32;
                             if (ih >= 0 && ih < Hin && iw >= 0 && iw < ri.w)
