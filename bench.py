@@ -33,6 +33,7 @@ import qasr  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 README_RTFX = 92.0 / 5.007   # 92 s clip in 5,007 ms on M2 Pro (README.md:136)
 README_ALIGN_RTFX = 92.0 / 18.005   # transcribe + align of the same clip (README.md:138)
+MFMA_F16_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense fp16 MFMA (no sparsity)
 
 
 def parse():
@@ -102,6 +103,34 @@ def pmc_traffic(kernel_prefix: str):
             if k["name"].startswith(kernel_prefix) and "hbm_read_bytes" in k:
                 return k["hbm_read_bytes"] + k.get("hbm_write_bytes", 0), os.path.relpath(f, ROOT)
     return None, None
+
+
+def encoder_flops(hp, n_samples: int) -> float:
+    """Algorithmic FLOPs of the ASR audio encoder for one clip (SURVEY.md §8(d):
+    278.0 GFLOP per 30 s): conv front-end per 100-frame chunk (3x3 s2 convs,
+    conv_out), full-attention transformer over all frames, post projections."""
+    T = qasr.mel_frames(n_samples)
+    C, D, F, L = hp.conv_channels, hp.d_model, hp.enc_ffn, hp.enc_layers
+    o = lambda w: (w - 1) // 2 + 1
+    mac, N = 0, 0
+    for c0 in range(0, T, 100):
+        w1 = o(min(100, T - c0)); w2 = o(w1); w3 = o(w2)
+        mac += 64 * w1 * C * 9 + 32 * w2 * C * 9 * C + 16 * w3 * C * 9 * C + w3 * 16 * C * D
+        N += w3
+    mac += L * (4 * N * D * D + 2 * N * D * F + 2 * N * N * D) + N * D * (D + hp.hidden_size)
+    return 2.0 * mac
+
+
+def decode_bytes(hp, q8: bool, batch: int, prompt: int, ntok: int) -> float:
+    """Algorithmic HBM bytes of the decode loop: every step
+    streams the decoder weights once (shared by the batch) plus each sequence's
+    K/V cache rows 0..n_kv-1 (fp16, all layers)."""
+    H, hd = hp.hidden_size, hp.head_dim
+    per_layer = (hp.n_heads * hd + 2 * hp.n_kv_heads * hd) * H + H * hp.n_heads * hd + 3 * hp.dec_ffn * H
+    w = hp.dec_layers * per_layer * (34 / 32 if q8 else 2) + hp.vocab_size * H * 2
+    kv_row = hp.dec_layers * 2 * hp.n_kv_heads * hd * 2
+    kv = sum(kv_row * (prompt + s + 1) for s in range(ntok))
+    return ntok * w + batch * kv
 
 
 def workload(args, ntok: int, align: bool) -> str:
@@ -217,12 +246,30 @@ def main():
     if probe_n:
         avg_s = probe_ms / probe_n / 1e3
         achieved = probe_b / avg_s / 1e9
-        mr = next(r for r in (1, 2, 4, 8, args.batch) if r >= args.batch)   # gemv_mr row bucket
-        traffic, src = pmc_traffic(f"void qasr::gemv_kernel<3, 4, {mr},")
-        out["roofline"] = {"kernel": "gemv_kernel<EPI_ARGMAX> (decode LM head, tied 151936x1024 f16 + fused argmax)",
+        if args.batch <= 8:
+            mr = next(r for r in (1, 2, 4, 8) if r >= args.batch)   # gemv_mr row bucket
+            kname = "gemv_kernel<EPI_ARGMAX>"
+            traffic, src = pmc_traffic(f"void qasr::gemv_kernel<3, 4, {mr},")
+        else:
+            kname = "gemm_skinny_kernel<EPI_ARGMAX>"
+            traffic, src = pmc_traffic("void qasr::gemm_skinny_kernel<4, 4, 2, 3")
+        out["roofline"] = {"kernel": kname + " (decode LM head, tied 151936x1024 f16 + fused argmax)",
                            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
                            "bytes_per_launch": probe_b, "avg_launch_us": round(avg_s * 1e6, 2), "launches": probe_n}
+    # the north-star fractions of the two stages: encoder
+    # FLOPs against the dense fp16 MFMA peak, decode bytes against HBM
+    enc_s = tm["encode"] / args.steps / 1e3
+    if enc_s > 0:
+        ef = args.batch * encoder_flops(m.hp, n)
+        out["encoder_roofline"] = {"bound": "mfma", "achieved": round(ef / enc_s / 1e12, 1), "peak": MFMA_F16_PEAK_TFLOPS,
+                                   "unit": "TFLOP/s", "frac": round(ef / enc_s / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
+                                   "flops_per_step": ef}
+    dec_s = tm["decode"] / args.steps / 1e3
+    if dec_s > 0:
+        db = decode_bytes(m.hp, args.q8, args.batch, P, ntok)
+        out["decode_hbm"] = {"achieved": round(db / dec_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(db / dec_s / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_step": db}
     if N == 1 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(model_path, args.cpu_sample_seconds, args.tok_rate, args.cpu_threads)
     print(json.dumps(out), flush=True)
