@@ -16,6 +16,8 @@
 // A operand modes: dense row-major, or an implicit im2col gather over the
 // NHWC conv activations (3x3, stride 2, pad 1) so conv2/conv3 of the audio
 // encoder never materialise im2col buffers (src/audio_encoder.cpp:116-128).
+#include <type_traits>
+
 #include "dev_common.h"
 #include "kernels.h"
 
@@ -446,24 +448,29 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
     const int K = g.K;
     const int ncg = (g.N + CPW - 1) / CPW;
     int cg = blockIdx.x * 4 + wid;
-    half8 wv[CPW][NR][NK];
-    // unconditional loads (clamped addresses, masked after): a conditional
-    // load makes hipcc wait vmcnt(0) at the branch join, which would serialise
-    // the weight stream behind the x prologue
-    auto wload = [&](int cgi) {
+    half8 wv[2][CPW][NR][NK];   // double-buffered: group i+1 is in flight while group i computes
+    // Unconditional loads through a bounds-checked buffer descriptor: rows past
+    // N get an out-of-range offset and return zeros without a memory access.
+    // (A conditional load makes hipcc wait vmcnt(0) at the branch join, which
+    // would serialise the weight stream behind the x prologue / the compute.)
+    const uint32_t wbytes = (uint32_t)((long)g.N * NR * K * 2);
+    const __amdgpu_buffer_rsrc_t wsrd = __builtin_amdgcn_make_buffer_rsrc((void *)g.W, (short)0, (int)wbytes, 0x00020000);
+    auto wload = [&](auto bc, int cgi) {
+        constexpr int b = decltype(bc)::value;
 #pragma unroll
         for (int c = 0; c < CPW; c++)
 #pragma unroll
             for (int r = 0; r < NR; r++)
 #pragma unroll
                 for (int t = 0; t < NK; t++) {
-                    const int o = min(cgi * CPW + c, g.N - 1), k = min(t * 512 + lane * 8, K - 8);
+                    const int o = cgi * CPW + c, k = min(t * 512 + lane * 8, K - 8);
                     long wrow = o;
                     if constexpr (EPI == EPI_SWIGLU_F16) wrow = 32L * (o >> 4) + (o & 15) + 16 * r;
-                    wv[c][r][t] = __builtin_nontemporal_load((const half8 *)(g.W + wrow * K + k));
+                    const uint32_t off = o < g.N ? (uint32_t)((wrow * K + k) * 2) : wbytes;
+                    wv[b][c][r][t] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(wsrd, off, 0, 2));   // nt
                 }
     };
-    if (cg < ncg) wload(cg);
+    wload(std::integral_constant<int, 0>{}, cg);
     // ---- prologue: x rows -> fp16 in LDS (optionally RMS-normalised); each
     //      thread owns 4 consecutive elements per 1024-wide pass, one vector load each
     constexpr int KP = (NK * 512 + 1023) / 1024;
@@ -534,8 +541,10 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
     unsigned long long best[MR];
 #pragma unroll
     for (int m = 0; m < MR; m++) best[m] = 0ull;
-    for (; cg < ncg; cg += gridDim.x * 4) {
-        const int col0 = cg * CPW;
+    const int stride = gridDim.x * 4;
+    auto process = [&](auto bc, int cgi) {
+        constexpr int b = decltype(bc)::value;
+        const int col0 = cgi * CPW;
         float acc[CPW][NR][MR];
 #pragma unroll
         for (int c = 0; c < CPW; c++)
@@ -555,11 +564,9 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
 #pragma unroll
                     for (int r = 0; r < NR; r++)
 #pragma unroll
-                        for (int e = 0; e < 8; e++) acc[c][r][m] = fmaf((float)wv[c][r][t][e], (float)xv[e], acc[c][r][m]);
+                        for (int e = 0; e < 8; e++) acc[c][r][m] = fmaf((float)wv[b][c][r][t][e], (float)xv[e], acc[c][r][m]);
             }
         }
-        const int nxt = cg + gridDim.x * 4;
-        if (nxt < ncg) wload(nxt);   // next group's weights in flight during the reductions
 #pragma unroll
         for (int c = 0; c < CPW; c++) {
             const int o = col0 + c;
@@ -589,6 +596,16 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
                 }
             }
         }
+    };
+    while (cg < ncg) {
+        const int n1 = cg + stride;
+        wload(std::integral_constant<int, 1>{}, n1);   // past the end: no memory access
+        process(std::integral_constant<int, 0>{}, cg);
+        if (n1 >= ncg) break;
+        const int n2 = n1 + stride;
+        wload(std::integral_constant<int, 0>{}, n2);
+        process(std::integral_constant<int, 1>{}, n1);
+        cg = n2;
     }
     if constexpr (EPI != EPI_ARGMAX) {
         if (g.trace) { __syncthreads(); trace_mark(g.trace, 1); }
@@ -831,7 +848,8 @@ template <int EPI, int CPW, int MR, int NK>
 static void run_gemv(const GemvArgs &g, hipStream_t s) {
     const int per_block = 4 * CPW;
     int blocks = (g.N + per_block - 1) / per_block;
-    if (blocks > 1024) blocks = 1024;   // 256 CUs x 4 resident workgroups, grid-stride beyond
+    static const int cap = [] { const char *e = getenv("QASR_GEMV_BLOCKS"); return e ? atoi(e) : 1024; }();
+    if (blocks > cap) blocks = cap;   // 256 CUs x 4 resident workgroups, grid-stride beyond
     const size_t lds = (size_t)MR * g.K * 2;
     hipLaunchKernelGGL((gemv_kernel<EPI, CPW, MR, NK>), dim3(blocks), dim3(256), lds, s, g);
 }
