@@ -250,7 +250,12 @@ template <int AMODE, int EPI>
 static void dispatch_tiles(const GemmArgs &g, hipStream_t s) {
     if constexpr (AMODE != AM_DENSE) {
         // conv: K = 9*C, slab group must stay inside one tap -> C % (32*KS) == 0
-        if (g.N % 96 == 0 && g.C % 96 == 0) {
+        static const int wide = [] { const char *e = getenv("QASR_CONV_WIDE"); return e ? atoi(e) : 1; }();
+        if (wide && g.N == 480) {
+            // all 480 output channels per block: the gathered A tile is read once
+            // (N/96 = 5 re-reads of the im2col rows otherwise), W stays L2-resident
+            run_gemm<64, 480, 1, AMODE, EPI>(g, s);
+        } else if (g.N % 96 == 0 && g.C % 96 == 0) {
             if (g.M >= 4096) run_gemm<128, 96, 3, AMODE, EPI>(g, s);
             else run_gemm<64, 96, 3, AMODE, EPI>(g, s);
         } else {
