@@ -94,6 +94,12 @@ __device__ __forceinline__ float gelu_lut(float x, const uint16_t *__restrict__ 
     if (x >= 10.0f) return x;
     return u16_to_f(lut[f_to_u16(x)]);
 }
+// the same, as the fp16 bits of the result (what a following fp16 store writes)
+__device__ __forceinline__ uint32_t gelu_lut_bits(float x, const uint16_t *__restrict__ lut) {
+    if (x <= -10.0f) return 0u;
+    if (x >= 10.0f) return f_to_u16(x);
+    return lut[f_to_u16(x)];
+}
 
 // ggml quantize_row_q8_0 (x86 path) for one value of a 32-block whose |max| is
 // amax: d = fp16(amax / 127), q = round-half-even(v * 127 / amax)

@@ -18,43 +18,73 @@ __device__ __forceinline__ int find_chunk_e(const int *__restrict__ starts, int 
 // src/audio_encoder.cpp:105-112: ggml_conv_2d(1 -> C) = im2col(fp16) x fp16
 // kernel.  K = 9 is below ggml's SIMD step, so ggml's vec_dot_f16 sums the 9
 // exact fp16 products in double (its scalar leftover loop); we do the same.
-// One wave per output position; lanes sweep the C output channels (coalesced
-// NHWC stores).
+// One wave per CONV1_ROWS consecutive output positions; lane l owns output
+// channels 8l .. 8l+7 (its 72 fp16 weights and 8 biases stay in registers), so
+// each position costs one broadcast 9-tap input gather and one 16-byte NHWC
+// store per lane.
+#define CONV1_ROWS 4
 __global__ __launch_bounds__(256) void conv1_kernel(const float *__restrict__ mel, const ChunkDesc *__restrict__ chunks,
                                                     const int *__restrict__ row1_start, int n_chunks, int rows1,
                                                     const uint16_t *__restrict__ w, const float *__restrict__ b,
                                                     const uint16_t *__restrict__ lut, int C, uint16_t *__restrict__ act1) {
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * CONV1_ROWS;
     const int lane = threadIdx.x & 63;
-    if (row >= rows1) return;
-    const int c = find_chunk_e(row1_start, n_chunks, row);
-    const ChunkDesc cd = chunks[c];
-    const int local = row - cd.row1;
-    const int oh = local / cd.W1, ow = local - oh * cd.W1;
-    float in[9];
+    if (row0 >= rows1 || lane * 8 >= C) return;
+    const int oc0 = lane * 8;
+    float wf[8][9];
+    {
+        const u32x4 *wp = (const u32x4 *)(w + oc0 * 9);   // 72 consecutive halves
+        uint16_t wh[72];
 #pragma unroll
-    for (int kh = 0; kh < 3; kh++)
+        for (int i = 0; i < 9; i++) {
+            const u32x4 v = wp[i];
 #pragma unroll
-        for (int kw = 0; kw < 3; kw++) {
-            const int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;   // ih: mel bin, iw: frame in chunk
-            float v = 0.0f;
-            if (ih >= 0 && ih < 128 && iw >= 0 && iw < cd.Lv) v = mel[cd.mel_off + (long)ih * cd.T + iw];
-            in[kh * 3 + kw] = h2f(f2h(v));
+            for (int e = 0; e < 4; e++) { wh[8 * i + 2 * e] = v[e] & 0xffffu; wh[8 * i + 2 * e + 1] = v[e] >> 16; }
         }
-    for (int oc = lane; oc < C; oc += 64) {
-        double s = 0.0;
 #pragma unroll
-        for (int t = 0; t < 9; t++) s += (double)(in[t] * u16_to_f(w[oc * 9 + t]));
-        const float v = fadd_rn((float)s, b[oc]);
-        act1[(long)row * C + oc] = f_to_u16(gelu_lut(v, lut));
+        for (int o = 0; o < 8; o++)
+#pragma unroll
+            for (int t = 0; t < 9; t++) wf[o][t] = u16_to_f(wh[o * 9 + t]);
+    }
+    const float4 b0 = *(const float4 *)(b + oc0), b1 = *(const float4 *)(b + oc0 + 4);
+    const float bias[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    for (int r = 0; r < CONV1_ROWS; r++) {
+        const int row = row0 + r;
+        if (row >= rows1) break;
+        const int c = find_chunk_e(row1_start, n_chunks, row);
+        const ChunkDesc cd = chunks[c];
+        const int local = row - cd.row1;
+        const int oh = local / cd.W1, ow = local - oh * cd.W1;
+        float in[9];
+#pragma unroll
+        for (int kh = 0; kh < 3; kh++)
+#pragma unroll
+            for (int kw = 0; kw < 3; kw++) {
+                const int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;   // ih: mel bin, iw: frame in chunk
+                float v = 0.0f;
+                if (ih >= 0 && ih < 128 && iw >= 0 && iw < cd.Lv) v = mel[cd.mel_off + (long)ih * cd.T + iw];
+                in[kh * 3 + kw] = h2f(f2h(v));
+            }
+        uint32_t packed[4];
+#pragma unroll
+        for (int o = 0; o < 8; o++) {
+            double sd = 0.0;
+#pragma unroll
+            for (int t = 0; t < 9; t++) sd += (double)(in[t] * wf[o][t]);
+            const float v = fadd_rn((float)sd, bias[o]);
+            const uint32_t h = gelu_lut_bits(v, lut);
+            if (o & 1) packed[o >> 1] |= h << 16; else packed[o >> 1] = h;
+        }
+        *(u32x4 *)(act1 + (long)row * C + oc0) = u32x4{packed[0], packed[1], packed[2], packed[3]};
     }
 }
 
 void launch_conv1(const float *mel, const ChunkDesc *chunks, const int *row1_start, int n_chunks, int rows1,
                   const uint16_t *w, const float *b, const uint16_t *gelu, int C, uint16_t *act1, hipStream_t s) {
     if (rows1 <= 0) return;
-    hipLaunchKernelGGL(conv1_kernel, dim3((rows1 + 3) / 4), dim3(256), 0, s, mel, chunks, row1_start, n_chunks, rows1, w, b,
-                       gelu, C, act1);
+    const int per_block = 4 * CONV1_ROWS;
+    hipLaunchKernelGGL(conv1_kernel, dim3((rows1 + per_block - 1) / per_block), dim3(256), 0, s, mel, chunks, row1_start,
+                       n_chunks, rows1, w, b, gelu, C, act1);
 }
 
 // ------------------------------------------------------------------ norms
