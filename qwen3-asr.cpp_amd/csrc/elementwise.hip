@@ -27,9 +27,12 @@ __global__ __launch_bounds__(256) void conv1_kernel(const float *__restrict__ me
                                                     const int *__restrict__ row1_start, int n_chunks, int rows1,
                                                     const uint16_t *__restrict__ w, const float *__restrict__ b,
                                                     const uint16_t *__restrict__ lut, int C, uint16_t *__restrict__ act1) {
-    const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * CONV1_ROWS;
+    // grid (positions / 16, chunk): no row -> chunk search
+    const ChunkDesc cd = chunks[blockIdx.y];
+    const int nloc = 64 * cd.W1;
+    const int loc0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * CONV1_ROWS;
     const int lane = threadIdx.x & 63;
-    if (row0 >= rows1 || lane * 8 >= C) return;
+    if (loc0 >= nloc || lane * 8 >= C) return;
     const int oc0 = lane * 8;
     float wf[8][9];
     {
@@ -49,11 +52,9 @@ __global__ __launch_bounds__(256) void conv1_kernel(const float *__restrict__ me
     const float4 b0 = *(const float4 *)(b + oc0), b1 = *(const float4 *)(b + oc0 + 4);
     const float bias[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
     for (int r = 0; r < CONV1_ROWS; r++) {
-        const int row = row0 + r;
-        if (row >= rows1) break;
-        const int c = find_chunk_e(row1_start, n_chunks, row);
-        const ChunkDesc cd = chunks[c];
-        const int local = row - cd.row1;
+        const int local = loc0 + r;
+        if (local >= nloc) break;
+        const int row = cd.row1 + local;
         const int oh = local / cd.W1, ow = local - oh * cd.W1;
         float in[9];
 #pragma unroll
@@ -83,8 +84,9 @@ void launch_conv1(const float *mel, const ChunkDesc *chunks, const int *row1_sta
                   const uint16_t *w, const float *b, const uint16_t *gelu, int C, uint16_t *act1, hipStream_t s) {
     if (rows1 <= 0) return;
     const int per_block = 4 * CONV1_ROWS;
-    hipLaunchKernelGGL(conv1_kernel, dim3((rows1 + per_block - 1) / per_block), dim3(256), 0, s, mel, chunks, row1_start,
-                       n_chunks, rows1, w, b, gelu, C, act1);
+    const int max_loc = 64 * ((100 - 1) / 2 + 1);   // chunks hold <= 100 mel frames (ASR and aligner)
+    hipLaunchKernelGGL(conv1_kernel, dim3((max_loc + per_block - 1) / per_block, n_chunks), dim3(256), 0, s, mel, chunks,
+                       row1_start, n_chunks, rows1, w, b, gelu, C, act1);
 }
 
 // ------------------------------------------------------------------ norms
