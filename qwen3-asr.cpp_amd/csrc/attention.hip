@@ -404,12 +404,22 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     uint16_t *kc = a.kc + cbase * 128, *vc = a.vc + cbase * 128;
     const int k0 = sp * SPL;
     const int sub = lane >> 4, dl = (lane & 15) * 8;
-    constexpr int KPW = SPL / DWAVES / 4;   // key rows per lane (4 or 16)
-    half8 kv[KPW], vv[KPW];
+    const int q4 = lane >> 4, c16 = lane & 15;
+    constexpr int KPW = SPL / DWAVES / 4;   // V rows per lane (4 or 16)
+    constexpr int TW = SPL / DWAVES / 16;   // 16-key MFMA tiles per wave (1 or 4)
+    // K in the v_mfma_f32_16x16x32_f16 B layout: tile t, step s -> key 16t + c16
+    // of this wave's range, dims 32s + 8q4 .. +8 (16 rows x 64 B per load)
+    half8 kk[TW][4], vv[KPW];
+#pragma unroll
+    for (int t = 0; t < TW; t++)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++) {
+            const int key = min(k0 + wid * (SPL / DWAVES) + 16 * t + c16, a.max_ctx - 1);
+            kk[t][s4] = *(const half8 *)(kc + (long)key * 128 + 32 * s4 + 8 * q4);
+        }
 #pragma unroll
     for (int i = 0; i < KPW; i++) {
         const int key = min(k0 + wid * (SPL / DWAVES) + i * 4 + sub, a.max_ctx - 1);
-        kv[i] = *(const half8 *)(kc + (long)key * 128 + dl);
         vv[i] = *(const half8 *)(vc + (long)key * 128 + dl);
     }
     // No exit test on the position anywhere: with one, hipcc hoists the
@@ -445,26 +455,33 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
         vc[(long)pos * 128 + lane + 64] = v1;
     }
     __syncthreads();
-    // ---- scores: 16 lanes per key row, 8 dims each
+    // ---- scores S = Q K^T on MFMA: A = the two q heads (rows 0, 1; rows 2-15
+    //      zero), B = K^T; lane (q4 = 0, c16) gets S[head r][key c16] in acc[r].
+    //      Exact fp16 x fp16 products summed in fp32 (ggml FA: Q cast to fp16).
     if (a.trace) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); trace_mark(a.trace, 1); }
-    const half8 q0 = *(const half8 *)&qs[0][dl], q1 = *(const half8 *)&qs[1][dl];
+    half8 qa[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; s4++)
+        qa[s4] = c16 < 2 ? *(const half8 *)&qs[c16][32 * s4 + 8 * q4] : half8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < TW; t++) {
+        const int j = wid * (SPL / DWAVES) + 16 * t + c16;
+        if (k0 + j == pos)
+#pragma unroll
+            for (int s4 = 0; s4 < 4; s4++) kk[t][s4] = *(const half8 *)&knew[32 * s4 + 8 * q4];
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(qa[s4], kk[t][s4], acc, 0, 0, 0);
+        if (q4 == 0) {
+            const bool ok = k0 + j < k1;
+            sc[0][j] = ok ? acc[0] * a.scale : -INFINITY;
+            sc[1][j] = ok ? acc[1] * a.scale : -INFINITY;
+        }
+    }
 #pragma unroll
     for (int i = 0; i < KPW; i++) {
         const int j = wid * (SPL / DWAVES) + i * 4 + sub;
-        if (k0 + j == pos) { kv[i] = *(const half8 *)&knew[dl]; vv[i] = *(const half8 *)&vnew[dl]; }
-        float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; e++) {
-            s0 = fmaf((float)kv[i][e], (float)q0[e], s0);
-            s1 = fmaf((float)kv[i][e], (float)q1[e], s1);
-        }
-        s0 = row16_sum(s0);   // the key's 16 lanes
-        s1 = row16_sum(s1);
-        if ((lane & 15) == 0) {
-            const bool ok = k0 + j < k1;
-            sc[0][j] = ok ? s0 * a.scale : -INFINITY;
-            sc[1][j] = ok ? s1 * a.scale : -INFINITY;
-        }
+        if (k0 + j == pos) vv[i] = *(const half8 *)&vnew[dl];
     }
     __syncthreads();
     trace_mark(a.trace, 6);
@@ -487,7 +504,8 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     }
     __syncthreads();
     trace_mark(a.trace, 7);
-    // ---- P.V
+    // ---- P.V in fp32 (probabilities kept fp32: a Q8_0 o-proj re-quantises
+    //      this output, so its rounding must not move)
     float acc0[8], acc1[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) { acc0[e] = 0.f; acc1[e] = 0.f; }
@@ -497,8 +515,9 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
         const float p0 = sc[0][j], p1 = sc[1][j];
 #pragma unroll
         for (int e = 0; e < 8; e++) {
-            acc0[e] = fmaf((float)vv[i][e], p0, acc0[e]);
-            acc1[e] = fmaf((float)vv[i][e], p1, acc1[e]);
+            const float v = (float)vv[i][e];
+            acc0[e] = fmaf(v, p0, acc0[e]);
+            acc1[e] = fmaf(v, p1, acc1[e]);
         }
     }
     // per-(wave, row) partial sums go to LDS; the 16-way sum happens once, below
