@@ -1,0 +1,55 @@
+"""GPU: the decode-batch kernels (B > 8: gemm_skinny_kernel / gemm_skinny_q8_kernel
+row blocks and K-split waves, 256-key attention splits, the skinny LM head with
+argmax, Q8_0 quantisation fused into the norm and the attention combiner) at
+the batch sizes the bench runs.
+
+Every row of a batch holds the same sequence, so every row must come out
+bit-identical to row 0 (an output row depends only on its own inputs and on
+the same instruction sequence, whatever row block or tile it lands in), and
+row 0 must match the oracle within the tolerances of tests/test_gpu_parity.py
+(F16) and tests/test_gpu_q8.py (Q8_0, fp32-accumulating oracle attention)."""
+import numpy as np
+import pytest
+
+import oracle_py as op
+import qasr
+
+pytestmark = pytest.mark.gpu
+SR = 16000
+FA32 = op.OracleModel.FA_V_F32
+
+
+@pytest.mark.parametrize("B,secs", [(64, 1.3), (100, 1.3), (64, 24.0)])
+@pytest.mark.parametrize("path", ["f16", "q8"])
+def test_decode_batch_rows_identical_and_match_oracle(path, B, secs, gpu, tiny_gguf, tiny_q8_gguf, tiny_oracle,
+                                                      tiny_q8_oracle):
+    """(64, 24 s): a ~330-token context, so the 256-key attention splits and
+    their combine run with more than one split per sequence"""
+    q8 = path == "q8"
+    om = tiny_q8_oracle if q8 else tiny_oracle
+    m = qasr.Model(tiny_q8_gguf if q8 else tiny_gguf)
+    feats = om.encode(op.log_mel(qasr.synth_pcm(9100 + B, int(secs * SR))))
+    ids, pos = m.build_prompt(feats.shape[0])
+    steps = 3
+    c = qasr.Context(m, max_batch=B, max_ctx=len(ids) + steps + 8)
+    try:
+        _, am = c.prefill([ids] * B, [feats] * B, [pos] * B, want_logits=False)
+        assert len(set(int(a) for a in am)) == 1
+        tok0 = int(am[0])
+        toks, out = [tok0] * B, []
+        for s in range(steps):
+            lg, am = c.decode_step(toks, [len(ids) + s] * B)
+            out.append(lg)
+            toks = [int(am[0])] * B
+    finally:
+        c.close()
+        m.close()
+    for s, lg in enumerate(out):
+        for b in range(1, B):
+            assert np.array_equal(lg[b], lg[0]), (s, b)
+    dec = op.OracleDecoder(om, len(ids) + steps + 8, FA32 if q8 else 0)
+    dec.forward(ids, 0, feats, pos)
+    ref = dec.forward([tok0], len(ids))   # the first decode step, same fed token
+    scale = float(np.abs(ref).max())
+    tol = (2e-2 if q8 else 1e-2) * scale
+    assert np.abs(out[0][0] - ref).max() <= tol, (np.abs(out[0][0] - ref).max(), tol)

@@ -77,6 +77,22 @@ def test_full_transcribe_tokens(full):
     assert r.tokens[0] == ora
 
 
+def test_full_batch64_rows_identical(full):
+    """the bench's batch shapes (64 rows: skinny QKV / o / gate-up / down and
+    LM-head tilings of the 0.6B model): 64 identical clips give 64 identical
+    token streams, and the first token equals the batch-1 (GEMV) path's"""
+    m, c, _ = full
+    pcm = qasr.synth_pcm(9300, int(1.1 * SR))
+    cb = qasr.Context(m, max_batch=64, max_ctx=128)
+    try:
+        r = cb.transcribe([pcm] * 64, max_tokens=6, ignore_eos=True)
+    finally:
+        cb.close()
+    r1 = c.transcribe([pcm], max_tokens=6, ignore_eos=True)
+    assert all(t == r.tokens[0] for t in r.tokens)
+    assert len(r.tokens[0]) == 6 and r.tokens[0][0] == r1.tokens[0][0]
+
+
 def test_full_30s_batch_properties(full):
     """30 s clips (configs[0]/[2] length): batched == single, deterministic,
     budget met, token ids in range."""
