@@ -262,10 +262,20 @@ static void dispatch_tiles(const GemmArgs &g, hipStream_t s) {
             run_gemm<64, 64, 1, AMODE, EPI>(g, s);
         }
     } else {
+        // tiles per shape from tools/gemm_bench.hip (MI355X): large M -> 128x128
+        // (one 32-deep slab per stage up to K = 1024); ~1.2k rows (a 92 s
+        // clip) -> 64x64 with 4 slabs per stage for the narrow, deep
+        // projections (N <= 1024), 96x64 for the wide ones (N >= 3072)
         const bool big = g.M >= 2048 && g.N % 128 == 0;
-        if (g.K % 64 == 0) {
-            if (big) run_gemm<128, 128, 2, AMODE, EPI>(g, s);
-            else run_gemm<64, 64, 2, AMODE, EPI>(g, s);
+        if (big && g.K % 64 == 0) {
+            if (g.K <= 1024) run_gemm<128, 128, 1, AMODE, EPI>(g, s);
+            else run_gemm<128, 128, 2, AMODE, EPI>(g, s);
+        } else if (!big && g.N <= 1024 && g.K % 128 == 0 && g.K >= 2048) {
+            run_gemm<64, 64, 4, AMODE, EPI>(g, s);
+        } else if (!big && g.N >= 3072 && g.N % 64 == 0 && g.K % 64 == 0) {
+            run_gemm<96, 64, 2, AMODE, EPI>(g, s);
+        } else if (g.K % 64 == 0) {
+            run_gemm<64, 64, 2, AMODE, EPI>(g, s);
         } else {
             run_gemm<64, 64, 1, AMODE, EPI>(g, s);
         }
