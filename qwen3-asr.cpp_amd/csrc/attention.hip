@@ -605,7 +605,15 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {
     if (a.B <= 0) return;
     if (a.B <= 8) {
-        hipLaunchKernelGGL(decode_attn_kernel<DSPLIT>, dim3(a.grid_splits, a.n_kv_head, a.B), dim3(256), 0, s, a);
+        // >= 1k keys: 128-key splits (half the partials to combine, still >= 64
+        // workgroups per 8 kv heads); shorter contexts keep 64-key splits
+        static const int spl1 = [] { const char *e = getenv("QASR_ATT_SPL1"); return e ? atoi(e) : 0; }();
+        if (spl1 == 128 || (spl1 == 0 && a.grid_splits >= 16)) {
+            const int g2 = (a.grid_splits * DSPLIT + 127) / 128;
+            hipLaunchKernelGGL(decode_attn_kernel<128>, dim3(g2, a.n_kv_head, a.B), dim3(256), 0, s, a);
+        } else {
+            hipLaunchKernelGGL(decode_attn_kernel<DSPLIT>, dim3(a.grid_splits, a.n_kv_head, a.B), dim3(256), 0, s, a);
+        }
     } else {   // batches: longer splits (fewer workgroups and partials per sequence)
         static const int spl = [] { const char *e = getenv("QASR_ATT_SPL"); return e ? atoi(e) : 256; }();
         if (spl == 128) {
