@@ -53,3 +53,30 @@ def test_decode_batch_rows_identical_and_match_oracle(path, B, secs, gpu, tiny_g
     scale = float(np.abs(ref).max())
     tol = (2e-2 if q8 else 1e-2) * scale
     assert np.abs(out[0][0] - ref).max() <= tol, (np.abs(out[0][0] - ref).max(), tol)
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_decode_long_context_splits(B, gpu, tiny_gguf, tiny_oracle):
+    """contexts past 1k keys: batch <= 8 switches to 128-key attention splits
+    (13 of them here); text-only prompt of 1100 ids, every row against the oracle"""
+    m = qasr.Model(tiny_gguf)
+    rng = np.random.default_rng(21)
+    ids = [int(t) for t in rng.integers(0, 151643, 1100)]
+    c = qasr.Context(m, max_batch=B, max_ctx=1200)
+    try:
+        c.prefill([ids] * B, want_logits=False)
+        toks = [int(t) for t in rng.integers(0, 151643, 3)]
+        outs = []
+        for s, t in enumerate(toks):
+            lg, _ = c.decode_step([t] * B, [len(ids) + s] * B)
+            outs.append(lg)
+    finally:
+        c.close()
+        m.close()
+    dec = op.OracleDecoder(tiny_oracle, 1200)
+    dec.forward(ids, 0)
+    for s, t in enumerate(toks):
+        ref = dec.forward([t], len(ids) + s)
+        tol = 1e-2 * float(np.abs(ref).max())
+        for b in range(B):
+            assert np.abs(outs[s][b] - ref).max() <= tol, (s, b, np.abs(outs[s][b] - ref).max(), tol)
