@@ -5,15 +5,6 @@
 
 namespace qasr {
 
-__device__ __forceinline__ int find_chunk_e(const int *__restrict__ starts, int n, int r) {
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-        int mid = (lo + hi + 1) >> 1;
-        if (starts[mid] <= r) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-}
-
 // ------------------------------------------------------------------ conv1
 // src/audio_encoder.cpp:105-112: ggml_conv_2d(1 -> C) = im2col(fp16) x fp16
 // kernel.  K = 9 is below ggml's SIMD step, so ggml's vec_dot_f16 sums the 9
