@@ -373,8 +373,11 @@ __device__ __forceinline__ void ld_sc1_x4_burst9(const floatx4 *src, int tid, in
         : "memory");
 }
 
-template <int SPL>
-__global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
+// FUSED (batch 1, qkv_attn1_kernel): the raw q/k/v come from the QKV workgroups of
+// the same launch -- requested after this split's K/V, once the kv group's
+// arrival counter (qcnt) shows all 64 of its QKV workgroups, with sc1 loads.
+template <int SPL, bool FUSED>
+__device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs &a, const int sp, const int g, const int b, const int nsp) {
     __shared__ __attribute__((aligned(16))) uint16_t qs[2][128];
     __shared__ __attribute__((aligned(16))) uint16_t knew[128];
     __shared__ __attribute__((aligned(16))) uint16_t vnew[128];
@@ -385,16 +388,20 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     __shared__ float lsum[2];
     __shared__ int last;
     __shared__ floatx4 stage[32 * 66];   // combine: up to 32 splits x 2 heads x 33 float4
-    const int b = blockIdx.z, g = blockIdx.y, sp = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
-    trace_mark(a.trace, 0);
+    const long blk = sp + (long)nsp * (g + (long)a.n_kv_head * b);   // dev-trace row
+    auto mark = [&](int slot) {
+        if (a.trace && tid == 0) a.trace[blk * 8 + slot] = rt_now();
+    };
+    mark(0);
     // ---- the token's raw vectors, one per wave: wave 0/1 = q heads 2g/2g+1,
     //      wave 2 = k, wave 3 = v of group g; lane owns dims lane and lane + 64
     //      (the NEOX RoPE pair), so norm and rotation need no LDS round trip
     const float *raw = a.qkv + (long)b * (QD + 2 * KD);
     const float *src = wid < 2 ? raw + (2 * g + wid) * 128 : raw + QD + (wid - 2) * KD + g * 128;
-    const float x0 = src[lane], x1 = src[lane + 64];
+    float x0 = 0.f, x1 = 0.f;
+    if constexpr (!FUSED) { x0 = src[lane]; x1 = src[lane + 64]; }
     const float *nw = wid < 2 ? a.q_norm : a.k_norm;
     const float w0 = nw[lane], w1 = nw[lane + 64];
     // ---- every K/V row of the split (addresses depend on blockIdx only; decode
@@ -427,9 +434,31 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     // latencies in series).  The host sizes the grid to the context
     // (grid_splits, a 256-key bucket); a split past this sequence's end is
     // fully masked and publishes an empty partial (m = -inf, l = 0, O = 0).
+    if constexpr (FUSED) {
+        // wait for the kv group's 64 QKV workgroups (bounded: a lost arrival must
+        // not hang the GPU), then read their write-through outputs with sc1 loads
+        __shared__ int qready;
+        if (tid == 0) {
+            int ok = 0;
+            for (int it = 0; it < (1 << 22); it++) {
+                // replica sp % 8 of the group's counter (8 replicas, one 64-B line each):
+                // the pollers of a group spread over 8 lines instead of one hot word
+                if (__hip_atomic_load(a.qcnt + (g * 8 + (sp & 7)) * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 64u) {
+                    ok = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+            qready = ok;
+        }
+        __syncthreads();
+        const uint32_t *sr = (const uint32_t *)src;
+        x0 = __uint_as_float(__hip_atomic_load(sr + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        x1 = __uint_as_float(__hip_atomic_load(sr + lane + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        (void)qready;
+    }
     const int pos = a.pos[b];
     const int nkv = pos + 1;
-    const int nsp = gridDim.x;
     const int k1 = min(nkv, k0 + SPL);
     const bool lastsp = sp == (nkv - 1) / SPL;
     const float2 cs = *(const float2 *)(a.rope + ((long)pos * 64 + lane) * 2);
@@ -458,7 +487,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     // ---- scores S = Q K^T on MFMA: A = the two q heads (rows 0, 1; rows 2-15
     //      zero), B = K^T; lane (q4 = 0, c16) gets S[head r][key c16] in acc[r].
     //      Exact fp16 x fp16 products summed in fp32 (ggml FA: Q cast to fp16).
-    if (a.trace) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); trace_mark(a.trace, 1); }
+    if (a.trace) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); mark(1); }
     half8 qa[4];
 #pragma unroll
     for (int s4 = 0; s4 < 4; s4++)
@@ -484,7 +513,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
         if (k0 + j == pos) vv[i] = *(const half8 *)&vnew[dl];
     }
     __syncthreads();
-    trace_mark(a.trace, 6);
+    mark(6);
     // ---- split-local softmax statistics: wave h owns head h, lane = key (mod 64)
     if (wid < 2) {
         constexpr int KL = SPL / 64;
@@ -503,7 +532,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
         if (lane == 0) { cml[wid][0] = M; cml[wid][1] = l; }
     }
     __syncthreads();
-    trace_mark(a.trace, 7);
+    mark(7);
     // ---- P.V in fp32 (probabilities kept fp32: a Q8_0 o-proj re-quantises
     //      this output, so its rounding must not move)
     float acc0[8], acc1[8];
@@ -526,7 +555,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     *(floatx4 *)&ored[wid * 4 + sub][1][dl] = floatx4{acc1[0], acc1[1], acc1[2], acc1[3]};
     *(floatx4 *)&ored[wid * 4 + sub][1][dl + 4] = floatx4{acc1[4], acc1[5], acc1[6], acc1[7]};
     __syncthreads();
-    trace_mark(a.trace, 2);
+    mark(2);
     // ---- publish this split's partial: [2 heads][O 128 | m, l, 0, 0], 16-B sc1 stores
     float *gpart = a.part + (((long)b * a.n_kv_head + g) * a.max_splits) * 2 * 132;
     if (tid < 66) {
@@ -547,14 +576,18 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     unsigned int *cnt = a.counter + (long)b * a.n_kv_head + g;
     if (tid == 0) last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nsp - 1;
     __syncthreads();
-    trace_mark(a.trace, 3);
+    mark(3);
     if (!last) return;
     // ---- last arriver: combine the partials of both heads (empty ones weigh 0).
     //      Passes of up to 32 splits are staged through LDS with one burst of
     //      16-B sc1 loads each (a per-split load loop would serialise ~nsp
     //      memory latencies).  Wave h derives head h's split weights once
     //      (lane = split); passes merge with the usual online rescale.
-    if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (FUSED)   // every split is past its wait: re-arm the 8 replicas
+            for (int r = 0; r < 8; r++) __hip_atomic_store(a.qcnt + (g * 8 + r) * 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const int hh = tid >> 7, d = tid & 127;
     float M = -INFINITY, L = 0.f, O = 0.f;
     for (int s0 = 0; s0 < nsp; s0 += 32) {
@@ -562,7 +595,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
         const floatx4 *srcp = (const floatx4 *)(gpart + (long)s0 * 264);
         floatx4 v[9];
         ld_sc1_x4_burst9(srcp, tid, n4, v);
-        if (s0 == 0) trace_mark(a.trace, 5);
+        if (s0 == 0) mark(5);
         __syncthreads();   // previous pass's readers are done with stage / wsp
 #pragma unroll
         for (int j = 0; j < 9; j++)
@@ -599,7 +632,114 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
         if ((d & 31) == 0) a.outd[e >> 5] = q8_scale(am);
     } else if (a.out32) a.out32[(long)b * QD + (2 * g + hh) * 128 + d] = O * inv;
     else a.out[(long)b * QD + (2 * g + hh) * 128 + d] = f_to_u16(O * inv);
-    trace_mark(a.trace, 4);
+    mark(4);
+}
+
+template <int SPL>
+__global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
+    decode_attn_body<SPL, false>(a, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x);
+}
+
+// ------------------------------------------------- batch 1: QKV + attention
+// One launch for the batch-1 QKV projection and the attention it feeds.
+// Blocks [0, 512): the QKV GEMV (gemv1_kernel's arithmetic, K = 1024, 2 rows
+// per wave, RMS norm / layer-0 embedding gather per wave), block q serving kv
+// group q / 64 (its 256 q rows, 128 k rows, 128 v rows); outputs are stored
+// write-through (sc1), every wave drains, and one lane counts the block into
+// qcnt[group] (MI355X_MICROARCH.md hand-off table, row 1).  Blocks past 512:
+// the group's attention splits, which issue their K/V loads before waiting
+// for the count -- the K/V stream overlaps the projection instead of
+// following a kernel boundary.  Dispatch order puts the QKV blocks first; the
+// wait is bounded so no order can hang the GPU.
+template <int SPL>
+__global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnArgs a) {
+    constexpr int K = 1024, NT = 2, RPW = 2;
+    if (blockIdx.x >= 512) {
+        const int j = blockIdx.x - 512, nsp = (gridDim.x - 512) / a.n_kv_head;
+        decode_attn_body<SPL, true>(a, j % nsp, j / nsp, 0, nsp);
+        return;
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int grp = blockIdx.x >> 6, loc = blockIdx.x & 63;
+    if (q.trace && threadIdx.x == 0) q.trace[blockIdx.x * 8] = rt_now();
+    const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
+    // the block's 8 rows: q rows of heads 2g, 2g+1, then k, then v of group g
+    const int rbase = loc < 32 ? grp * 256 + loc * 8 : loc < 48 ? QD + grp * 128 + (loc - 32) * 8 : QD + KD + grp * 128 + (loc - 48) * 8;
+    const int row0 = rbase + wid * RPW;
+    half8 wv[RPW][NT];
+#pragma unroll
+    for (int r = 0; r < RPW; r++)
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+            wv[r][t] = __builtin_nontemporal_load((const half8 *)(q.W + (long)(row0 + r) * K + t * 512 + lane * 8));
+    float xf[NT][8];
+    if (q.embd_ids) {   // layer 0: x = token_embd[id]
+        const uint16_t *er = q.embd + (long)q.embd_ids[0] * K;
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            const half8 h = *(const half8 *)(er + t * 512 + lane * 8);
+#pragma unroll
+            for (int e = 0; e < 8; e++) xf[t][e] = (float)h[e];
+        }
+        if (q.x_store && blockIdx.x == 0 && wid == 0)
+#pragma unroll
+            for (int t = 0; t < NT; t++) {
+                *(float4 *)(q.x_store + t * 512 + lane * 8) = make_float4(xf[t][0], xf[t][1], xf[t][2], xf[t][3]);
+                *(float4 *)(q.x_store + t * 512 + lane * 8 + 4) = make_float4(xf[t][4], xf[t][5], xf[t][6], xf[t][7]);
+            }
+    } else {
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            const float4 u = *(const float4 *)(q.x + t * 512 + lane * 8);
+            const float4 v = *(const float4 *)(q.x + t * 512 + lane * 8 + 4);
+            xf[t][0] = u.x; xf[t][1] = u.y; xf[t][2] = u.z; xf[t][3] = u.w;
+            xf[t][4] = v.x; xf[t][5] = v.y; xf[t][6] = v.z; xf[t][7] = v.w;
+        }
+    }
+    double ss = 0.0;   // ggml_rms_norm: double sum of fp32 squares
+#pragma unroll
+    for (int t = 0; t < NT; t++)
+#pragma unroll
+        for (int e = 0; e < 8; e++) ss += (double)(xf[t][e] * xf[t][e]);
+    ss = wave_sum_d(ss);
+    const float scale = 1.0f / sqrtf((float)(ss / K) + q.eps);
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+        const float4 u = *(const float4 *)(q.norm_w + t * 512 + lane * 8);
+        const float4 v = *(const float4 *)(q.norm_w + t * 512 + lane * 8 + 4);
+        const float w[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 8; e++) xf[t][e] = (float)f2h(fmul_rn(fmul_rn(xf[t][e], scale), w[e]));
+    }
+#pragma unroll
+    for (int r = 0; r < RPW; r++) {
+        float acc = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+            for (int e = 0; e < 8; e++) acc = fmaf((float)wv[r][t][e], xf[t][e], acc);
+        acc = wave_sum(acc);
+        if (lane == 0) __hip_atomic_store((uint32_t *)(q.out_f32 + row0 + r), __float_as_uint(acc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < 8)   // one lane per replica of the group's counter
+        __hip_atomic_fetch_add(a.qcnt + (grp * 8 + threadIdx.x) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (q.trace && threadIdx.x == 0) q.trace[blockIdx.x * 8 + 1] = rt_now();
+}
+
+bool launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, hipStream_t s) {
+    static const int off = [] { const char *e = getenv("QASR_FUSE_QKV"); return e && e[0] == '0'; }();
+    if (off || a.B != 1 || !a.qcnt || q.M != 1 || q.K != 1024 || q.Wd || !q.norm_w || q.xh || q.bias || q.res || a.out32 || a.outq ||
+        q.N != a.n_head * 128 + 2 * a.n_kv_head * 128 || a.n_head != 2 * a.n_kv_head || a.n_kv_head * 64 != 512)
+        return false;
+    static const int env = [] { const char *e = getenv("QASR_ATT_SPL1"); return e ? atoi(e) : 0; }();
+    const int spl1 = env == 64 || env == 128 ? env : a.grid_splits >= 16 ? 128 : 64;   // as launch_decode_attention
+    const int ns = (a.grid_splits * DSPLIT + spl1 - 1) / spl1;
+    const dim3 grid(512 + ns * a.n_kv_head);
+    if (spl1 == 128) hipLaunchKernelGGL(qkv_attn1_kernel<128>, grid, dim3(256), 0, s, q, a);
+    else hipLaunchKernelGGL(qkv_attn1_kernel<DSPLIT>, grid, dim3(256), 0, s, q, a);
+    return true;
 }
 
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {

@@ -106,6 +106,7 @@ struct qasr_ctx {
     int *d_pos = nullptr, *d_nkv = nullptr, *d_slot = nullptr, *d_step = nullptr;
     float *d_x = nullptr, *d_qkv = nullptr, *d_part = nullptr, *d_logits = nullptr;
     unsigned int *d_counter = nullptr, *d_done = nullptr;
+    unsigned int *d_qcnt = nullptr;   // fused batch-1 QKV + attention: QKV-block arrivals per kv group
     uint16_t *d_q = nullptr, *d_att = nullptr, *d_act = nullptr, *d_xh = nullptr;
     unsigned long long *d_amax = nullptr;
     int max_splits = 0, hist_cap = 0;
@@ -560,6 +561,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_x32, (size_t)B * std::max(QD, std::max(hp.hidden, hp.dec_ffn)) * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_part, (size_t)B * hp.n_kv_head * c->max_splits * 2 * 132 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_counter, (size_t)B * hp.n_kv_head * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_qcnt, (size_t)hp.n_kv_head * 8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_logits, (size_t)B * hp.vocab * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_amax, (size_t)B * 8)))
@@ -568,6 +570,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     for (int b = 0; b < B; b++) slots[b] = b;
     HIPCHK(hipMemcpy(c->d_slot, slots.data(), B * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(c->d_counter, 0, (size_t)B * hp.n_kv_head * 4));
+    HIPCHK(hipMemset(c->d_qcnt, 0, (size_t)hp.n_kv_head * 8 * 16 * 4));
     HIPCHK(hipMemset(c->d_done, 0, 4));
     HIPCHK(hipMemset(c->kc, 0, kv * 2));   // decode attention reads whole splits and masks: keep every row finite
     HIPCHK(hipMemset(c->vc, 0, kv * 2));
@@ -919,13 +922,16 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
             return c->d_trace && l == c->trace_layer ? c->d_trace + (size_t)k * 4096 * 8 : nullptr;
         };
         const bool q8 = m->q8;
+        GemvArgs q1{};   // batch-1 QKV projection, launched together with the attention when fusable
+        bool q1_pending = false;
         if (skinny) {
             GemvArgs q{};
             q.x = x; q.ldx = H; q.norm_w = L.attn_norm; q.eps = hp.rms_eps; q.W = L.wqkv; q.Wd = L.wqkv_d; q.K = H;
             q.N = QD + 2 * KD; q.M = B; q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
             if (l == 0) { q.embd_ids = c->d_tok; q.embd = m->embd; q.x_store = x; }   // fused embedding gather
             q.trace = tr(0);
-            if (!(skip & 1)) launch_gemv(EPI_F32, q, s);
+            if (B == 1 && !q8 && !skip) { q1 = q; q1_pending = true; }
+            else if (!(skip & 1)) launch_gemv(EPI_F32, q, s);
         } else {
             GemmArgs q{};
             q.M = B; q.N = QD + 2 * KD; q.K = H; q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
@@ -945,7 +951,9 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
         da.out32 = q8 && skinny ? c->d_att32 : nullptr;
         if (q8 && !skinny) { da.outq = c->d_q8a; da.outd = c->d_q8d; }
         da.trace = tr(1);
-        if (!(skip & 2)) launch_decode_attention(da, s);
+        da.qcnt = c->d_qcnt;
+        if (q1_pending && !launch_qkv_attention1(q1, da, s)) launch_gemv(EPI_F32, q1, s), q1_pending = false;
+        if (!q1_pending && !(skip & 2)) launch_decode_attention(da, s);
         if (skinny) {
             GemvArgs o{};
             if (q8) { o.x = c->d_att32; o.ldx = QD; o.Wd = L.wo_d; }

@@ -182,8 +182,12 @@ struct DecodeAttnArgs {
     float *out32;                        // non-null: fp32 output instead (input of a Q8_0 o-proj)
     int8_t *outq; float *outd;           // non-null: Q8_0 output [B][QD] int8 + [B][QD/32] scales
     unsigned long long *trace;           // dev trace: per block [start, K/V landed, partial ready, counted, end, burst landed]
+    unsigned int *qcnt;                  // [n_kv_head][8 replicas][16] QKV-block arrivals of the fused batch-1 launch, zero at rest
 };
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
+// batch 1, f16: the QKV projection (q: GemvArgs of the rmsnorm+QKV GEMV, K = 1024)
+// and the attention in one launch (attention.hip); false = not taken
+bool launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, hipStream_t s);
 int decode_split_len();
 int decode_max_splits();
 
