@@ -377,7 +377,7 @@ __device__ __forceinline__ void ld_sc1_x4_burst9(const floatx4 *src, int tid, in
 // the same launch -- requested after this split's K/V, once the kv group's
 // arrival counter (qcnt) shows all 64 of its QKV workgroups, with sc1 loads.
 template <int SPL, bool FUSED>
-__device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs &a, const int sp, const int g, const int b, const int nsp) {
+__device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const int sp, const int g, const int b, const int nsp) {
     __shared__ __attribute__((aligned(16))) uint16_t qs[2][128];
     __shared__ __attribute__((aligned(16))) uint16_t knew[128];
     __shared__ __attribute__((aligned(16))) uint16_t vnew[128];
