@@ -404,6 +404,8 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     if constexpr (!FUSED) { x0 = src[lane]; x1 = src[lane + 64]; }
     const float *nw = wid < 2 ? a.q_norm : a.k_norm;
     const float w0 = nw[lane], w1 = nw[lane + 64];
+    if constexpr (FUSED)   // let the QKV blocks' weight stream get ahead in the memory queues
+        for (int i = 0; i < a.fuse_delay; i++) __builtin_amdgcn_s_sleep(8);
     // ---- every K/V row of the split (addresses depend on blockIdx only; decode
     //      contexts use identity sequence slots).  Rows past the position are
     //      masked below; the cache is zero-initialised so they are finite.
@@ -737,8 +739,12 @@ bool launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, hipStream
     const int spl1 = env == 64 || env == 128 ? env : a.grid_splits >= 16 ? 128 : 64;   // as launch_decode_attention
     const int ns = (a.grid_splits * DSPLIT + spl1 - 1) / spl1;
     const dim3 grid(512 + ns * a.n_kv_head);
-    if (spl1 == 128) hipLaunchKernelGGL(qkv_attn1_kernel<128>, grid, dim3(256), 0, s, q, a);
-    else hipLaunchKernelGGL(qkv_attn1_kernel<DSPLIT>, grid, dim3(256), 0, s, q, a);
+    // ~2 us: measured optimum on MI355X (tools/job_delay.sh: 0 -> 236.3, 10 -> 232.0, 18 -> 240.3 ms decode)
+    static const int delay = [] { const char *e = getenv("QASR_FUSE_DELAY"); return e ? atoi(e) : 10; }();
+    DecodeAttnArgs ad = a;
+    ad.fuse_delay = delay;
+    if (spl1 == 128) hipLaunchKernelGGL(qkv_attn1_kernel<128>, grid, dim3(256), 0, s, q, ad);
+    else hipLaunchKernelGGL(qkv_attn1_kernel<DSPLIT>, grid, dim3(256), 0, s, q, ad);
     return true;
 }
 

@@ -183,6 +183,7 @@ struct DecodeAttnArgs {
     int8_t *outq; float *outd;           // non-null: Q8_0 output [B][QD] int8 + [B][QD/32] scales
     unsigned long long *trace;           // dev trace: per block [start, K/V landed, partial ready, counted, end, burst landed]
     unsigned int *qcnt;                  // [n_kv_head][8 replicas][16] QKV-block arrivals of the fused batch-1 launch, zero at rest
+    int fuse_delay;                      // fused launch: attention blocks idle fuse_delay x ~0.2 us before their K/V loads
 };
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
 // batch 1, f16: the QKV projection (q: GemvArgs of the rmsnorm+QKV GEMV, K = 1024)
