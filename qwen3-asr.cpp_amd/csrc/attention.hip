@@ -353,29 +353,34 @@ __device__ __forceinline__ void st_sc1_x4(float *p, float4 f) {
 // nine 16-B sc1 loads (element tid + 256 j of src, clamped to n4 - 1) issued
 // back to back and drained in the same asm block, so no copy of an output can
 // be scheduled before the data has landed
-__device__ __forceinline__ void ld_sc1_x4_burst9(const floatx4 *src, int tid, int n4, floatx4 *v) {
-    const floatx4 *p[9];
+__device__ __forceinline__ void ld_sc1_x4_burst5(const floatx4 *src, int tid, int n4, floatx4 *v) {
+    const floatx4 *p[5];
 #pragma unroll
-    for (int j = 0; j < 9; j++) p[j] = src + min(tid + 256 * j, n4 - 1);
+    for (int j = 0; j < 5; j++) p[j] = src + min(tid + 256 * j, n4 - 1);
     asm volatile(
-        "global_load_dwordx4 %0, %9, off sc1\n\t"
-        "global_load_dwordx4 %1, %10, off sc1\n\t"
-        "global_load_dwordx4 %2, %11, off sc1\n\t"
-        "global_load_dwordx4 %3, %12, off sc1\n\t"
-        "global_load_dwordx4 %4, %13, off sc1\n\t"
-        "global_load_dwordx4 %5, %14, off sc1\n\t"
-        "global_load_dwordx4 %6, %15, off sc1\n\t"
-        "global_load_dwordx4 %7, %16, off sc1\n\t"
-        "global_load_dwordx4 %8, %17, off sc1\n\t"
+        "global_load_dwordx4 %0, %5, off sc1\n\t"
+        "global_load_dwordx4 %1, %6, off sc1\n\t"
+        "global_load_dwordx4 %2, %7, off sc1\n\t"
+        "global_load_dwordx4 %3, %8, off sc1\n\t"
+        "global_load_dwordx4 %4, %9, off sc1\n\t"
         "s_waitcnt vmcnt(0)"
-        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8])
-        : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7]), "v"(p[8])
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4])
+        : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4])
+        : "memory");
+}
+// four 16-B sc1 loads (p, p + 512 halves, p + 1024, p + 1536) drained in the same asm block
+__device__ __forceinline__ void ld_sc1_x4_4(const uint16_t *p, u32x4 *v) {
+    asm volatile(
+        "global_load_dwordx4 %0, %4, off sc1\n\t"
+        "global_load_dwordx4 %1, %4, off offset:1024 sc1\n\t"
+        "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\t"
+        "global_load_dwordx4 %3, %4, off offset:3072 sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
+        : "v"(p)
         : "memory");
 }
 
-// FUSED (batch 1, qkv_attn1_kernel): the raw q/k/v come from the QKV workgroups of
-// the same launch -- requested after this split's K/V, once the kv group's
-// arrival counter (qcnt) shows all 64 of its QKV workgroups, with sc1 loads.
 template <int SPL, bool FUSED>
 __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const int sp, const int g, const int b, const int nsp) {
     __shared__ __attribute__((aligned(16))) uint16_t qs[2][128];
@@ -387,7 +392,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     __shared__ float wsp[2][32];         // combine: per-split weights of a pass
     __shared__ float lsum[2];
     __shared__ int last;
-    __shared__ floatx4 stage[32 * 66];   // combine: up to 32 splits x 2 heads x 33 float4
+    __shared__ floatx4 stage[16 * 66];   // combine: passes of up to 16 splits x 2 heads x 33 float4
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
     const long blk = sp + (long)nsp * (g + (long)a.n_kv_head * b);   // dev-trace row
@@ -592,15 +597,15 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     }
     const int hh = tid >> 7, d = tid & 127;
     float M = -INFINITY, L = 0.f, O = 0.f;
-    for (int s0 = 0; s0 < nsp; s0 += 32) {
-        const int ns = min(32, nsp - s0), n4 = ns * 66;
+    for (int s0 = 0; s0 < nsp; s0 += 16) {
+        const int ns = min(16, nsp - s0), n4 = ns * 66;
         const floatx4 *srcp = (const floatx4 *)(gpart + (long)s0 * 264);
-        floatx4 v[9];
-        ld_sc1_x4_burst9(srcp, tid, n4, v);
+        floatx4 v[5];
+        ld_sc1_x4_burst5(srcp, tid, n4, v);
         if (s0 == 0) mark(5);
         __syncthreads();   // previous pass's readers are done with stage / wsp
 #pragma unroll
-        for (int j = 0; j < 9; j++)
+        for (int j = 0; j < 5; j++)
             if (tid + 256 * j < n4) stage[tid + 256 * j] = v[j];
         __syncthreads();
         const float *sf = (const float *)stage;
@@ -633,7 +638,18 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
         a.outq[e] = q8_quant(v, am);
         if ((d & 31) == 0) a.outd[e >> 5] = q8_scale(am);
     } else if (a.out32) a.out32[(long)b * QD + (2 * g + hh) * 128 + d] = O * inv;
-    else a.out[(long)b * QD + (2 * g + hh) * 128 + d] = f_to_u16(O * inv);
+    else if (FUSED && a.att_done) {
+        // the o-proj blocks of this launch read it: write-through 4-byte pairs,
+        // every wave drained, then one arrival per replica of att_done
+        const uint32_t h = f_to_u16(O * inv);
+        const uint32_t hn = __shfl_xor(h, 1, 64);
+        if ((d & 1) == 0)
+            __hip_atomic_store((uint32_t *)(a.out + (long)b * QD + (2 * g + hh) * 128 + d), h | (hn << 16), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid < 8) __hip_atomic_fetch_add(a.att_done + tid * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else a.out[(long)b * QD + (2 * g + hh) * 128 + d] = f_to_u16(O * inv);
     mark(4);
 }
 
@@ -653,11 +669,57 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
 // for the count -- the K/V stream overlaps the projection instead of
 // following a kernel boundary.  Dispatch order puts the QKV blocks first; the
 // wait is bounded so no order can hang the GPU.
+// Blocks past the attention splits (when att_done is set): the o-projection
+// (gemv1 arithmetic, K = 2048, one row per wave, + residual): weights
+// requested after a delay, a bounded wait for all kv groups' combiners
+// (att_done replica block % 8), then the fp16 attention output and the
+// residual row read with sc1 loads.  att_done is re-armed by the down-proj
+// launch that follows (GemvArgs.zero8).
+__device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnArgs a, int j) {
+    constexpr int K = 2048, NT = 4;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int row = j * 4 + wid;
+    for (int i = 0; i < a.oproj_delay; i++) __builtin_amdgcn_s_sleep(8);
+    half8 wv[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) wv[t] = __builtin_nontemporal_load((const half8 *)(o.W + (long)row * K + t * 512 + lane * 8));
+    __shared__ int oready;
+    if (threadIdx.x == 0) {
+        int ok = 0;
+        for (int it = 0; it < (1 << 22); it++) {
+            if (__hip_atomic_load(a.att_done + (j & 7) * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)a.n_kv_head) {
+                ok = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+        oready = ok;
+    }
+    __syncthreads();
+    (void)oready;
+    u32x4 xv[NT];
+    ld_sc1_x4_4(o.xh + lane * 8, xv);
+    const float res = __uint_as_float(__hip_atomic_load((const uint32_t *)(o.res + row), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    float acc = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+        const half8 h = __builtin_bit_cast(half8, xv[t]);
+#pragma unroll
+        for (int e = 0; e < 8; e++) acc = fmaf((float)wv[t][e], (float)h[e], acc);
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) o.out_f32[row] = fadd_rn(acc, res);
+}
+
 template <int SPL>
-__global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnArgs a) {
+__global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnArgs a, GemvArgs o) {
     constexpr int K = 1024, NT = 2, RPW = 2;
     if (blockIdx.x >= 512) {
-        const int j = blockIdx.x - 512, nsp = (gridDim.x - 512) / a.n_kv_head;
+        const int j = blockIdx.x - 512, nsp = a.grid_splits, nat = nsp * a.n_kv_head;   // grid_splits: this launch's splits
+        if (j >= nat) {
+            oproj1_body(o, a, j - nat);
+            return;
+        }
         decode_attn_body<SPL, true>(a, j % nsp, j / nsp, 0, nsp);
         return;
     }
@@ -683,12 +745,13 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
 #pragma unroll
             for (int e = 0; e < 8; e++) xf[t][e] = (float)h[e];
         }
-        if (q.x_store && blockIdx.x == 0 && wid == 0)
+        if (q.x_store && blockIdx.x == 0 && wid == 0)   // write-through: the fused o-proj adds it as its residual
 #pragma unroll
-            for (int t = 0; t < NT; t++) {
-                *(float4 *)(q.x_store + t * 512 + lane * 8) = make_float4(xf[t][0], xf[t][1], xf[t][2], xf[t][3]);
-                *(float4 *)(q.x_store + t * 512 + lane * 8 + 4) = make_float4(xf[t][4], xf[t][5], xf[t][6], xf[t][7]);
-            }
+            for (int t = 0; t < NT; t++)
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                    __hip_atomic_store((uint32_t *)(q.x_store + t * 512 + lane * 8 + e), __float_as_uint(xf[t][e]), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
     } else {
 #pragma unroll
         for (int t = 0; t < NT; t++) {
@@ -730,22 +793,31 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
     if (q.trace && threadIdx.x == 0) q.trace[blockIdx.x * 8 + 1] = rt_now();
 }
 
-bool launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, hipStream_t s) {
+int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, hipStream_t s) {
     static const int off = [] { const char *e = getenv("QASR_FUSE_QKV"); return e && e[0] == '0'; }();
     if (off || a.B != 1 || !a.qcnt || q.M != 1 || q.K != 1024 || q.Wd || !q.norm_w || q.xh || q.bias || q.res || a.out32 || a.outq ||
         q.N != a.n_head * 128 + 2 * a.n_kv_head * 128 || a.n_head != 2 * a.n_kv_head || a.n_kv_head * 64 != 512)
-        return false;
+        return 0;
     static const int env = [] { const char *e = getenv("QASR_ATT_SPL1"); return e ? atoi(e) : 0; }();
     const int spl1 = env == 64 || env == 128 ? env : a.grid_splits >= 16 ? 128 : 64;   // as launch_decode_attention
     const int ns = (a.grid_splits * DSPLIT + spl1 - 1) / spl1;
-    const dim3 grid(512 + ns * a.n_kv_head);
+    // the o-projection joins when it is the plain batch-1 f16 one (K = 2048, + residual)
+    static const int fuse_o = [] { const char *e = getenv("QASR_FUSE_O"); return e && e[0] == '0' ? 0 : 1; }();
+    const bool with_o = fuse_o && o && a.att_done && o->M == 1 && o->K == 2048 && o->N == 1024 && o->xh && o->res &&
+                        !o->Wd && !o->bias && !o->norm_w && o->xh == a.out;
+    const dim3 grid(512 + ns * a.n_kv_head + (with_o ? o->N / 4 : 0));
     // ~2 us: measured optimum on MI355X (tools/job_delay.sh: 0 -> 236.3, 10 -> 232.0, 18 -> 240.3 ms decode)
     static const int delay = [] { const char *e = getenv("QASR_FUSE_DELAY"); return e ? atoi(e) : 10; }();
+    static const int odelay = [] { const char *e = getenv("QASR_FUSE_ODELAY"); return e ? atoi(e) : 20; }();
     DecodeAttnArgs ad = a;
     ad.fuse_delay = delay;
-    if (spl1 == 128) hipLaunchKernelGGL(qkv_attn1_kernel<128>, grid, dim3(256), 0, s, q, ad);
-    else hipLaunchKernelGGL(qkv_attn1_kernel<DSPLIT>, grid, dim3(256), 0, s, q, ad);
-    return true;
+    ad.oproj_delay = odelay;
+    ad.grid_splits = ns;   // the kernel's split count
+    if (!with_o) ad.att_done = nullptr;
+    const GemvArgs oa = with_o ? *o : GemvArgs{};
+    if (spl1 == 128) hipLaunchKernelGGL(qkv_attn1_kernel<128>, grid, dim3(256), 0, s, q, ad, oa);
+    else hipLaunchKernelGGL(qkv_attn1_kernel<DSPLIT>, grid, dim3(256), 0, s, q, ad, oa);
+    return with_o ? 2 : 1;
 }
 
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {

@@ -107,6 +107,7 @@ struct qasr_ctx {
     float *d_x = nullptr, *d_qkv = nullptr, *d_part = nullptr, *d_logits = nullptr;
     unsigned int *d_counter = nullptr, *d_done = nullptr;
     unsigned int *d_qcnt = nullptr;   // fused batch-1 QKV + attention: QKV-block arrivals per kv group
+    unsigned int *d_attdone = nullptr;   // fused batch-1 o-proj: combiner arrivals (8 replicas)
     uint16_t *d_q = nullptr, *d_att = nullptr, *d_act = nullptr, *d_xh = nullptr;
     unsigned long long *d_amax = nullptr;
     int max_splits = 0, hist_cap = 0;
@@ -562,6 +563,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_part, (size_t)B * hp.n_kv_head * c->max_splits * 2 * 132 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_counter, (size_t)B * hp.n_kv_head * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_qcnt, (size_t)hp.n_kv_head * 8 * 16 * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_attdone, (size_t)8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_logits, (size_t)B * hp.vocab * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_amax, (size_t)B * 8)))
@@ -571,6 +573,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     HIPCHK(hipMemcpy(c->d_slot, slots.data(), B * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(c->d_counter, 0, (size_t)B * hp.n_kv_head * 4));
     HIPCHK(hipMemset(c->d_qcnt, 0, (size_t)hp.n_kv_head * 8 * 16 * 4));
+    HIPCHK(hipMemset(c->d_attdone, 0, (size_t)8 * 16 * 4));
     HIPCHK(hipMemset(c->d_done, 0, 4));
     HIPCHK(hipMemset(c->kc, 0, kv * 2));   // decode attention reads whole splits and masks: keep every row finite
     HIPCHK(hipMemset(c->vc, 0, kv * 2));
@@ -952,15 +955,23 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
         if (q8 && !skinny) { da.outq = c->d_q8a; da.outd = c->d_q8d; }
         da.trace = tr(1);
         da.qcnt = c->d_qcnt;
-        if (q1_pending && !launch_qkv_attention1(q1, da, s)) launch_gemv(EPI_F32, q1, s), q1_pending = false;
-        if (!q1_pending && !(skip & 2)) launch_decode_attention(da, s);
+        GemvArgs o{};
         if (skinny) {
-            GemvArgs o{};
             if (q8) { o.x = c->d_att32; o.ldx = QD; o.Wd = L.wo_d; }
             else { o.xh = c->d_att; o.ldxh = QD; }
             o.trace = tr(2);
             o.W = L.wo; o.K = QD; o.N = H; o.M = B; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
-            if (!(skip & 4)) launch_gemv(EPI_F32, o, s);
+        }
+        bool o_fused = false;
+        if (q1_pending) {
+            da.att_done = c->d_attdone;
+            const int r = launch_qkv_attention1(q1, da, &o, s);
+            if (r == 0) { launch_gemv(EPI_F32, q1, s); q1_pending = false; }
+            o_fused = r == 2;
+        }
+        if (!q1_pending && !(skip & 2)) launch_decode_attention(da, s);
+        if (skinny) {
+            if (!o_fused && !(skip & 4)) launch_gemv(EPI_F32, o, s);
             GemvArgs gu{};
             gu.x = x; gu.ldx = H; gu.norm_w = L.ffn_norm; gu.eps = hp.rms_eps; gu.W = L.wgu; gu.Wd = L.wgu_d; gu.K = H; gu.N = F; gu.M = B;
             if (q8) { gu.out_f32 = c->d_act32; gu.ldo = F; }
@@ -971,6 +982,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
             if (q8) { dn.x = c->d_act32; dn.ldx = F; dn.Wd = L.wd_d; }
             else { dn.xh = c->d_act; dn.ldxh = F; }
             dn.W = L.wd; dn.K = F; dn.N = H; dn.M = B; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
+            if (o_fused) dn.zero8 = c->d_attdone;   // re-arm the fused o-proj's arrival counters
             dn.trace = tr(4);
             if (!(skip & 16)) launch_gemv(EPI_F32, dn, s);
         } else if (q8) {

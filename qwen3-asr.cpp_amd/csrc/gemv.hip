@@ -28,6 +28,7 @@ __global__ __launch_bounds__(256) void gemv1_kernel(GemvArgs g) {
     const int lane = threadIdx.x & 63;
     const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
     trace_mark(g.trace, 0);
+    if (g.zero8 && blockIdx.x == 0 && threadIdx.x < 8) g.zero8[threadIdx.x * 16] = 0u;   // fused o-proj counters
     half8 wv[RPW][NR][NT];
 #pragma unroll
     for (int r = 0; r < RPW; r++)

@@ -114,6 +114,7 @@ struct GemvArgs {
     // and re-arms amax and done (both zero at rest)
     unsigned int *done; int32_t *tok_out; int32_t *hist; int hist_stride; int *step; int *pos;
     unsigned long long *trace;           // dev trace: per block [start, end, ...] (8 slots, 100 MHz clock) or null
+    unsigned int *zero8;                 // gemv1: block 0 re-arms these 8 replicated counters (16-word stride)
 };
 void launch_gemv(int epi, const GemvArgs &g, hipStream_t s);
 // gemv.hip: one-row f16 fast path of launch_gemv (false = not covered)
@@ -184,11 +185,15 @@ struct DecodeAttnArgs {
     unsigned long long *trace;           // dev trace: per block [start, K/V landed, partial ready, counted, end, burst landed]
     unsigned int *qcnt;                  // [n_kv_head][8 replicas][16] QKV-block arrivals of the fused batch-1 launch, zero at rest
     int fuse_delay;                      // fused launch: attention blocks idle fuse_delay x ~0.2 us before their K/V loads
+    unsigned int *att_done;              // [8 replicas][16] combiner arrivals for the fused o-proj (re-armed by the down-proj)
+    int oproj_delay;                     // fused launch: o-proj blocks idle oproj_delay x ~0.2 us before their weight loads
 };
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
 // batch 1, f16: the QKV projection (q: GemvArgs of the rmsnorm+QKV GEMV, K = 1024)
 // and the attention in one launch (attention.hip); false = not taken
-bool launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, hipStream_t s);
+// (and, when o is the plain batch-1 o-projection, that too); returns 0 = not
+// taken, 1 = QKV + attention, 2 = QKV + attention + o-projection
+int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, hipStream_t s);
 int decode_split_len();
 int decode_max_splits();
 
