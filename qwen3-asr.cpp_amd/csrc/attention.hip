@@ -14,6 +14,7 @@
 //
 // Decoder single token: split-K flash decoding (VALU; 2 q heads per kv head)
 // + a combine kernel.
+#include <algorithm>
 #include <cstdlib>
 
 #include "dev_common.h"
@@ -805,7 +806,23 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     static const int fuse_o = [] { const char *e = getenv("QASR_FUSE_O"); return e && e[0] == '0' ? 0 : 1; }();
     const bool with_o = fuse_o && o && a.att_done && o->M == 1 && o->K == 2048 && o->N == 1024 && o->xh && o->res &&
                         !o->Wd && !o->bias && !o->norm_w && o->xh == a.out;
-    const dim3 grid(512 + ns * a.n_kv_head + (with_o ? o->N / 4 : 0));
+    // every block of the launch must be co-resident (blocks wait on earlier
+    // ones): fall back to separate launches for contexts that would not fit
+    static const int slots = [] {
+        int nb = 0, nb2 = 0, dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(qkv_attn1_kernel<128>), 256, 0) !=
+                hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, reinterpret_cast<const void *>(qkv_attn1_kernel<DSPLIT>), 256, 0) !=
+                hipSuccess)
+            return 0;   // unknown capacity: never fuse
+        return std::min(nb, nb2) * cus;
+    }();
+    const bool fit_o = 512 + ns * a.n_kv_head + 256 <= slots;
+    if (512 + ns * a.n_kv_head > slots) return 0;
+    const bool with_o2 = with_o && fit_o;
+    const dim3 grid(512 + ns * a.n_kv_head + (with_o2 ? o->N / 4 : 0));
     // ~2 us: measured optimum on MI355X (tools/job_delay.sh: 0 -> 236.3, 10 -> 232.0, 18 -> 240.3 ms decode)
     static const int delay = [] { const char *e = getenv("QASR_FUSE_DELAY"); return e ? atoi(e) : 10; }();
     static const int odelay = [] { const char *e = getenv("QASR_FUSE_ODELAY"); return e ? atoi(e) : 20; }();
@@ -813,11 +830,11 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     ad.fuse_delay = delay;
     ad.oproj_delay = odelay;
     ad.grid_splits = ns;   // the kernel's split count
-    if (!with_o) ad.att_done = nullptr;
-    const GemvArgs oa = with_o ? *o : GemvArgs{};
+    if (!with_o2) ad.att_done = nullptr;
+    const GemvArgs oa = with_o2 ? *o : GemvArgs{};
     if (spl1 == 128) hipLaunchKernelGGL(qkv_attn1_kernel<128>, grid, dim3(256), 0, s, q, ad, oa);
     else hipLaunchKernelGGL(qkv_attn1_kernel<DSPLIT>, grid, dim3(256), 0, s, q, ad, oa);
-    return with_o ? 2 : 1;
+    return with_o2 ? 2 : 1;
 }
 
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {
