@@ -108,6 +108,7 @@ struct qasr_ctx {
     unsigned int *d_counter = nullptr, *d_done = nullptr;
     unsigned int *d_qcnt = nullptr;   // fused batch-1 QKV + attention: QKV-block arrivals per kv group
     unsigned int *d_attdone = nullptr;   // fused batch-1 o-proj: combiner arrivals (8 replicas)
+    unsigned int *d_ffncnt = nullptr;    // fused batch-1 FFN: gate/up arrivals, [layer][32 shards][16]
     uint16_t *d_q = nullptr, *d_att = nullptr, *d_act = nullptr, *d_xh = nullptr;
     unsigned long long *d_amax = nullptr;
     int max_splits = 0, hist_cap = 0;
@@ -564,6 +565,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_counter, (size_t)B * hp.n_kv_head * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_qcnt, (size_t)hp.n_kv_head * 8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_attdone, (size_t)8 * 16 * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_ffncnt, (size_t)hp.dec_layers * 512 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_logits, (size_t)B * hp.vocab * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_amax, (size_t)B * 8)))
@@ -574,6 +576,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     HIPCHK(hipMemset(c->d_counter, 0, (size_t)B * hp.n_kv_head * 4));
     HIPCHK(hipMemset(c->d_qcnt, 0, (size_t)hp.n_kv_head * 8 * 16 * 4));
     HIPCHK(hipMemset(c->d_attdone, 0, (size_t)8 * 16 * 4));
+    HIPCHK(hipMemset(c->d_ffncnt, 0, (size_t)hp.dec_layers * 512 * 4));
     HIPCHK(hipMemset(c->d_done, 0, 4));
     HIPCHK(hipMemset(c->kc, 0, kv * 2));   // decode attention reads whole splits and masks: keep every row finite
     HIPCHK(hipMemset(c->vc, 0, kv * 2));
@@ -977,14 +980,17 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
             if (q8) { gu.out_f32 = c->d_act32; gu.ldo = F; }
             else { gu.out_f16 = c->d_act; gu.ldo16 = F; }
             gu.trace = tr(3);
-            if (!(skip & 8)) launch_gemv(q8 ? EPI_SWIGLU_F32 : EPI_SWIGLU_F16, gu, s);
             GemvArgs dn{};
             if (q8) { dn.x = c->d_act32; dn.ldx = F; dn.Wd = L.wd_d; }
             else { dn.xh = c->d_act; dn.ldxh = F; }
             dn.W = L.wd; dn.K = F; dn.N = H; dn.M = B; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
             if (o_fused) dn.zero8 = c->d_attdone;   // re-arm the fused o-proj's arrival counters
             dn.trace = tr(4);
-            if (!(skip & 16)) launch_gemv(EPI_F32, dn, s);
+            if (skip & 24 || hp.dec_layers < 2 ||
+                !launch_ffn1(gu, dn, c->d_ffncnt + (size_t)l * 512, c->d_ffncnt + (size_t)((l + 1) % hp.dec_layers) * 512, s)) {
+                if (!(skip & 8)) launch_gemv(q8 ? EPI_SWIGLU_F32 : EPI_SWIGLU_F16, gu, s);
+                if (!(skip & 16)) launch_gemv(EPI_F32, dn, s);
+            }
         } else if (q8) {
             GemmArgs o{};
             o.M = B; o.N = H; o.K = QD; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;

@@ -163,6 +163,161 @@ static bool gemv1_k(const GemvArgs &g, hipStream_t s) {
     }
 }
 
+// ------------------------------------------------ batch 1: gate/up + down
+// One launch for the batch-1 FFN (text_decoder.cpp:545-560: rms_norm * w ->
+// silu(gate) * up -> down + residual).  Blocks [0, F/4): the gate/up GEMV
+// (gemv1_kernel<EPI_SWIGLU_F16, K, 1> arithmetic, 4 outputs per block); the
+// block's 4 fp16 outputs leave as two write-through 32-bit stores, the wave
+// drains, and its lane 0 counts the block into shard b % 32 of the layer's
+// counter (MI355X_MICROARCH.md inter-workgroup hand-off, row 2 with sharded
+// replicas: one counter of 768 arrivals serialises ~12 ns per atomic at the
+// memory side, ~9 us; 32 shards hold 24 each).  Blocks past F/4: the down
+// projection (gemv1_kernel<EPI_F32, F, 1> arithmetic + residual), which
+// requests its weights once the gate/up stream is under way (both at once
+// just split the same HBM queue: measured slower than two launches), then
+// polls the 32 shards (one lane each, one wave) and reads the activation
+// with sc1 loads -- the down weight stream overlaps the gate/up one instead of
+// following a kernel boundary.  Counters are per layer; block 0 re-arms the
+// next layer's (its last use ended a whole step ago), so the fusion needs two
+// or more layers.  The residual x is read by the gate/up blocks and rewritten
+// (row by row) by the down blocks only after every gate/up block has arrived.
+__device__ __forceinline__ void ld_sc1_x4_6(const uint16_t *p, u32x4 *v) {
+    asm volatile(
+        "global_load_dwordx4 %0, %6, off sc1\n\t"
+        "global_load_dwordx4 %1, %6, off offset:1024 sc1\n\t"
+        "global_load_dwordx4 %2, %6, off offset:2048 sc1\n\t"
+        "global_load_dwordx4 %3, %6, off offset:3072 sc1\n\t"
+        "global_load_dwordx4 %4, %7, off sc1\n\t"
+        "global_load_dwordx4 %5, %7, off offset:1024 sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5])
+        : "v"(p), "v"(p + 2048)
+        : "memory");
+}
+
+template <int K, int F>
+__global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, unsigned int *cnt, unsigned int *cnt_next, int wdelay, int delay) {
+    constexpr int NT = K / 512, NTD = F / 512, NGU = F / 4;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (blockIdx.x >= NGU) {   // ---- down projection
+        const int j = blockIdx.x - NGU, row = j * 4 + wid;
+        if (d.trace && threadIdx.x == 0) d.trace[j * 8] = rt_now();
+        for (int i = 0; i < wdelay; i++) __builtin_amdgcn_s_sleep(8);   // let the gate/up stream go first
+        half8 wv[NTD];
+#pragma unroll
+        for (int t = 0; t < NTD; t++) wv[t] = __builtin_nontemporal_load((const half8 *)(d.W + (long)row * F + t * 512 + lane * 8));
+        // one polling lane per block, and only once the gate/up stream is
+        // nearly done: pollers beside a weight stream cost it bandwidth
+        // (MI355X_MICROARCH.md, polling-cost)
+        if (wid == 0) {   // lane s polls shard s; every shard holds NGU / 32 arrivals when done
+            for (int i = 0; i < delay; i++) __builtin_amdgcn_s_sleep(8);
+            for (int it = 0; it < (1 << 20); it++) {
+                const unsigned v = lane < 32 ? __hip_atomic_load(cnt + lane * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+                if (__all(v >= (unsigned)(NGU / 32))) break;
+                __builtin_amdgcn_s_sleep(8);
+            }
+        }
+        __syncthreads();
+        u32x4 xv[NTD];
+        static_assert(NTD == 6, "ld_sc1_x4_6 covers F = 3072");
+        ld_sc1_x4_6(d.xh + lane * 8, xv);
+        const float res = d.res[row];
+        float acc = 0.f;
+#pragma unroll
+        for (int t = 0; t < NTD; t++) {
+            const half8 h = __builtin_bit_cast(half8, xv[t]);
+#pragma unroll
+            for (int e = 0; e < 8; e++) acc = fmaf((float)wv[t][e], (float)h[e], acc);
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) d.out_f32[row] = fadd_rn(acc, res);
+        if (d.trace && threadIdx.x == 0) d.trace[j * 8 + 1] = rt_now();
+        return;
+    }
+    // ---- gate/up (16-row interleave: output o = rows 32 (o / 16) + o % 16 and + 16)
+    if (g.trace && threadIdx.x == 0) g.trace[blockIdx.x * 8] = rt_now();
+    if (blockIdx.x == 0 && threadIdx.x < 32) {   // re-arm: the next layer's shards and the fused o-proj's counters
+        cnt_next[threadIdx.x * 16] = 0u;
+        if (d.zero8 && threadIdx.x < 8) d.zero8[threadIdx.x * 16] = 0u;
+    }
+    const int o = blockIdx.x * 4 + wid;
+    half8 wv[2][NT];
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+            wv[q][t] = __builtin_nontemporal_load((const half8 *)(g.W + (32L * (o >> 4) + (o & 15) + 16 * q) * K + t * 512 + lane * 8));
+    float xf[NT][8];
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+        const float4 a = *(const float4 *)(g.x + t * 512 + lane * 8);
+        const float4 b = *(const float4 *)(g.x + t * 512 + lane * 8 + 4);
+        xf[t][0] = a.x; xf[t][1] = a.y; xf[t][2] = a.z; xf[t][3] = a.w;
+        xf[t][4] = b.x; xf[t][5] = b.y; xf[t][6] = b.z; xf[t][7] = b.w;
+    }
+    double ss = 0.0;   // ggml_rms_norm: double sum of fp32 squares
+#pragma unroll
+    for (int t = 0; t < NT; t++)
+#pragma unroll
+        for (int e = 0; e < 8; e++) ss += (double)(xf[t][e] * xf[t][e]);
+    ss = wave_sum_d(ss);
+    const float scale = 1.0f / sqrtf((float)(ss / K) + g.eps);
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+        const float4 a = *(const float4 *)(g.norm_w + t * 512 + lane * 8);
+        const float4 b = *(const float4 *)(g.norm_w + t * 512 + lane * 8 + 4);
+        const float w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int e = 0; e < 8; e++) xf[t][e] = (float)f2h(fmul_rn(fmul_rn(xf[t][e], scale), w[e]));
+    }
+    float acc[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        acc[q] = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+            for (int e = 0; e < 8; e++) acc[q] = fmaf((float)wv[q][t][e], xf[t][e], acc[q]);
+        acc[q] = wave_sum(acc[q]);
+    }
+    __shared__ uint16_t outs[4];
+    if (lane == 0) outs[wid] = f_to_u16(silu1(acc[0]) * acc[1]);
+    __syncthreads();
+    if (wid == 0) {
+        if (lane < 2)
+            __hip_atomic_store((uint32_t *)(g.out_f16 + blockIdx.x * 4) + lane, (uint32_t)outs[2 * lane] | ((uint32_t)outs[2 * lane + 1] << 16),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add(cnt + (blockIdx.x & 31) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (g.trace && threadIdx.x == 0) g.trace[blockIdx.x * 8 + 1] = rt_now();
+}
+
+// the plain batch-1 f16 FFN (K = 1024, F = 3072) in one launch when every
+// block is co-resident; false = not covered (two launch_gemv calls instead)
+bool launch_ffn1(const GemvArgs &g, const GemvArgs &d, unsigned int *cnt, unsigned int *cnt_next, hipStream_t s) {
+    static const int off = [] { const char *e = getenv("QASR_FUSE_FFN"); return e && e[0] == '0'; }();
+    if (off || !cnt || !cnt_next || cnt_next == cnt || g.M != 1 || d.M != 1 || g.Wd || d.Wd || g.K != 1024 || g.N != 3072 || !g.x || g.xh || !g.norm_w || g.embd_ids ||
+        !g.out_f16 || d.K != 3072 || d.N != 1024 || d.xh != g.out_f16 || !d.res || d.bias || d.norm_w || !d.out_f32)
+        return false;
+    static const int slots = [] {
+        int nb = 0, dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(ffn1_kernel<1024, 3072>), 256, 0) != hipSuccess)
+            return 0;   // unknown capacity: never fuse
+        return nb * cus;
+    }();
+    const int grid = 3072 / 4 + 1024 / 4;
+    if (grid > slots) return false;   // down blocks wait on gate/up blocks: all must be resident
+    // s_sleep(8) units (~0.2 us): down weights requested ~3 us after the gate/up
+    // ones, first poll ~1 us later (tools/job_ffn3.sh, 92 s decode: unfused
+    // 224.8 ms; 12/4 217.9, 14/4 208.2 (x3), 16/4 210.0, 14/2 210.8, 14/6 210.0, 20/6 221.0)
+    static const int delay = [] { const char *e = getenv("QASR_FFN_DELAY"); return e ? atoi(e) : 4; }();
+    static const int wdelay = [] { const char *e = getenv("QASR_FFN_WDELAY"); return e ? atoi(e) : 14; }();
+    hipLaunchKernelGGL((ffn1_kernel<1024, 3072>), dim3(grid), dim3(256), 0, s, g, d, cnt, cnt_next, wdelay, delay);
+    return true;
+}
+
 // single-row f16 projections of the decode step; false = not covered (the
 // caller falls back to gemm.hip's multi-row kernel)
 bool launch_gemv1(int epi, const GemvArgs &g, hipStream_t s) {

@@ -119,6 +119,10 @@ struct GemvArgs {
 void launch_gemv(int epi, const GemvArgs &g, hipStream_t s);
 // gemv.hip: one-row f16 fast path of launch_gemv (false = not covered)
 bool launch_gemv1(int epi, const GemvArgs &g, hipStream_t s);
+// gemv.hip: batch-1 f16 gate/up + down in one launch; cnt = this layer's 32 x 16
+// words (zero on entry), cnt_next = the next layer's, re-armed here
+// (false = not covered)
+bool launch_ffn1(const GemvArgs &gu, const GemvArgs &dn, unsigned int *cnt, unsigned int *cnt_next, hipStream_t s);
 
 // ---------------------------------------------------------------- norms
 // LayerNorm (ggml_norm + mul + add) fp32 [M][D] -> fp16 y, or fp32 y32 when

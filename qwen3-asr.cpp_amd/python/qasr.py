@@ -180,6 +180,7 @@ class Model:
         hp = Hparams()
         _check(lib().qasr_model_hparams(self.h, C.byref(hp)), "qasr_model_hparams")
         self.hp = hp
+        self.path = path
 
     def close(self):
         if self.h:
