@@ -152,3 +152,29 @@ def test_full_fused_launches_match_separate(full, tmp_path, knob):
     assert np.abs(lg[0] - lo).max() <= bar
     assert np.abs(np.load(l) - lo).max() <= bar
     assert np.abs(np.load(l) - lg[0]).max() <= bar
+
+
+_LONG = r"""
+import sys, numpy as np, qasr
+m = qasr.Model(sys.argv[1]); c = qasr.Context(m, max_batch=1, max_ctx=1280)
+r = c.transcribe([qasr.synth_pcm(15000, 80 * 16000)], max_tokens=24, ignore_eos=True)
+np.save(sys.argv[2], np.asarray(r.tokens[0], np.int32))
+c.close(); m.close()
+"""
+
+
+def test_full_fused_launches_long_context(full, tmp_path):
+    """80 s clip (prompt ~1.06k tokens: 128-key attention splits, 10 per kv
+    group): the fused batch-1 launches and the separate ones (child with both
+    knobs = 0) produce the same 24 greedy tokens."""
+    import subprocess
+    import sys
+    m, _, _ = full
+    c1 = qasr.Context(m, max_batch=1, max_ctx=1280)
+    r = c1.transcribe([qasr.synth_pcm(15000, 80 * SR)], max_tokens=24, ignore_eos=True)
+    c1.close()
+    env = dict(os.environ, QASR_FUSE_FFN="0", QASR_FUSE_QKV="0")
+    t = str(tmp_path / "t.npy")
+    subprocess.run([sys.executable, "-c", _LONG, m.path, t], env=env, check=True, timeout=120,
+                   cwd=os.path.dirname(qasr.__file__))
+    assert list(np.load(t)) == list(r.tokens[0])
