@@ -145,6 +145,29 @@ int qasr_set_system_prompt(qasr_ctx *c, const int32_t *ids, int n);
 int qasr_transcribe_batch(qasr_ctx *c, const float *const *pcm, const int *n, int B, int max_tokens,
                           int ignore_eos, int32_t *tokens, int *n_tokens, qasr_timings *t);
 
+/* ---- per-context options (no reference counterpart: MI355X launch tuning) -- */
+/* Batch-1 decode runs two fused launches per layer whose roles wait on each
+ * other in-launch.  Options, defaulted from the environment
+ * variable in brackets at qasr_ctx_create:
+ *   "fuse_ffn" [QASR_FUSE_FFN], "fuse_qkv" [QASR_FUSE_QKV], "fuse_o" [QASR_FUSE_O]
+ *       1/0: the fused launch or the separate launches (same arithmetic)
+ *   "ffn_delay", "ffn_wdelay", "qkv_delay", "o_delay"  in-launch delays (~0.2 us units)
+ *   "att_spl1" [QASR_ATT_SPL1]   batch <= 8 attention key split: 0 auto, 64, 128
+ *   "poll_limit" [QASR_POLL_LIMIT]  bounded in-launch waits (polls); a wait that
+ *       runs out makes the call fail with QASR_ERR_DEVICE
+ *   "handoff_fence" [QASR_HANDOFF_FENCE]  1: agent-scope release/acquire fences
+ *       around every in-launch hand-off (diagnostic)
+ *   "dec_layers"  diagnostic: decode steps run only the first n decoder layers (0 = all)
+ * Read-only: "slots_ffn", "slots_qkv" (co-resident workgroups of the fused
+ * kernels on the context's device).  Setting an option drops captured decode
+ * graphs.  Unknown names: QASR_ERR_ARG. */
+int qasr_ctx_set_option(qasr_ctx *c, const char *name, int value);
+int qasr_ctx_get_option(const qasr_ctx *c, const char *name, int *value);
+/* diagnostic copy of decode-step state (after qasr_decode_step): "x" fp32
+ * [max_batch][hidden] residual stream, "act" fp16 [max_batch][ffn] SwiGLU
+ * output, "qkv" fp32 [max_batch][q+k+v], "att" fp16 [max_batch][n_head*128] */
+int qasr_debug_read(qasr_ctx *c, const char *buffer, void *dst, int64_t bytes);
+
 /* ---- measurement ---------------------------------------------------------- */
 /* Probe one kernel of the greedy decode step with HIP events on the context's
  * stream during qasr_run (kernel 1 = LM-head GEMV + fused argmax).  Costs one

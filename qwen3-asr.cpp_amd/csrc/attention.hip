@@ -445,10 +445,12 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     if constexpr (FUSED) {
         // wait for the kv group's 64 QKV workgroups (bounded: a lost arrival must
         // not hang the GPU), then read their write-through outputs with sc1 loads
-        __shared__ int qready;
+        // A wait that runs out sets DEVERR_QKV_WAIT and the split still
+        // publishes (its partial is then garbage, the call returns an error):
+        // skipping it would only strand the combiner and the o-proj blocks.
         if (tid == 0) {
             int ok = 0;
-            for (int it = 0; it < (1 << 22); it++) {
+            for (int it = 0; it < a.poll_limit; it++) {
                 // replica sp % 8 of the group's counter (8 replicas, one 64-B line each):
                 // the pollers of a group spread over 8 lines instead of one hot word
                 if (__hip_atomic_load(a.qcnt + (g * 8 + (sp & 7)) * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 64u) {
@@ -457,13 +459,16 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
                 }
                 __builtin_amdgcn_s_sleep(4);
             }
-            qready = ok;
+            if (a.fence) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            if (!ok) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_QKV_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
         const uint32_t *sr = (const uint32_t *)src;
         x0 = __uint_as_float(__hip_atomic_load(sr + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         x1 = __uint_as_float(__hip_atomic_load(sr + lane + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        (void)qready;
     }
     const int pos = a.pos[b];
     const int nkv = pos + 1;
@@ -649,6 +654,11 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
                                __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (a.fence && tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (a.fence) __syncthreads();
         if (tid < 8) __hip_atomic_fetch_add(a.att_done + tid * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else a.out[(long)b * QD + (2 * g + hh) * 128 + d] = f_to_u16(O * inv);
     mark(4);
@@ -687,17 +697,22 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
     __shared__ int oready;
     if (threadIdx.x == 0) {
         int ok = 0;
-        for (int it = 0; it < (1 << 22); it++) {
+        for (int it = 0; it < a.poll_limit; it++) {
             if (__hip_atomic_load(a.att_done + (j & 7) * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)a.n_kv_head) {
                 ok = 1;
                 break;
             }
             __builtin_amdgcn_s_sleep(4);
         }
+        if (a.fence) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (!ok) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_O_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         oready = ok;
     }
     __syncthreads();
-    (void)oready;
+    if (!oready) return;   // reported through the error word; x keeps its old row
     u32x4 xv[NT];
     ld_sc1_x4_4(o.xh + lane * 8, xv);
     const float res = __uint_as_float(__hip_atomic_load((const uint32_t *)(o.res + row), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -789,46 +804,43 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (a.fence && threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (a.fence) __syncthreads();
     if (threadIdx.x < 8)   // one lane per replica of the group's counter
         __hip_atomic_fetch_add(a.qcnt + (grp * 8 + threadIdx.x) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (q.trace && threadIdx.x == 0) q.trace[blockIdx.x * 8 + 1] = rt_now();
 }
 
-int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, hipStream_t s) {
-    static const int off = [] { const char *e = getenv("QASR_FUSE_QKV"); return e && e[0] == '0'; }();
-    if (off || a.B != 1 || !a.qcnt || q.M != 1 || q.K != 1024 || q.Wd || !q.norm_w || q.xh || q.bias || q.res || a.out32 || a.outq ||
-        q.N != a.n_head * 128 + 2 * a.n_kv_head * 128 || a.n_head != 2 * a.n_kv_head || a.n_kv_head * 64 != 512)
+// batch <= 8 key split: cfg 64 / 128, else 128 from 1k keys (half the
+// partials to combine, still >= 64 workgroups per 8 kv heads)
+static int split1(int spl1, int grid_splits) { return spl1 == 64 || spl1 == 128 ? spl1 : grid_splits >= 16 ? 128 : 64; }
+
+int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s) {
+    if (!cfg.qkv || !cfg.err || a.B != 1 || !a.qcnt || q.M != 1 || q.K != 1024 || q.Wd || !q.norm_w || q.xh || q.bias || q.res ||
+        a.out32 || a.outq || q.N != a.n_head * 128 + 2 * a.n_kv_head * 128 || a.n_head != 2 * a.n_kv_head || a.n_kv_head * 64 != 512)
         return 0;
-    static const int env = [] { const char *e = getenv("QASR_ATT_SPL1"); return e ? atoi(e) : 0; }();
-    const int spl1 = env == 64 || env == 128 ? env : a.grid_splits >= 16 ? 128 : 64;   // as launch_decode_attention
+    const int spl1 = split1(cfg.spl1, a.grid_splits);   // as launch_decode_attention
     const int ns = (a.grid_splits * DSPLIT + spl1 - 1) / spl1;
     // the o-projection joins when it is the plain batch-1 f16 one (K = 2048, + residual)
-    static const int fuse_o = [] { const char *e = getenv("QASR_FUSE_O"); return e && e[0] == '0' ? 0 : 1; }();
-    const bool with_o = fuse_o && o && a.att_done && o->M == 1 && o->K == 2048 && o->N == 1024 && o->xh && o->res &&
+    const bool with_o = cfg.o && o && a.att_done && o->M == 1 && o->K == 2048 && o->N == 1024 && o->xh && o->res &&
                         !o->Wd && !o->bias && !o->norm_w && o->xh == a.out;
     // every block of the launch must be co-resident (blocks wait on earlier
     // ones): fall back to separate launches for contexts that would not fit
-    static const int slots = [] {
-        int nb = 0, nb2 = 0, dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(qkv_attn1_kernel<128>), 256, 0) !=
-                hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, reinterpret_cast<const void *>(qkv_attn1_kernel<DSPLIT>), 256, 0) !=
-                hipSuccess)
-            return 0;   // unknown capacity: never fuse
-        return std::min(nb, nb2) * cus;
-    }();
+    const int slots = spl1 == 128 ? cfg.slots_qkv128 : cfg.slots_qkv64;
     const bool fit_o = 512 + ns * a.n_kv_head + 256 <= slots;
     if (512 + ns * a.n_kv_head > slots) return 0;
     const bool with_o2 = with_o && fit_o;
     const dim3 grid(512 + ns * a.n_kv_head + (with_o2 ? o->N / 4 : 0));
-    // ~2 us: measured optimum on MI355X (tools/job_delay.sh: 0 -> 236.3, 10 -> 232.0, 18 -> 240.3 ms decode)
-    static const int delay = [] { const char *e = getenv("QASR_FUSE_DELAY"); return e ? atoi(e) : 10; }();
-    static const int odelay = [] { const char *e = getenv("QASR_FUSE_ODELAY"); return e ? atoi(e) : 20; }();
+    // K/V delay ~2 us: measured optimum on MI355X (tools/job_delay.sh: 0 -> 236.3, 10 -> 232.0, 18 -> 240.3 ms decode)
     DecodeAttnArgs ad = a;
-    ad.fuse_delay = delay;
-    ad.oproj_delay = odelay;
+    ad.fuse_delay = cfg.qkv_delay;
+    ad.oproj_delay = cfg.o_delay;
+    ad.poll_limit = cfg.poll_limit;
+    ad.fence = cfg.fence;
+    ad.err = cfg.err;
     ad.grid_splits = ns;   // the kernel's split count
     if (!with_o2) ad.att_done = nullptr;
     const GemvArgs oa = with_o2 ? *o : GemvArgs{};
@@ -840,10 +852,7 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {
     if (a.B <= 0) return;
     if (a.B <= 8) {
-        // >= 1k keys: 128-key splits (half the partials to combine, still >= 64
-        // workgroups per 8 kv heads); shorter contexts keep 64-key splits
-        static const int spl1 = [] { const char *e = getenv("QASR_ATT_SPL1"); return e ? atoi(e) : 0; }();
-        if (spl1 == 128 || (spl1 == 0 && a.grid_splits >= 16)) {
+        if (split1(a.spl1, a.grid_splits) == 128) {
             const int g2 = (a.grid_splits * DSPLIT + 127) / 128;
             hipLaunchKernelGGL(decode_attn_kernel<128>, dim3(g2, a.n_kv_head, a.B), dim3(256), 0, s, a);
         } else {
@@ -859,6 +868,21 @@ void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {
             hipLaunchKernelGGL(decode_attn_kernel<256>, dim3(g4, a.n_kv_head, a.B), dim3(256), 0, s, a);
         }
     }
+}
+
+int fused_slots_ffn();   // gemv.hip
+
+void fused_slots(FuseCfg &cfg) {
+    auto slots_of = [](const void *kernel) {
+        int nb = 0, dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, 256, 0) != hipSuccess)
+            return 0;   // unknown capacity: never fuse
+        return nb * cus;
+    };
+    cfg.slots_qkv64 = slots_of(reinterpret_cast<const void *>(qkv_attn1_kernel<DSPLIT>));
+    cfg.slots_qkv128 = slots_of(reinterpret_cast<const void *>(qkv_attn1_kernel<128>));
+    cfg.slots_ffn = fused_slots_ffn();
 }
 
 int decode_split_len() { return DSPLIT; }

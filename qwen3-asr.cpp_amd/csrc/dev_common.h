@@ -14,11 +14,21 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define WAVE 64
 
 __device__ __forceinline__ float h2f(f16 h) { return (float)h; }
+// The fp32 value as rounded, opaque to the optimiser.  Without it LLVM folds
+// fptrunc(fmul/fadd) into v_fma_mixlo_f16, which rounds the product straight
+// to fp16 -- one rounding where ggml (and the reference) round to fp32 first
+// and then to fp16: the two differ on rare ties, and a kernel that got the
+// fold disagreed with one that did not (measured: tools/diag_fused2.py, one
+// fp16 ulp on 386 of 3072 SwiGLU outputs at decoder layer 18).
+__device__ __forceinline__ float rn32(float f) {
+    asm("" : "+v"(f));
+    return f;
+}
 // fp32 -> fp16 round-to-nearest-even (v_cvt_f16_f32 under the default mode),
 // identical to ggml's GGML_CPU_FP32_TO_FP16 / F16C _cvtss_sh(x, 0).
-__device__ __forceinline__ f16 f2h(float f) { return (f16)f; }
+__device__ __forceinline__ f16 f2h(float f) { return (f16)rn32(f); }
 __device__ __forceinline__ float u16_to_f(uint16_t u) { return (float)__builtin_bit_cast(f16, u); }
-__device__ __forceinline__ uint16_t f_to_u16(float f) { return __builtin_bit_cast(uint16_t, (f16)f); }
+__device__ __forceinline__ uint16_t f_to_u16(float f) { return __builtin_bit_cast(uint16_t, (f16)rn32(f)); }
 
 // 100 MHz constant clock shared by all CUs (dev trace timestamps)
 __device__ __forceinline__ unsigned long long rt_now() { return __builtin_amdgcn_s_memrealtime(); }

@@ -121,6 +121,9 @@ struct qasr_ctx {
     std::vector<long> staged_off;
     bool eager = false;            // QASR_NO_GRAPH=1: launch the decode step eagerly (profilers)
     int dev_skip = 0;              // QASR_DEV_SKIP bitmask: profiling only, omits decode kernels
+    FuseCfg fuse;                  // batch-1 fused launches: switches, delays, co-residency of this device
+    unsigned int *d_err = nullptr; // sticky device error word of the fused launches (DevErr bits)
+    int dbg_layers = 0;            // diagnostic: decode steps run only the first n decoder layers (0 = all)
     // QASR_DEV_TRACE=<file>: per-block timestamps of one decode layer's kernels
     // (layer QASR_DEV_TRACE_LAYER, default 10) of the last step, dumped by qasr_run
     std::string trace_path;
@@ -156,6 +159,44 @@ struct qasr_ctx {
         if (st) (void)hipStreamDestroy(st);
     }
 };
+
+// per-context options of the fused batch-1 launches: name (qasr_ctx_set_option),
+// environment default, field
+struct FuseOption {
+    const char *name, *env;
+    int FuseCfg::*field;
+};
+static const std::vector<FuseOption> &fuse_options() {
+    static const std::vector<FuseOption> v = {
+        {"fuse_ffn", "QASR_FUSE_FFN", &FuseCfg::ffn},          {"fuse_qkv", "QASR_FUSE_QKV", &FuseCfg::qkv},
+        {"fuse_o", "QASR_FUSE_O", &FuseCfg::o},                {"ffn_delay", "QASR_FFN_DELAY", &FuseCfg::ffn_delay},
+        {"ffn_wdelay", "QASR_FFN_WDELAY", &FuseCfg::ffn_wdelay}, {"qkv_delay", "QASR_FUSE_DELAY", &FuseCfg::qkv_delay},
+        {"o_delay", "QASR_FUSE_ODELAY", &FuseCfg::o_delay},    {"att_spl1", "QASR_ATT_SPL1", &FuseCfg::spl1},
+        {"poll_limit", "QASR_POLL_LIMIT", &FuseCfg::poll_limit}, {"handoff_fence", "QASR_HANDOFF_FENCE", &FuseCfg::fence},
+    };
+    return v;
+}
+
+// the fused launches' sticky device error word: read (and cleared) after every
+// call that ran decode steps; a bounded wait that ran out is a device error
+static int check_dev_err(qasr_ctx *c) {
+    unsigned e = 0;
+    HIPCHK(hipMemcpyAsync(&e, c->d_err, 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (!e) return 0;
+    // a wait that gave up can leave late arrivals in the counters: back to rest
+    HIPCHK(hipMemsetAsync(c->d_err, 0, 4, c->st));
+    HIPCHK(hipMemsetAsync(c->d_ffncnt, 0, (size_t)c->m->hp.dec_layers * 512 * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->d_qcnt, 0, (size_t)c->m->hp.n_kv_head * 8 * 16 * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->d_attdone, 0, (size_t)8 * 16 * 4, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    std::string what;
+    if (e & DEVERR_QKV_WAIT) what += " attention<-QKV";
+    if (e & DEVERR_O_WAIT) what += " o-proj<-attention";
+    if (e & DEVERR_FFN_WAIT) what += " down<-gate/up";
+    return fail(QASR_ERR_DEVICE, "fused decode launch: an in-launch wait timed out (" + what.substr(1) +
+                                     "); outputs of this call are invalid (another process or context sharing the GPU?)");
+}
 
 static int dev_alloc(qasr_ctx *c, void **p, size_t bytes) {
     HIPCHK(hipMalloc(p, bytes ? bytes : 256));
@@ -540,6 +581,11 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     c->eager = ng && ng[0] == '1';
     const char *ds = getenv("QASR_DEV_SKIP");
     if (ds) c->dev_skip = atoi(ds);
+    // fused-launch options: environment defaults, per-context overrides via qasr_ctx_set_option
+    for (const auto &o : fuse_options()) {
+        if (const char *e = getenv(o.env)) c->fuse.*(o.field) = atoi(e);
+    }
+    fused_slots(c->fuse);   // co-residency on this context's device
     if (const char *tp = getenv("QASR_DEV_TRACE")) {
         c->trace_path = tp;
         if (const char *tl = getenv("QASR_DEV_TRACE_LAYER")) c->trace_layer = atoi(tl);
@@ -566,7 +612,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_qcnt, (size_t)hp.n_kv_head * 8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_attdone, (size_t)8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_ffncnt, (size_t)hp.dec_layers * 512 * 4)) ||
-        (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_err, 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_logits, (size_t)B * hp.vocab * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_amax, (size_t)B * 8)))
         return rc;
@@ -578,6 +624,8 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     HIPCHK(hipMemset(c->d_attdone, 0, (size_t)8 * 16 * 4));
     HIPCHK(hipMemset(c->d_ffncnt, 0, (size_t)hp.dec_layers * 512 * 4));
     HIPCHK(hipMemset(c->d_done, 0, 4));
+    HIPCHK(hipMemset(c->d_err, 0, 4));
+    c->fuse.err = c->d_err;
     HIPCHK(hipMemset(c->kc, 0, kv * 2));   // decode attention reads whole splits and masks: keep every row finite
     HIPCHK(hipMemset(c->vc, 0, kv * 2));
     HIPCHK(hipMemset(c->d_amax, 0, (size_t)B * 8));
@@ -586,6 +634,60 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
 }
 
 extern "C" void qasr_ctx_free(qasr_ctx *c) { delete c; }
+
+extern "C" int qasr_ctx_set_option(qasr_ctx *c, const char *name, int value) {
+    if (!c || !name) return fail(QASR_ERR_ARG, "bad arguments");
+    const std::string n = name;
+    if (n == "dec_layers") {
+        if (value < 0 || value > c->m->hp.dec_layers) return fail(QASR_ERR_ARG, "dec_layers out of range");
+        c->dbg_layers = value;
+        c->drop_graphs();
+        return 0;
+    }
+    for (const auto &o : fuse_options())
+        if (n == o.name) {
+            if (n == "poll_limit" && value <= 0) return fail(QASR_ERR_ARG, "poll_limit must be positive");
+            c->fuse.*(o.field) = value;
+            c->drop_graphs();   // captured steps hold the old launch configuration
+            HIPCHK(hipSetDevice(c->m->device));   // arrival counters back to rest
+            HIPCHK(hipMemsetAsync(c->d_ffncnt, 0, (size_t)c->m->hp.dec_layers * 512 * 4, c->st));
+            HIPCHK(hipMemsetAsync(c->d_qcnt, 0, (size_t)c->m->hp.n_kv_head * 8 * 16 * 4, c->st));
+            HIPCHK(hipMemsetAsync(c->d_attdone, 0, (size_t)8 * 16 * 4, c->st));
+            HIPCHK(hipStreamSynchronize(c->st));
+            return 0;
+        }
+    return fail(QASR_ERR_ARG, "unknown option '" + n + "'");
+}
+
+extern "C" int qasr_ctx_get_option(const qasr_ctx *c, const char *name, int *value) {
+    if (!c || !name || !value) return fail(QASR_ERR_ARG, "bad arguments");
+    const std::string n = name;
+    if (n == "dec_layers") { *value = c->dbg_layers; return 0; }
+    if (n == "slots_ffn") { *value = c->fuse.slots_ffn; return 0; }
+    if (n == "slots_qkv") { *value = std::min(c->fuse.slots_qkv64, c->fuse.slots_qkv128); return 0; }
+    for (const auto &o : fuse_options())
+        if (n == o.name) { *value = c->fuse.*(o.field); return 0; }
+    return fail(QASR_ERR_ARG, "unknown option '" + n + "'");
+}
+
+extern "C" int qasr_debug_read(qasr_ctx *c, const char *buffer, void *dst, int64_t bytes) {
+    if (!c || !buffer || !dst || bytes < 0) return fail(QASR_ERR_ARG, "bad arguments");
+    const Hparams &hp = c->m->hp;
+    const int64_t B = c->max_batch, QD = hp.n_head * 128, KD = hp.n_kv_head * 128;
+    const std::string n = buffer;
+    const void *src = nullptr;
+    int64_t cap = 0;
+    if (n == "x") { src = c->d_x; cap = B * hp.hidden * 4; }
+    else if (n == "act") { src = c->d_act; cap = B * hp.dec_ffn * 2; }
+    else if (n == "qkv") { src = c->d_qkv; cap = B * (QD + 2 * KD) * 4; }
+    else if (n == "att") { src = c->d_att; cap = B * QD * 2; }
+    else return fail(QASR_ERR_ARG, "unknown buffer '" + n + "'");
+    if (bytes > cap) return fail(QASR_ERR_ARG, "read past the buffer");
+    HIPCHK(hipSetDevice(c->m->device));
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
 
 // ------------------------------------------------------------ size helpers
 extern "C" int qasr_mel_frames(int n) { return mel_frames(n); }
@@ -922,7 +1024,8 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
     if ((part == 0 || part == 1) && !skinny) launch_embed(c->d_tok, B, m->embd, H, nullptr, nullptr, x, s);
     const int skip = c->dev_skip;   // profiling only (QASR_DEV_SKIP): drop kernels to price them
     if (c->d_trace && (part == 0 || part == 1)) (void)hipMemsetAsync(c->d_trace, 0, 6 * 4096 * 8 * 8, s);
-    for (int l = 0; (part == 0 || part == 1) && l < hp.dec_layers; l++) {
+    const int nl = c->dbg_layers > 0 ? c->dbg_layers : hp.dec_layers;   // diagnostic layer cap
+    for (int l = 0; (part == 0 || part == 1) && l < nl; l++) {
         const DecLayer &L = m->dec[l];
         auto tr = [&](int k) -> unsigned long long * {
             return c->d_trace && l == c->trace_layer ? c->d_trace + (size_t)k * 4096 * 8 : nullptr;
@@ -958,6 +1061,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
         if (q8 && !skinny) { da.outq = c->d_q8a; da.outd = c->d_q8d; }
         da.trace = tr(1);
         da.qcnt = c->d_qcnt;
+        da.spl1 = c->fuse.spl1;
         GemvArgs o{};
         if (skinny) {
             if (q8) { o.x = c->d_att32; o.ldx = QD; o.Wd = L.wo_d; }
@@ -968,7 +1072,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
         bool o_fused = false;
         if (q1_pending) {
             da.att_done = c->d_attdone;
-            const int r = launch_qkv_attention1(q1, da, &o, s);
+            const int r = launch_qkv_attention1(q1, da, &o, c->fuse, s);
             if (r == 0) { launch_gemv(EPI_F32, q1, s); q1_pending = false; }
             o_fused = r == 2;
         }
@@ -986,10 +1090,11 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
             dn.W = L.wd; dn.K = F; dn.N = H; dn.M = B; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
             if (o_fused) dn.zero8 = c->d_attdone;   // re-arm the fused o-proj's arrival counters
             dn.trace = tr(4);
-            if (skip & 24 || hp.dec_layers < 2 ||
-                !launch_ffn1(gu, dn, c->d_ffncnt + (size_t)l * 512, c->d_ffncnt + (size_t)((l + 1) % hp.dec_layers) * 512, s)) {
+            if (skip & 24 || nl < 2 ||
+                !launch_ffn1(gu, dn, c->d_ffncnt + (size_t)l * 512, c->d_ffncnt + (size_t)((l + 1) % nl) * 512, c->fuse, s)) {
                 if (!(skip & 8)) launch_gemv(q8 ? EPI_SWIGLU_F32 : EPI_SWIGLU_F16, gu, s);
                 if (!(skip & 16)) launch_gemv(EPI_F32, dn, s);
+                else if (o_fused) (void)hipMemsetAsync(c->d_attdone, 0, 8 * 16 * 4, s);   // the skipped down-proj re-arms these
             }
         } else if (q8) {
             GemmArgs o{};
@@ -1242,7 +1347,7 @@ extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_pa
     if (logits) HIPCHK(hipMemcpyAsync(logits, c->d_logits, (size_t)B * c->m->hp.vocab * 4, hipMemcpyDeviceToHost, c->st));
     if (argmax) HIPCHK(hipMemcpyAsync(argmax, c->d_tok, B * 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
-    return 0;
+    return check_dev_err(c);
 }
 
 extern "C" int qasr_stage_audio(qasr_ctx *c, const float *const *pcm, const int *n, int B) {
@@ -1328,6 +1433,7 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
     }
     HIPCHK(hipEventRecord(c->ev[4], s));
     HIPCHK(hipEventSynchronize(c->ev[4]));
+    if ((rc = check_dev_err(c))) return rc;
     if ((rc = probe_collect(c, steps))) return rc;
     if (c->d_trace) {   // dev trace dump: raw [6][4096][8] u64
         std::vector<unsigned long long> tr((size_t)6 * 4096 * 8);

@@ -195,29 +195,46 @@ __device__ __forceinline__ void ld_sc1_x4_6(const uint16_t *p, u32x4 *v) {
         : "memory");
 }
 
+struct FfnCtl {
+    unsigned int *cnt, *cnt_next;   // this layer's 32 arrival shards (16-word stride), the next layer's
+    unsigned int *err;              // sticky device error word
+    int wdelay, delay, poll_limit, fence;
+};
+
 template <int K, int F>
-__global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, unsigned int *cnt, unsigned int *cnt_next, int wdelay, int delay) {
+__global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, FfnCtl c) {
     constexpr int NT = K / 512, NTD = F / 512, NGU = F / 4;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (blockIdx.x >= NGU) {   // ---- down projection
         const int j = blockIdx.x - NGU, row = j * 4 + wid;
         if (d.trace && threadIdx.x == 0) d.trace[j * 8] = rt_now();
-        for (int i = 0; i < wdelay; i++) __builtin_amdgcn_s_sleep(8);   // let the gate/up stream go first
+        for (int i = 0; i < c.wdelay; i++) __builtin_amdgcn_s_sleep(8);   // let the gate/up stream go first
         half8 wv[NTD];
 #pragma unroll
         for (int t = 0; t < NTD; t++) wv[t] = __builtin_nontemporal_load((const half8 *)(d.W + (long)row * F + t * 512 + lane * 8));
         // one polling lane per block, and only once the gate/up stream is
         // nearly done: pollers beside a weight stream cost it bandwidth
         // (MI355X_MICROARCH.md, polling-cost)
+        __shared__ int ready;
         if (wid == 0) {   // lane s polls shard s; every shard holds NGU / 32 arrivals when done
-            for (int i = 0; i < delay; i++) __builtin_amdgcn_s_sleep(8);
-            for (int it = 0; it < (1 << 20); it++) {
-                const unsigned v = lane < 32 ? __hip_atomic_load(cnt + lane * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
-                if (__all(v >= (unsigned)(NGU / 32))) break;
+            for (int i = 0; i < c.delay; i++) __builtin_amdgcn_s_sleep(8);
+            int ok = 0;
+            for (int it = 0; it < c.poll_limit; it++) {
+                const unsigned v = lane < 32 ? __hip_atomic_load(c.cnt + lane * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+                if (__all(v >= (unsigned)(NGU / 32))) { ok = 1; break; }
                 __builtin_amdgcn_s_sleep(8);
+            }
+            if (c.fence) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            if (lane == 0) {
+                ready = ok;
+                if (!ok) __hip_atomic_fetch_or(c.err, (unsigned)DEVERR_FFN_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         __syncthreads();
+        if (!ready) return;   // reported through the error word; x keeps its old row
         u32x4 xv[NTD];
         static_assert(NTD == 6, "ld_sc1_x4_6 covers F = 3072");
         ld_sc1_x4_6(d.xh + lane * 8, xv);
@@ -237,7 +254,7 @@ __global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, unsig
     // ---- gate/up (16-row interleave: output o = rows 32 (o / 16) + o % 16 and + 16)
     if (g.trace && threadIdx.x == 0) g.trace[blockIdx.x * 8] = rt_now();
     if (blockIdx.x == 0 && threadIdx.x < 32) {   // re-arm: the next layer's shards and the fused o-proj's counters
-        cnt_next[threadIdx.x * 16] = 0u;
+        c.cnt_next[threadIdx.x * 16] = 0u;
         if (d.zero8 && threadIdx.x < 8) d.zero8[threadIdx.x * 16] = 0u;
     }
     const int o = blockIdx.x * 4 + wid;
@@ -288,35 +305,42 @@ __global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, unsig
             __hip_atomic_store((uint32_t *)(g.out_f16 + blockIdx.x * 4) + lane, (uint32_t)outs[2 * lane] | ((uint32_t)outs[2 * lane + 1] << 16),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add(cnt + (blockIdx.x & 31) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c.fence) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (lane == 0) __hip_atomic_fetch_add(c.cnt + (blockIdx.x & 31) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (g.trace && threadIdx.x == 0) g.trace[blockIdx.x * 8 + 1] = rt_now();
 }
 
 // the plain batch-1 f16 FFN (K = 1024, F = 3072) in one launch when every
 // block is co-resident; false = not covered (two launch_gemv calls instead)
-bool launch_ffn1(const GemvArgs &g, const GemvArgs &d, unsigned int *cnt, unsigned int *cnt_next, hipStream_t s) {
-    static const int off = [] { const char *e = getenv("QASR_FUSE_FFN"); return e && e[0] == '0'; }();
-    if (off || !cnt || !cnt_next || cnt_next == cnt || g.M != 1 || d.M != 1 || g.Wd || d.Wd || g.K != 1024 || g.N != 3072 || !g.x || g.xh || !g.norm_w || g.embd_ids ||
-        !g.out_f16 || d.K != 3072 || d.N != 1024 || d.xh != g.out_f16 || !d.res || d.bias || d.norm_w || !d.out_f32)
+bool launch_ffn1(const GemvArgs &g, const GemvArgs &d, unsigned int *cnt, unsigned int *cnt_next, const FuseCfg &cfg,
+                 hipStream_t s) {
+    if (!cfg.ffn || !cfg.err || !cnt || !cnt_next || cnt_next == cnt || g.M != 1 || d.M != 1 || g.Wd || d.Wd || g.K != 1024 ||
+        g.N != 3072 || !g.x || g.xh || !g.norm_w || g.embd_ids || !g.out_f16 || d.K != 3072 || d.N != 1024 || d.xh != g.out_f16 ||
+        !d.res || d.bias || d.norm_w || !d.out_f32)
         return false;
-    static const int slots = [] {
-        int nb = 0, dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(ffn1_kernel<1024, 3072>), 256, 0) != hipSuccess)
-            return 0;   // unknown capacity: never fuse
-        return nb * cus;
-    }();
     const int grid = 3072 / 4 + 1024 / 4;
-    if (grid > slots) return false;   // down blocks wait on gate/up blocks: all must be resident
-    // s_sleep(8) units (~0.2 us): down weights requested ~3 us after the gate/up
-    // ones, first poll ~1 us later (tools/job_ffn3.sh, 92 s decode: unfused
-    // 224.8 ms; 12/4 217.9, 14/4 208.2 (x3), 16/4 210.0, 14/2 210.8, 14/6 210.0, 20/6 221.0)
-    static const int delay = [] { const char *e = getenv("QASR_FFN_DELAY"); return e ? atoi(e) : 4; }();
-    static const int wdelay = [] { const char *e = getenv("QASR_FFN_WDELAY"); return e ? atoi(e) : 14; }();
-    hipLaunchKernelGGL((ffn1_kernel<1024, 3072>), dim3(grid), dim3(256), 0, s, g, d, cnt, cnt_next, wdelay, delay);
+    if (grid > cfg.slots_ffn) return false;   // down blocks wait on gate/up blocks: all must be resident
+    // delays in s_sleep(8) units (~0.2 us): down weights requested ~3 us after the
+    // gate/up ones, first poll ~1 us later (tools/job_ffn3.sh, 92 s decode:
+    // unfused 224.8 ms; 12/4 217.9, 14/4 208.2 (x3), 16/4 210.0, 14/2 210.8, 14/6 210.0, 20/6 221.0)
+    const FfnCtl c{cnt, cnt_next, cfg.err, cfg.ffn_wdelay, cfg.ffn_delay, cfg.poll_limit, cfg.fence};
+    hipLaunchKernelGGL((ffn1_kernel<1024, 3072>), dim3(grid), dim3(256), 0, s, g, d, c);
     return true;
 }
+
+static int slots_of(const void *kernel) {
+    int nb = 0, dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, 256, 0) != hipSuccess)
+        return 0;   // unknown capacity: never fuse
+    return nb * cus;
+}
+
+int fused_slots_ffn() { return slots_of(reinterpret_cast<const void *>(ffn1_kernel<1024, 3072>)); }
 
 // single-row f16 projections of the decode step; false = not covered (the
 // caller falls back to gemm.hip's multi-row kernel)

@@ -119,10 +119,35 @@ struct GemvArgs {
 void launch_gemv(int epi, const GemvArgs &g, hipStream_t s);
 // gemv.hip: one-row f16 fast path of launch_gemv (false = not covered)
 bool launch_gemv1(int epi, const GemvArgs &g, hipStream_t s);
+
+// Batch-1 fused launches (a role waits in-launch on another role's output):
+// per-context switches, delays and the device's co-residency capacity.  Every
+// wait is bounded by poll_limit polls; a wait that runs out sets a bit in the
+// sticky device word *err (the host turns it into QASR_ERR_DEVICE) and its
+// workgroup skips the dependent store.
+enum DevErr : unsigned {
+    DEVERR_QKV_WAIT = 1u,    // attention split gave up on its kv group's QKV blocks
+    DEVERR_O_WAIT = 2u,      // fused o-projection gave up on the attention combiners
+    DEVERR_FFN_WAIT = 4u,    // fused down-projection gave up on the gate/up blocks
+};
+struct FuseCfg {
+    int ffn = 1, qkv = 1, o = 1;        // fused launches on/off
+    int ffn_delay = 4, ffn_wdelay = 14; // down blocks: first poll / weight request, s_sleep(8) units (~0.2 us)
+    int qkv_delay = 10, o_delay = 20;   // attention K/V request / o-proj weight request delays
+    int spl1 = 0;                       // batch-1 attention split: 0 = auto (64, or 128 from 1k keys)
+    int poll_limit = 1 << 20;           // bounded waits: polls (s_sleep(4..8) apart) before giving up
+    int fence = 0;                      // 1 = agent release before each arrival, acquire after each wait
+    int slots_ffn = 0, slots_qkv64 = 0, slots_qkv128 = 0;   // co-resident workgroups on this device
+    unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
+};
+// co-resident workgroup capacity of the fused kernels on the current device
+// (occupancy query x CUs); 0 = unknown (never fuse)
+void fused_slots(FuseCfg &cfg);
 // gemv.hip: batch-1 f16 gate/up + down in one launch; cnt = this layer's 32 x 16
 // words (zero on entry), cnt_next = the next layer's, re-armed here
 // (false = not covered)
-bool launch_ffn1(const GemvArgs &gu, const GemvArgs &dn, unsigned int *cnt, unsigned int *cnt_next, hipStream_t s);
+bool launch_ffn1(const GemvArgs &gu, const GemvArgs &dn, unsigned int *cnt, unsigned int *cnt_next, const FuseCfg &cfg,
+                 hipStream_t s);
 
 // ---------------------------------------------------------------- norms
 // LayerNorm (ggml_norm + mul + add) fp32 [M][D] -> fp16 y, or fp32 y32 when
@@ -191,13 +216,17 @@ struct DecodeAttnArgs {
     int fuse_delay;                      // fused launch: attention blocks idle fuse_delay x ~0.2 us before their K/V loads
     unsigned int *att_done;              // [8 replicas][16] combiner arrivals for the fused o-proj (re-armed by the down-proj)
     int oproj_delay;                     // fused launch: o-proj blocks idle oproj_delay x ~0.2 us before their weight loads
+    int poll_limit;                      // fused launch: bounded waits (FuseCfg)
+    int fence;                           // fused launch: agent release/acquire around the hand-offs (FuseCfg)
+    unsigned int *err;                   // fused launch: sticky device error word (DevErr bits)
+    int spl1;                            // batch <= 8: key split (0 = auto: 64, or 128 from 1k keys)
 };
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
 // batch 1, f16: the QKV projection (q: GemvArgs of the rmsnorm+QKV GEMV, K = 1024)
 // and the attention in one launch (attention.hip); false = not taken
 // (and, when o is the plain batch-1 o-projection, that too); returns 0 = not
 // taken, 1 = QKV + attention, 2 = QKV + attention + o-projection
-int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, hipStream_t s);
+int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s);
 int decode_split_len();
 int decode_max_splits();
 

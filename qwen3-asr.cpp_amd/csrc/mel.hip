@@ -9,8 +9,11 @@
 // exact products (host-precomputed twiddle table built with the reference's
 // own angle expression, mel_dft_twiddles) and its sequential tap order per
 // (frame, bin), so every fp64 intermediate follows the same FMA chain as the
-// reference build -- parity is bit-level in practice, and the whole stage is
-// a few microseconds per 30 s clip, far below the encoder.
+// reference build (C++ under g++ -O3 -march=native contracts by default:
+// re += a*cos -> fma, im -= a*sin -> fma(-a, sin, im), |X|^2 -> fma(re, re,
+// im*im), the mel dot -> fma; this file is built with -ffp-contract=off, so
+// every fma here is written out) -- parity is bit-level in practice, and the
+// whole stage is a few microseconds per 30 s clip, far below the encoder.
 //
 // Layout: one workgroup = FPB consecutive frames of one clip.  The windows of
 // the FPB frames are staged in LDS (coalesced PCM reads, reflect padding
@@ -73,7 +76,7 @@ __global__ __launch_bounds__(256) void mel_power_kernel(const float *__restrict_
             }
         }
 #pragma unroll
-        for (int f = 0; f < MEL_FPB; f++) pw[f][tid] = re[f] * re[f] + im[f] * im[f];
+        for (int f = 0; f < MEL_FPB; f++) pw[f][tid] = fma(re[f], re[f], im[f] * im[f]);   // as g++ contracts re*re + im*im
     }
     __syncthreads();
     double bmax = -1e300;

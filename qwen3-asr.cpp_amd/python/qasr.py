@@ -26,6 +26,7 @@ EXPORTS = [
     "qasr_mel", "qasr_encode", "qasr_encode_conv", "qasr_prefill", "qasr_decode_step",
     "qasr_stage_audio", "qasr_run", "qasr_set_system_prompt", "qasr_transcribe_batch",
     "qasr_set_probe", "qasr_get_probe",
+    "qasr_ctx_set_option", "qasr_ctx_get_option", "qasr_debug_read",
     "qasr_detokenize", "qasr_tokenize",
     "qasr_load_wav", "qasr_write_wav", "qasr_synth_pcm", "qasr_write_synthetic_gguf",
     "qasr_align", "qasr_align_tokenize", "qasr_model_load_korean_dict", "qasr_fix_timestamps",
@@ -77,6 +78,8 @@ def lib() -> C.CDLL:
             "qasr_transcribe_batch": ([P, C.POINTER(F), IP, I, I, I, I32P, IP, C.POINTER(Timings)], I),
             "qasr_set_probe": ([P, I], I),
             "qasr_get_probe": ([P, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_double)], I),
+            "qasr_ctx_set_option": ([P, C.c_char_p, I], I), "qasr_ctx_get_option": ([P, C.c_char_p, IP], I),
+            "qasr_debug_read": ([P, C.c_char_p, P, C.c_int64], I),
             "qasr_detokenize": ([P, I32P, I, C.c_char_p, I], I), "qasr_tokenize": ([P, C.c_char_p, I32P, I], I),
             "qasr_load_wav": ([C.c_char_p, F, I, IP], I), "qasr_write_wav": ([C.c_char_p, F, I, I], I),
             "qasr_synth_pcm": ([C.c_uint64, I, F], I),
@@ -347,6 +350,24 @@ class Context:
     def set_system_prompt(self, ids: Sequence[int]) -> None:
         a = np.ascontiguousarray(ids, np.int32)
         _check(lib().qasr_set_system_prompt(self.h, _i32(a) if len(a) else None, len(a)), "qasr_set_system_prompt")
+
+    def set_option(self, name: str, value: int) -> None:
+        _check(lib().qasr_ctx_set_option(self.h, name.encode(), int(value)), "qasr_ctx_set_option")
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int(0)
+        _check(lib().qasr_ctx_get_option(self.h, name.encode(), C.byref(v)), "qasr_ctx_get_option")
+        return v.value
+
+    def debug_read(self, buffer: str) -> np.ndarray:
+        """Decode-step state after decode_step: x (fp32), act (fp16), qkv (fp32), att (fp16)."""
+        hp = self.model.hp
+        qd, kd = hp.n_heads * 128, hp.n_kv_heads * 128
+        n, dt = {"x": (hp.hidden_size, np.float32), "act": (hp.dec_ffn, np.float16),
+                 "qkv": (qd + 2 * kd, np.float32), "att": (qd, np.float16)}[buffer]
+        out = np.zeros((self.max_batch, n), dt)
+        _check(lib().qasr_debug_read(self.h, buffer.encode(), out.ctypes.data_as(C.c_void_p), out.nbytes), "qasr_debug_read")
+        return out
 
     def set_probe(self, kernel: int) -> None:
         _check(lib().qasr_set_probe(self.h, kernel), "qasr_set_probe")
