@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--model", default=os.environ.get("QASR_MODEL", ""))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-seconds", type=float, default=10.0)
+    ap.add_argument("--probe-layer", type=int, default=14, help="decoder layer whose fused launches are probed")
     ap.add_argument("--cpu-threads", type=int, default=4, help="reference's effective ggml thread count")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--q8", action="store_true", help="Q8_0 synthetic model (configs[2] weights)")
@@ -67,25 +68,52 @@ def synthetic_model(rank: int, config: str = "full", wtype: int = 1) -> str:
     return path
 
 
-def cpu_baseline(model_path: str, secs: float, tok_rate: float, threads: int):
-    """Oracle (C restatement of the reference CPU path) on a bounded sample."""
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(model_path: str, secs: float, tok_rate: float, threads: int, full_secs: float, full_tok: int):
+    """Oracle (C restatement of the reference CPU path, ggml numerics) on a
+    bounded sample, at the reference's effective thread count (4: ggml's
+    default; mel single-threaded as the reference) and at
+    every core this process may use.  The configs[1] figure is extrapolated
+    per stage from the sample: mel / encoder / prefill x (full / sample
+    seconds), decode x (full / sample tokens)."""
     import oracle_py as op
-    op.set_threads(threads)
-    om = op.OracleModel(model_path)
     n = int(secs * 16000)
     pcm = qasr.synth_pcm(1000, n)
     ntok = int(math.ceil(tok_rate * secs))
-    t0 = time.perf_counter()
-    toks, t = om.transcribe(pcm, max_tokens=ntok, ignore_eos=True)
-    dt = time.perf_counter() - t0
+    om = op.OracleModel(model_path)
+    allc = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 10 ** 6))
+    runs = {}
+    for th in sorted({threads, allc}):
+        op.set_threads(th)
+        t0 = time.perf_counter()
+        _, t = om.transcribe(pcm, max_tokens=ntok, ignore_eos=True)
+        dt = time.perf_counter() - t0
+        est = (t[0] + t[1]) / 1e3 * (full_secs / secs) + t[2] / 1e3 * (full_tok / ntok)
+        runs[th] = {"rtfx": round(secs / dt, 4), "wall_s": round(dt, 3),
+                    "stage_ms": {"mel": round(t[0], 1), "encode+prefill": round(t[1], 1), "decode": round(t[2], 1)},
+                    "est_configs1_rtfx": round(full_secs / est, 4)}
+    r4 = runs[threads]
     return {
-        "value": round(secs / dt, 4),
+        "value": r4["rtfx"],
         "unit": "audio-sec/wall-sec (RTFx)",
         "cores": threads,
         "kind": "port",
-        "sample": f"one {secs:g} s synthetic clip, {ntok}-token greedy budget, full-size synthetic f16 model; "
-                  f"mel single-thread fp64 DFT as the reference, encoder/decoder {threads} threads "
-                  f"(mel {t[0]:.0f} ms, encode {t[1]:.0f} ms, decode {t[2]:.0f} ms)",
+        "sample": f"one {secs:g} s synthetic clip, {ntok}-token greedy budget, full-size synthetic f16 model, "
+                  f"{threads} threads (ggml's default; mel single-thread fp64 DFT as the reference); "
+                  f"extrapolated to configs[1] ({full_secs:g} s, {full_tok} tokens): {r4['est_configs1_rtfx']} RTFx",
+        "runs_by_threads": runs,
+        "all_cores": allc,
+        "nproc": os.cpu_count(),
+        "cpu_model": cpu_model(),
     }
 
 
@@ -103,6 +131,51 @@ def pmc_traffic(kernel_prefix: str):
             if k["name"].startswith(kernel_prefix) and "hbm_read_bytes" in k:
                 return k["hbm_read_bytes"] + k.get("hbm_write_bytes", 0), os.path.relpath(f, ROOT)
     return None, None
+
+
+def profiled_mfma():
+    """Time-weighted MFMA utilisation of the encoder / prefill MFMA kernels
+    from the newest committed rocprofv3 MFMA-counter pass (tools/prof_report.py)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        ks = [k for k in d.get("kernels", []) if "mfma_util" in k]
+        if not ks:
+            continue
+        t = sum(k["total_ms"] for k in ks)
+        top = max(ks, key=lambda k: k["total_ms"])
+        return {"mfma_util": round(sum(k["mfma_util"] * k["total_ms"] for k in ks) / t, 4), "kernels": len(ks),
+                "kernel_ms": round(t, 3), "top_kernel": top["name"][:96], "top_mfma_util": top["mfma_util"],
+                "top_mfma_tflops": top.get("mfma_tflops"), "source": os.path.relpath(f, ROOT)}
+    return None
+
+
+def roofline_entry(kind: int, batch: int, total_ms: float, n: int, bytes_per_launch: float, layer: int) -> dict:
+    """HBM roofline of one probed launch group: algorithmic bytes per launch
+    (engine.hip probe_bytes: weights + the layer's K/V rows at each step's
+    n_kv, averaged over the probed steps) / its mean HIP-event duration."""
+    avg_s = total_ms / n / 1e3
+    achieved = bytes_per_launch / avg_s / 1e9
+    b1 = batch == 1
+    if kind == 2:
+        kname = ("qkv_attn1_kernel (batch 1: rmsnorm + QKV GEMV + split-K attention + o-proj, one launch)" if b1 else
+                 "decode layer QKV projection + attention (kernel group)")
+        prefix = "void qasr::qkv_attn1_kernel<" if b1 else None
+    elif kind == 3:
+        kname = "ffn1_kernel (batch 1: rmsnorm + gate/up SwiGLU + down + residual, one launch)" if b1 else \
+            "decode layer FFN (kernel group)"
+        prefix = "void qasr::ffn1_kernel<" if b1 else None
+    else:
+        kname = "LM head (tied 151936x1024 f16 GEMV + fused argmax)"
+        prefix = f"void qasr::gemv_kernel<3, 4, {next(r for r in (1, 2, 4, 8) if r >= batch)}," if batch <= 8 else None
+    traffic, src = pmc_traffic(prefix) if prefix else (None, None)
+    return {"kernel": kname + (f", decoder layer {layer}" if kind != 1 else ""), "bound": "hbm",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic, "traffic_source": src, "bytes_per_launch": round(bytes_per_launch),
+            "avg_launch_us": round(avg_s * 1e6, 2), "launches": n}
 
 
 def encoder_flops(hp, n_samples: int) -> float:
@@ -190,7 +263,8 @@ def main():
         if actx:
             align_all()
     if not args.no_probe:
-        ctx.set_probe(1)
+        ctx.set_option("probe_layer", args.probe_layer)
+        ctx.set_probe(2)   # the dominant kernel: layer probe_layer's QKV + attention (+ o-proj) launch
     barrier()
     t0 = time.perf_counter()
     res = None
@@ -213,6 +287,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     probe_ms, probe_n, probe_b = ctx.get_probe() if not args.no_probe else (0.0, 0, 0.0)
+    extra = {}
+    if not args.no_probe:   # untimed: one more run per secondary kernel
+        for kind in (3, 1):
+            ctx.set_probe(kind)
+            ctx.run(ntok, ignore_eos=True)
+            extra[kind] = ctx.get_probe()
+        ctx.set_probe(0)
     assert all(len(x) == ntok for x in res.tokens), "decode budget not met"
     if rank != 0:
         if dist is not None:
@@ -244,19 +325,8 @@ def main():
         "stage_ms_per_step_rank0": {k: round(v / args.steps, 3) for k, v in tm.items()},
     }
     if probe_n:
-        avg_s = probe_ms / probe_n / 1e3
-        achieved = probe_b / avg_s / 1e9
-        if args.batch <= 8:
-            mr = next(r for r in (1, 2, 4, 8) if r >= args.batch)   # gemv_mr row bucket
-            kname = "gemv_kernel<EPI_ARGMAX>"
-            traffic, src = pmc_traffic(f"void qasr::gemv_kernel<3, 4, {mr},")
-        else:
-            kname = "gemm_skinny_kernel<EPI_ARGMAX>"
-            traffic, src = pmc_traffic("void qasr::gemm_skinny_kernel<4, 4, 2, 3")
-        out["roofline"] = {"kernel": kname + " (decode LM head, tied 151936x1024 f16 + fused argmax)",
-                           "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
-                           "bytes_per_launch": probe_b, "avg_launch_us": round(avg_s * 1e6, 2), "launches": probe_n}
+        out["roofline"] = roofline_entry(2, args.batch, probe_ms, probe_n, probe_b, args.probe_layer)
+        out["roofline_other"] = [roofline_entry(k, args.batch, *v, args.probe_layer) for k, v in extra.items() if v[1]]
     # the north-star fractions of the two stages: encoder
     # FLOPs against the dense fp16 MFMA peak, decode bytes against HBM
     enc_s = tm["encode"] / args.steps / 1e3
@@ -264,14 +334,15 @@ def main():
         ef = args.batch * encoder_flops(m.hp, n)
         out["encoder_roofline"] = {"bound": "mfma", "achieved": round(ef / enc_s / 1e12, 1), "peak": MFMA_F16_PEAK_TFLOPS,
                                    "unit": "TFLOP/s", "frac": round(ef / enc_s / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
-                                   "flops_per_step": ef}
+                                   "flops_per_step": ef, "profiled": profiled_mfma()}
     dec_s = tm["decode"] / args.steps / 1e3
     if dec_s > 0:
         db = decode_bytes(m.hp, args.q8, args.batch, P, ntok)
         out["decode_hbm"] = {"achieved": round(db / dec_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(db / dec_s / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_step": db}
     if N == 1 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(model_path, args.cpu_sample_seconds, args.tok_rate, args.cpu_threads)
+        out["cpu_baseline"] = cpu_baseline(model_path, args.cpu_sample_seconds, args.tok_rate, args.cpu_threads,
+                                           args.seconds, ntok)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -169,9 +169,14 @@ int qasr_ctx_get_option(const qasr_ctx *c, const char *name, int *value);
 int qasr_debug_read(qasr_ctx *c, const char *buffer, void *dst, int64_t bytes);
 
 /* ---- measurement ---------------------------------------------------------- */
-/* Probe one kernel of the greedy decode step with HIP events on the context's
- * stream during qasr_run (kernel 1 = LM-head GEMV + fused argmax).  Costs one
- * extra graph launch per step while enabled; 0 disables and resets. */
+/* Probe one launch group of every greedy decode step of qasr_run with HIP
+ * events on the context's stream: kernel 1 = LM head + fused argmax; 2 = the
+ * QKV projection + attention (+ o-projection) of decoder layer "probe_layer"
+ * (option, default 14) -- at batch 1 the fused qkv_attn1_kernel; 3 = that
+ * layer's FFN (batch 1: ffn1_kernel).  The rest of each step replays as two
+ * graphs around it (one extra graph launch per step); 0 disables.  Setting a
+ * probe resets the totals; bytes_per_launch = mean algorithmic HBM bytes of
+ * the probed launches (weights + the layer's K/V rows at each step's n_kv). */
 int qasr_set_probe(qasr_ctx *c, int kernel);
 int qasr_get_probe(qasr_ctx *c, double *total_ms, int64_t *launches, double *bytes_per_launch);
 

@@ -130,9 +130,12 @@ struct qasr_ctx {
     int trace_layer = 10;
     unsigned long long *d_trace = nullptr;   // [6 kernels][4096 blocks][8]
     // kernel probe: HIP-event timing of one decode-step kernel inside qasr_run
-    int probe = 0;
-    double probe_ms = 0.0;
+    int probe = 0;                 // 0 off, 1 LM head, 2 layer QKV + attention, 3 layer FFN
+    int probe_layer = 14;          // decoder layer whose groups probes 2 / 3 time
+    bool probe_o_fused = false;    // the probed layer's o-projection runs inside the QKV launch
+    double probe_ms = 0.0, probe_bytes = 0.0;
     long probe_n = 0;
+    std::vector<int> run_P;        // prompt lengths of the current qasr_run (decode step k: n_kv = P_b + k + 1)
     std::vector<hipEvent_t> pev;
     // decode graphs, one set per attention split-grid bucket (the grid must
     // cover the longest sequence's context: it grows by 64 keys per split)
@@ -141,6 +144,7 @@ struct qasr_ctx {
     int graph_B = -1;
     bool graph_logits = false;
     int graph_base = 0;            // max prompt length of the current run: step k feeds position base + k
+    int graph_probe_group = -1;    // launch group timed between events (pre/post graphs split around it)
     void drop_graphs() {
         for (auto &kv : graphs) {
             if (kv.second.full) (void)hipGraphExecDestroy(kv.second.full);
@@ -638,6 +642,13 @@ extern "C" void qasr_ctx_free(qasr_ctx *c) { delete c; }
 extern "C" int qasr_ctx_set_option(qasr_ctx *c, const char *name, int value) {
     if (!c || !name) return fail(QASR_ERR_ARG, "bad arguments");
     const std::string n = name;
+    if (n == "probe_layer") {
+        if (value < 0 || value >= c->m->hp.dec_layers) return fail(QASR_ERR_ARG, "probe_layer out of range");
+        c->probe_layer = value;
+        c->drop_graphs();
+        c->graph_probe_group = -1;
+        return 0;
+    }
     if (n == "dec_layers") {
         if (value < 0 || value > c->m->hp.dec_layers) return fail(QASR_ERR_ARG, "dec_layers out of range");
         c->dbg_layers = value;
@@ -663,6 +674,7 @@ extern "C" int qasr_ctx_get_option(const qasr_ctx *c, const char *name, int *val
     if (!c || !name || !value) return fail(QASR_ERR_ARG, "bad arguments");
     const std::string n = name;
     if (n == "dec_layers") { *value = c->dbg_layers; return 0; }
+    if (n == "probe_layer") { *value = c->probe_layer; return 0; }
     if (n == "slots_ffn") { *value = c->fuse.slots_ffn; return 0; }
     if (n == "slots_qkv") { *value = std::min(c->fuse.slots_qkv64, c->fuse.slots_qkv128); return 0; }
     for (const auto &o : fuse_options())
@@ -1010,10 +1022,24 @@ static void dec_gemm(int epi, const GemmArgs &g, hipStream_t s) {
     if (!launch_gemm_skinny(epi, g, s)) launch_gemm(AM_DENSE, epi, g, s);
 }
 
-// one decode step for B sequences: token d_tok at position d_pos
-// part: 0 = whole step, 1 = embed + layers, 2 = LM head (+argmax), 3 = bookkeeping;
+// Launch groups of one decode step, in stream order (decoder cut at nl layers):
+//   0          embedding gather (batches; batch <= 8 fuses it into layer 0)
+//   1 + 2l     layer l: QKV projection + attention (+ o-projection when fused)
+//   2 + 2l     layer l: o-projection (when separate) + FFN
+//   1 + 2nl    final norm + LM head + argmax (+ bookkeeping at batch <= 8)
+//   2 + 2nl    bookkeeping (batches)
+// A step is emitted as the groups in [lo, hi): whole (graph replay), or split
+// around one probed group that runs between HIP events.
+struct StepRange {
+    int lo, hi;
+    bool in(int g) const { return g >= lo && g < hi; }
+};
+static constexpr StepRange kWholeStep{0, 1 << 30};
+static int step_layers(const qasr_ctx *c) { return c->dbg_layers > 0 ? c->dbg_layers : c->m->hp.dec_layers; }
+
+// one decode step for B sequences: token d_tok at position d_pos;
 // splits: attention grid (64-key splits) covering the longest context of the step
-static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, int splits) {
+static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange r, int splits) {
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
     const int H = hp.hidden, QD = hp.n_head * 128, KD = hp.n_kv_head * 128, F = hp.dec_ffn;
@@ -1021,37 +1047,18 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
     float *x = c->d_x;
     const bool skinny = B <= 8;
     const size_t layer_kv = (size_t)c->max_batch * hp.n_kv_head * c->max_ctx * 128;
-    if ((part == 0 || part == 1) && !skinny) launch_embed(c->d_tok, B, m->embd, H, nullptr, nullptr, x, s);
+    const int nl = step_layers(c);   // diagnostic layer cap
+    if (r.in(0) && !skinny) launch_embed(c->d_tok, B, m->embd, H, nullptr, nullptr, x, s);
     const int skip = c->dev_skip;   // profiling only (QASR_DEV_SKIP): drop kernels to price them
-    if (c->d_trace && (part == 0 || part == 1)) (void)hipMemsetAsync(c->d_trace, 0, 6 * 4096 * 8 * 8, s);
-    const int nl = c->dbg_layers > 0 ? c->dbg_layers : hp.dec_layers;   // diagnostic layer cap
-    for (int l = 0; (part == 0 || part == 1) && l < nl; l++) {
+    if (c->d_trace && r.in(0)) (void)hipMemsetAsync(c->d_trace, 0, 6 * 4096 * 8 * 8, s);
+    for (int l = 0; l < nl; l++) {
+        const bool ga = r.in(1 + 2 * l), gb = r.in(2 + 2 * l);
+        if (!ga && !gb) continue;
         const DecLayer &L = m->dec[l];
         auto tr = [&](int k) -> unsigned long long * {
             return c->d_trace && l == c->trace_layer ? c->d_trace + (size_t)k * 4096 * 8 : nullptr;
         };
         const bool q8 = m->q8;
-        GemvArgs q1{};   // batch-1 QKV projection, launched together with the attention when fusable
-        bool q1_pending = false;
-        if (skinny) {
-            GemvArgs q{};
-            q.x = x; q.ldx = H; q.norm_w = L.attn_norm; q.eps = hp.rms_eps; q.W = L.wqkv; q.Wd = L.wqkv_d; q.K = H;
-            q.N = QD + 2 * KD; q.M = B; q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
-            if (l == 0) { q.embd_ids = c->d_tok; q.embd = m->embd; q.x_store = x; }   // fused embedding gather
-            q.trace = tr(0);
-            if (B == 1 && !q8 && !skip) { q1 = q; q1_pending = true; }
-            else if (!(skip & 1)) launch_gemv(EPI_F32, q, s);
-        } else {
-            GemmArgs q{};
-            q.M = B; q.N = QD + 2 * KD; q.K = H; q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
-            if (q8) {
-                launch_rmsnorm_q8(x, H, B, H, L.attn_norm, hp.rms_eps, c->d_q8a, c->d_q8d, s);
-                gemm_q8_pre(c, EPI_F32, q, L.wqkv, L.wqkv_d, s);
-            } else {
-                launch_rmsnorm_f16(x, H, nullptr, B, H, L.attn_norm, hp.rms_eps, c->d_xh, s);
-                q.A = c->d_xh; q.lda = H; q.W = L.wqkv; q.ldw = H; dec_gemm(EPI_F32, q, s);
-            }
-        }
         DecodeAttnArgs da{};
         da.qkv = c->d_qkv; da.q_norm = L.q_norm; da.k_norm = L.k_norm; da.eps = hp.rms_eps; da.rope = c->rope;
         da.pos = c->d_pos; da.kc = c->kc + l * layer_kv; da.vc = c->vc + l * layer_kv; da.seq_slot = c->d_slot; da.B = B;
@@ -1069,14 +1076,41 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
             o.trace = tr(2);
             o.W = L.wo; o.K = QD; o.N = H; o.M = B; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
         }
-        bool o_fused = false;
-        if (q1_pending) {
-            da.att_done = c->d_attdone;
-            const int r = launch_qkv_attention1(q1, da, &o, c->fuse, s);
-            if (r == 0) { launch_gemv(EPI_F32, q1, s); q1_pending = false; }
-            o_fused = r == 2;
+        GemvArgs q1{};   // batch-1 QKV projection, launched together with the attention when fusable
+        if (skinny) {
+            q1.x = x; q1.ldx = H; q1.norm_w = L.attn_norm; q1.eps = hp.rms_eps; q1.W = L.wqkv; q1.Wd = L.wqkv_d; q1.K = H;
+            q1.N = QD + 2 * KD; q1.M = B; q1.out_f32 = c->d_qkv; q1.ldo = QD + 2 * KD;
+            if (l == 0) { q1.embd_ids = c->d_tok; q1.embd = m->embd; q1.x_store = x; }   // fused embedding gather
+            q1.trace = tr(0);
         }
-        if (!q1_pending && !(skip & 2)) launch_decode_attention(da, s);
+        const bool fusable = skinny && B == 1 && !q8 && !skip;
+        if (fusable) da.att_done = c->d_attdone;
+        // 0 = separate launches, 1 = QKV + attention, 2 = + o-projection (decided without launching)
+        const int fmode = fusable ? launch_qkv_attention1(q1, da, &o, c->fuse, s, true) : 0;
+        const bool o_fused = fmode == 2;
+        if (l == std::min(c->probe_layer, nl - 1)) c->probe_o_fused = o_fused;
+        if (ga) {
+            if (fmode) {
+                (void)launch_qkv_attention1(q1, da, &o, c->fuse, s, false);
+            } else {
+                if (skinny) {
+                    if (!(skip & 1)) launch_gemv(EPI_F32, q1, s);
+                } else {
+                    GemmArgs q{};
+                    q.M = B; q.N = QD + 2 * KD; q.K = H; q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
+                    if (q8) {
+                        launch_rmsnorm_q8(x, H, B, H, L.attn_norm, hp.rms_eps, c->d_q8a, c->d_q8d, s);
+                        gemm_q8_pre(c, EPI_F32, q, L.wqkv, L.wqkv_d, s);
+                    } else {
+                        launch_rmsnorm_f16(x, H, nullptr, B, H, L.attn_norm, hp.rms_eps, c->d_xh, s);
+                        q.A = c->d_xh; q.lda = H; q.W = L.wqkv; q.ldw = H; dec_gemm(EPI_F32, q, s);
+                    }
+                }
+                da.att_done = nullptr;
+                if (!(skip & 2)) launch_decode_attention(da, s);
+            }
+        }
+        if (!gb) continue;
         if (skinny) {
             if (!o_fused && !(skip & 4)) launch_gemv(EPI_F32, o, s);
             GemvArgs gu{};
@@ -1097,9 +1131,9 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
                 else if (o_fused) (void)hipMemsetAsync(c->d_attdone, 0, 8 * 16 * 4, s);   // the skipped down-proj re-arms these
             }
         } else if (q8) {
-            GemmArgs o{};
-            o.M = B; o.N = H; o.K = QD; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
-            gemm_q8_pre(c, EPI_F32, o, L.wo, L.wo_d, s);
+            GemmArgs ob{};
+            ob.M = B; ob.N = H; ob.K = QD; ob.res = x; ob.ldr = H; ob.out_f32 = x; ob.ldo = H;
+            gemm_q8_pre(c, EPI_F32, ob, L.wo, L.wo_d, s);
             launch_rmsnorm_q8(x, H, B, H, L.ffn_norm, hp.rms_eps, c->d_q8a, c->d_q8d, s);
             GemmArgs gu{};
             gu.M = B; gu.N = 2 * F; gu.K = H; gu.out_f32 = c->d_x32; gu.ldo = F;
@@ -1108,9 +1142,9 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
             dn.M = B; dn.N = H; dn.K = F; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
             gemm_q8(c, EPI_F32, dn, c->d_x32, nullptr, F, 0, L.wd, L.wd_d, s, c->d_q8a, c->d_q8d, true);
         } else {
-            GemmArgs o{};
-            o.A = c->d_att; o.lda = QD; o.W = L.wo; o.ldw = QD; o.M = B; o.N = H; o.K = QD; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
-            dec_gemm(EPI_F32, o, s);
+            GemmArgs ob{};
+            ob.A = c->d_att; ob.lda = QD; ob.W = L.wo; ob.ldw = QD; ob.M = B; ob.N = H; ob.K = QD; ob.res = x; ob.ldr = H; ob.out_f32 = x; ob.ldo = H;
+            dec_gemm(EPI_F32, ob, s);
             launch_rmsnorm_f16(x, H, nullptr, B, H, L.ffn_norm, hp.rms_eps, c->d_xh, s);
             GemmArgs gu{};
             gu.A = c->d_xh; gu.lda = H; gu.W = L.wgu; gu.ldw = H; gu.M = B; gu.N = 2 * F; gu.K = H; gu.out_f16 = c->d_act; gu.ldo16 = F;
@@ -1120,43 +1154,64 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, int part, 
             dec_gemm(EPI_F32, dn, s);
         }
     }
-    if (part == 3 && skinny) return;   // bookkeeping is fused into the LM-head GEMV
-    if (part == 3) goto bookkeeping;
-    if (part == 1) return;
-    if (skinny) {   // amax / done are zero at rest: the LM head's last workgroup re-arms them
-        GemvArgs lm{};
-        lm.x = x; lm.ldx = H; lm.norm_w = m->out_norm; lm.eps = hp.rms_eps; lm.W = m->embd; lm.K = H; lm.N = hp.vocab; lm.M = B;
-        lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
-        lm.done = c->d_done; lm.tok_out = c->d_tok; lm.hist = c->d_hist; lm.hist_stride = c->hist_cap; lm.step = c->d_step;
-        lm.pos = c->d_pos;
-        launch_gemv(EPI_ARGMAX, lm, s);
-        return;
-    } else {
-        launch_fill_u64(c->d_amax, B, 0ull, s);
-        launch_rmsnorm_f16(x, H, nullptr, B, H, m->out_norm, hp.rms_eps, c->d_xh, s);
-        GemmArgs lm{};
-        lm.A = c->d_xh; lm.lda = H; lm.W = m->embd; lm.ldw = H; lm.M = B; lm.N = hp.vocab; lm.K = H;
-        lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
-        dec_gemm(EPI_ARGMAX, lm, s);
+    if (r.in(1 + 2 * nl)) {
+        if (skinny) {   // amax / done are zero at rest: the LM head's last workgroup re-arms them
+            GemvArgs lm{};
+            lm.x = x; lm.ldx = H; lm.norm_w = m->out_norm; lm.eps = hp.rms_eps; lm.W = m->embd; lm.K = H; lm.N = hp.vocab; lm.M = B;
+            lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
+            lm.done = c->d_done; lm.tok_out = c->d_tok; lm.hist = c->d_hist; lm.hist_stride = c->hist_cap; lm.step = c->d_step;
+            lm.pos = c->d_pos;
+            launch_gemv(EPI_ARGMAX, lm, s);
+        } else {
+            launch_fill_u64(c->d_amax, B, 0ull, s);
+            launch_rmsnorm_f16(x, H, nullptr, B, H, m->out_norm, hp.rms_eps, c->d_xh, s);
+            GemmArgs lm{};
+            lm.A = c->d_xh; lm.lda = H; lm.W = m->embd; lm.ldw = H; lm.M = B; lm.N = hp.vocab; lm.K = H;
+            lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
+            dec_gemm(EPI_ARGMAX, lm, s);
+        }
     }
-    if (part == 2) return;
-bookkeeping:
-    launch_step_advance(c->d_pos, c->d_nkv, c->d_step, B, s);
-    launch_argmax_finish(c->d_amax, B, c->d_tok, c->d_hist, c->hist_cap, c->d_step, s);
-    launch_fill_u64(c->d_amax, B, 0ull, s);   // re-arm (zero at rest)
+    if (r.in(2 + 2 * nl) && !skinny) {   // bookkeeping (fused into the LM-head GEMV at batch <= 8)
+        launch_step_advance(c->d_pos, c->d_nkv, c->d_step, B, s);
+        launch_argmax_finish(c->d_amax, B, c->d_tok, c->d_hist, c->hist_cap, c->d_step, s);
+        launch_fill_u64(c->d_amax, B, 0ull, s);   // re-arm (zero at rest)
+    }
 }
 
-// algorithmic HBM bytes of one launch of the probed kernel (decode LM head:
-// the tied 151936 x 1024 fp16 embedding streamed once + x rows + logits/keys)
-static double probe_bytes(qasr_ctx *c, int B) {
+// Kernel probes (qasr_set_probe): HIP events on the context stream around one
+// launch group of every decode step of qasr_run; the rest of the step replays
+// as two graphs around it.
+//   1 = LM head + argmax (group 1 + 2nl)
+//   2 = layer probe_layer's QKV + attention (+ o-projection): at batch 1 the
+//       fused qkv_attn1_kernel, the dominant kernel of the headline decode
+//   3 = layer probe_layer's o-projection (if separate) + FFN: at batch 1 the
+//       fused ffn1_kernel
+static int probe_group(const qasr_ctx *c) {
+    const int nl = step_layers(c), pl = std::min(c->probe_layer, nl - 1);
+    return c->probe == 1 ? 1 + 2 * nl : c->probe == 2 ? 1 + 2 * pl : 2 + 2 * pl;
+}
+
+// algorithmic HBM bytes of one launch of the probed group at decode step k
+// (SURVEY.md §8(d)): weights streamed once for the batch + each sequence's
+// K/V rows of the layer (fp16, n_kv = P_b + k + 1 keys) + activations
+static double probe_bytes(const qasr_ctx *c, int B, int k) {
     const Hparams &hp = c->m->hp;
-    return (double)hp.vocab * hp.hidden * 2 + (double)B * hp.hidden * 4 + (double)B * 8;
+    const double H = hp.hidden, QD = hp.n_head * 128.0, KD = hp.n_kv_head * 128.0, F = hp.dec_ffn;
+    const double wb = c->m->q8 ? 34.0 / 32.0 : 2.0;   // bytes per linear weight (Q8_0 block: 34 B / 32)
+    if (c->probe == 1) return (double)hp.vocab * H * 2 + B * H * 4 + B * 8.0;
+    if (c->probe == 2) {
+        double kv = 0;
+        for (int b = 0; b < B; b++) kv += (double)(c->run_P[b] + k + 1) * KD * 2 * 2;
+        const bool o_in = c->probe_o_fused;
+        return (QD + 2 * KD) * H * wb + (o_in ? H * QD * wb : 0.0) + kv + B * H * 4 * (o_in ? 3 : 1) + B * (QD + 2 * KD) * 4;
+    }
+    return 3 * F * H * wb + (c->probe_o_fused ? 0.0 : H * QD * wb) + B * H * 4 * 3;
 }
 
-static int capture(qasr_ctx *c, int B, bool want_logits, int part, int splits, hipGraphExec_t *out) {
+static int capture(qasr_ctx *c, int B, bool want_logits, StepRange r, int splits, hipGraphExec_t *out) {
     hipGraph_t gr;
     HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
-    decode_step_kernels(c, B, want_logits, part, splits);
+    decode_step_kernels(c, B, want_logits, r, splits);
     HIPCHK(hipStreamEndCapture(c->st, &gr));
     HIPCHK(hipGraphInstantiate(out, gr, nullptr, nullptr, 0));
     HIPCHK(hipGraphDestroy(gr));
@@ -1172,10 +1227,12 @@ static int split_bucket(qasr_ctx *c, int pos) {
 
 // prepare decode graphs for batch B; base = longest prompt (step k feeds base + k)
 static int decode_graph(qasr_ctx *c, int B, bool want_logits, int base) {
-    if (c->graph_B != B || c->graph_logits != want_logits) c->drop_graphs();
+    const int pg = c->probe ? probe_group(c) : -1;
+    if (c->graph_B != B || c->graph_logits != want_logits || c->graph_probe_group != pg) c->drop_graphs();
     c->graph_B = B;
     c->graph_logits = want_logits;
     c->graph_base = base;
+    c->graph_probe_group = pg;
     return 0;
 }
 
@@ -1183,24 +1240,26 @@ static int step_graphs(qasr_ctx *c, int splits, qasr_ctx::StepGraphs **out) {
     auto &gs = c->graphs[splits];
     const int B = c->graph_B;
     int rc;
-    if (!gs.full) {
-        if ((rc = capture(c, B, c->graph_logits, 0, splits, &gs.full)) || (rc = capture(c, B, c->graph_logits, 1, splits, &gs.pre)))
+    if (!gs.full && (rc = capture(c, B, c->graph_logits, kWholeStep, splits, &gs.full))) return rc;
+    if (c->probe && !gs.pre) {
+        const int g = c->graph_probe_group;
+        if ((rc = capture(c, B, c->graph_logits, StepRange{0, g}, splits, &gs.pre)) ||
+            (rc = capture(c, B, c->graph_logits, StepRange{g + 1, 1 << 30}, splits, &gs.post)))
             return rc;
-        if (B > 8 && (rc = capture(c, B, c->graph_logits, 3, splits, &gs.post))) return rc;   // skinny: fused into the LM head
     }
     *out = &gs;
     return 0;
 }
 
-// one greedy step (k = 0-based step of the run); under a probe the LM head
-// runs eagerly between HIP events
+// one greedy step (k = 0-based step of the run); under a probe the probed
+// group runs eagerly between HIP events
 static int launch_step(qasr_ctx *c, int B, int k) {
     const int splits = split_bucket(c, c->graph_base + k);
     qasr_ctx::StepGraphs *gs = nullptr;
     int rc;
     if (!c->eager && (rc = step_graphs(c, splits, &gs))) return rc;
     if (!c->probe) {
-        if (c->eager) decode_step_kernels(c, B, c->graph_logits, 0, splits);
+        if (c->eager) decode_step_kernels(c, B, c->graph_logits, kWholeStep, splits);
         else HIPCHK(hipGraphLaunch(gs->full, c->st));
         return 0;
     }
@@ -1209,32 +1268,35 @@ static int launch_step(qasr_ctx *c, int B, int k) {
         HIPCHK(hipEventCreate(&e));
         c->pev.push_back(e);
     }
-    if (c->eager) decode_step_kernels(c, B, c->graph_logits, 1, splits);
+    const int g = c->graph_probe_group;
+    if (c->eager) decode_step_kernels(c, B, c->graph_logits, StepRange{0, g}, splits);
     else HIPCHK(hipGraphLaunch(gs->pre, c->st));
     HIPCHK(hipEventRecord(c->pev[2 * k], c->st));
-    decode_step_kernels(c, B, c->graph_logits, 2, splits);
+    decode_step_kernels(c, B, c->graph_logits, StepRange{g, g + 1}, splits);
     HIPCHK(hipEventRecord(c->pev[2 * k + 1], c->st));
-    if (c->eager) decode_step_kernels(c, B, c->graph_logits, 3, splits);
-    else if (gs->post) HIPCHK(hipGraphLaunch(gs->post, c->st));
+    if (c->eager) decode_step_kernels(c, B, c->graph_logits, StepRange{g + 1, 1 << 30}, splits);
+    else HIPCHK(hipGraphLaunch(gs->post, c->st));
     return 0;
 }
 
-static int probe_collect(qasr_ctx *c, int nsteps) {
+static int probe_collect(qasr_ctx *c, int B, int nsteps) {
     if (!c->probe) return 0;
     for (int k = 0; k < nsteps; k++) {
         float ms = 0.f;
         HIPCHK(hipEventElapsedTime(&ms, c->pev[2 * k], c->pev[2 * k + 1]));
         c->probe_ms += ms;
         c->probe_n++;
+        c->probe_bytes += probe_bytes(c, B, k);
     }
     return 0;
 }
 
 extern "C" int qasr_set_probe(qasr_ctx *c, int kernel) {
-    if (!c || kernel < 0 || kernel > 1) return fail(QASR_ERR_ARG, "bad probe id");
+    if (!c || kernel < 0 || kernel > 3) return fail(QASR_ERR_ARG, "bad probe id");
     c->probe = kernel;
     c->probe_ms = 0.0;
     c->probe_n = 0;
+    c->probe_bytes = 0.0;
     return 0;
 }
 
@@ -1242,7 +1304,7 @@ extern "C" int qasr_get_probe(qasr_ctx *c, double *total_ms, int64_t *launches, 
     if (!c) return fail(QASR_ERR_ARG, "null context");
     if (total_ms) *total_ms = c->probe_ms;
     if (launches) *launches = c->probe_n;
-    if (bytes_per_launch) *bytes_per_launch = c->graph_B > 0 ? probe_bytes(c, c->graph_B) : 0.0;
+    if (bytes_per_launch) *bytes_per_launch = c->probe_n ? c->probe_bytes / c->probe_n : 0.0;
     return 0;
 }
 
@@ -1342,7 +1404,7 @@ extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_pa
     HIPCHK(hipMemcpyAsync(c->d_pos, pos.data(), B * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemcpyAsync(c->d_nkv, nkv.data(), B * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemsetAsync(c->d_step, 0, 4, c->st));
-    decode_step_kernels(c, B, logits != nullptr, 0, split_bucket(c, *std::max_element(pos.begin(), pos.end())));
+    decode_step_kernels(c, B, logits != nullptr, kWholeStep, split_bucket(c, *std::max_element(pos.begin(), pos.end())));
     HIPCHK(hipGetLastError());
     if (logits) HIPCHK(hipMemcpyAsync(logits, c->d_logits, (size_t)B * c->m->hp.vocab * 4, hipMemcpyDeviceToHost, c->st));
     if (argmax) HIPCHK(hipMemcpyAsync(argmax, c->d_tok, B * 4, hipMemcpyDeviceToHost, c->st));
@@ -1397,6 +1459,7 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
     if ((rc = run_prefill(c, ids, P, c->feats.as<float>(), ap, Nb, false))) return rc;
     HIPCHK(hipEventRecord(c->ev[3], s));
     // greedy loop (src/qwen3_asr.cpp:270-296): step k feeds token k at position P+k-1
+    c->run_P = P;
     if ((rc = decode_graph(c, B, false, *std::max_element(P.begin(), P.end())))) return rc;
     std::vector<int32_t> hist((size_t)B * c->hist_cap);
     int steps = 0;
@@ -1434,7 +1497,7 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
     HIPCHK(hipEventRecord(c->ev[4], s));
     HIPCHK(hipEventSynchronize(c->ev[4]));
     if ((rc = check_dev_err(c))) return rc;
-    if ((rc = probe_collect(c, steps))) return rc;
+    if ((rc = probe_collect(c, B, steps))) return rc;
     if (c->d_trace) {   // dev trace dump: raw [6][4096][8] u64
         std::vector<unsigned long long> tr((size_t)6 * 4096 * 8);
         HIPCHK(hipMemcpy(tr.data(), c->d_trace, tr.size() * 8, hipMemcpyDeviceToHost));

@@ -226,7 +226,9 @@ void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
 // and the attention in one launch (attention.hip); false = not taken
 // (and, when o is the plain batch-1 o-projection, that too); returns 0 = not
 // taken, 1 = QKV + attention, 2 = QKV + attention + o-projection
-int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s);
+// dry = true: only the decision (nothing launched)
+int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s,
+                          bool dry = false);
 int decode_split_len();
 int decode_max_splits();
 
