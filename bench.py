@@ -153,11 +153,18 @@ def profiled_mfma():
     return None
 
 
-def roofline_entry(kind: int, batch: int, total_ms: float, n: int, bytes_per_launch: float, layer: int) -> dict:
+def roofline_entry(kind: int, batch: int, total_ms: float, n: int, bytes_per_launch: float, dev_ms: float, dev_n: int,
+                   layer: int) -> dict:
     """HBM roofline of one probed launch group: algorithmic bytes per launch
     (engine.hip probe_bytes: weights + the layer's K/V rows at each step's
-    n_kv, averaged over the probed steps) / its mean HIP-event duration."""
-    avg_s = total_ms / n / 1e3
+    n_kv, averaged over the probed steps) / its mean duration.  Both clocks of
+    the same launches in the timed region: HIP events on the context stream
+    around the launch (includes ~2.5 us of dispatch + event processing), and
+    the device clock folded in-kernel (first workgroup start -> last
+    workgroup end: what rocprofv3 --kernel-trace reports as the kernel's
+    duration).  achieved / frac use the device clock where it exists."""
+    ev_s = total_ms / n / 1e3
+    avg_s = dev_ms / dev_n / 1e3 if dev_n else ev_s
     achieved = bytes_per_launch / avg_s / 1e9
     b1 = batch == 1
     if kind == 2:
@@ -175,7 +182,9 @@ def roofline_entry(kind: int, batch: int, total_ms: float, n: int, bytes_per_lau
     return {"kernel": kname + (f", decoder layer {layer}" if kind != 1 else ""), "bound": "hbm",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic, "traffic_source": src, "bytes_per_launch": round(bytes_per_launch),
-            "avg_launch_us": round(avg_s * 1e6, 2), "launches": n}
+            "avg_launch_us": round(avg_s * 1e6, 2), "clock": "device" if dev_n else "hip_events",
+            "avg_launch_us_hip_events": round(ev_s * 1e6, 2), "launches": n,
+            "frac_hip_events": round(bytes_per_launch / ev_s / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def encoder_flops(hp, n_samples: int) -> float:
@@ -286,13 +295,13 @@ def main():
         t = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    probe_ms, probe_n, probe_b = ctx.get_probe() if not args.no_probe else (0.0, 0, 0.0)
+    probe = (*ctx.get_probe(), *ctx.get_probe_device()) if not args.no_probe else None
     extra = {}
     if not args.no_probe:   # untimed: one more run per secondary kernel
         for kind in (3, 1):
             ctx.set_probe(kind)
             ctx.run(ntok, ignore_eos=True)
-            extra[kind] = ctx.get_probe()
+            extra[kind] = (*ctx.get_probe(), *ctx.get_probe_device())
         ctx.set_probe(0)
     assert all(len(x) == ntok for x in res.tokens), "decode budget not met"
     if rank != 0:
@@ -324,8 +333,8 @@ def main():
         "decode_tokens_per_s": round(N * args.batch * ntok * args.steps / dt, 2),
         "stage_ms_per_step_rank0": {k: round(v / args.steps, 3) for k, v in tm.items()},
     }
-    if probe_n:
-        out["roofline"] = roofline_entry(2, args.batch, probe_ms, probe_n, probe_b, args.probe_layer)
+    if probe and probe[1]:
+        out["roofline"] = roofline_entry(2, args.batch, *probe, args.probe_layer)
         out["roofline_other"] = [roofline_entry(k, args.batch, *v, args.probe_layer) for k, v in extra.items() if v[1]]
     # the north-star fractions of the two stages: encoder
     # FLOPs against the dense fp16 MFMA peak, decode bytes against HBM

@@ -179,6 +179,11 @@ int qasr_debug_read(qasr_ctx *c, const char *buffer, void *dst, int64_t bytes);
  * the probed launches (weights + the layer's K/V rows at each step's n_kv). */
 int qasr_set_probe(qasr_ctx *c, int kernel);
 int qasr_get_probe(qasr_ctx *c, double *total_ms, int64_t *launches, double *bytes_per_launch);
+/* The same launches timed by the device clock (first workgroup start -> last
+ * workgroup end, 100 MHz s_memrealtime, folded in-kernel by the batch <= 8
+ * decode kernels): the kernels' own duration, without the ~2.5 us of dispatch
+ * and event processing an event pair around one launch includes. */
+int qasr_get_probe_device(qasr_ctx *c, double *total_ms, int64_t *launches);
 
 /* ---- forced alignment (Qwen3-ForcedAligner model files) ------------------- */
 /* Device part of ForcedAligner::align for one clip: text_ids are the words'

@@ -666,7 +666,9 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
 
 template <int SPL>
 __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
+    stamp_start(a.stamp);
     decode_attn_body<SPL, false>(a, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x);
+    stamp_end(a.stamp);
 }
 
 // ------------------------------------------------- batch 1: QKV + attention
@@ -730,13 +732,12 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
 template <int SPL>
 __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnArgs a, GemvArgs o) {
     constexpr int K = 1024, NT = 2, RPW = 2;
+    stamp_start(a.stamp);
     if (blockIdx.x >= 512) {
         const int j = blockIdx.x - 512, nsp = a.grid_splits, nat = nsp * a.n_kv_head;   // grid_splits: this launch's splits
-        if (j >= nat) {
-            oproj1_body(o, a, j - nat);
-            return;
-        }
-        decode_attn_body<SPL, true>(a, j % nsp, j / nsp, 0, nsp);
+        if (j >= nat) oproj1_body(o, a, j - nat);
+        else decode_attn_body<SPL, true>(a, j % nsp, j / nsp, 0, nsp);
+        stamp_end(a.stamp);
         return;
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -812,6 +813,7 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
     if (threadIdx.x < 8)   // one lane per replica of the group's counter
         __hip_atomic_fetch_add(a.qcnt + (grp * 8 + threadIdx.x) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (q.trace && threadIdx.x == 0) q.trace[blockIdx.x * 8 + 1] = rt_now();
+    stamp_end(a.stamp);
 }
 
 // batch <= 8 key split: cfg 64 / 128, else 128 from 1k keys (half the

@@ -36,6 +36,21 @@ __device__ __forceinline__ void trace_mark(unsigned long long *tr, int slot) {
     if (tr && threadIdx.x == 0) tr[(long)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 8 + slot] = rt_now();
 }
 
+// kernel-duration probe (qasr_set_probe): lane 0 of each workgroup folds its
+// start / end time (the 100 MHz clock) into shard blockIdx % 32 of a
+// per-launch record: min-starts at st[32 * shard], max-ends at
+// st[STAMP_ENDS + 32 * shard] -- every shard on a 256-B line of its own (one
+// line taking every block's atomic serialised them at the memory side: +6 us
+// on a 1024-block launch); no-return atomics, 32 per line; null (one untaken
+// branch) unless this launch is probed
+#define STAMP_ENDS (32 * 32)
+__device__ __forceinline__ void stamp_start(unsigned long long *st) {
+    if (st && threadIdx.x == 0) atomicMin(st + 32 * (blockIdx.x & 31), rt_now());
+}
+__device__ __forceinline__ void stamp_end(unsigned long long *st) {
+    if (st && threadIdx.x == 0) atomicMax(st + STAMP_ENDS + 32 * (blockIdx.x & 31), rt_now());
+}
+
 // DPP lane moves (VALU, no LDS round trip): quad_perm xor1 / xor2, row half
 // mirror (lane i <-> 7-i in 8), row mirror (lane i <-> 15-i in 16)
 template <int CTRL>

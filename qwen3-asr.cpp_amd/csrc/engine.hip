@@ -19,9 +19,12 @@
 #include "../../include/qasr_capi.h"
 #include "../host/gguf.h"
 #include "../host/qasr_host.h"
+#include "dev_common.h"
 #include "kernels.h"
 
 using namespace qasr;
+
+static constexpr int kStampRec = 2 * STAMP_ENDS;   // u64 per probed launch record (dev_common.h stamp_start/end)
 
 static thread_local std::string g_err;
 
@@ -133,7 +136,10 @@ struct qasr_ctx {
     int probe = 0;                 // 0 off, 1 LM head, 2 layer QKV + attention, 3 layer FFN
     int probe_layer = 14;          // decoder layer whose groups probes 2 / 3 time
     bool probe_o_fused = false;    // the probed layer's o-projection runs inside the QKV launch
-    double probe_ms = 0.0, probe_bytes = 0.0;
+    double probe_ms = 0.0, probe_bytes = 0.0, probe_dev_ms = 0.0;
+    long probe_dev_n = 0;
+    unsigned long long *d_pstamp = nullptr;   // per decode step: [32 min-starts | 32 max-ends] of the probed launches
+    unsigned long long *cur_stamp = nullptr;  // record of the group being emitted (probe only)
     long probe_n = 0;
     std::vector<int> run_P;        // prompt lengths of the current qasr_run (decode step k: n_kv = P_b + k + 1)
     std::vector<hipEvent_t> pev;
@@ -617,6 +623,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_attdone, (size_t)8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_ffncnt, (size_t)hp.dec_layers * 512 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_err, 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_pstamp, (size_t)max_ctx * kStampRec * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_logits, (size_t)B * hp.vocab * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_amax, (size_t)B * 8)))
         return rc;
@@ -1048,6 +1055,8 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
     const bool skinny = B <= 8;
     const size_t layer_kv = (size_t)c->max_batch * hp.n_kv_head * c->max_ctx * 128;
     const int nl = step_layers(c);   // diagnostic layer cap
+    // probed group (emitted alone): every launch in it folds its block times into one record
+    unsigned long long *stamp = r.hi - r.lo == 1 ? c->cur_stamp : nullptr;
     if (r.in(0) && !skinny) launch_embed(c->d_tok, B, m->embd, H, nullptr, nullptr, x, s);
     const int skip = c->dev_skip;   // profiling only (QASR_DEV_SKIP): drop kernels to price them
     if (c->d_trace && r.in(0)) (void)hipMemsetAsync(c->d_trace, 0, 6 * 4096 * 8 * 8, s);
@@ -1069,12 +1078,14 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         da.trace = tr(1);
         da.qcnt = c->d_qcnt;
         da.spl1 = c->fuse.spl1;
+        da.stamp = stamp;
         GemvArgs o{};
         if (skinny) {
             if (q8) { o.x = c->d_att32; o.ldx = QD; o.Wd = L.wo_d; }
             else { o.xh = c->d_att; o.ldxh = QD; }
             o.trace = tr(2);
             o.W = L.wo; o.K = QD; o.N = H; o.M = B; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
+            o.stamp = stamp;
         }
         GemvArgs q1{};   // batch-1 QKV projection, launched together with the attention when fusable
         if (skinny) {
@@ -1082,6 +1093,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             q1.N = QD + 2 * KD; q1.M = B; q1.out_f32 = c->d_qkv; q1.ldo = QD + 2 * KD;
             if (l == 0) { q1.embd_ids = c->d_tok; q1.embd = m->embd; q1.x_store = x; }   // fused embedding gather
             q1.trace = tr(0);
+            q1.stamp = stamp;
         }
         const bool fusable = skinny && B == 1 && !q8 && !skip;
         if (fusable) da.att_done = c->d_attdone;
@@ -1118,12 +1130,14 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             if (q8) { gu.out_f32 = c->d_act32; gu.ldo = F; }
             else { gu.out_f16 = c->d_act; gu.ldo16 = F; }
             gu.trace = tr(3);
+            gu.stamp = stamp;
             GemvArgs dn{};
             if (q8) { dn.x = c->d_act32; dn.ldx = F; dn.Wd = L.wd_d; }
             else { dn.xh = c->d_act; dn.ldxh = F; }
             dn.W = L.wd; dn.K = F; dn.N = H; dn.M = B; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
             if (o_fused) dn.zero8 = c->d_attdone;   // re-arm the fused o-proj's arrival counters
             dn.trace = tr(4);
+            dn.stamp = stamp;
             if (skip & 24 || nl < 2 ||
                 !launch_ffn1(gu, dn, c->d_ffncnt + (size_t)l * 512, c->d_ffncnt + (size_t)((l + 1) % nl) * 512, c->fuse, s)) {
                 if (!(skip & 8)) launch_gemv(q8 ? EPI_SWIGLU_F32 : EPI_SWIGLU_F16, gu, s);
@@ -1161,6 +1175,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
             lm.done = c->d_done; lm.tok_out = c->d_tok; lm.hist = c->d_hist; lm.hist_stride = c->hist_cap; lm.step = c->d_step;
             lm.pos = c->d_pos;
+            lm.stamp = stamp;
             launch_gemv(EPI_ARGMAX, lm, s);
         } else {
             launch_fill_u64(c->d_amax, B, 0ull, s);
@@ -1272,15 +1287,39 @@ static int launch_step(qasr_ctx *c, int B, int k) {
     if (c->eager) decode_step_kernels(c, B, c->graph_logits, StepRange{0, g}, splits);
     else HIPCHK(hipGraphLaunch(gs->pre, c->st));
     HIPCHK(hipEventRecord(c->pev[2 * k], c->st));
+    c->cur_stamp = k < c->max_ctx ? c->d_pstamp + (size_t)k * kStampRec : nullptr;
     decode_step_kernels(c, B, c->graph_logits, StepRange{g, g + 1}, splits);
+    c->cur_stamp = nullptr;
     HIPCHK(hipEventRecord(c->pev[2 * k + 1], c->st));
     if (c->eager) decode_step_kernels(c, B, c->graph_logits, StepRange{g + 1, 1 << 30}, splits);
     else HIPCHK(hipGraphLaunch(gs->post, c->st));
     return 0;
 }
 
+// arm the device-clock records of a run's probed launches (qasr_run): per
+// step kStampRec u64, starts (~0) then ends (0), one 256-B line per shard
+static int probe_arm(qasr_ctx *c, int nsteps) {
+    if (!c->probe || nsteps <= 0) return 0;
+    const int n = std::min(nsteps, c->max_ctx);
+    launch_fill_u64(c->d_pstamp, n * kStampRec, ~0ull, c->st);
+    HIPCHK(hipMemset2DAsync(c->d_pstamp + STAMP_ENDS, kStampRec * 8, 0, STAMP_ENDS * 8, n, c->st));
+    return 0;
+}
+
 static int probe_collect(qasr_ctx *c, int B, int nsteps) {
     if (!c->probe) return 0;
+    const int n = std::min(nsteps, c->max_ctx);
+    // the first word of every shard line: [step][64]
+    std::vector<unsigned long long> st((size_t)n * 64);
+    if (n > 0)
+        HIPCHK(hipMemcpy2D(st.data(), 8, c->d_pstamp, 32 * 8, 8, (size_t)n * 64, hipMemcpyDeviceToHost));
+    for (int k = 0; k < n; k++) {   // first block start -> last block end, 100 MHz clock
+        unsigned long long t0 = ~0ull, t1 = 0;
+        for (int i = 0; i < 32; i++) { t0 = std::min(t0, st[(size_t)k * 64 + i]); t1 = std::max(t1, st[(size_t)k * 64 + 32 + i]); }
+        if (t0 == ~0ull || t1 <= t0) continue;   // launches without records (batch > 8 groups)
+        c->probe_dev_ms += (double)(t1 - t0) * 1e-5;
+        c->probe_dev_n++;
+    }
     for (int k = 0; k < nsteps; k++) {
         float ms = 0.f;
         HIPCHK(hipEventElapsedTime(&ms, c->pev[2 * k], c->pev[2 * k + 1]));
@@ -1297,6 +1336,15 @@ extern "C" int qasr_set_probe(qasr_ctx *c, int kernel) {
     c->probe_ms = 0.0;
     c->probe_n = 0;
     c->probe_bytes = 0.0;
+    c->probe_dev_ms = 0.0;
+    c->probe_dev_n = 0;
+    return 0;
+}
+
+extern "C" int qasr_get_probe_device(qasr_ctx *c, double *total_ms, int64_t *launches) {
+    if (!c) return fail(QASR_ERR_ARG, "null context");
+    if (total_ms) *total_ms = c->probe_dev_ms;
+    if (launches) *launches = c->probe_dev_n;
     return 0;
 }
 
@@ -1461,6 +1509,7 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
     // greedy loop (src/qwen3_asr.cpp:270-296): step k feeds token k at position P+k-1
     c->run_P = P;
     if ((rc = decode_graph(c, B, false, *std::max_element(P.begin(), P.end())))) return rc;
+    if ((rc = probe_arm(c, max_tokens - 1))) return rc;
     std::vector<int32_t> hist((size_t)B * c->hist_cap);
     int steps = 0;
     if (ignore_eos) {

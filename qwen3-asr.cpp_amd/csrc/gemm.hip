@@ -460,6 +460,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
     constexpr int NR = EPI == EPI_SWIGLU_F16 ? 2 : 1;   // weight rows per output
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     trace_mark(g.trace, 0);
+    stamp_start(g.stamp);
     const int K = g.K;
     const int ncg = (g.N + CPW - 1) / CPW;
     int cg = blockIdx.x * 4 + wid;
@@ -660,6 +661,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
             }
         }
     }
+    stamp_end(g.stamp);
 }
 
 // ================================================================ Q8_0 GEMV

@@ -28,6 +28,7 @@ __global__ __launch_bounds__(256) void gemv1_kernel(GemvArgs g) {
     const int lane = threadIdx.x & 63;
     const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
     trace_mark(g.trace, 0);
+    stamp_start(g.stamp);
     if (g.zero8 && blockIdx.x == 0 && threadIdx.x < 8) g.zero8[threadIdx.x * 16] = 0u;   // fused o-proj counters
     half8 wv[RPW][NR][NT];
 #pragma unroll
@@ -136,6 +137,7 @@ __global__ __launch_bounds__(256) void gemv1_kernel(GemvArgs g) {
         }
     }
     if (g.trace) { __syncthreads(); trace_mark(g.trace, 1); }
+    stamp_end(g.stamp);
 }
 
 template <int EPI, int K, int RPW>
@@ -205,6 +207,7 @@ template <int K, int F>
 __global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, FfnCtl c) {
     constexpr int NT = K / 512, NTD = F / 512, NGU = F / 4;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    stamp_start(g.stamp);
     if (blockIdx.x >= NGU) {   // ---- down projection
         const int j = blockIdx.x - NGU, row = j * 4 + wid;
         if (d.trace && threadIdx.x == 0) d.trace[j * 8] = rt_now();
@@ -234,7 +237,7 @@ __global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, FfnCt
             }
         }
         __syncthreads();
-        if (!ready) return;   // reported through the error word; x keeps its old row
+        if (!ready) { stamp_end(g.stamp); return; }   // reported through the error word; x keeps its old row
         u32x4 xv[NTD];
         static_assert(NTD == 6, "ld_sc1_x4_6 covers F = 3072");
         ld_sc1_x4_6(d.xh + lane * 8, xv);
@@ -249,6 +252,7 @@ __global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, FfnCt
         acc = wave_sum(acc);
         if (lane == 0) d.out_f32[row] = fadd_rn(acc, res);
         if (d.trace && threadIdx.x == 0) d.trace[j * 8 + 1] = rt_now();
+        stamp_end(g.stamp);
         return;
     }
     // ---- gate/up (16-row interleave: output o = rows 32 (o / 16) + o % 16 and + 16)
@@ -312,6 +316,7 @@ __global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, FfnCt
         if (lane == 0) __hip_atomic_fetch_add(c.cnt + (blockIdx.x & 31) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (g.trace && threadIdx.x == 0) g.trace[blockIdx.x * 8 + 1] = rt_now();
+    stamp_end(g.stamp);
 }
 
 // the plain batch-1 f16 FFN (K = 1024, F = 3072) in one launch when every

@@ -115,6 +115,7 @@ struct GemvArgs {
     unsigned int *done; int32_t *tok_out; int32_t *hist; int hist_stride; int *step; int *pos;
     unsigned long long *trace;           // dev trace: per block [start, end, ...] (8 slots, 100 MHz clock) or null
     unsigned int *zero8;                 // gemv1: block 0 re-arms these 8 replicated counters (16-word stride)
+    unsigned long long *stamp;           // kernel-duration probe record (dev_common.h stamp_start/end) or null
 };
 void launch_gemv(int epi, const GemvArgs &g, hipStream_t s);
 // gemv.hip: one-row f16 fast path of launch_gemv (false = not covered)
@@ -220,6 +221,7 @@ struct DecodeAttnArgs {
     int fence;                           // fused launch: agent release/acquire around the hand-offs (FuseCfg)
     unsigned int *err;                   // fused launch: sticky device error word (DevErr bits)
     int spl1;                            // batch <= 8: key split (0 = auto: 64, or 128 from 1k keys)
+    unsigned long long *stamp;           // kernel-duration probe record or null
 };
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
 // batch 1, f16: the QKV projection (q: GemvArgs of the rmsnorm+QKV GEMV, K = 1024)

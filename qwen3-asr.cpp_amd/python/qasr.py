@@ -25,7 +25,7 @@ EXPORTS = [
     "qasr_mel_frames", "qasr_encoder_frames", "qasr_prompt_len", "qasr_build_prompt",
     "qasr_mel", "qasr_encode", "qasr_encode_conv", "qasr_prefill", "qasr_decode_step",
     "qasr_stage_audio", "qasr_run", "qasr_set_system_prompt", "qasr_transcribe_batch",
-    "qasr_set_probe", "qasr_get_probe",
+    "qasr_set_probe", "qasr_get_probe", "qasr_get_probe_device",
     "qasr_ctx_set_option", "qasr_ctx_get_option", "qasr_debug_read",
     "qasr_detokenize", "qasr_tokenize",
     "qasr_load_wav", "qasr_write_wav", "qasr_synth_pcm", "qasr_write_synthetic_gguf",
@@ -78,6 +78,7 @@ def lib() -> C.CDLL:
             "qasr_transcribe_batch": ([P, C.POINTER(F), IP, I, I, I, I32P, IP, C.POINTER(Timings)], I),
             "qasr_set_probe": ([P, I], I),
             "qasr_get_probe": ([P, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_double)], I),
+            "qasr_get_probe_device": ([P, C.POINTER(C.c_double), C.POINTER(C.c_int64)], I),
             "qasr_ctx_set_option": ([P, C.c_char_p, I], I), "qasr_ctx_get_option": ([P, C.c_char_p, IP], I),
             "qasr_debug_read": ([P, C.c_char_p, P, C.c_int64], I),
             "qasr_detokenize": ([P, I32P, I, C.c_char_p, I], I), "qasr_tokenize": ([P, C.c_char_p, I32P, I], I),
@@ -376,6 +377,12 @@ class Context:
         ms, n, b = C.c_double(0), C.c_int64(0), C.c_double(0)
         _check(lib().qasr_get_probe(self.h, C.byref(ms), C.byref(n), C.byref(b)), "qasr_get_probe")
         return ms.value, n.value, b.value
+
+    def get_probe_device(self):
+        """(total ms, launches) of the probed launches by the device clock"""
+        ms, n = C.c_double(0), C.c_int64(0)
+        _check(lib().qasr_get_probe_device(self.h, C.byref(ms), C.byref(n)), "qasr_get_probe_device")
+        return ms.value, n.value
 
     # ---- forced aligner ------------------------------------------------------
     def align(self, pcm: np.ndarray, text_ids: Sequence[int]):
