@@ -132,8 +132,16 @@ int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_past, int B,
                      float *logits, int32_t *argmax);
 
 /* ---- whole path ----------------------------------------------------------- */
-/* Stage PCM into device HBM (one H2D copy); qasr_run then works from HBM. */
+/* Stage PCM into device HBM (one H2D copy); qasr_run then works from HBM.
+ * Any number of clips may be staged (a pool); qasr_run needs B <= max_batch,
+ * qasr_run_staged runs subsets of a larger pool. */
 int qasr_stage_audio(qasr_ctx *c, const float *const *pcm, const int *n, int B);
+/* Greedy transcription of staged clips clips[0..B) (indices into the last
+ * qasr_stage_audio call, B <= max_batch) as one batch, from HBM; outputs as
+ * qasr_run.  The multi-GPU sharded driver stages a rank's whole shard once
+ * and runs it batch by batch (bench.py --utterances). */
+int qasr_run_staged(qasr_ctx *c, const int *clips, int B, int max_tokens, int ignore_eos, int32_t *tokens,
+                    int *n_tokens, qasr_timings *t);
 /* Greedy transcription of the staged clips: tokens [B][max_tokens],
  * n_tokens[B] (trailing EOS popped as src/qwen3_asr.cpp:298-300).
  * ignore_eos != 0: fixed budget of max_tokens steps (throughput mode). */
@@ -168,7 +176,25 @@ int qasr_ctx_get_option(const qasr_ctx *c, const char *name, int *value);
  * output, "qkv" fp32 [max_batch][q+k+v], "att" fp16 [max_batch][n_head*128] */
 int qasr_debug_read(qasr_ctx *c, const char *buffer, void *dst, int64_t bytes);
 
+/* Per-token callback (Qwen3ASR::set_progress_callback, src/qwen3_asr.cpp:255-291):
+ * called synchronously on the caller's thread after every greedy token of
+ * qasr_run / qasr_run_staged -- the prefill's token first (n_generated = 1) --
+ * for every sequence still decoding, in sequence order.  Each step then
+ * synchronises the stream (the token must reach the host), so a callback
+ * costs throughput; NULL removes it. */
+int qasr_set_token_callback(qasr_ctx *c, void (*cb)(void *user, int seq, int n_generated, int32_t token), void *user);
+
 /* ---- measurement ---------------------------------------------------------- */
+/* --profile (src/timing.h QWEN3_TIMER sections, src/main.cpp:409-411): on = 1
+ * records per-section device time (HIP events) of every qasr_run --
+ * mel_spectrogram, audio_encoding.{total,conv_chunk,transformer},
+ * decode.initial_forward, decode.token (one per step), transcribe.total --
+ * accumulated until the next qasr_set_profile (which resets).  The run also
+ * carries roctx ranges "qasr.run" / "qasr.decode" for rocprofv3 --marker-trace. */
+int qasr_set_profile(qasr_ctx *c, int on);
+/* the report in QWEN3_TIMER_REPORT's layout; returns its length, writes at
+ * most cap-1 bytes + NUL */
+int qasr_profile_report(qasr_ctx *c, char *out, int cap);
 /* Probe one launch group of every greedy decode step of qasr_run with HIP
  * events on the context's stream: kernel 1 = LM head + fused argmax; 2 = the
  * QKV projection + attention (+ o-projection) of decoder layer "probe_layer"

@@ -73,10 +73,13 @@ public:
     bool is_loaded() const { return model_ != nullptr; }
     const text_decoder_config &get_config() const { return config_; }
 
-    // MI355X additions: device selection and batched transcription.
+    // MI355X additions: device selection, batched transcription, and the
+    // --profile report (src/timing.h sections, device time, of the last call)
     void set_device(int device) { device_ = device; }
     std::vector<transcribe_result> transcribe_batch(const std::vector<std::vector<float>> &clips,
                                                     const transcribe_params &params = transcribe_params());
+    void set_profile(bool on) { profile_ = on; }
+    const std::string &profile_report() const { return profile_report_; }
 
 private:
     transcribe_result transcribe_internal(const float *samples, int n_samples, const transcribe_params &params);
@@ -88,6 +91,8 @@ private:
     text_decoder_config config_;
     std::string error_msg_;
     progress_callback_t progress_callback_;
+    bool profile_ = false;
+    std::string profile_report_;
 };
 
 bool load_audio_file(const std::string &path, std::vector<float> &samples, int &sample_rate);

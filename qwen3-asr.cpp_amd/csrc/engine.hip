@@ -4,6 +4,7 @@
 //   greedy decode (HIP-graph replayed step) -> token ids
 // restating Qwen3ASR::transcribe_internal (src/qwen3_asr.cpp:81-149) on HIP.
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <cmath>
@@ -12,6 +13,8 @@
 #include <cstring>
 #include <functional>
 #include <memory>
+#include <mutex>
+#include <optional>
 #include <string>
 #include <map>
 #include <vector>
@@ -127,6 +130,15 @@ struct qasr_ctx {
     FuseCfg fuse;                  // batch-1 fused launches: switches, delays, co-residency of this device
     unsigned int *d_err = nullptr; // sticky device error word of the fused launches (DevErr bits)
     int dbg_layers = 0;            // diagnostic: decode steps run only the first n decoder layers (0 = all)
+    // --profile (src/timing.h QWEN3_TIMER sections): per-section device time from
+    // HIP events, accumulated over calls until qasr_set_profile resets it
+    bool profile_on = false;
+    std::map<std::string, std::pair<double, long>> prof;   // section -> (total ms, calls)
+    std::vector<hipEvent_t> step_ev;                       // per decode step, profile only
+    // per-token callback (src/qwen3_asr.cpp:264-291): called synchronously
+    // after every greedy step of qasr_run, in order, for every live sequence
+    void (*tok_cb)(void *user, int seq, int n_generated, int32_t token) = nullptr;
+    void *tok_cb_user = nullptr;
     // QASR_DEV_TRACE=<file>: per-block timestamps of one decode layer's kernels
     // (layer QASR_DEV_TRACE_LAYER, default 10) of the last step, dumped by qasr_run
     std::string trace_path;
@@ -163,6 +175,7 @@ struct qasr_ctx {
         (void)hipSetDevice(m->device);
         drop_graphs();
         for (auto &e : pev) (void)hipEventDestroy(e);
+        for (auto &e : step_ev) (void)hipEventDestroy(e);
         for (auto &b : owned) (void)hipFree(b.p);
         for (auto &e : ev) if (e) (void)hipEventDestroy(e);
         if (pin) (void)hipHostFree(pin);
@@ -207,6 +220,27 @@ static int check_dev_err(qasr_ctx *c) {
     return fail(QASR_ERR_DEVICE, "fused decode launch: an in-launch wait timed out (" + what.substr(1) +
                                      "); outputs of this call are invalid (another process or context sharing the GPU?)");
 }
+
+// The batch-1 fused launches assume the whole GPU is theirs (every workgroup
+// of a launch co-resident: a role waits on another role in-launch).  Calls
+// that can take them hold their device's lock, so contexts driven from
+// several host threads on one GPU run those calls one at a time instead of
+// sharing the CUs (a GPU shared with another PROCESS is not covered: a wait
+// that runs out then fails the call with QASR_ERR_DEVICE; QASR_FUSE_*=0 or
+// qasr_ctx_set_option turns the fused launches off).
+static std::mutex &device_lock(int device) {
+    static std::mutex m[64];
+    return m[(unsigned)device % 64];
+}
+static bool takes_fused(const qasr_ctx *c, int B) { return B == 1 && !c->m->q8 && (c->fuse.ffn || c->fuse.qkv); }
+
+// a roctx range for the lifetime of the object (rocprofv3 --marker-trace)
+struct RoctxRange {
+    explicit RoctxRange(const char *name) { roctxRangePushA(name); }
+    ~RoctxRange() { roctxRangePop(); }
+    RoctxRange(const RoctxRange &) = delete;
+    RoctxRange &operator=(const RoctxRange &) = delete;
+};
 
 static int dev_alloc(qasr_ctx *c, void **p, size_t bytes) {
     HIPCHK(hipMalloc(p, bytes ? bytes : 256));
@@ -833,6 +867,7 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
         launch_gemm(AM_DENSE, EPI_F32, o, s);
     }
     HIPCHK(hipGetLastError());
+    if (c->profile_on) HIPCHK(hipEventRecord(c->ev[5], s));   // conv front-end | transformer
     if (conv_only) return 0;
 
     // attention segments: whole clips (ASR: full attention, src/audio_encoder.cpp:466-486)
@@ -1448,6 +1483,8 @@ extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_pa
         pos[b] = n_past[b];
         nkv[b] = n_past[b] + 1;
     }
+    std::unique_lock<std::mutex> dev_lk;
+    if (takes_fused(c, B)) dev_lk = std::unique_lock<std::mutex>(device_lock(c->m->device));
     HIPCHK(hipMemcpyAsync(c->d_tok, tok, B * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemcpyAsync(c->d_pos, pos.data(), B * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemcpyAsync(c->d_nkv, nkv.data(), B * 4, hipMemcpyHostToDevice, c->st));
@@ -1462,7 +1499,6 @@ extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_pa
 
 extern "C" int qasr_stage_audio(qasr_ctx *c, const float *const *pcm, const int *n, int B) {
     if (!c || !pcm || !n || B <= 0) return fail(QASR_ERR_ARG, "bad arguments");
-    if (B > c->max_batch) return fail(QASR_ERR_ARG, "batch exceeds context max_batch");
     HIPCHK(hipSetDevice(c->m->device));
     c->staged_n.assign(n, n + B);
     c->staged_off.assign(B, 0);
@@ -1480,12 +1516,16 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
     if (!c || max_tokens <= 0 || !tokens || !n_tokens) return fail(QASR_ERR_ARG, "bad arguments");
     const int B = (int)c->staged_n.size();
     if (B == 0) return fail(QASR_ERR_STATE, "no staged audio");
+    if (B > c->max_batch) return fail(QASR_ERR_ARG, "staged clips exceed the context's max_batch (qasr_run_staged runs subsets)");
     HIPCHK(hipSetDevice(c->m->device));
+    std::unique_lock<std::mutex> dev_lk;
+    if (takes_fused(c, B)) dev_lk = std::unique_lock<std::mutex>(device_lock(c->m->device));
     HIPCHK(hipStreamSynchronize(c->st));
     c->pin_used = 0;
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
     hipStream_t s = c->st;
+    RoctxRange run_range("qasr.run");   // host-side ranges for rocprofv3 --marker-trace
     HIPCHK(hipEventRecord(c->ev[0], s));
     std::vector<long> mo;
     std::vector<int> T;
@@ -1512,9 +1552,45 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
     if ((rc = probe_arm(c, max_tokens - 1))) return rc;
     std::vector<int32_t> hist((size_t)B * c->hist_cap);
     int steps = 0;
-    if (ignore_eos) {
+    std::optional<RoctxRange> dec_range(std::in_place, "qasr.decode");
+    // profile: an event after every step (decode.token); k = 0-based step
+    auto step = [&](int k) -> int {
+        int r = launch_step(c, B, k);
+        if (r || !c->profile_on) return r;
+        while ((int)c->step_ev.size() <= k) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreate(&e));
+            c->step_ev.push_back(e);
+        }
+        HIPCHK(hipEventRecord(c->step_ev[k], s));
+        return 0;
+    };
+    if (c->tok_cb) {
+        // per-token callback (src/qwen3_asr.cpp:255-291): every token reaches
+        // the host as it is produced -- one synchronisation per step
+        std::vector<char> live(B, 1);
+        std::vector<int32_t> tok(B);
+        auto deliver = [&](int n_gen) -> int {
+            HIPCHK(hipMemcpyAsync(tok.data(), c->d_tok, B * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            for (int b = 0; b < B; b++) {
+                if (!live[b]) continue;
+                c->tok_cb(c->tok_cb_user, b, n_gen, tok[b]);
+                if (!ignore_eos && tok[b] == hp.eos_id) live[b] = 0;
+            }
+            return 0;
+        };
+        if ((rc = deliver(1))) return rc;
+        int k = 1;
+        for (; k < max_tokens && std::count(live.begin(), live.end(), 1) > 0; k++) {
+            if ((rc = step(k - 1)) || (rc = deliver(k + 1))) return rc;
+        }
+        steps = k - 1;
+        HIPCHK(hipMemcpyAsync(hist.data(), c->d_hist, hist.size() * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    } else if (ignore_eos) {
         for (int k = 1; k < max_tokens; k++)
-            if ((rc = launch_step(c, B, k - 1))) return rc;
+            if ((rc = step(k - 1))) return rc;
         steps = max_tokens - 1;
         HIPCHK(hipMemcpyAsync(hist.data(), c->d_hist, hist.size() * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -1535,7 +1611,7 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
         while (done + 1 < max_tokens && (st = all_done(done)) == 0) {
             const int todo = std::min(chunk, max_tokens - 1 - done);
             for (int k = 0; k < todo; k++)
-                if ((rc = launch_step(c, B, done + k))) return rc;
+                if ((rc = step(done + k))) return rc;
             done += todo;
         }
         if (st < 0) return fail(QASR_ERR_DEVICE, "device copy failed in decode loop");
@@ -1543,10 +1619,28 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
         HIPCHK(hipStreamSynchronize(s));
         steps = done;
     }
+    dec_range.reset();
     HIPCHK(hipEventRecord(c->ev[4], s));
     HIPCHK(hipEventSynchronize(c->ev[4]));
     if ((rc = check_dev_err(c))) return rc;
     if ((rc = probe_collect(c, B, steps))) return rc;
+    if (c->profile_on) {   // the reference's QWEN3_TIMER sections (src/timing.h), device time
+        auto add = [&](const char *name, hipEvent_t e0, hipEvent_t e1) -> int {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+            auto &v = c->prof[name];
+            v.first += ms;
+            v.second += 1;
+            return 0;
+        };
+        if ((rc = add("mel_spectrogram", c->ev[0], c->ev[1])) || (rc = add("audio_encoding.total", c->ev[1], c->ev[2])) ||
+            (rc = add("audio_encoding.conv_chunk", c->ev[1], c->ev[5])) ||
+            (rc = add("audio_encoding.transformer", c->ev[5], c->ev[2])) ||
+            (rc = add("decode.initial_forward", c->ev[2], c->ev[3])) || (rc = add("transcribe.total", c->ev[0], c->ev[4])))
+            return rc;
+        for (int k = 0; k < steps; k++)
+            if ((rc = add("decode.token", k ? c->step_ev[k - 1] : c->ev[3], c->step_ev[k]))) return rc;
+    }
     if (c->d_trace) {   // dev trace dump: raw [6][4096][8] u64
         std::vector<unsigned long long> tr((size_t)6 * 4096 * 8);
         HIPCHK(hipMemcpy(tr.data(), c->d_trace, tr.size() * 8, hipMemcpyDeviceToHost));
@@ -1576,6 +1670,63 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
         t->n_decode_steps = steps;
     }
     return 0;
+}
+
+extern "C" int qasr_run_staged(qasr_ctx *c, const int *clips, int B, int max_tokens, int ignore_eos, int32_t *tokens,
+                               int *n_tokens, qasr_timings *t) {
+    if (!c || !clips || B <= 0) return fail(QASR_ERR_ARG, "bad arguments");
+    if (B > c->max_batch) return fail(QASR_ERR_ARG, "subset exceeds the context's max_batch");
+    std::vector<int> n(B);
+    std::vector<long> off(B);
+    for (int b = 0; b < B; b++) {
+        if (clips[b] < 0 || clips[b] >= (int)c->staged_n.size()) return fail(QASR_ERR_ARG, "staged clip index out of range");
+        n[b] = c->staged_n[clips[b]];
+        off[b] = c->staged_off[clips[b]];
+    }
+    std::swap(n, c->staged_n);
+    std::swap(off, c->staged_off);
+    const int rc = qasr_run(c, max_tokens, ignore_eos, tokens, n_tokens, t);
+    std::swap(n, c->staged_n);   // the staged pool stays for the next subset
+    std::swap(off, c->staged_off);
+    return rc;
+}
+
+extern "C" int qasr_set_token_callback(qasr_ctx *c, void (*cb)(void *user, int seq, int n_generated, int32_t token), void *user) {
+    if (!c) return fail(QASR_ERR_ARG, "null context");
+    c->tok_cb = cb;
+    c->tok_cb_user = user;
+    return 0;
+}
+
+extern "C" int qasr_set_profile(qasr_ctx *c, int on) {
+    if (!c) return fail(QASR_ERR_ARG, "null context");
+    c->profile_on = on != 0;
+    c->prof.clear();
+    return 0;
+}
+
+// QWEN3_TIMER_REPORT's table (src/timing.h:32-48) over the sections recorded since qasr_set_profile
+extern "C" int qasr_profile_report(qasr_ctx *c, char *out, int cap) {
+    if (!c) return fail(QASR_ERR_ARG, "null context");
+    std::string r = "\n================================================================================\n"
+                    "                         TIMING PROFILE REPORT\n"
+                    "================================================================================\n";
+    char line[160];
+    snprintf(line, sizeof line, "%-45s %12s %8s %12s\n", "Section", "Total (ms)", "Calls", "Avg (ms)");
+    r += line;
+    r += "--------------------------------------------------------------------------------\n";
+    for (const auto &kv : c->prof) {
+        snprintf(line, sizeof line, "%-45s %12.2f %8ld %12.2f\n", kv.first.c_str(), kv.second.first, kv.second.second,
+                 kv.second.second ? kv.second.first / kv.second.second : 0.0);
+        r += line;
+    }
+    r += "================================================================================\n";
+    if (out && cap > 0) {
+        const size_t n = std::min(r.size(), (size_t)cap - 1);
+        memcpy(out, r.data(), n);
+        out[n] = 0;
+    }
+    return (int)r.size();
 }
 
 extern "C" int qasr_set_system_prompt(qasr_ctx *c, const int32_t *ids, int n) {

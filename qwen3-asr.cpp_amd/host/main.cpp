@@ -1,10 +1,17 @@
 // main.cpp -- qwen3-asr-cli: the three modes of src/main.cpp (transcription
 // :361-414, forced alignment --align :301-359, transcribe + align -a :416-500)
 // with the same flags and output, plus MI355X additions: --device, batch file
-// lists (-f may repeat, transcription mode), --synthetic to write a synthetic
-// GGUF (tiny|full|aligner|aligner-tiny) for testing.
+// lists (-f may repeat, --file-list, transcription mode), --devices to shard a
+// file list over several GPUs (one host thread and model replica per GPU,
+// longest-first assignment: the sharded counterpart of the reference's shell
+// loop, docs/usage.md:240-252), --synthetic to write a synthetic GGUF
+// (tiny|full|aligner|aligner-tiny) for testing.
 #include <algorithm>
+#include <atomic>
 #include <cctype>
+#include <chrono>
+#include <sys/stat.h>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -20,7 +27,8 @@ struct cli_params {
     std::string aligner_model_path;
     std::vector<std::string> audio_paths;
     std::string output_path, language, synthetic, align_text;
-    int32_t max_tokens = 1024, n_threads = 4, device = 0;
+    int32_t max_tokens = 1024, n_threads = 4, device = 0, batch = 16;
+    std::vector<int> devices;   // --devices: shard the files over these GPUs
     bool print_progress = false, print_timing = true, print_tokens = false, profile = false;
     bool align_mode = false, transcribe_align_mode = false;
 };
@@ -38,6 +46,9 @@ static void usage(const char *prog) {
     fprintf(stderr, "  --tokens               Print token IDs\n");
     fprintf(stderr, "  --profile              Print timing profile\n");
     fprintf(stderr, "  --device <n>           HIP device index (default: 0)\n");
+    fprintf(stderr, "  --file-list <path>     Text file with one audio path per line (added to the -f files)\n");
+    fprintf(stderr, "  --devices <i,j,...>    Shard the audio files over these HIP devices (one replica each)\n");
+    fprintf(stderr, "  --batch <n>            Clips per GPU batch with --devices / several files (default: 16)\n");
     fprintf(stderr, "  --synthetic <cfg>      Write a synthetic GGUF (tiny|full|aligner|aligner-tiny) to --model and exit\n");
     fprintf(stderr, "\nForced Alignment:\n");
     fprintf(stderr, "  --align                Enable forced alignment mode\n");
@@ -64,6 +75,25 @@ static bool parse(int argc, char **argv, cli_params &p) {
         else if (!strcmp(a, "-t") || !strcmp(a, "--threads")) { if (!val(v)) return false; p.n_threads = atoi(v.c_str()); }
         else if (!strcmp(a, "--max-tokens")) { if (!val(v)) return false; p.max_tokens = atoi(v.c_str()); }
         else if (!strcmp(a, "--device")) { if (!val(v)) return false; p.device = atoi(v.c_str()); }
+        else if (!strcmp(a, "--batch")) { if (!val(v)) return false; p.batch = std::max(1, atoi(v.c_str())); }
+        else if (!strcmp(a, "--devices")) {
+            if (!val(v)) return false;
+            for (size_t k = 0; k < v.size();) {
+                const size_t e = v.find(',', k);
+                p.devices.push_back(atoi(v.substr(k, e == std::string::npos ? std::string::npos : e - k).c_str()));
+                if (e == std::string::npos) break;
+                k = e + 1;
+            }
+        }
+        else if (!strcmp(a, "--file-list")) {
+            if (!val(v)) return false;
+            std::ifstream f(v);
+            if (!f) { fprintf(stderr, "Error: cannot read file list %s\n", v.c_str()); return false; }
+            for (std::string line; std::getline(f, line);) {
+                while (!line.empty() && (line.back() == '\r' || line.back() == ' ')) line.pop_back();
+                if (!line.empty()) p.audio_paths.push_back(line);
+            }
+        }
         else if (!strcmp(a, "--synthetic")) { if (!val(p.synthetic)) return false; }
         else if (!strcmp(a, "--progress")) p.print_progress = true;
         else if (!strcmp(a, "--no-timing")) p.print_timing = false;
@@ -257,12 +287,84 @@ static int run_transcribe_and_align(const cli_params &p) {
     return write_output(p, alignment_to_json(r) + "\n");
 }
 
+// --devices: one host thread per GPU, each with its own model replica and
+// context (the reference's objects are single-threaded; so are ours), the
+// files assigned longest-first by size, each GPU's share transcribed in
+// batches of --batch clips; output in input order
+static int run_transcription_sharded(const cli_params &p) {
+    const size_t N = p.audio_paths.size();
+    const int G = (int)p.devices.size();
+    std::vector<long long> size(N);
+    for (size_t i = 0; i < N; i++) {
+        struct stat st;
+        size[i] = stat(p.audio_paths[i].c_str(), &st) == 0 ? (long long)st.st_size : 0;
+    }
+    std::vector<size_t> order(N);
+    for (size_t i = 0; i < N; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return size[a] > size[b]; });
+    std::vector<std::vector<size_t>> shard(G);
+    std::vector<long long> load(G, 0);
+    for (size_t i : order) {   // longest processing time first
+        const int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        shard[g].push_back(i);
+        load[g] += size[i];
+    }
+    fprintf(stderr, "qwen3-asr-cli (sharded)\n  Model: %s\n  Files: %zu over %d GPU(s), batches of %d\n\n", p.model_path.c_str(), N, G,
+            p.batch);
+    std::vector<qwen3_asr::transcribe_result> results(N);
+    std::vector<std::string> errors(G);
+    std::atomic<long long> samples{0};
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; g++) {
+        th.emplace_back([&, g] {
+            qwen3_asr::Qwen3ASR asr;
+            asr.set_device(p.devices[g]);
+            if (!asr.load_model(p.model_path)) { errors[g] = asr.get_error(); return; }
+            qwen3_asr::transcribe_params tp;
+            tp.max_tokens = p.max_tokens;
+            tp.language = p.language;
+            tp.print_timing = false;
+            for (size_t k = 0; k < shard[g].size(); k += p.batch) {
+                const size_t e = std::min(shard[g].size(), k + (size_t)p.batch);
+                std::vector<std::vector<float>> clips;
+                for (size_t j = k; j < e; j++) {
+                    std::vector<float> s;
+                    int sr = 0;
+                    if (!qwen3_asr::load_audio_file(p.audio_paths[shard[g][j]], s, sr) || sr != 16000) {
+                        errors[g] = "bad audio " + p.audio_paths[shard[g][j]];
+                        return;
+                    }
+                    samples += (long long)s.size();
+                    clips.push_back(std::move(s));
+                }
+                auto rs = asr.transcribe_batch(clips, tp);
+                for (size_t j = k; j < e; j++) results[shard[g][j]] = std::move(rs[j - k]);
+            }
+        });
+    }
+    for (auto &t : th) t.join();
+    const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    for (int g = 0; g < G; g++)
+        if (!errors[g].empty()) { fprintf(stderr, "Error (device %d): %s\n", p.devices[g], errors[g].c_str()); return 1; }
+    std::string all;
+    for (size_t i = 0; i < N; i++) {
+        if (!results[i].success) { fprintf(stderr, "Error (%s): %s\n", p.audio_paths[i].c_str(), results[i].error_msg.c_str()); return 1; }
+        all += results[i].text + "\n";
+    }
+    if (p.print_timing)
+        fprintf(stderr, "Sharded timing: %.1f s of audio in %.3f s over %d GPU(s) (RTFx %.1f, model loads included)\n",
+                samples.load() / 16000.0, wall, G, samples.load() / 16000.0 / wall);
+    return write_output(p, all);
+}
+
 static int run_transcription(const cli_params &p) {
     fprintf(stderr, "qwen3-asr-cli\n  Model: %s\n", p.model_path.c_str());
     for (auto &a : p.audio_paths) fprintf(stderr, "  Audio: %s\n", a.c_str());
     fprintf(stderr, "  Threads: %d\n\n", p.n_threads);
     qwen3_asr::Qwen3ASR asr;
     asr.set_device(p.device);
+    asr.set_profile(p.profile);
     if (!asr.load_model(p.model_path)) { fprintf(stderr, "Error: %s\n", asr.get_error().c_str()); return 1; }
     qwen3_asr::transcribe_params tp;
     tp.max_tokens = p.max_tokens;
@@ -293,7 +395,9 @@ static int run_transcription(const cli_params &p) {
         }
         all += r.text + "\n";
     }
-    return write_output(p, all);
+    const int rc = write_output(p, all);
+    if (p.profile) fprintf(stderr, "%s", asr.profile_report().c_str());   // src/main.cpp:409-411
+    return rc;
 }
 
 int main(int argc, char **argv) {
@@ -309,5 +413,6 @@ int main(int argc, char **argv) {
     }
     if (p.transcribe_align_mode) return run_transcribe_and_align(p);
     if (p.align_mode) return run_alignment(p);
+    if (!p.devices.empty()) return run_transcription_sharded(p);
     return run_transcription(p);
 }

@@ -11,6 +11,21 @@
 
 namespace qwen3_asr {
 
+// per-token callback trampoline (qasr_set_token_callback): the reference calls
+// progress_callback(n_generated, max_tokens) after every token and prints every
+// 10th (src/qwen3_asr.cpp:255-291); a batch reports its first clip
+struct TokenCb {
+    const progress_callback_t *cb;
+    int max_tokens;
+    bool print;
+};
+static void token_cb(void *user, int seq, int n_generated, int32_t) {
+    const TokenCb *t = (const TokenCb *)user;
+    if (seq != 0) return;
+    if (t->cb && *t->cb) (*t->cb)(n_generated, t->max_tokens);
+    if (t->print && n_generated % 10 == 0) fprintf(stderr, "Generated %d tokens...\n", n_generated);
+}
+
 static int64_t now_ms() {
     return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -110,12 +125,25 @@ std::vector<transcribe_result> Qwen3ASR::transcribe_batch(const std::vector<std:
         return out;
     }
     qasr_set_system_prompt(ctx_, sys.data(), (int)sys.size());
+    qasr_set_profile(ctx_, profile_ ? 1 : 0);   // resets the sections: the report covers this call
     std::vector<int32_t> toks((size_t)B * params.max_tokens);
     std::vector<int> nt(B);
     qasr_timings tm{};
-    if (qasr_transcribe_batch(ctx_, ptr.data(), n.data(), B, params.max_tokens, 0, toks.data(), nt.data(), &tm) != 0) {
+    TokenCb tcb{&progress_callback_, params.max_tokens, params.print_progress};
+    const bool per_token = progress_callback_ || params.print_progress;
+    qasr_set_token_callback(ctx_, per_token ? token_cb : nullptr, per_token ? &tcb : nullptr);
+    const int rc = qasr_transcribe_batch(ctx_, ptr.data(), n.data(), B, params.max_tokens, 0, toks.data(), nt.data(), &tm);
+    qasr_set_token_callback(ctx_, nullptr, nullptr);
+    if (rc != 0) {
         for (auto &r : out) r.error_msg = std::string("Decoding failed: ") + qasr_last_error();
         return out;
+    }
+    if (profile_) {
+        const int len = qasr_profile_report(ctx_, nullptr, 0);
+        std::string rep(std::max(len, 0) + 1, '\0');
+        qasr_profile_report(ctx_, &rep[0], (int)rep.size());
+        rep.resize(std::max(len, 0));
+        profile_report_ = rep;
     }
     const int64_t t1 = now_ms();
     for (int b = 0; b < B; b++) {
@@ -131,8 +159,6 @@ std::vector<transcribe_result> Qwen3ASR::transcribe_batch(const std::vector<std:
         r.t_encode_ms = (int64_t)tm.t_encode_ms;
         r.t_decode_ms = (int64_t)(tm.t_prefill_ms + tm.t_decode_ms);
         r.t_total_ms = t1 - t0;
-        if (progress_callback_)
-            for (int k = 1; k <= (int)r.tokens.size(); k++) progress_callback_(k, params.max_tokens);
     }
     return out;
 }
@@ -140,7 +166,6 @@ std::vector<transcribe_result> Qwen3ASR::transcribe_batch(const std::vector<std:
 transcribe_result Qwen3ASR::transcribe_internal(const float *samples, int n_samples, const transcribe_params &params) {
     std::vector<std::vector<float>> one(1, std::vector<float>(samples, samples + n_samples));
     transcribe_result r = transcribe_batch(one, params)[0];
-    if (r.success && params.print_progress) fprintf(stderr, "Tokens generated: %zu\n", r.tokens.size());
     if (r.success && params.print_timing) {
         fprintf(stderr, "\nTiming:\n");
         fprintf(stderr, "  Mel spectrogram: %lld ms\n", (long long)r.t_mel_ms);

@@ -24,9 +24,10 @@ EXPORTS = [
     "qasr_ctx_create", "qasr_ctx_free",
     "qasr_mel_frames", "qasr_encoder_frames", "qasr_prompt_len", "qasr_build_prompt",
     "qasr_mel", "qasr_encode", "qasr_encode_conv", "qasr_prefill", "qasr_decode_step",
-    "qasr_stage_audio", "qasr_run", "qasr_set_system_prompt", "qasr_transcribe_batch",
+    "qasr_stage_audio", "qasr_run", "qasr_run_staged", "qasr_set_system_prompt", "qasr_transcribe_batch",
     "qasr_set_probe", "qasr_get_probe", "qasr_get_probe_device",
     "qasr_ctx_set_option", "qasr_ctx_get_option", "qasr_debug_read",
+    "qasr_set_token_callback", "qasr_set_profile", "qasr_profile_report",
     "qasr_detokenize", "qasr_tokenize",
     "qasr_load_wav", "qasr_write_wav", "qasr_synth_pcm", "qasr_write_synthetic_gguf",
     "qasr_align", "qasr_align_tokenize", "qasr_model_load_korean_dict", "qasr_fix_timestamps",
@@ -49,6 +50,8 @@ class Timings(C.Structure):
 
 
 _lib = None
+# void (*)(void *user, int seq, int n_generated, int32_t token)
+TOKEN_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.c_int32)
 
 
 def lib() -> C.CDLL:
@@ -74,6 +77,7 @@ def lib() -> C.CDLL:
             "qasr_decode_step": ([P, I32P, IP, I, F, I32P], I),
             "qasr_stage_audio": ([P, C.POINTER(F), IP, I], I),
             "qasr_run": ([P, I, I, I32P, IP, C.POINTER(Timings)], I),
+            "qasr_run_staged": ([P, IP, I, I, I, I32P, IP, C.POINTER(Timings)], I),
             "qasr_set_system_prompt": ([P, I32P, I], I),
             "qasr_transcribe_batch": ([P, C.POINTER(F), IP, I, I, I, I32P, IP, C.POINTER(Timings)], I),
             "qasr_set_probe": ([P, I], I),
@@ -81,6 +85,8 @@ def lib() -> C.CDLL:
             "qasr_get_probe_device": ([P, C.POINTER(C.c_double), C.POINTER(C.c_int64)], I),
             "qasr_ctx_set_option": ([P, C.c_char_p, I], I), "qasr_ctx_get_option": ([P, C.c_char_p, IP], I),
             "qasr_debug_read": ([P, C.c_char_p, P, C.c_int64], I),
+            "qasr_set_token_callback": ([P, TOKEN_CB, P], I),
+            "qasr_set_profile": ([P, I], I), "qasr_profile_report": ([P, C.c_char_p, I], I),
             "qasr_detokenize": ([P, I32P, I, C.c_char_p, I], I), "qasr_tokenize": ([P, C.c_char_p, I32P, I], I),
             "qasr_load_wav": ([C.c_char_p, F, I, IP], I), "qasr_write_wav": ([C.c_char_p, F, I, I], I),
             "qasr_synth_pcm": ([C.c_uint64, I, F], I),
@@ -342,10 +348,23 @@ class Context:
 
     def run(self, max_tokens: int, ignore_eos: bool = False) -> RunResult:
         B = len(self._staged)
+        if B > self.max_batch:
+            raise QasrError(f"{B} staged clips exceed max_batch {self.max_batch}: use run_staged")
         toks = np.zeros((B, max_tokens), np.int32)
         nt = np.zeros(B, np.int32)
         t = Timings()
         _check(lib().qasr_run(self.h, max_tokens, int(ignore_eos), _i32(toks), _i(nt), C.byref(t)), "qasr_run")
+        return RunResult([toks[b, :nt[b]].tolist() for b in range(B)], t)
+
+    def run_staged(self, clips: Sequence[int], max_tokens: int, ignore_eos: bool = False) -> RunResult:
+        """transcribe staged clips (indices into the last stage_audio call) as one batch"""
+        idx = np.ascontiguousarray(clips, np.int32)
+        B = len(idx)
+        toks = np.zeros((B, max_tokens), np.int32)
+        nt = np.zeros(B, np.int32)
+        t = Timings()
+        _check(lib().qasr_run_staged(self.h, _i(idx), B, max_tokens, int(ignore_eos), _i32(toks), _i(nt), C.byref(t)),
+               "qasr_run_staged")
         return RunResult([toks[b, :nt[b]].tolist() for b in range(B)], t)
 
     def set_system_prompt(self, ids: Sequence[int]) -> None:
@@ -369,6 +388,20 @@ class Context:
         out = np.zeros((self.max_batch, n), dt)
         _check(lib().qasr_debug_read(self.h, buffer.encode(), out.ctypes.data_as(C.c_void_p), out.nbytes), "qasr_debug_read")
         return out
+
+    def set_token_callback(self, fn) -> None:
+        """fn(seq, n_generated, token) after every greedy token of run() (None removes)"""
+        self._tok_cb = TOKEN_CB(lambda _u, seq, n, tok: fn(seq, n, tok)) if fn else None
+        _check(lib().qasr_set_token_callback(self.h, self._tok_cb if fn else TOKEN_CB(), None), "qasr_set_token_callback")
+
+    def set_profile(self, on: bool) -> None:
+        _check(lib().qasr_set_profile(self.h, int(on)), "qasr_set_profile")
+
+    def profile_report(self) -> str:
+        n = lib().qasr_profile_report(self.h, None, 0)
+        buf = C.create_string_buffer(n + 1)
+        lib().qasr_profile_report(self.h, buf, n + 1)
+        return buf.raw[:n].decode()
 
     def set_probe(self, kernel: int) -> None:
         _check(lib().qasr_set_probe(self.h, kernel), "qasr_set_probe")

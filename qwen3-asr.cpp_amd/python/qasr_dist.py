@@ -1,7 +1,11 @@
 """qasr_dist -- utterance-level data parallelism.
 
 One process per GPU; utterances are independent, so each rank transcribes its
-own shard with no collective on the data path.  torch.distributed (RCCL over
+own shard with no collective on the data path (configs[3]: a 1000-utterance
+f16 batch sharded over the node's GPUs; configs[4]: the same with the
+ForcedAligner leg on every utterance).  The reference's only batch mode is a
+shell loop over files (docs/usage.md:240-252); this is its sharded
+counterpart.  torch.distributed (RCCL over
 xGMI on the GPU box, gloo in CPU tests) is used only to
   - synchronise the timed region (barrier) and take the max wall time,
   - gather the per-utterance token-id arrays to rank 0 at the end
@@ -9,7 +13,9 @@ xGMI on the GPU box, gloo in CPU tests) is used only to
 """
 from __future__ import annotations
 
-from typing import List, Sequence
+import math
+import time
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -69,3 +75,55 @@ def gather_tokens(local: dict, dist, device=None):
             out[idx] = a[p + 2:p + 2 + ln].tolist()
             p += 2 + ln
     return out
+
+
+def utterance_set(n: int, seed: int = 0, lo: float = 5.0, hi: float = 30.0, sr: int = 16000) -> List[Tuple[int, int]]:
+    """n seeded utterances: (pcm seed, samples), lengths
+    U[lo, hi] seconds (lo == hi: fixed length), whole 10 ms hops."""
+    rng = np.random.default_rng(seed)
+    secs = rng.uniform(lo, hi, n) if hi > lo else np.full(n, lo)
+    return [(1000 + i, int(round(float(s) * 100)) * (sr // 100)) for i, s in enumerate(secs)]
+
+
+def budget(samples: int, tok_rate: float, sr: int = 16000) -> int:
+    """fixed greedy decode budget: ceil(tok_rate x seconds)"""
+    return max(1, int(math.ceil(tok_rate * samples / sr)))
+
+
+def batches_of(shard: Sequence[int], lengths: Sequence[int], batch: int) -> List[List[int]]:
+    """a rank's utterances longest first, cut into batches of similar length
+    (each batch decodes to its longest clip's budget; sorted, that overshoot
+    stays small)"""
+    order = sorted(shard, key=lambda i: (-int(lengths[i]), i))
+    return [order[k:k + batch] for k in range(0, len(order), batch)]
+
+
+def run_shard(transcribe: Callable[[List[int], int], List[List[int]]], utts: Sequence[Tuple[int, int]], rank: int,
+              world: int, batch: int, tok_rate: float, dist=None, device=None,
+              after_batch: Optional[Callable[[List[int], List[List[int]]], None]] = None) -> Dict:
+    """The sharded data-parallel driver.  transcribe(indices, max_tokens) ->
+    token lists for those utterances (already staged by the caller, e.g. in
+    HBM); each utterance keeps its own budget's worth of tokens.  Barrier ->
+    timed pass over this rank's batches -> barrier; the wall time is the max
+    over ranks; the token ids are gathered to rank 0 (the only collectives).
+    Returns {"tokens" (rank 0: all utterances), "wall_s", "audio_s",
+    "decode_tokens", "local"}."""
+    lengths = [n for _, n in utts]
+    shard = shard_longest_first(lengths, world)[rank]
+    plan = batches_of(shard, lengths, batch)
+    if dist is not None and dist.is_initialized():
+        dist.barrier()
+    t0 = time.perf_counter()
+    local: Dict[int, List[int]] = {}
+    for idx in plan:
+        toks = transcribe(idx, max(budget(lengths[i], tok_rate) for i in idx))
+        for i, t in zip(idx, toks):
+            local[i] = list(t[:budget(lengths[i], tok_rate)])
+        if after_batch is not None:
+            after_batch(idx, [local[i] for i in idx])
+    if dist is not None and dist.is_initialized():
+        dist.barrier()
+    wall = max_over_ranks(time.perf_counter() - t0, dist, device)
+    merged = gather_tokens(local, dist, device)
+    return {"tokens": merged, "wall_s": wall, "audio_s": sum(lengths) / 16000.0,
+            "decode_tokens": sum(budget(n, tok_rate) for n in lengths), "local": local, "batches": len(plan)}

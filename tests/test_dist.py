@@ -56,3 +56,64 @@ def test_gloo_world2_gather_and_max():
     assert t0 == t1 == 2.0
     assert m1 is None
     assert m0 == {i: [i * 10 + k for k in range(i + 1)] for i in range(5)}
+
+
+def test_utterance_set_and_batches():
+    from qasr_dist import batches_of, budget, utterance_set
+    u = utterance_set(1000, seed=0)
+    assert len(u) == 1000 and len({s for s, _ in u}) == 1000
+    secs = [n / 16000 for _, n in u]
+    assert 5.0 <= min(secs) and max(secs) <= 30.0 and all(n % 160 == 0 for _, n in u)
+    assert utterance_set(1000, seed=0) == u and utterance_set(1000, seed=1) != u
+    assert budget(30 * 16000, 3.5) == 105 and budget(92 * 16000, 3.5) == 322
+    lens = [n for _, n in u]
+    b = batches_of(list(range(100)), lens, 64)
+    assert [len(x) for x in b] == [64, 36]
+    assert all(lens[x[i]] >= lens[x[i + 1]] for x in b for i in range(len(x) - 1))
+
+
+def _driver_worker(rank, world, port, q):
+    """the full sharded driver loop with a stub transcriber (token k of
+    utterance i = i * 1000 + k): sharding, per-utterance budgets, timing,
+    gather to rank 0"""
+    import torch.distributed as dist
+    from qasr_dist import run_shard, utterance_set
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    utts = utterance_set(37, seed=3)
+    calls = []
+
+    def transcribe(idx, max_tokens):
+        calls.append((list(idx), max_tokens))
+        return [[i * 1000 + k for k in range(max_tokens)] for i in idx]
+
+    res = run_shard(transcribe, utts, rank, world, batch=8, tok_rate=3.5, dist=dist)
+    q.put((rank, res["tokens"], res["wall_s"], sorted(res["local"]), calls))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_sharded_driver(world):
+    import math
+    import torch.multiprocessing as mp
+    from qasr_dist import utterance_set
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_driver_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=180) for _ in range(world)), key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    utts = utterance_set(37, seed=3)
+    want = {i: [i * 1000 + k for k in range(math.ceil(3.5 * n / 16000))] for i, (_, n) in enumerate(utts)}
+    assert res[0][1] == want and all(r[1] is None for r in res[1:])
+    assert len({r[2] for r in res}) == 1   # one max-over-ranks wall time
+    shards = [r[3] for r in res]
+    assert sorted(i for s in shards for i in s) == list(range(37))
+    for _, _, _, mine, calls in res:   # batches of <= 8, each decoded to its longest clip's budget
+        assert all(len(idx) <= 8 and mt == max(math.ceil(3.5 * utts[i][1] / 16000) for i in idx) for idx, mt in calls)
+        assert sorted(i for idx, _ in calls for i in idx) == mine

@@ -1,0 +1,131 @@
+"""GPU: the boundary's host-facing features beyond the hot path's numerics --
+per-token callback, --profile sections, staged pools run in subsets, the CLI's
+sharded --devices / --file-list mode, and the sharded bench driver."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import qasr
+
+pytestmark = pytest.mark.gpu
+SR = 16000
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "qwen3-asr.cpp_amd", "qwen3-asr-cli")
+
+
+@pytest.fixture(scope="module")
+def tiny(gpu, tiny_gguf):
+    m = qasr.Model(tiny_gguf)
+    c = qasr.Context(m, max_batch=4, max_ctx=256)
+    yield m, c
+    c.close()
+    m.close()
+
+
+def test_token_callback_is_per_token(tiny):
+    """src/qwen3_asr.cpp:255-291: called after every token, the prefill's
+    first, with the running count; the delivered ids are the result's."""
+    m, c = tiny
+    clips = [qasr.synth_pcm(31000 + i, (2 + i) * SR) for i in range(2)]
+    seen = {0: [], 1: []}
+    c.set_token_callback(lambda seq, n, tok: seen[seq].append((n, tok)))
+    try:
+        r = c.transcribe(clips, max_tokens=12, ignore_eos=True)
+    finally:
+        c.set_token_callback(None)
+    for b in range(2):
+        assert [n for n, _ in seen[b]] == list(range(1, 13))
+        assert [t for _, t in seen[b]] == r.tokens[b]
+    assert c.transcribe(clips, max_tokens=12, ignore_eos=True).tokens == r.tokens   # no callback: same ids
+
+
+def test_token_callback_stops_at_eos(tiny):
+    m, c = tiny
+    pcm = qasr.synth_pcm(31500, 2 * SR)
+    seen = []
+    c.set_token_callback(lambda seq, n, tok: seen.append(tok))
+    try:
+        r = c.transcribe([pcm], max_tokens=40)
+    finally:
+        c.set_token_callback(None)
+    eos = m.hp.eos_id
+    if seen and seen[-1] == eos:
+        assert seen[:-1] == r.tokens[0]   # trailing EOS popped from the result (src/qwen3_asr.cpp:298-300)
+    else:
+        assert seen == r.tokens[0] and len(seen) == 40
+
+
+def test_profile_sections(tiny):
+    m, c = tiny
+    c.set_profile(True)
+    try:
+        c.transcribe([qasr.synth_pcm(31600, 3 * SR)], max_tokens=9, ignore_eos=True)
+        rep = c.profile_report()
+    finally:
+        c.set_profile(False)
+    assert "TIMING PROFILE REPORT" in rep
+    rows = {ln.split()[0]: ln.split()[1:] for ln in rep.splitlines() if ln[:1].isalpha() and not ln.startswith("Section")}
+    for k in ("mel_spectrogram", "audio_encoding.total", "audio_encoding.conv_chunk", "audio_encoding.transformer",
+              "decode.initial_forward", "decode.token", "transcribe.total"):
+        assert k in rows, (k, rep)
+    assert int(rows["decode.token"][1]) == 8
+    assert float(rows["transcribe.total"][0]) > 0
+
+
+def test_staged_pool_subsets(tiny):
+    """qasr_run_staged: a pool larger than max_batch, run in subsets, gives
+    the same ids as each clip alone"""
+    m, c = tiny
+    clips = [qasr.synth_pcm(32000 + i, int((1.5 + 0.7 * i) * SR)) for i in range(6)]
+    alone = [c.transcribe([x], max_tokens=6, ignore_eos=True).tokens[0] for x in clips]
+    c.stage_audio(clips)
+    with pytest.raises(qasr.QasrError):
+        c.run(6, ignore_eos=True)   # 6 staged > max_batch 4
+    got = {}
+    for sub in ([0, 2], [5, 1, 3, 4]):
+        r = c.run_staged(sub, 6, ignore_eos=True)
+        got.update(zip(sub, r.tokens))
+    assert [got[i] for i in range(6)] == alone
+
+
+def test_cli_sharded_file_list(tiny, tmp_path, tiny_gguf):
+    """qwen3-asr-cli --devices / --file-list / --batch: outputs in input
+    order, identical to one file at a time; --profile prints the report"""
+    paths = []
+    for i in range(3):
+        p = str(tmp_path / f"c{i}.wav")
+        qasr.write_wav(p, qasr.synth_pcm(33000 + i, int((1.2 + i) * SR)))
+        paths.append(p)
+    lst = tmp_path / "list.txt"
+    lst.write_text("\n".join(paths) + "\n")
+    env = dict(os.environ, LD_LIBRARY_PATH=os.path.dirname(CLI))
+    one = []
+    for p in paths:
+        r = subprocess.run([CLI, "-m", tiny_gguf, "-f", p, "--max-tokens", "8", "--no-timing"], capture_output=True,
+                           text=True, env=env, timeout=120)
+        assert r.returncode == 0, r.stderr
+        one.append(r.stdout)
+    r = subprocess.run([CLI, "-m", tiny_gguf, "--devices", "0", "--file-list", str(lst), "--batch", "2",
+                        "--max-tokens", "8"], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout == "".join(one)
+    assert "Sharded timing" in r.stderr
+    r = subprocess.run([CLI, "-m", tiny_gguf, "-f", paths[0], "--max-tokens", "8", "--profile"], capture_output=True,
+                       text=True, env=env, timeout=120)
+    assert r.returncode == 0 and "TIMING PROFILE REPORT" in r.stderr and "decode.token" in r.stderr
+
+
+def test_bench_utterance_driver(gpu):
+    """bench.py --utterances (configs[3] driver) at a small size: every
+    utterance transcribed to its budget, one JSON line, strong scaling"""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--utterances", "24", "--utt-min", "2",
+                        "--utt-max", "6", "--batch", "8", "--steps", "1", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')][-1])
+    assert line["scaling"] == "strong" and line["n_gpus"] == 1 and line["config"]["utterances"] == 24
+    assert line["value"] > 0 and line["decode_tokens_per_s"] > 0

@@ -189,3 +189,34 @@ def test_full_fused_wait_timeout_is_an_error(full):
         assert c1.transcribe([pcm], max_tokens=4, ignore_eos=True).tokens == ref
     finally:
         c1.close()
+
+
+def test_full_two_threads_one_device(full):
+    """Contexts driven from two host threads on one GPU: the calls that can
+    take the fused batch-1 launches hold the device's lock (a fused launch
+    needs every CU), so both threads get the same ids as sequential runs and
+    no in-launch wait times out."""
+    import threading
+    m, _, _ = full
+    clips = [qasr.synth_pcm(16000 + i, 2 * SR) for i in range(2)]
+    ctxs = [qasr.Context(m, max_batch=1, max_ctx=256) for _ in range(2)]
+    try:
+        ref = [ctxs[i].transcribe([clips[i]], max_tokens=16, ignore_eos=True).tokens[0] for i in range(2)]
+        out, err = [None, None], []
+
+        def work(i):
+            try:
+                for _ in range(3):
+                    out[i] = ctxs[i].transcribe([clips[i]], max_tokens=16, ignore_eos=True).tokens[0]
+            except Exception as e:   # noqa: BLE001
+                err.append(e)
+        th = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not err, err
+        assert out == ref
+    finally:
+        for c in ctxs:
+            c.close()
