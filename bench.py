@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-seconds", type=float, default=10.0)
     ap.add_argument("--probe-layer", type=int, default=14, help="decoder layer whose fused launches are probed")
+    ap.add_argument("--fa-exact-decode", type=int, default=None, choices=(0, 1),
+                    help="decode attention numerics: 1 = ggml's fp16 V accumulation, 0 = fp32 accumulation (batch 1 "
+                         "takes the fused QKV + attention launch); default: the engine's (exact for Q8_0 only)")
     ap.add_argument("--cpu-threads", type=int, default=4, help="reference's effective ggml thread count")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--q8", action="store_true", help="Q8_0 synthetic model (configs[2] weights)")
@@ -160,7 +163,7 @@ def profiled_mfma():
 
 
 def roofline_entry(kind: int, batch: int, total_ms: float, n: int, bytes_per_launch: float, dev_ms: float, dev_n: int,
-                   layer: int) -> dict:
+                   layer: int, exact: bool = False) -> dict:
     """HBM roofline of one probed launch group: algorithmic bytes per launch
     (engine.hip probe_bytes: weights + the layer's K/V rows at each step's
     n_kv, averaged over the probed steps) / its mean duration.  Both clocks of
@@ -173,7 +176,11 @@ def roofline_entry(kind: int, batch: int, total_ms: float, n: int, bytes_per_lau
     avg_s = dev_ms / dev_n / 1e3 if dev_n else ev_s
     achieved = bytes_per_launch / avg_s / 1e9
     b1 = batch == 1
-    if kind == 2:
+    if kind == 2 and exact:
+        kname = ("decode layer QKV GEMV + decode_attn_exact_kernel (ggml fp16-accumulating attention), "
+                 "first start to last end" if b1 else "decode layer QKV projection + exact attention (kernel group)")
+        prefix = None
+    elif kind == 2:
         kname = ("qkv_attn1_kernel (batch 1: rmsnorm + QKV GEMV + split-K attention + o-proj, one launch)" if b1 else
                  "decode layer QKV projection + attention (kernel group)")
         prefix = "void qasr::qkv_attn1_kernel<" if b1 else None
@@ -348,6 +355,10 @@ def main():
     def align_all():
         for pcm, t in zip(clips, texts):
             actx.align_json(pcm, t)
+    if args.fa_exact_decode is not None:
+        ctx.set_option("fa_exact_decode", args.fa_exact_decode)
+    fx = ctx.get_option("fa_exact_decode")
+    exact = fx > 0 or (fx < 0 and args.q8)
     for _ in range(args.warmup):
         ctx.run(ntok, ignore_eos=True)
         if actx:
@@ -412,11 +423,14 @@ def main():
         "config": {"workload": workload(args, ntok, bool(actx)), "clips_per_gpu": args.batch,
                    "clip_seconds": args.seconds, "decode_tokens": ntok, "parallelism": f"dp{N} (utterance sharding)"},
         "decode_tokens_per_s": round(N * args.batch * ntok * args.steps / dt, 2),
+        "decode_attention": "fp16 V accumulation per key (ggml CPU flash-attention numerics)" if exact else
+                            "fp32 V accumulation (split-K)",
         "stage_ms_per_step_rank0": {k: round(v / args.steps, 3) for k, v in tm.items()},
     }
     if probe and probe[1]:
-        out["roofline"] = roofline_entry(2, args.batch, *probe, args.probe_layer)
-        out["roofline_other"] = [roofline_entry(k, args.batch, *v, args.probe_layer) for k, v in extra.items() if v[1]]
+        out["roofline"] = roofline_entry(2, args.batch, *probe, args.probe_layer, exact)
+        out["roofline_other"] = [roofline_entry(k, args.batch, *v, args.probe_layer, exact) for k, v in extra.items()
+                                 if v[1]]
     # the north-star fractions of the two stages: encoder
     # FLOPs against the dense fp16 MFMA peak, decode bytes against HBM
     enc_s = tm["encode"] / args.steps / 1e3

@@ -268,6 +268,34 @@ static float dot_f16(const uint16_t *x, const uint16_t *y, int n) {
 #endif
 }
 
+/* ggml_vec_mad_f16: y = fp16(fma(x, v, y)) per element (F16C: 8 lanes
+ * cvtph -> fmadd -> cvtps RNE; the scalar tail the same ops one at a time) */
+static void vec_mad_f16(uint16_t *y, const uint16_t *x, int n, float v) {
+    int i = 0;
+#ifdef QO_SIMD
+    const __m256 vv = _mm256_set1_ps(v);
+    for (; i + 8 <= n; i += 8) {
+        const __m256 a = _mm256_cvtph_ps(_mm_loadu_si128((const __m128i *)(y + i)));
+        const __m256 b = _mm256_cvtph_ps(_mm_loadu_si128((const __m128i *)(x + i)));
+        _mm_storeu_si128((__m128i *)(y + i), _mm256_cvtps_ph(_mm256_fmadd_ps(b, vv, a), _MM_FROUND_TO_NEAREST_INT));
+    }
+#endif
+    for (; i < n; i++) y[i] = qo_f32_to_f16(fmaf(qo_f16_to_f32(x[i]), v, qo_f16_to_f32(y[i])));
+}
+
+/* ggml_vec_scale_f16: y = fp16(y * v) */
+static void vec_scale_f16(uint16_t *y, int n, float v) {
+    int i = 0;
+#ifdef QO_SIMD
+    const __m256 vv = _mm256_set1_ps(v);
+    for (; i + 8 <= n; i += 8) {
+        const __m256 a = _mm256_cvtph_ps(_mm_loadu_si128((const __m128i *)(y + i)));
+        _mm_storeu_si128((__m128i *)(y + i), _mm256_cvtps_ph(_mm256_mul_ps(a, vv), _MM_FROUND_TO_NEAREST_INT));
+    }
+#endif
+    for (; i < n; i++) y[i] = qo_f32_to_f16(qo_f16_to_f32(y[i]) * v);
+}
+
 /* ggml_vec_dot_f32 (fp32 x fp32, fp32 lanes) */
 static float dot_f32(const float *x, const float *y, int n) {
     float acc[16] = {0};
@@ -769,12 +797,12 @@ static float *dec_stack(qo_dec *dd, const int32_t *tokens, int n_tokens, const f
                         M = s;
                         ms = expf(Mold - M);
                         if (dd->flags & QO_FA_V_F32) for (int d = 0; d < HD; d++) acc32[d] *= ms;
-                        else for (int d = 0; d < HD; d++) acc16[d] = qo_f32_to_f16(qo_f16_to_f32(acc16[d]) * ms);
+                        else vec_scale_f16(acc16, HD, ms);
                     } else {
                         vs = expf(s - M);
                     }
                     if (dd->flags & QO_FA_V_F32) for (int d = 0; d < HD; d++) acc32[d] += qo_f16_to_f32(vr[d]) * vs;
-                    else for (int d = 0; d < HD; d++) acc16[d] = qo_f32_to_f16(fmaf(qo_f16_to_f32(vr[d]), vs, qo_f16_to_f32(acc16[d])));
+                    else vec_mad_f16(acc16, vr, HD, vs);
                     S = S * ms + vs;
                 }
                 if (!(dd->flags & QO_FA_V_F32)) for (int d = 0; d < HD; d++) acc32[d] = qo_f16_to_f32(acc16[d]);

@@ -160,8 +160,12 @@ __global__ __launch_bounds__(256) void qkv_post_kernel(QkvPostArgs a) {
         const int g = hh - nh - nkv;
         const float *v = src + QD + KD + g * 128;
         uint16_t *dst = a.vc + (((long)seq * nkv + g) * a.max_ctx + pos) * 128;
-        dst[lane] = f_to_u16(v[lane]);
-        dst[lane + 64] = f_to_u16(v[lane + 64]);
+        const uint16_t v0 = f_to_u16(v[lane]), v1 = f_to_u16(v[lane + 64]);
+        dst[lane] = v0;
+        dst[lane + 64] = v1;
+        uint16_t *t = a.vt + ((long)seq * nkv + g) * 128 * vt_ctx(a.max_ctx);
+        t[vt_index(pos, lane)] = v0;
+        t[vt_index(pos, lane + 64)] = v1;
         return;
     }
     const bool isq = hh < nh;
@@ -432,11 +436,12 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
             const int key = min(k0 + wid * (SPL / DWAVES) + 16 * t + c16, a.max_ctx - 1);
             kk[t][s4] = *(const half8 *)(kc + (long)key * 128 + 32 * s4 + 8 * q4);
         }
+    if (!a.scores)   // scores mode reads no V
 #pragma unroll
-    for (int i = 0; i < KPW; i++) {
-        const int key = min(k0 + wid * (SPL / DWAVES) + i * 4 + sub, a.max_ctx - 1);
-        vv[i] = *(const half8 *)(vc + (long)key * 128 + dl);
-    }
+        for (int i = 0; i < KPW; i++) {
+            const int key = min(k0 + wid * (SPL / DWAVES) + i * 4 + sub, a.max_ctx - 1);
+            vv[i] = *(const half8 *)(vc + (long)key * 128 + dl);
+        }
     // No exit test on the position anywhere: with one, hipcc hoists the
     // dependent pos load and the test in front of the K/V requests (two memory
     // latencies in series).  The host sizes the grid to the context
@@ -495,6 +500,9 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
         vnew[lane] = v0; vnew[lane + 64] = v1;
         vc[(long)pos * 128 + lane] = v0;
         vc[(long)pos * 128 + lane + 64] = v1;
+        uint16_t *t = a.vt + ((long)b * a.n_kv_head + g) * 128 * vt_ctx(a.max_ctx);
+        t[vt_index(pos, lane)] = v0;
+        t[vt_index(pos, lane + 64)] = v1;
     }
     __syncthreads();
     // ---- scores S = Q K^T on MFMA: A = the two q heads (rows 0, 1; rows 2-15
@@ -527,6 +535,16 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     }
     __syncthreads();
     mark(6);
+    if constexpr (!FUSED) {
+        if (a.scores) {   // front half of the exact attention (fa_exact.hip): this split's scaled scores
+            float *dst = a.scores + ((long)b * a.n_head + 2 * g) * a.max_ctx + k0;
+            for (int i = tid; i < 2 * SPL; i += 256) {
+                const int hh = i / SPL, j = i - hh * SPL;
+                if (k0 + j < k1) dst[(long)hh * a.max_ctx + j] = sc[hh][j];
+            }
+            return;
+        }
+    }
     // ---- split-local softmax statistics: wave h owns head h, lane = key (mod 64)
     if (wid < 2) {
         constexpr int KL = SPL / 64;

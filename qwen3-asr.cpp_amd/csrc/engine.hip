@@ -96,6 +96,7 @@ struct qasr_ctx {
     hipStream_t st = nullptr;
     hipEvent_t ev[8] = {};
     uint16_t *kc = nullptr, *vc = nullptr;
+    uint16_t *vt = nullptr;        // V^T cache (kernels.h vt_ctx): the exact decode attention's V
     float *rope = nullptr;
     std::vector<DevBuf> owned;     // everything hipMalloc'ed by the context
     // grow-on-demand scratch
@@ -111,6 +112,7 @@ struct qasr_ctx {
     int32_t *d_tok = nullptr, *d_hist = nullptr;
     int *d_pos = nullptr, *d_nkv = nullptr, *d_slot = nullptr, *d_step = nullptr;
     float *d_x = nullptr, *d_qkv = nullptr, *d_part = nullptr, *d_logits = nullptr;
+    float *d_scores = nullptr;     // exact decode attention: [B][n_head][max_ctx] scaled scores
     unsigned int *d_counter = nullptr, *d_done = nullptr;
     unsigned int *d_qcnt = nullptr;   // fused batch-1 QKV + attention: QKV-block arrivals per kv group
     unsigned int *d_attdone = nullptr;   // fused batch-1 o-proj: combiner arrivals (8 replicas)
@@ -196,6 +198,8 @@ static const std::vector<FuseOption> &fuse_options() {
         {"ffn_wdelay", "QASR_FFN_WDELAY", &FuseCfg::ffn_wdelay}, {"qkv_delay", "QASR_FUSE_DELAY", &FuseCfg::qkv_delay},
         {"o_delay", "QASR_FUSE_ODELAY", &FuseCfg::o_delay},    {"att_spl1", "QASR_ATT_SPL1", &FuseCfg::spl1},
         {"poll_limit", "QASR_POLL_LIMIT", &FuseCfg::poll_limit}, {"handoff_fence", "QASR_HANDOFF_FENCE", &FuseCfg::fence},
+        {"fa_exact_prefill", "QASR_FA_EXACT_PREFILL", &FuseCfg::fa_exact_prefill},
+        {"fa_exact_decode", "QASR_FA_EXACT_DECODE", &FuseCfg::fa_exact_decode},
     };
     return v;
 }
@@ -232,7 +236,17 @@ static std::mutex &device_lock(int device) {
     static std::mutex m[64];
     return m[(unsigned)device % 64];
 }
-static bool takes_fused(const qasr_ctx *c, int B) { return B == 1 && !c->m->q8 && (c->fuse.ffn || c->fuse.qkv); }
+// decode attention with ggml's fp16 V accumulation (fa_exact.hip)?
+static bool exact_decode(const qasr_ctx *c) {
+    return c->fuse.fa_exact_decode > 0 || (c->fuse.fa_exact_decode < 0 && c->m->q8);
+}
+// V^T cache elements of one layer
+static size_t layer_vt(const qasr_ctx *c) {
+    return (size_t)c->max_batch * c->m->hp.n_kv_head * 128 * vt_ctx(c->max_ctx);
+}
+static bool takes_fused(const qasr_ctx *c, int B) {
+    return B == 1 && !c->m->q8 && (c->fuse.ffn || (c->fuse.qkv && !exact_decode(c)));
+}
 
 // a roctx range for the lifetime of the object (rocprofv3 --marker-trace)
 struct RoctxRange {
@@ -610,9 +624,13 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
     const Hparams &hp = m->hp;
-    const size_t kv = (size_t)hp.dec_layers * max_batch * hp.n_kv_head * max_ctx * 128;
+    // + padding rows: fa_exact.hip's chains read V a few batches past the context
+    const size_t kv = (size_t)hp.dec_layers * max_batch * hp.n_kv_head * max_ctx * 128 + kKvPadRows * 128;
     int rc = 0;
     if ((rc = dev_alloc(c.get(), (void **)&c->kc, kv * 2)) || (rc = dev_alloc(c.get(), (void **)&c->vc, kv * 2))) return rc;
+    const size_t vt = (size_t)hp.dec_layers * layer_vt(c.get());
+    if ((rc = dev_alloc(c.get(), (void **)&c->vt, vt * 2))) return rc;
+    HIPCHK(hipMemset(c->vt, 0, vt * 2));
     std::vector<float> rope;
     rope_table(rope, max_ctx, 128, hp.rope_theta);
     if ((rc = dev_alloc(c.get(), (void **)&c->rope, rope.size() * 4))) return rc;
@@ -653,6 +671,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_x32, (size_t)B * std::max(QD, std::max(hp.hidden, hp.dec_ffn)) * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_part, (size_t)B * hp.n_kv_head * c->max_splits * 2 * 132 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_counter, (size_t)B * hp.n_kv_head * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_scores, (size_t)B * hp.n_head * max_ctx * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_qcnt, (size_t)hp.n_kv_head * 8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_attdone, (size_t)8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_ffncnt, (size_t)hp.dec_layers * 512 * 4)) ||
@@ -992,12 +1011,14 @@ static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const st
         qa.q_norm = L.q_norm; qa.k_norm = L.k_norm; qa.eps = hp.rms_eps; qa.rope = c->rope;
         qa.n_head = hp.n_head; qa.n_kv_head = hp.n_kv_head; qa.q_out = c->pq.as<uint16_t>();
         qa.kc = c->kc + l * layer_kv; qa.vc = c->vc + l * layer_kv; qa.max_ctx = c->max_ctx;
+        qa.vt = c->vt + l * layer_vt(c);
         launch_qkv_post(qa, s);
         PrefillAttnArgs pa{};
         pa.q = c->pq.as<uint16_t>(); pa.kc = qa.kc; pa.vc = qa.vc; pa.seq_row0 = d_srow0; pa.seq_len = d_slen;
         pa.seq_slot = d_sslot; pa.n_seq = B; pa.max_len = maxp; pa.n_head = hp.n_head; pa.n_kv_head = hp.n_kv_head;
         pa.max_ctx = c->max_ctx; pa.scale = 1.0f / sqrtf(128.0f); pa.out = c->patt.as<uint16_t>(); pa.out32 = x32;
-        launch_prefill_attention(pa, s);
+        if (c->fuse.fa_exact_prefill) launch_prefill_attention_exact(pa, s);   // ggml CPU FA numerics
+        else launch_prefill_attention(pa, s);
         GemmArgs o{};
         o.M = rows; o.N = H; o.K = QD; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
         if (q8) gemm_q8(c, EPI_F32, o, x32, nullptr, QD, 0, L.wo, L.wo_d, s);
@@ -1106,6 +1127,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         DecodeAttnArgs da{};
         da.qkv = c->d_qkv; da.q_norm = L.q_norm; da.k_norm = L.k_norm; da.eps = hp.rms_eps; da.rope = c->rope;
         da.pos = c->d_pos; da.kc = c->kc + l * layer_kv; da.vc = c->vc + l * layer_kv; da.seq_slot = c->d_slot; da.B = B;
+        da.vt = c->vt + l * layer_vt(c);
         da.n_head = hp.n_head; da.n_kv_head = hp.n_kv_head; da.max_ctx = c->max_ctx; da.max_splits = c->max_splits; da.grid_splits = splits;
         da.scale = 1.0f / sqrtf(128.0f); da.part = c->d_part; da.counter = c->d_counter; da.out = c->d_att;
         da.out32 = q8 && skinny ? c->d_att32 : nullptr;
@@ -1130,7 +1152,8 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             q1.trace = tr(0);
             q1.stamp = stamp;
         }
-        const bool fusable = skinny && B == 1 && !q8 && !skip;
+        const bool exact = exact_decode(c);
+        const bool fusable = skinny && B == 1 && !q8 && !skip && !exact;
         if (fusable) da.att_done = c->d_attdone;
         // 0 = separate launches, 1 = QKV + attention, 2 = + o-projection (decided without launching)
         const int fmode = fusable ? launch_qkv_attention1(q1, da, &o, c->fuse, s, true) : 0;
@@ -1154,7 +1177,14 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
                     }
                 }
                 da.att_done = nullptr;
-                if (!(skip & 2)) launch_decode_attention(da, s);
+                if (skip & 2) {
+                } else if (exact) {   // ggml CPU FA numerics: scores by the splits, then the in-order chain
+                    da.scores = c->d_scores;
+                    launch_decode_attention(da, s);
+                    launch_decode_attention_exact(da, s);
+                } else {
+                    launch_decode_attention(da, s);
+                }
             }
         }
         if (!gb) continue;

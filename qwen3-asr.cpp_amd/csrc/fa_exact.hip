@@ -1,0 +1,502 @@
+// fa_exact.hip -- decoder attention with ggml's CPU flash-attention numerics.
+//
+// ggml_flash_attn_ext on the CPU backend (the reference's Linux path,
+// src/text_decoder.cpp:534-540; SURVEY.md §8(a) viii) walks the keys of one
+// query row in order: s = (fp16 q . fp16 k) * scale; a new maximum rescales
+// the fp16 V accumulator (ggml_vec_scale_f16: y = fp16(y * ms)), every key
+// adds v * vs into it (ggml_vec_mad_f16: y = fp16(fma(v, vs, y))), and
+// S = S * ms + vs in fp32; the output is fp32(acc) * (1 / S).  The fp16
+// rounding after every key makes the result order-dependent: it cannot be
+// split over keys, so each (query, head, dimension) is one sequential chain.
+// At a 1.2k-token prompt that rounding moves the attention output by ~1 % of
+// its scale against an fp32 accumulator (tests/test_gpu_full.py, configs[1]).
+//
+// Reproduced exactly: the chain -- the running maximum and each key's
+// (ms, vs) (a prefix maximum is exact, so a wave scan gives the sequential
+// loop's values) and every fp16 rounding of the accumulator, in key order.
+// Not reproduced: the scores' fp32 summation order (MFMA vs
+// ggml_vec_dot_f16) and S, summed here in parallel as sum_k exp(s_k - M) (the
+// sequential S * ms + vs up to fp32 rounding, ~1e-7 relative) -- both far
+// below the fp16 accumulator's own rounding.
+//
+// The chain step is v_fma_mix_f32 (fp16 v and accumulator, fp32 vs, one fp32
+// rounding) and then an fp16 conversion.  LLVM folds fptrunc(fma) into
+// v_fma_mixlo_f16, which rounds once, straight to fp16 (dev_common.h rn32).
+// A pair of values converted as a vector becomes v_cvt_pk_f16_f32 and does not
+// fold (this file is built with -fno-slp-vectorize, so the two fmas stay mix
+// instructions on the fp16 halves instead of one v_pk_fma_f32 behind four
+// conversions); the single-value form converts in inline asm.
+//
+// Prefill: one workgroup = 16 query rows of one head (one MFMA column each);
+// keys in chunks of PX_KC: (1) scores on MFMA -> LDS, (2) per row the (ms, vs)
+// weights by wave scans -> LDS, (3) the chain, wave w running rows 2w, 2w + 1
+// with two dimensions per lane, V staged in LDS once for all rows.
+// Decode: launch_decode_attention in scores mode writes the scaled scores;
+// then one workgroup per (query head, sequence): both waves derive the
+// weights, each runs the chain for 64 dimensions, one per lane (the shortest
+// per-key latency: v_fma_mix_f32, one wait state, v_cvt_f16_f32), V from the
+// V^T cache copy (kernels.h vt_ctx) in 16-B loads of 8 keys.
+//
+// Measured per-key costs (tools/micro/chain_lat.hip, one wave): fp32 fma
+// chain 9.8 cycles, one dimension 13.3, two dimensions 14.0, four rows x two
+// dimensions 62 -- a wave issues a VALU instruction every ~5 cycles, and
+// more waves per SIMD do not slow each other.
+#include "dev_common.h"
+#include "kernels.h"
+
+namespace qasr {
+
+#define PX_ROWS 16   // prefill query rows per workgroup
+#define PX_KC 128    // prefill keys per chunk
+#define FX_B 16      // chain batch: keys whose V and weights are in registers together
+
+// ggml_vec_mad_f16 on two dimensions packed in one dword: fp16(fma(v, vs, acc))
+__device__ __forceinline__ half2v fx_mad2(half2v acc, uint32_t v, float vs) {
+    const half2v vv = __builtin_bit_cast(half2v, v);
+    const float f0 = fmaf((float)vv.x, vs, (float)acc.x);
+    const float f1 = fmaf((float)vv.y, vs, (float)acc.y);
+    return __builtin_convertvector((floatx2){f0, f1}, half2v);
+}
+// ggml_vec_scale_f16: fp16(acc * ms)
+__device__ __forceinline__ half2v fx_scale2(half2v acc, float ms) {
+    return __builtin_convertvector((floatx2){(float)acc.x * ms, (float)acc.y * ms}, half2v);
+}
+// one value: the conversion in asm (a scalar fptrunc would fold into mixlo)
+__device__ __forceinline__ f16 fx_cvt(float f) {
+    f16 h;
+    asm("v_cvt_f16_f32 %0, %1" : "=v"(h) : "v"(f));
+    return h;
+}
+__device__ __forceinline__ f16 fx_mad1(f16 acc, uint16_t v, float vs) {
+    return fx_cvt(fmaf((float)__builtin_bit_cast(f16, v), vs, (float)acc));
+}
+
+// DPP lane move with -inf where the source lane is out of range or its row
+// is masked off (bound_ctrl off: the lane keeps the -inf of `old`)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_ninf(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, -INFINITY), __builtin_bit_cast(int, v),
+                                                                 CTRL, ROWS, 0xF, false));
+}
+// inclusive prefix maximum over the 64 lanes, all in VALU DPP: Hillis-Steele
+// in each 16-lane row (row_shr 1, 2, 4, 8), then row_bcast:15 (each row's
+// last lane into the next row) and row_bcast:31 (lane 31 into rows 2, 3)
+__device__ __forceinline__ float wave_scan_max(float x) {
+    x = fmaxf(x, dpp_ninf<0x111, 0xF>(x));
+    x = fmaxf(x, dpp_ninf<0x112, 0xF>(x));
+    x = fmaxf(x, dpp_ninf<0x114, 0xF>(x));
+    x = fmaxf(x, dpp_ninf<0x118, 0xF>(x));
+    x = fmaxf(x, dpp_ninf<0x142, 0xA>(x));
+    x = fmaxf(x, dpp_ninf<0x143, 0xC>(x));
+    return x;
+}
+
+// Weights of n keys (n <= KPL * 64) of one row, one wave: src[j] = the scaled
+// score (src may be sc itself), sc[j] = vs_j on return, ms[j] = ms_j (1 where no new
+// maximum; a masked key (-inf) gives vs = 0, ms = 1 -- ggml skips it, and a
+// zero weight leaves the fp16 accumulator unchanged); fl[b * fls] = 1 where
+// batch b (FX_B keys) holds a new maximum.  M: running maximum (in/out);
+// S: rescaled to the new maximum, plus this chunk's sum.
+template <int KPL>
+__device__ __forceinline__ void fx_weights(const float *src, float *sc, float *ms, uint32_t *fl, int fls, int n, float &M,
+                                           float &S) {
+    const int lane = threadIdx.x & 63;
+    float v[KPL];
+    float lm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < KPL; i++) {   // independent loads (src: LDS, or the scores in global memory)
+        const int j = lane * KPL + i;
+        v[i] = j < n ? src[j] : -INFINITY;
+    }
+#pragma unroll
+    for (int i = 0; i < KPL; i++) lm = fmaxf(lm, v[i]);
+    const float inc = wave_scan_max(lm);   // inclusive prefix maximum over the lanes
+    float Mp = fmaxf(M, dpp_ninf<0x138, 0xF>(inc));   // wave_shr:1 -> the exclusive prefix (lane 0: -inf)
+    bool nm = false;
+#pragma unroll
+    for (int i = 0; i < KPL; i++) {
+        const int j = lane * KPL + i;
+        const float s = v[i];
+        float m1 = 1.0f, w = 0.0f;
+        if (s > Mp) {   // new maximum: ms = expf(Mold - M) (0 before the first key), vs = 1
+            m1 = expf(Mp - s);
+            w = 1.0f;
+            Mp = s;
+            nm = true;
+        } else if (s != -INFINITY) {
+            w = expf(s - Mp);
+        }
+        if (j < n) {
+            sc[j] = w;
+            ms[j] = m1;
+        }
+    }
+    const float Mn = fmaxf(M, lane_f(inc, 63));
+    float ps = 0.0f;
+#pragma unroll
+    for (int i = 0; i < KPL; i++) ps += v[i] == -INFINITY ? 0.0f : expf(v[i] - Mn);
+    ps = wave_sum(ps);
+    S = (M == -INFINITY ? 0.0f : S * expf(M - Mn)) + ps;
+    M = Mn;
+    constexpr int LPB = FX_B / KPL;   // lanes per batch
+    const unsigned long long bal = __ballot(nm);
+    if (lane % LPB == 0 && lane * KPL < n) {
+        const unsigned long long grp = (bal >> lane) & ((1ull << LPB) - 1ull);
+        fl[(lane / LPB) * fls] = grp != 0ull;
+    }
+}
+
+// One batch of FX_B keys for R rows, two dimensions per lane: v[i] = the
+// lane's V dword of key j0 + i; row r's weights at vs / ms + r * ld + j0.  The
+// fast path (a full batch, no new maximum in any of the rows) is three VALU
+// instructions per row and key; a batch with a new maximum scales every key
+// (ggml_vec_scale_f16 runs only on a new maximum, but ms = 1 is exact).
+template <int R>
+__device__ __forceinline__ void fx_batch2(const uint32_t *v, const float *vs, const float *ms, int ld, int j0, int nb,
+                                          uint32_t any, half2v *acc) {
+    if (nb == FX_B && !any) {
+#pragma unroll
+        for (int i = 0; i < FX_B; i++)
+#pragma unroll
+            for (int r = 0; r < R; r++) acc[r] = fx_mad2(acc[r], v[i], vs[r * ld + j0 + i]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < FX_B; i++) {
+            if (i < nb) {
+#pragma unroll
+                for (int r = 0; r < R; r++) {   // ms = 1 scales exactly (an fp16 value times 1, rounded to fp16)
+                    acc[r] = fx_scale2(acc[r], ms[r * ld + j0 + i]);
+                    acc[r] = fx_mad2(acc[r], v[i], vs[r * ld + j0 + i]);
+                }
+            }
+        }
+    }
+}
+// the chain over keys [0, n) of a chunk for R rows, V from the chunk's LDS
+// image (vl = this lane's dword of key 0, 64 dwords per key); row r's batch
+// flags at fl[b * PX_ROWS + r]
+template <int R>
+__device__ __forceinline__ void fx_chain2(const uint32_t *vl, int n, const float *vs, const float *ms, int ld,
+                                          const uint32_t *fl, half2v *acc) {
+    for (int j0 = 0; j0 < n; j0 += FX_B) {
+        uint32_t v[FX_B];
+#pragma unroll
+        for (int i = 0; i < FX_B; i++) v[i] = vl[(j0 + i) * 64];   // rows past n: staged padding, unused
+        uint32_t any = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) any |= fl[(j0 / FX_B) * PX_ROWS + r];
+        fx_batch2<R>(v, vs, ms, ld, j0, min(FX_B, n - j0), __builtin_amdgcn_readfirstlane(any), acc);
+    }
+}
+
+// FX_STAMPS (tools/micro/fx_bench.hip only): per-workgroup phase cycles of the
+// prefill kernel, wave 0: [start, end, scores, weights, chain, chunks]
+#ifdef FX_STAMPS
+__device__ unsigned long long fx_stamps[1 << 16][8];
+#define FX_CLK(v) const unsigned long long v = clock64()
+#define FX_ADD(i, d) tsum[i] += (d)
+#else
+#define FX_CLK(v)
+#define FX_ADD(i, d)
+#endif
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+// ------------------------------------------------------------------ prefill
+// grid (ceil(max_len / 16), n_head, n_seq), block 512: rows q0 .. q0 + 15,
+// longest rows first; wave w owns rows 2w, 2w + 1 (two rows a wave: the chain
+// is issue-bound at ~5 cycles an instruction per wave, so fewer rows per wave
+// shorten the longest workgroups, which bound the launch).  Per chunk the V
+// rows go global -> LDS by LDS-DMA (global_load_lds_dwordx4, issued first,
+// landing while the scores and weights are computed): one copy serves all
+// 16 rows.
+#define PX_SCS (PX_KC + 4)   // score row stride (floats): the MFMA writes of 16 rows hit 16 banks
+#define PX_W 8               // waves per workgroup
+#define PX_R (PX_ROWS / PX_W)
+__global__ __launch_bounds__(64 * PX_W) void prefill_attn_exact_kernel(PrefillAttnArgs a) {
+    __shared__ __attribute__((aligned(16))) float sc[PX_ROWS][PX_SCS];   // scores, then vs
+    __shared__ __attribute__((aligned(16))) float msw[PX_ROWS][PX_SCS];
+    __shared__ __attribute__((aligned(16))) uint32_t fl[PX_KC / FX_B][PX_ROWS];
+    __shared__ __attribute__((aligned(16))) uint32_t vsh[PX_KC * 64];    // the chunk's V rows
+    const int sq = blockIdx.z, h = blockIdx.y;
+    const int L = a.seq_len[sq];
+    const int nqb = (a.max_len + PX_ROWS - 1) / PX_ROWS;
+    const int q0 = (nqb - 1 - (int)blockIdx.x) * PX_ROWS;
+    if (q0 >= L) return;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int g = lane >> 4, ql = lane & 15;
+    const int hk = h / (a.n_head / a.n_kv_head);
+    const int row0 = a.seq_row0[sq];
+    const int QD = a.n_head * 128;
+    const long cbase = ((long)a.seq_slot[sq] * a.n_kv_head + hk) * a.max_ctx;
+    const uint16_t *kc = a.kc + cbase * 128, *vc = a.vc + cbase * 128;
+    // B fragment of query column ql (row q0 + ql; zero past the sequence)
+    half8 qf[4];
+    const bool qv = q0 + ql < L;
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+        qf[s] = qv ? *(const half8 *)(a.q + (long)(row0 + q0 + ql) * QD + h * 128 + 32 * s + 8 * g) : half8{};
+    const int lim = qv ? q0 + ql : -1;   // causal: keys <= the query's position
+    const int kend = min(L, q0 + PX_ROWS);
+    const int r0 = PX_R * wid;                           // this wave's first row
+    const int wlast = min(L - 1, q0 + r0 + PX_R - 1);    // its last key (its longest row)
+    float M[PX_R], S[PX_R];
+    half2v acc[PX_R];
+#pragma unroll
+    for (int r = 0; r < PX_R; r++) {
+        M[r] = -INFINITY;
+        S[r] = 0.0f;
+        acc[r] = half2v{0, 0};
+    }
+#ifdef FX_STAMPS
+    unsigned long long tsum[4] = {0, 0, 0, 0};
+    FX_CLK(tk0);
+#endif
+    for (int c0 = 0; c0 < kend; c0 += PX_KC) {
+        const int n = min(PX_KC, kend - c0);
+        __syncthreads();   // the previous chunk's chains are done with sc / msw / fl / vsh
+        FX_CLK(ta);
+        // V rows c0 .. c0 + PX_KC - 1 -> LDS: 1 KiB (4 rows) per wave-instruction
+#pragma unroll
+        for (int it = wid; it < PX_KC / 4; it += PX_W)
+            __builtin_amdgcn_global_load_lds((glb_void *)(vc + (long)(c0 + 4 * it + (lane >> 4)) * 128 + 8 * (lane & 15)),
+                                             (lds_void *)(vsh + it * 256), 16, 0, 0);
+        // (1) scores: 16-key tile t = wid
+        {
+            const int t = wid;
+            const int key = min(c0 + t * 16 + ql, kend - 1);
+            half8 kf[4];
+#pragma unroll
+            for (int s = 0; s < 4; s++) kf[s] = *(const half8 *)(kc + (long)key * 128 + 32 * s + 8 * g);
+            if (t * 16 < n) {
+                floatx4 sacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < 4; s++) sacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], qf[s], sacc, 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 4; i++) {   // C row = key 4g + i of the tile, column = query ql
+                    const int k = c0 + t * 16 + 4 * g + i;
+                    sc[ql][t * 16 + 4 * g + i] = k <= lim ? sacc[i] * a.scale : -INFINITY;
+                }
+            }
+        }
+        __syncthreads();
+        FX_CLK(tb);
+        FX_ADD(0, tb - ta);
+        // (2) weights of the wave's rows
+#pragma unroll
+        for (int r = 0; r < PX_R; r++)
+            fx_weights<PX_KC / 64>(sc[r0 + r], sc[r0 + r], msw[r0 + r], &fl[0][r0 + r], PX_ROWS, n, M[r], S[r]);
+        __syncthreads();   // (the V image has landed: the barrier drains the LDS-DMA)
+        FX_CLK(tc);
+        FX_ADD(1, tc - tb);
+        // (3) the chain, up to the wave's longest row (a shorter row sees zero weights)
+        const int nw = min(n, wlast + 1 - c0);
+        if (nw > 0) fx_chain2<PX_R>(vsh + lane, nw, sc[r0], msw[r0], PX_SCS, &fl[0][r0], acc);
+        FX_CLK(td);
+        FX_ADD(2, td - tc);
+        FX_ADD(3, 1);
+    }
+#ifdef FX_STAMPS
+    if (tid == 0) {
+        unsigned long long *st = fx_stamps[blockIdx.x + gridDim.x * blockIdx.y];
+        st[0] = tk0;
+        st[1] = clock64();
+        for (int i = 0; i < 4; i++) st[2 + i] = tsum[i];
+        st[6] = q0;
+    }
+#endif
+#pragma unroll
+    for (int r = 0; r < PX_R; r++) {
+        const int q = q0 + r0 + r;
+        if (q >= L) continue;
+        const float inv = S[r] == 0.0f ? 0.0f : 1.0f / S[r];
+        const float o0 = (float)acc[r].x * inv, o1 = (float)acc[r].y * inv;
+        const long o = (long)(row0 + q) * QD + h * 128 + 2 * lane;
+        if (a.out32) {
+            a.out32[o] = o0;
+            a.out32[o + 1] = o1;
+        } else {
+            *(uint32_t *)(a.out + o) = (uint32_t)f_to_u16(o0) | ((uint32_t)f_to_u16(o1) << 16);
+        }
+    }
+}
+
+void launch_prefill_attention_exact(const PrefillAttnArgs &a, hipStream_t s) {
+    if (a.n_seq <= 0 || a.max_len <= 0) return;
+    dim3 grid((a.max_len + PX_ROWS - 1) / PX_ROWS, a.n_head, a.n_seq);
+    hipLaunchKernelGGL(prefill_attn_exact_kernel, grid, dim3(64 * PX_W), 0, s, a);
+}
+
+// ------------------------------------------------------------------- decode
+// The chain for one row, one dimension per lane, V from the V^T cache (this
+// lane's dimension: 8 keys per 16-B load, a wave's loads 1 KiB contiguous).
+// No LDS: each wave derives the whole chunk's weights itself, lane L holding
+// keys 32 L .. 32 L + 31 in registers, and the chain takes key k's weight
+// with v_readlane (an SGPR operand of v_fma_mix_f32, in the slot the mix ->
+// convert dependency leaves empty).  Measured alternatives that lost (tools/
+// micro/fx_bench.hip): weights read from LDS just in time (~15 cycles a key
+// of exposed latency), V prefetched through a four-slot register ring (the
+// loop-carried wait counts came out vmcnt(0)) or an LDS-DMA ring (~60 cycles
+// of issue per 1 KiB piece).
+#define DX_B 32    // keys per lane of the weights = keys sharing one fast/slow decision
+#define DX_Q 64    // keys of V per register buffer (two in turn)
+__device__ __forceinline__ uint16_t fx_elem(const u32x4 *v, int i) {   // key i of the step (i constant)
+    const uint32_t w = v[i >> 3][(i >> 1) & 3];
+    return (uint16_t)((i & 1) ? (w >> 16) : (w & 0xffffu));
+}
+__device__ __forceinline__ float fx_lane(float x, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+}
+// keys [j0, j0 + DX_Q) of the chunk from registers v; w / m: the weights
+// registers (key 32 L + i in lane L, element i); flags: bit L = a new maximum
+// among lane L's keys
+__device__ __forceinline__ void fx_step1(const u32x4 *v, int j0, int n, const float *w, const float *m,
+                                         unsigned long long flags, f16 &acc) {
+#pragma unroll
+    for (int bq = 0; bq < DX_Q / DX_B; bq++) {
+        const int jb = j0 + bq * DX_B;
+        const int L = jb / DX_B;
+        const int nb = min(DX_B, n - jb);
+        if (nb == DX_B && !((flags >> L) & 1ull)) {
+#pragma unroll
+            for (int i = 0; i < DX_B; i++) acc = fx_mad1(acc, fx_elem(v, bq * DX_B + i), fx_lane(w[i], L));
+        } else if (nb > 0) {
+#pragma unroll
+            for (int i = 0; i < DX_B; i++) {
+                if (i < nb) {
+                    acc = fx_cvt((float)acc * fx_lane(m[i], L));   // ms = 1: exact
+                    acc = fx_mad1(acc, fx_elem(v, bq * DX_B + i), fx_lane(w[i], L));
+                }
+            }
+        }
+    }
+}
+__device__ __forceinline__ void fx_loadQ(u32x4 *v, const uint16_t *__restrict__ vt, int loff, int j0) {
+#pragma unroll
+    for (int i = 0; i < DX_Q / 8; i++) v[i] = *(const u32x4 *)(vt + (long)(j0 / 8 + i) * 1024 + loff);
+}
+// vt: the wave's key block 0 of the chunk (uniform: the loads take a scalar
+// base and the lane offset loff = 8 lane, kernels.h vt_index: 1024 halves
+// per block; the region carries read-ahead slack).  Two register buffers in
+// turn, the next step's loads issued before the current step's arithmetic --
+// unconditionally (slack), so the wait counts stay exact.
+__device__ __forceinline__ void fx_chain1(const uint16_t *__restrict__ vt, int loff, int n, const float *w, const float *m,
+                                          unsigned long long flags, f16 &acc) {
+    u32x4 va[DX_Q / 8], vb[DX_Q / 8];
+    fx_loadQ(va, vt, loff, 0);
+    for (int j0 = 0; j0 < n; j0 += 2 * DX_Q) {
+        fx_loadQ(vb, vt, loff, j0 + DX_Q);
+        fx_step1(va, j0, n, w, m, flags, acc);
+        fx_loadQ(va, vt, loff, j0 + 2 * DX_Q);
+        fx_step1(vb, j0 + DX_Q, n, w, m, flags, acc);
+    }
+}
+
+// The weights of a chunk's n keys (n <= 64 DX_B) for one wave, in registers:
+// lane L's keys 32 L + i -> w[i] = vs, m[i] = ms; flags bit L = a new maximum
+// among them.  M: running maximum (in/out); returns this chunk's S at the new
+// maximum (per lane a sequential S = S * ms + vs as ggml, the lanes combined
+// in fp32).
+__device__ __forceinline__ float fx_weights_reg(const float *src, int n, float &M, float *w, float *m,
+                                                unsigned long long &flags) {
+    const int lane = threadIdx.x & 63;
+    float lm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < DX_B; i++) {
+        const int j = lane * DX_B + i;
+        w[i] = j < n ? src[j] : -INFINITY;   // the score, replaced by vs below
+    }
+#pragma unroll
+    for (int i = 0; i < DX_B; i++) lm = fmaxf(lm, w[i]);
+    const float inc = wave_scan_max(lm);
+    float Mp = fmaxf(M, dpp_ninf<0x138, 0xF>(inc));
+    const float Mn = fmaxf(M, lane_f(inc, 63));
+    float Sl = 0.0f;
+    bool nm = false;
+#pragma unroll
+    for (int i = 0; i < DX_B; i++) {
+        const float s = w[i];
+        float m1 = 1.0f, v1 = 0.0f;
+        if (s > Mp) {   // new maximum: ms = expf(Mold - M) (0 before the first key), vs = 1
+            m1 = expf(Mp - s);
+            v1 = 1.0f;
+            Mp = s;
+            nm = true;
+        } else if (s != -INFINITY) {
+            v1 = expf(s - Mp);
+        }
+        Sl = Sl * m1 + v1;
+        w[i] = v1;
+        m[i] = m1;
+    }
+    const float S = wave_sum(Mp == -INFINITY ? 0.0f : Sl * expf(Mp - Mn));
+    flags = __ballot(nm);
+    M = Mn;
+    return S;
+}
+
+// grid (n_head, B), block 128: query head h of sequence b, wave w running
+// dimensions 64 w + lane; the two waves share nothing (each derives the
+// weights itself).
+__global__ __launch_bounds__(128) void decode_attn_exact_kernel(DecodeAttnArgs a) {
+    stamp_start(a.stamp);
+    const int h = blockIdx.x, b = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int g = h / (a.n_head / a.n_kv_head);
+    const int nkv = a.pos[b] + 1;
+    const float *sg = a.scores + ((long)b * a.n_head + h) * a.max_ctx;
+    const long vtc = vt_ctx(a.max_ctx);
+    const int wu = __builtin_amdgcn_readfirstlane(wid);   // uniform: a scalar load base
+    const uint16_t *vcol = a.vt + ((long)b * a.n_kv_head + g) * 128 * vtc + 64 * wu * 8;   // the wave's key block 0
+    float M = -INFINITY, S = 0.0f;
+    f16 acc = 0;
+#ifdef FX_STAMPS
+    unsigned long long tsum[4] = {0, 0, 0, 0};
+    FX_CLK(tk0);
+#endif
+    for (int c0 = 0; c0 < nkv; c0 += 64 * DX_B) {
+        FX_CLK(ta);
+        const int n = min(64 * DX_B, nkv - c0);
+        float w[DX_B], m[DX_B];
+        unsigned long long flags;
+        const float Mold = M;
+        const float Sc = fx_weights_reg(sg + c0, n, M, w, m, flags);
+        S = (Mold == -INFINITY ? 0.0f : S * expf(Mold - M)) + Sc;
+        FX_CLK(tb);
+        FX_ADD(0, tb - ta);
+        fx_chain1(vcol + (long)c0 * 128, 8 * lane, n, w, m, flags, acc);
+        FX_CLK(tc);
+        FX_ADD(1, tc - tb);
+    }
+#ifdef FX_STAMPS
+    if (lane == 0) {
+        unsigned long long *st = fx_stamps[60000 + 2 * (blockIdx.x + gridDim.x * blockIdx.y) + wid];
+        st[0] = tk0;
+        st[1] = clock64();
+        st[2] = tsum[0];
+        st[3] = tsum[1];
+    }
+#endif
+    const float ov = (float)acc * (S == 0.0f ? 0.0f : 1.0f / S);   // ggml: VKQ32 = fp32(VKQ16) * (1 / S)
+    const long e = (long)b * a.n_head * 128 + h * 128 + 64 * wid + lane;
+    if (a.outq) {   // Q8_0 for the o-proj of a decode batch: a 32-block = 32 lanes
+        float am = fabsf(ov);
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+        a.outq[e] = q8_quant(ov, am);
+        if ((lane & 31) == 0) a.outd[e >> 5] = q8_scale(am);
+    } else if (a.out32) {
+        a.out32[e] = ov;
+    } else {
+        a.out[e] = f_to_u16(ov);
+    }
+    stamp_end(a.stamp);
+}
+
+void launch_decode_attention_exact(const DecodeAttnArgs &a, hipStream_t s) {
+    if (a.B <= 0) return;
+    hipLaunchKernelGGL(decode_attn_exact_kernel, dim3(a.n_head, a.B), dim3(128), 0, s, a);
+}
+
+}  // namespace qasr

@@ -138,6 +138,9 @@ struct FuseCfg {
     int spl1 = 0;                       // batch-1 attention split: 0 = auto (64, or 128 from 1k keys)
     int poll_limit = 1 << 20;           // bounded waits: polls (s_sleep(4..8) apart) before giving up
     int fence = 0;                      // 1 = agent release before each arrival, acquire after each wait
+    int fa_exact_prefill = 1;           // prefill attention with ggml's CPU FA numerics (fa_exact.hip)
+    int fa_exact_decode = -1;           // decode attention likewise: 1 on, 0 off (fp32 V accumulation), -1 = on for
+                                        // Q8_0 models only (batch 1 exact skips the fused QKV + attention launch)
     int slots_ffn = 0, slots_qkv64 = 0, slots_qkv128 = 0;   // co-resident workgroups on this device
     unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
 };
@@ -168,6 +171,18 @@ void launch_rmsnorm_q8(const float *x, int ldx, int M, int D, const float *w, fl
 void launch_enc_attention(const float *qkv, const int *seg_start, const int *seg_len, int n_seg, int max_len,
                           int D, int H, uint16_t *out, hipStream_t s, float *out32 = nullptr);
 
+// rows of padding after the last K/V cache region: the exact-attention chains
+// (fa_exact.hip) load V a few batches ahead without clamping
+constexpr long kKvPadRows = 256;
+// V^T cache for the decode chain of fa_exact.hip: per (layer, slot, kv head)
+// vt_ctx / 8 key blocks of [128 d][8 keys] fp16 -- one dimension's 8 keys in
+// 16 B, a wave's 64 dimensions of a block in 1 KiB contiguous (a plain
+// [d][key] layout put every lane of a load on its own page).  vt_ctx =
+// max_ctx rounded up to 64 plus 384 keys of read-ahead slack.
+__host__ __device__ inline int vt_ctx(int max_ctx) { return (max_ctx + 63) / 64 * 64 + 384; }
+// element (key k, dimension d) of one (slot, kv head) region
+__host__ __device__ inline long vt_index(int k, int d) { return ((long)(k >> 3) * 128 + d) * 8 + (k & 7); }
+
 // decoder q/k RMSNorm + NEOX RoPE + fp16 KV-cache write (+ q fp16 out)
 struct QkvPostArgs {
     const float *qkv; int rows;          // [rows][QD + 2*KD] fp32 from the fused QKV GEMM
@@ -178,6 +193,7 @@ struct QkvPostArgs {
     uint16_t *q_out;                     // [rows][n_head*128] fp16
     uint16_t *kc, *vc;                   // this layer's cache base: [seq][kvh][max_ctx][128]
     int max_ctx;
+    uint16_t *vt;                        // this layer's V^T cache base: [seq][kvh][128][vt_ctx(max_ctx)]
 };
 void launch_qkv_post(const QkvPostArgs &a, hipStream_t s);
 
@@ -193,6 +209,9 @@ struct PrefillAttnArgs {
     int8_t *outq; float *outd;           // non-null: Q8_0 output [B][QD] int8 + [B][QD/32] scales
 };
 void launch_prefill_attention(const PrefillAttnArgs &a, hipStream_t s);
+// the same attention with ggml's CPU flash-attention numerics (fa_exact.hip):
+// keys in order per query row, fp16 V accumulator rounded after every key
+void launch_prefill_attention_exact(const PrefillAttnArgs &a, hipStream_t s);
 
 // decoder single-token attention, fused: q/k RMSNorm + RoPE, fp16 KV-cache
 // write of the new token and split-KV flash decoding (64-key splits); the last
@@ -203,6 +222,7 @@ struct DecodeAttnArgs {
     const float *rope;                   // [max_pos][64][2]
     const int *pos;                      // [B] position of the fed token (n_past)
     uint16_t *kc, *vc;                   // this layer's cache base
+    uint16_t *vt;                        // this layer's V^T cache base (the new token's V is written there too)
     const int *seq_slot;
     int B, n_head, n_kv_head, max_ctx, max_splits;
     int grid_splits;                     // launched splits: >= ceil((max pos + 1) / 64) over the batch
@@ -222,7 +242,15 @@ struct DecodeAttnArgs {
     unsigned int *err;                   // fused launch: sticky device error word (DevErr bits)
     int spl1;                            // batch <= 8: key split (0 = auto: 64, or 128 from 1k keys)
     unsigned long long *stamp;           // kernel-duration probe record or null
+    float *scores;                       // non-null (separate launch only): scores mode -- the splits write their
+                                         // scaled scores [B][n_head][max_ctx] (+ the new K/V rows) and stop there
 };
+// the decode attention with ggml's CPU flash-attention numerics (fa_exact.hip),
+// after launch_decode_attention in scores mode: per (query head, sequence) the
+// keys in order with the fp16 V accumulator; reads scores, pos, vc, n_head,
+// n_kv_head, max_ctx and writes one of out / out32 / outq+outd
+void launch_decode_attention_exact(const DecodeAttnArgs &a, hipStream_t s);
+
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
 // batch 1, f16: the QKV projection (q: GemvArgs of the rmsnorm+QKV GEMV, K = 1024)
 // and the attention in one launch (attention.hip); false = not taken

@@ -20,10 +20,20 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running (full-size model)")
 
 
+def _stale(target: str, src_globs) -> bool:
+    import glob
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(f) > t for g in src_globs for f in glob.glob(os.path.join(ROOT, g)))
+
+
 @pytest.fixture(scope="session")
 def built():
+    """the in-tree libraries, rebuilt (make) when missing or older than any
+    source they are built from -- a stale binary never passes silently"""
     lib = os.path.join(ROOT, "qwen3-asr.cpp_amd", "libqasr.so")
-    if not os.path.exists(lib):
+    if _stale(lib, ["qwen3-asr.cpp_amd/csrc/*", "qwen3-asr.cpp_amd/host/*", "include/*.h"]):
         subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "qwen3-asr.cpp_amd")], check=True)
     orc = os.path.join(ROOT, "oracle", "liboracle.so")
     if not os.path.exists(orc):

@@ -127,6 +127,7 @@ def test_full_fused_launches_match_separate(full, knob):
     dev_common.h rn32; tools/diag_fused2.py found the layer.)"""
     m, _, om = full
     c1 = qasr.Context(m, max_batch=1, max_ctx=512)
+    c1.set_option("fa_exact_decode", 0)   # the fused launches run the fp32-accumulating attention
     try:
         pcm = qasr.synth_pcm(14000, 3 * SR)
         feats = c1.encode(c1.mel([pcm]))[0]
@@ -155,6 +156,7 @@ def test_full_fused_launches_long_context(full):
     bit-identical decode-step logits."""
     m, _, _ = full
     c1 = qasr.Context(m, max_batch=1, max_ctx=1280)
+    c1.set_option("fa_exact_decode", 0)
     try:
         pcm = qasr.synth_pcm(15000, 80 * SR)
         r_f = c1.transcribe([pcm], max_tokens=24, ignore_eos=True)
@@ -177,6 +179,7 @@ def test_full_fused_wait_timeout_is_an_error(full):
     once the bound is restored."""
     m, _, _ = full
     c1 = qasr.Context(m, max_batch=1, max_ctx=256)
+    c1.set_option("fa_exact_decode", 0)   # every fused launch in play
     try:
         assert c1.get_option("slots_ffn") >= 1024 and c1.get_option("slots_qkv") >= 512 + 8 * 4 + 256
         pcm = qasr.synth_pcm(14000, 2 * SR)
@@ -220,3 +223,56 @@ def test_full_two_threads_one_device(full):
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.timeout(900)
+def test_full_configs1_92s(full):
+    """configs[1] at its full size (92 s clip, N = 1196 encoder frames,
+    P = 1211 prompt tokens): mel, encoder, prefill logits and 15
+    teacher-forced decode steps against the oracle, and the first 16 greedy
+    tokens of the whole GPU path exactly the oracle's."""
+    _, c, om = full
+    pcm = qasr.synth_pcm(16000, 92 * SR)
+    mel_o = op.log_mel(pcm)
+    mel_g = c.mel([pcm])[0]
+    assert mel_g.shape == mel_o.shape == (128, 9200)
+    assert np.abs(mel_g - mel_o).max() <= 1e-5
+    feats_o = om.encode(mel_o)
+    feats_g = c.encode([mel_o])[0]
+    assert feats_o.shape == (1196, 1024)
+    d = np.abs(feats_g - feats_o)
+    assert d.max() <= 2e-2 and d.mean() <= 1e-3, (d.max(), d.mean())
+    ids, pos = om.prompt(1196), 9
+    assert len(ids) == 1211
+    dec = op.OracleDecoder(om, 1300)
+    lo = [dec.forward(ids, 0, feats_o, pos)]
+    toks = [int(np.argmax(lo[0]))]
+    for k in range(1, 16):
+        lo.append(dec.forward([toks[-1]], len(ids) + k - 1))
+        toks.append(int(np.argmax(lo[-1])))
+    lg, am = c.prefill([ids], [feats_o], [pos])
+    scale = float(np.abs(lo[0]).max())
+    assert np.abs(lg[0] - lo[0]).max() <= 1e-2 * scale
+    assert int(am[0]) == toks[0]
+    # teacher-forced on the oracle's tokens, in both decode-attention modes:
+    # exact (fp16 V accumulation, ggml's) within the 1e-2 bar; the F16 default
+    # (fp32 accumulation) reported against it -- at 1.2k keys its distance to
+    # ggml's fp16 accumulator is larger than the exact mode's
+    errs = {}
+    for mode in (1, 0):
+        c.set_option("fa_exact_decode", mode)
+        c.prefill([ids], [feats_o], [pos])
+        e = []
+        for k in range(1, 16):
+            lg, am = c.decode_step([toks[k - 1]], [len(ids) + k - 1])
+            e.append(float(np.abs(lg[0] - lo[k]).max()) / float(np.abs(lo[k]).max()))
+        errs[mode] = e
+    try:
+        assert max(errs[1]) <= 1e-2, errs[1]
+        assert max(errs[0]) <= 3e-2, errs[0]
+        for mode in (1, -1):   # greedy: exact mode, then the default
+            c.set_option("fa_exact_decode", mode)
+            r = c.transcribe([pcm], max_tokens=16, ignore_eos=True)
+            assert r.tokens[0] == toks, mode
+    finally:
+        c.set_option("fa_exact_decode", -1)

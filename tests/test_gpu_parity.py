@@ -112,27 +112,36 @@ def test_prefill_logits_match_oracle(tiny, tiny_oracle):
         assert am[0] == op.olib().qo_argmax(op._f(lo), len(lo))
 
 
-def test_decode_steps_teacher_forced(tiny, tiny_oracle):
+@pytest.mark.parametrize("exact", [1, 0])
+def test_decode_steps_teacher_forced(tiny, tiny_oracle, exact):
+    """exact = 1: fa_exact.hip's fp16 V accumulation (ggml's), against the
+    default oracle; exact = 0 (the F16 default): the fp32-accumulating decode
+    attention of the fused batch-1 launches, against the oracle's QO_FA_V_F32
+    switch"""
     m, c = tiny
     rng = np.random.default_rng(7)
     pcm = qasr.synth_pcm(6100, SR)
     feats = tiny_oracle.encode(op.log_mel(pcm))
     ids, pos = m.build_prompt(feats.shape[0])
-    c.prefill([ids], [feats], [pos], want_logits=False)
-    d = op.OracleDecoder(tiny_oracle, 512)
-    d.forward(ids, 0, feats, pos)
-    n_past = len(ids)
-    worst = 0.0
-    for step in range(24):
-        tok = int(rng.integers(0, 151643))
-        lg, am = c.decode_step([tok], [n_past])
-        lo = d.forward([tok], n_past)
-        scale = float(np.abs(lo).max())
-        worst = max(worst, float(np.abs(lg[0] - lo).max()) / scale)
-        s = np.sort(lo)
-        if s[-1] - s[-2] > 0.05 * scale:
-            assert am[0] == int(np.argmax(lo)), step
-        n_past += 1
+    c.set_option("fa_exact_decode", exact)
+    try:
+        c.prefill([ids], [feats], [pos], want_logits=False)
+        d = op.OracleDecoder(tiny_oracle, 512, 0 if exact else op.OracleModel.FA_V_F32)
+        d.forward(ids, 0, feats, pos)
+        n_past = len(ids)
+        worst = 0.0
+        for step in range(24):
+            tok = int(rng.integers(0, 151643))
+            lg, am = c.decode_step([tok], [n_past])
+            lo = d.forward([tok], n_past)
+            scale = float(np.abs(lo).max())
+            worst = max(worst, float(np.abs(lg[0] - lo).max()) / scale)
+            s = np.sort(lo)
+            if s[-1] - s[-2] > 0.05 * scale:
+                assert am[0] == int(np.argmax(lo)), step
+            n_past += 1
+    finally:
+        c.set_option("fa_exact_decode", -1)   # the default: exact for Q8_0 models only
     assert worst <= 1e-2, worst
 
 

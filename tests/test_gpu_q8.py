@@ -9,11 +9,12 @@ neighbouring int8 quantum (amax/127, ~1 % of the block), so the oracle itself
 moves by that much under a 1e-6 relative input perturbation; the floor is
 measured in the test (2.5x the oracle's self-sensitivity).
 
-The decoder comparisons use the oracle's QO_FA_V_F32 switch: ggml's CPU flash
-attention accumulates V.P in fp16, the HIP kernels in fp32; with
-F16 weights that difference is absorbed by the fp16 rounding of the o-proj
-input, with Q8_0 it reaches the activation quantiser, so the Q8_0 arithmetic
-is isolated by comparing against the fp32-accumulating oracle."""
+The decoder comparisons use the oracle's default numerics: the prefill and
+decode attention kernels (csrc/fa_exact.hip) accumulate V.P in fp16 key by key
+as ggml's CPU flash attention does (src/text_decoder.cpp:534-540), so the
+attention output reaching the o-proj's activation quantiser is the oracle's
+up to the scores' summation order (round 1 compared against the
+fp32-accumulating QO_FA_V_F32 switch instead)."""
 import numpy as np
 import pytest
 
@@ -22,7 +23,6 @@ import qasr
 from test_gpu_parity import _margin_aware_equal, _stats
 
 pytestmark = pytest.mark.gpu
-FA32 = op.OracleModel.FA_V_F32
 
 SR = 16000
 
@@ -74,8 +74,8 @@ def test_q8_prefill_and_decode_match_oracle(tq8, tiny_q8_oracle):
     feats = tiny_q8_oracle.encode(op.log_mel(qasr.synth_pcm(6100, SR)))
     ids, pos = m.build_prompt(feats.shape[0])
     lg, _ = c.prefill([ids], [feats], [pos])
-    d = op.OracleDecoder(tiny_q8_oracle, 512, FA32)
-    dn = op.OracleDecoder(tiny_q8_oracle, 512, FA32)   # noise-floor twin: features perturbed by 1e-6
+    d = op.OracleDecoder(tiny_q8_oracle, 512)
+    dn = op.OracleDecoder(tiny_q8_oracle, 512)   # noise-floor twin: features perturbed by 1e-6
     lo = d.forward(ids, 0, feats, pos)
     ln = dn.forward(ids, 0, _perturb(feats), pos)
     tol = max(1e-2 * float(np.abs(lo).max()), 2.5 * float(np.abs(lo - ln).max()))
@@ -116,11 +116,10 @@ def test_batched_decode_gemm_path(path, gpu, tiny_gguf, tiny_q8_gguf, tiny_oracl
         toks = [int(t) for t in rng.integers(0, 151643, B)]
         lg, _ = c.decode_step(toks, [n_past] * B)
         for b in range(B):   # every row is one step after the same prefix: fork the oracle per row
-            fl = FA32 if path == "q8" else 0
-            db = op.OracleDecoder(om, 256, fl)
+            db = op.OracleDecoder(om, 256)
             db.forward(ids, 0, feats, pos)
             lo = db.forward([toks[b]], n_past)
-            dnb = op.OracleDecoder(om, 256, fl)
+            dnb = op.OracleDecoder(om, 256)
             dnb.forward(ids, 0, _perturb(feats), pos)
             ln = dnb.forward([toks[b]], n_past)
             tol = 1e-2 * float(np.abs(lo).max())
@@ -136,6 +135,6 @@ def test_q8_transcribe_matches_oracle(tq8, tiny_q8_oracle):
     _, c = tq8
     pcm = qasr.synth_pcm(7100, int(2.2 * SR))
     r = c.transcribe([pcm], max_tokens=24, ignore_eos=True)
-    ora, _ = tiny_q8_oracle.transcribe(pcm, max_tokens=24, ignore_eos=True, flags=FA32)
+    ora, _ = tiny_q8_oracle.transcribe(pcm, max_tokens=24, ignore_eos=True)
     assert len(r.tokens[0]) == 24
-    _margin_aware_equal(r.tokens[0], ora, tiny_q8_oracle, pcm, 24, flags=FA32)
+    _margin_aware_equal(r.tokens[0], ora, tiny_q8_oracle, pcm, 24)
