@@ -183,6 +183,11 @@ __global__ __launch_bounds__(256) void qkv_post_kernel(QkvPostArgs a) {
     const float2 cs = *(const float2 *)(a.rope + ((long)pos * 64 + lane) * 2);
     const float y0 = x0 * cs.x - x1 * cs.y;
     const float y1 = x0 * cs.y + x1 * cs.x;
+    if (a.q32) {   // fp32 copies (ForcedAligner: ggml_flash_attn_ext on fp32 Q and K)
+        float *d32 = isq ? a.q32 + (long)row * QD + hh * 128 : a.k32 + (long)row * KD + (hh - nh) * 128;
+        d32[lane] = y0;
+        d32[lane + 64] = y1;
+    }
     if (isq) {
         uint16_t *dst = a.q_out + (long)row * QD + hh * 128;
         dst[lane] = f_to_u16(y0);

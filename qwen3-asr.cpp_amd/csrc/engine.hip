@@ -104,6 +104,7 @@ struct qasr_ctx {
     DevBuf chunks, rs1, rs2, rs3, pepos, act1, act2, act3;
     DevBuf ex, exh, eqkv, eatt, eff, feats, segs;
     DevBuf px, pxh, pqkv, pq, patt, pact, prow, plast, pids, pxl;
+    DevBuf pq32, pk32;             // ForcedAligner prefill: fp32 Q / K rows
     DevBuf ats, atx, aam;          // aligner: timestamp-row indices, their normed rows, argmax keys
     DevBuf q8a, q8d, x32;          // Q8_0 models: quantised activations (int8 + scales), fp32 layer inputs
     float *d_att32 = nullptr, *d_act32 = nullptr;   // Q8_0 decode: fp32 attention output / SwiGLU output
@@ -989,6 +990,8 @@ static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const st
         (rc = ensure(c, c->pqkv, (size_t)rows * (QD + 2 * KD) * 4)) || (rc = ensure(c, c->pq, (size_t)rows * QD * 2)) ||
         (rc = ensure(c, c->patt, (size_t)rows * QD * 2)) || (rc = ensure(c, c->pact, (size_t)rows * F * 2)))
         return rc;
+    const bool al = hp.aligner;   // fp32 Q / K scores (src/forced_aligner.cpp:1041-1046)
+    if (al && ((rc = ensure(c, c->pq32, (size_t)rows * QD * 4)) || (rc = ensure(c, c->pk32, (size_t)rows * KD * 4)))) return rc;
     hipStream_t s = c->st;
     const int *d_seq = c->prow.as<int>(), *d_pos = d_seq + rows, *d_aud = d_seq + 2 * rows;
     const int *d_srow0 = d_seq + 3 * rows, *d_slen = d_srow0 + B, *d_sslot = d_slen + B;
@@ -1012,12 +1015,14 @@ static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const st
         qa.n_head = hp.n_head; qa.n_kv_head = hp.n_kv_head; qa.q_out = c->pq.as<uint16_t>();
         qa.kc = c->kc + l * layer_kv; qa.vc = c->vc + l * layer_kv; qa.max_ctx = c->max_ctx;
         qa.vt = c->vt + l * layer_vt(c);
+        if (al) { qa.q32 = c->pq32.as<float>(); qa.k32 = c->pk32.as<float>(); }
         launch_qkv_post(qa, s);
         PrefillAttnArgs pa{};
         pa.q = c->pq.as<uint16_t>(); pa.kc = qa.kc; pa.vc = qa.vc; pa.seq_row0 = d_srow0; pa.seq_len = d_slen;
         pa.seq_slot = d_sslot; pa.n_seq = B; pa.max_len = maxp; pa.n_head = hp.n_head; pa.n_kv_head = hp.n_kv_head;
         pa.max_ctx = c->max_ctx; pa.scale = 1.0f / sqrtf(128.0f); pa.out = c->patt.as<uint16_t>(); pa.out32 = x32;
-        if (c->fuse.fa_exact_prefill) launch_prefill_attention_exact(pa, s);   // ggml CPU FA numerics
+        if (al) { pa.q32 = qa.q32; pa.k32 = qa.k32; }
+        if (c->fuse.fa_exact_prefill || al) launch_prefill_attention_exact(pa, s);   // ggml CPU FA numerics
         else launch_prefill_attention(pa, s);
         GemmArgs o{};
         o.M = rows; o.N = H; o.K = QD; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;

@@ -263,7 +263,33 @@ __global__ __launch_bounds__(64 * PX_W) void prefill_attn_exact_kernel(PrefillAt
             __builtin_amdgcn_global_load_lds((glb_void *)(vc + (long)(c0 + 4 * it + (lane >> 4)) * 128 + 8 * (lane & 15)),
                                              (lds_void *)(vsh + it * 256), 16, 0, 0);
         // (1) scores: 16-key tile t = wid
-        {
+        if (a.k32) {   // fp32 Q and K (the aligner): v_mfma_f32_16x16x4_f32, exact fp32 products
+            const int t = wid;
+            if (t * 16 < n) {
+                // lane (row r = lane & 15, group g): dims 32 g .. 32 g + 31 of key r / query r
+                // (any split of the 128 dims works if A and B use the same one)
+                const int key = min(c0 + t * 16 + ql, kend - 1);
+                const float *kr = a.k32 + (long)(row0 + key) * (a.n_kv_head * 128) + hk * 128 + 32 * g;
+                const float *qr = a.q32 + (long)(row0 + min(q0 + ql, L - 1)) * QD + h * 128 + 32 * g;
+                float kv[32], qv2[32];
+#pragma unroll
+                for (int i = 0; i < 32; i += 4) {
+                    *(float4 *)&kv[i] = *(const float4 *)&kr[i];
+                    *(float4 *)&qv2[i] = qv ? *(const float4 *)&qr[i] : float4{0.f, 0.f, 0.f, 0.f};
+                }
+                floatx4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kk = 0; kk < 32; kk += 2) {   // two accumulators: the 40-cycle dependent latency
+                    s0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kv[kk], qv2[kk], s0, 0, 0, 0);
+                    s1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kv[kk + 1], qv2[kk + 1], s1, 0, 0, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int k = c0 + t * 16 + 4 * g + i;
+                    sc[ql][t * 16 + 4 * g + i] = k <= lim ? (s0[i] + s1[i]) * a.scale : -INFINITY;
+                }
+            }
+        } else {
             const int t = wid;
             const int key = min(c0 + t * 16 + ql, kend - 1);
             half8 kf[4];

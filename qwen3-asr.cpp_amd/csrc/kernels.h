@@ -194,6 +194,7 @@ struct QkvPostArgs {
     uint16_t *kc, *vc;                   // this layer's cache base: [seq][kvh][max_ctx][128]
     int max_ctx;
     uint16_t *vt;                        // this layer's V^T cache base: [seq][kvh][128][vt_ctx(max_ctx)]
+    float *q32, *k32;                    // non-null (ForcedAligner): also the fp32 rows [rows][QD] / [rows][KD]
 };
 void launch_qkv_post(const QkvPostArgs &a, hipStream_t s);
 
@@ -207,6 +208,9 @@ struct PrefillAttnArgs {
     uint16_t *out;                       // [rows][n_head*128] fp16
     float *out32;                        // non-null: fp32 output instead (input of a Q8_0 o-proj)
     int8_t *outq; float *outd;           // non-null: Q8_0 output [B][QD] int8 + [B][QD/32] scales
+    const float *q32, *k32;              // non-null (exact kernel only): fp32 scores from these fp32 rows, key k of
+                                         // sequence s at row seq_row0[s] + k (the aligner's K stays fp32,
+                                         // src/forced_aligner.cpp:1041-1046)
 };
 void launch_prefill_attention(const PrefillAttnArgs &a, hipStream_t s);
 // the same attention with ggml's CPU flash-attention numerics (fa_exact.hip):

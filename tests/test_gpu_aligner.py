@@ -2,11 +2,12 @@
 against the oracle's aligner restatement (src/forced_aligner.cpp:591-1306).
 
 Tolerances: encoder as the ASR encoder (max 2e-2, mean 1e-3 -- the
-reference's own tests/run_all_tests.sh:166); classify logits 1e-2 x the logit
-scale; timestamp classes identical wherever the oracle's own top-1/top-2
-margin exceeds 2 % of the logit scale (the HIP prefill rounds Q and K to fp16
-for its MFMA scores where the reference keeps K, hence Q, in fp32 -- DESIGN.md
-§3), and identical overall on >= 90 % of the rows."""
+reference's own tests/run_all_tests.sh:166); timestamp classes identical
+wherever the oracle's own top-1/top-2 margin exceeds its noise floor (0.5 % of
+the logit scale: the summation orders of the fp32 dots differ).  The prefill
+attention follows the reference's: Q and K in fp32 (fp32 MFMA scores), V cast
+to fp16 and accumulated in fp16 key by key (src/forced_aligner.cpp:1041-1046,
+csrc/fa_exact.hip)."""
 import os
 import subprocess
 
@@ -73,8 +74,8 @@ def test_aligner_classes_match_oracle(al, secs, text):
     srt = np.sort(olg, axis=1)
     margin = srt[:, -1] - srt[:, -2]
     same = np.array(cls) == np.array(ocls)
-    assert same[margin > 2e-2 * scale].all(), (cls, ocls, margin / scale)
-    assert same.mean() >= 0.9, (cls, ocls)
+    assert same[margin > 5e-3 * scale].all(), (cls, ocls, margin / scale)
+    assert same.all(), (cls, ocls, margin / scale)   # measured: every row, these seeds (no near-ties)
     assert t.t_encode_ms > 0 and t.t_total_ms > 0
 
 
@@ -150,7 +151,7 @@ def test_full_aligner_encode_and_classes(gpu, tmp_path_factory):
         srt = np.sort(olg, axis=1)
         margin = srt[:, -1] - srt[:, -2]
         same = np.array(cls) == np.array(ocls)
-        assert same[margin > 2e-2 * scale].all(), (cls, ocls)
+        assert same[margin > 5e-3 * scale].all(), (cls, ocls, margin / scale)
     finally:
         c.close()
         m.close()
