@@ -276,3 +276,51 @@ def test_full_configs1_92s(full):
             assert r.tokens[0] == toks, mode
     finally:
         c.set_option("fa_exact_decode", -1)
+
+
+@pytest.mark.timeout(900)
+def test_full_configs2_q8_b64_30s(gpu, tmp_path_factory):
+    """configs[2] at its full size: Qwen3-ASR-0.6B Q8_0 (synthetic weights),
+    64 x 30 s clips (P = 405 prompt tokens each, 105-token budget).  All 64
+    rows bit-identical (identical clips), every budget met, and row 0 against
+    the default-flag oracle: prefill logits and the first decode step within the
+    Q8_0 bars of tests/test_gpu_q8.py (1e-2 x the logit scale, or 2.5 x the
+    oracle's own sensitivity to a 1e-6 perturbation of the encoder features,
+    whichever is larger).  The decode attention runs the exact (fp16 V
+    accumulation) kernels, the Q8_0 default."""
+    p = str(tmp_path_factory.mktemp("fq8") / "full-q8.gguf")
+    qasr.write_synthetic_gguf(p, "full", 42, 8)
+    op.set_threads(min(16, os.cpu_count() or 1))
+    om = op.OracleModel(p)
+    m = qasr.Model(p)
+    B, n, budget = 64, 30 * SR, 105
+    pcm = qasr.synth_pcm(17000, n)
+    mel = op.log_mel(pcm)
+    feats = om.encode(mel)
+    ids, pos = m.build_prompt(feats.shape[0])
+    assert len(ids) == 405
+    c = qasr.Context(m, max_batch=B, max_ctx=len(ids) + budget + 8)
+    try:
+        assert c.get_option("fa_exact_decode") == -1   # the default: exact for Q8_0 models
+        r = c.transcribe([pcm] * B, max_tokens=budget, ignore_eos=True)
+        assert all(len(t) == budget for t in r.tokens)
+        assert all(t == r.tokens[0] for t in r.tokens)
+        lg, am = c.prefill([ids] * B, [feats] * B, [pos] * B)
+        for b in range(1, B):
+            assert np.array_equal(lg[b], lg[0]), b
+        tok0 = int(am[0])
+        lg1, _ = c.decode_step([tok0] * B, [len(ids)] * B)
+        for b in range(1, B):
+            assert np.array_equal(lg1[b], lg1[0]), b
+    finally:
+        c.close()
+        m.close()
+    rng = np.random.default_rng(5)
+    featsn = (feats * (1 + 1e-6 * rng.standard_normal(feats.shape))).astype(np.float32)
+    d, dn = op.OracleDecoder(om, len(ids) + 8), op.OracleDecoder(om, len(ids) + 8)
+    lo, ln = d.forward(ids, 0, feats, pos), dn.forward(ids, 0, featsn, pos)
+    tol = max(1e-2 * float(np.abs(lo).max()), 2.5 * float(np.abs(lo - ln).max()))
+    assert np.abs(lg[0] - lo).max() <= tol, (float(np.abs(lg[0] - lo).max()), tol)
+    lo1, ln1 = d.forward([tok0], len(ids)), dn.forward([tok0], len(ids))
+    tol1 = max(1e-2 * float(np.abs(lo1).max()), 2.5 * float(np.abs(lo1 - ln1).max()))
+    assert np.abs(lg1[0] - lo1).max() <= tol1, (float(np.abs(lg1[0] - lo1).max()), tol1)
