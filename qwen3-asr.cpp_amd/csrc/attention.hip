@@ -49,23 +49,36 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const float *__restrict__
     for (int d = 0; d < 4; d++) o[d] = floatx4{0.f, 0.f, 0.f, 0.f};
     float m_run = -INFINITY, l_run = 0.0f;
 
-    for (int k0 = 0; k0 < N; k0 += 64) {
-        __syncthreads();
-        // stage K and V tiles (64 keys x 64 dims fp32)
-        for (int i = tid; i < 64 * 16; i += 256) {
-            const int key = i >> 4, c4 = (i & 15) * 4;
-            float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
-            if (k0 + key < N) {
-                const float *rowp = qkv + (long)(r0 + k0 + key) * ld + h * 64 + c4;
-                kv = *(const float4 *)(rowp + D);
-                vv = *(const float4 *)(rowp + 2 * D);
+    // K / V tiles (64 keys x 64 dims fp32) go global -> registers one tile ahead
+    // (the next tile's loads are in flight during this tile's MFMAs: a
+    // load-then-compute loop paid a memory latency per tile, ~1/3 of the time
+    // at a 1.2k-frame clip), then registers -> LDS at the tile start
+    float4 kpre[4], vpre[4];
+    auto fetch = [&](int kb) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int i = tid + 256 * j, key = i >> 4, c4 = (i & 15) * 4;
+            kpre[j] = vpre[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (kb + key < N) {
+                const float *rowp = qkv + (long)(r0 + kb + key) * ld + h * 64 + c4;
+                kpre[j] = *(const float4 *)(rowp + D);
+                vpre[j] = *(const float4 *)(rowp + 2 * D);
             }
+        }
+    };
+    fetch(0);
+    for (int k0 = 0; k0 < N; k0 += 64) {
+        __syncthreads();   // the previous tile's readers are done
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int i = tid + 256 * j, key = i >> 4, c4 = (i & 15) * 4;
             float *kd = Ks + key * EKS + c4;
-            *(float2 *)kd = make_float2(kv.x, kv.y);
-            *(float2 *)(kd + 2) = make_float2(kv.z, kv.w);
-            *(float4 *)(Vs + key * EVS + c4) = vv;
+            *(float2 *)kd = make_float2(kpre[j].x, kpre[j].y);
+            *(float2 *)(kd + 2) = make_float2(kpre[j].z, kpre[j].w);
+            *(float4 *)(Vs + key * EVS + c4) = vpre[j];
         }
         __syncthreads();
+        if (k0 + 64 < N) fetch(k0 + 64);
         // S^T tiles: 4 key sub-tiles x 16 d-steps
         floatx4 st[4];
 #pragma unroll
