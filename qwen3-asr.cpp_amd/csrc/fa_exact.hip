@@ -146,25 +146,40 @@ __device__ __forceinline__ void fx_weights(const float *src, float *sc, float *m
     }
 }
 
-// One batch of FX_B keys for R rows, two dimensions per lane: v[i] = the
-// lane's V dword of key j0 + i; row r's weights at vs / ms + r * ld + j0.  The
-// fast path (a full batch, no new maximum in any of the rows) is three VALU
-// instructions per row and key; a batch with a new maximum scales every key
-// (ggml_vec_scale_f16 runs only on a new maximum, but ms = 1 is exact).
+// One full batch of FX_B keys for R rows, two dimensions per lane: v[i] = the
+// lane's V dword of key j0 + i; row r's weights at vs / ms + r * ld + j0.
+// Rows whose bit is set in SCALE hold a new maximum in the batch and scale
+// every key of it (ggml_vec_scale_f16 runs only on a new maximum, but ms = 1
+// is exact: an fp16 value times 1, rounded to fp16); the others take three
+// VALU instructions per key.
+template <int R, int SCALE>
+__device__ __forceinline__ void fx_body2(const uint32_t *v, const float *vs, const float *ms, int ld, int j0, half2v *acc) {
+#pragma unroll
+    for (int i = 0; i < FX_B; i++)
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            if constexpr (SCALE != 0)
+                if ((SCALE >> r) & 1) acc[r] = fx_scale2(acc[r], ms[r * ld + j0 + i]);
+            acc[r] = fx_mad2(acc[r], v[i], vs[r * ld + j0 + i]);
+        }
+}
 template <int R>
 __device__ __forceinline__ void fx_batch2(const uint32_t *v, const float *vs, const float *ms, int ld, int j0, int nb,
-                                          uint32_t any, half2v *acc) {
-    if (nb == FX_B && !any) {
-#pragma unroll
-        for (int i = 0; i < FX_B; i++)
-#pragma unroll
-            for (int r = 0; r < R; r++) acc[r] = fx_mad2(acc[r], v[i], vs[r * ld + j0 + i]);
-    } else {
+                                          uint32_t mask, half2v *acc) {
+    static_assert(R == 2, "row-mask dispatch written for two rows a wave");
+    if (nb == FX_B) {
+        switch (mask) {   // uniform
+        case 0: fx_body2<R, 0>(v, vs, ms, ld, j0, acc); break;
+        case 1: fx_body2<R, 1>(v, vs, ms, ld, j0, acc); break;
+        case 2: fx_body2<R, 2>(v, vs, ms, ld, j0, acc); break;
+        default: fx_body2<R, 3>(v, vs, ms, ld, j0, acc); break;
+        }
+    } else {   // the chunk's partial last batch
 #pragma unroll
         for (int i = 0; i < FX_B; i++) {
             if (i < nb) {
 #pragma unroll
-                for (int r = 0; r < R; r++) {   // ms = 1 scales exactly (an fp16 value times 1, rounded to fp16)
+                for (int r = 0; r < R; r++) {
                     acc[r] = fx_scale2(acc[r], ms[r * ld + j0 + i]);
                     acc[r] = fx_mad2(acc[r], v[i], vs[r * ld + j0 + i]);
                 }
@@ -182,10 +197,10 @@ __device__ __forceinline__ void fx_chain2(const uint32_t *vl, int n, const float
         uint32_t v[FX_B];
 #pragma unroll
         for (int i = 0; i < FX_B; i++) v[i] = vl[(j0 + i) * 64];   // rows past n: staged padding, unused
-        uint32_t any = 0;
+        uint32_t mask = 0;
 #pragma unroll
-        for (int r = 0; r < R; r++) any |= fl[(j0 / FX_B) * PX_ROWS + r];
-        fx_batch2<R>(v, vs, ms, ld, j0, min(FX_B, n - j0), __builtin_amdgcn_readfirstlane(any), acc);
+        for (int r = 0; r < R; r++) mask |= (fl[(j0 / FX_B) * PX_ROWS + r] ? 1u : 0u) << r;
+        fx_batch2<R>(v, vs, ms, ld, j0, min(FX_B, n - j0), __builtin_amdgcn_readfirstlane(mask), acc);
     }
 }
 
