@@ -118,6 +118,7 @@ struct qasr_ctx {
     unsigned int *d_qcnt = nullptr;   // fused batch-1 QKV + attention: QKV-block arrivals per kv group
     unsigned int *d_attdone = nullptr;   // fused batch-1 o-proj: combiner arrivals (8 replicas)
     unsigned int *d_ffncnt = nullptr;    // fused batch-1 FFN: gate/up arrivals, [layer][32 shards][16]
+    unsigned int *d_ocnt = nullptr;      // batch-1 layer launch: o-proj arrivals, [layer][32 shards][16]
     uint16_t *d_q = nullptr, *d_att = nullptr, *d_act = nullptr, *d_xh = nullptr;
     unsigned long long *d_amax = nullptr;
     int max_splits = 0, hist_cap = 0;
@@ -151,6 +152,7 @@ struct qasr_ctx {
     int probe = 0;                 // 0 off, 1 LM head, 2 layer QKV + attention, 3 layer FFN
     int probe_layer = 14;          // decoder layer whose groups probes 2 / 3 time
     bool probe_o_fused = false;    // the probed layer's o-projection runs inside the QKV launch
+    bool probe_layer_fused = false;   // ... and its FFN too (layer1_kernel)
     double probe_ms = 0.0, probe_bytes = 0.0, probe_dev_ms = 0.0;
     long probe_dev_n = 0;
     unsigned long long *d_pstamp = nullptr;   // per decode step: [32 min-starts | 32 max-ends] of the probed launches
@@ -199,6 +201,10 @@ static const std::vector<FuseOption> &fuse_options() {
         {"ffn_wdelay", "QASR_FFN_WDELAY", &FuseCfg::ffn_wdelay}, {"qkv_delay", "QASR_FUSE_DELAY", &FuseCfg::qkv_delay},
         {"o_delay", "QASR_FUSE_ODELAY", &FuseCfg::o_delay},    {"att_spl1", "QASR_ATT_SPL1", &FuseCfg::spl1},
         {"poll_limit", "QASR_POLL_LIMIT", &FuseCfg::poll_limit}, {"handoff_fence", "QASR_HANDOFF_FENCE", &FuseCfg::fence},
+        {"fuse_layer", "QASR_FUSE_LAYER", &FuseCfg::layer},
+        {"gu_delay", "QASR_GU_DELAY", &FuseCfg::gu_delay},
+        {"dn_wdelay", "QASR_DN_WDELAY", &FuseCfg::dn_wdelay},
+        {"dn_delay", "QASR_DN_DELAY", &FuseCfg::dn_delay},
         {"fa_exact_prefill", "QASR_FA_EXACT_PREFILL", &FuseCfg::fa_exact_prefill},
         {"fa_exact_decode", "QASR_FA_EXACT_DECODE", &FuseCfg::fa_exact_decode},
     };
@@ -215,6 +221,7 @@ static int check_dev_err(qasr_ctx *c) {
     // a wait that gave up can leave late arrivals in the counters: back to rest
     HIPCHK(hipMemsetAsync(c->d_err, 0, 4, c->st));
     HIPCHK(hipMemsetAsync(c->d_ffncnt, 0, (size_t)c->m->hp.dec_layers * 512 * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->d_ocnt, 0, (size_t)c->m->hp.dec_layers * 512 * 4, c->st));
     HIPCHK(hipMemsetAsync(c->d_qcnt, 0, (size_t)c->m->hp.n_kv_head * 8 * 16 * 4, c->st));
     HIPCHK(hipMemsetAsync(c->d_attdone, 0, (size_t)8 * 16 * 4, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
@@ -676,6 +683,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_qcnt, (size_t)hp.n_kv_head * 8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_attdone, (size_t)8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_ffncnt, (size_t)hp.dec_layers * 512 * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_ocnt, (size_t)hp.dec_layers * 512 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_err, 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_pstamp, (size_t)max_ctx * kStampRec * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_logits, (size_t)B * hp.vocab * 4)) ||
@@ -686,6 +694,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     HIPCHK(hipMemcpy(c->d_slot, slots.data(), B * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(c->d_counter, 0, (size_t)B * hp.n_kv_head * 4));
     HIPCHK(hipMemset(c->d_qcnt, 0, (size_t)hp.n_kv_head * 8 * 16 * 4));
+    HIPCHK(hipMemset(c->d_ocnt, 0, (size_t)hp.dec_layers * 512 * 4));
     HIPCHK(hipMemset(c->d_attdone, 0, (size_t)8 * 16 * 4));
     HIPCHK(hipMemset(c->d_ffncnt, 0, (size_t)hp.dec_layers * 512 * 4));
     HIPCHK(hipMemset(c->d_done, 0, 4));
@@ -723,6 +732,7 @@ extern "C" int qasr_ctx_set_option(qasr_ctx *c, const char *name, int value) {
             c->drop_graphs();   // captured steps hold the old launch configuration
             HIPCHK(hipSetDevice(c->m->device));   // arrival counters back to rest
             HIPCHK(hipMemsetAsync(c->d_ffncnt, 0, (size_t)c->m->hp.dec_layers * 512 * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->d_ocnt, 0, (size_t)c->m->hp.dec_layers * 512 * 4, c->st));
             HIPCHK(hipMemsetAsync(c->d_qcnt, 0, (size_t)c->m->hp.n_kv_head * 8 * 16 * 4, c->st));
             HIPCHK(hipMemsetAsync(c->d_attdone, 0, (size_t)8 * 16 * 4, c->st));
             HIPCHK(hipStreamSynchronize(c->st));
@@ -1157,15 +1167,37 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             q1.trace = tr(0);
             q1.stamp = stamp;
         }
+        GemvArgs gu{}, dn{};   // batch <= 8 FFN
+        if (skinny) {
+            gu.x = x; gu.ldx = H; gu.norm_w = L.ffn_norm; gu.eps = hp.rms_eps; gu.W = L.wgu; gu.Wd = L.wgu_d; gu.K = H; gu.N = F; gu.M = B;
+            if (q8) { gu.out_f32 = c->d_act32; gu.ldo = F; }
+            else { gu.out_f16 = c->d_act; gu.ldo16 = F; }
+            gu.trace = tr(3);
+            gu.stamp = stamp;
+            if (q8) { dn.x = c->d_act32; dn.ldx = F; dn.Wd = L.wd_d; }
+            else { dn.xh = c->d_act; dn.ldxh = F; }
+            dn.W = L.wd; dn.K = F; dn.N = H; dn.M = B; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
+            dn.trace = tr(4);
+            dn.stamp = stamp;
+        }
         const bool exact = exact_decode(c);
         const bool fusable = skinny && B == 1 && !q8 && !skip && !exact;
         if (fusable) da.att_done = c->d_attdone;
-        // 0 = separate launches, 1 = QKV + attention, 2 = + o-projection (decided without launching)
-        const int fmode = fusable ? launch_qkv_attention1(q1, da, &o, c->fuse, s, true) : 0;
+        unsigned int *ocnt = c->d_ocnt + (size_t)l * 512, *ocnt_next = c->d_ocnt + (size_t)((l + 1) % nl) * 512;
+        unsigned int *fcnt = c->d_ffncnt + (size_t)l * 512, *fcnt_next = c->d_ffncnt + (size_t)((l + 1) % nl) * 512;
+        // the whole layer in one launch (decided without launching), else 0 = separate
+        // launches, 1 = QKV + attention, 2 = + o-projection
+        const bool lfused = fusable && nl >= 2 && launch_layer1(q1, da, o, gu, dn, ocnt, ocnt_next, fcnt, fcnt_next, c->fuse, s, true);
+        const int fmode = lfused ? 0 : fusable ? launch_qkv_attention1(q1, da, &o, c->fuse, s, true) : 0;
         const bool o_fused = fmode == 2;
-        if (l == std::min(c->probe_layer, nl - 1)) c->probe_o_fused = o_fused;
+        if (l == std::min(c->probe_layer, nl - 1)) {
+            c->probe_o_fused = o_fused || lfused;
+            c->probe_layer_fused = lfused;
+        }
         if (ga) {
-            if (fmode) {
+            if (lfused) {
+                (void)launch_layer1(q1, da, o, gu, dn, ocnt, ocnt_next, fcnt, fcnt_next, c->fuse, s, false);
+            } else if (fmode) {
                 (void)launch_qkv_attention1(q1, da, &o, c->fuse, s, false);
             } else {
                 if (skinny) {
@@ -1192,24 +1224,11 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
                 }
             }
         }
-        if (!gb) continue;
+        if (!gb || lfused) continue;   // (the layer launch ran the o-projection and the FFN)
         if (skinny) {
             if (!o_fused && !(skip & 4)) launch_gemv(EPI_F32, o, s);
-            GemvArgs gu{};
-            gu.x = x; gu.ldx = H; gu.norm_w = L.ffn_norm; gu.eps = hp.rms_eps; gu.W = L.wgu; gu.Wd = L.wgu_d; gu.K = H; gu.N = F; gu.M = B;
-            if (q8) { gu.out_f32 = c->d_act32; gu.ldo = F; }
-            else { gu.out_f16 = c->d_act; gu.ldo16 = F; }
-            gu.trace = tr(3);
-            gu.stamp = stamp;
-            GemvArgs dn{};
-            if (q8) { dn.x = c->d_act32; dn.ldx = F; dn.Wd = L.wd_d; }
-            else { dn.xh = c->d_act; dn.ldxh = F; }
-            dn.W = L.wd; dn.K = F; dn.N = H; dn.M = B; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
             if (o_fused) dn.zero8 = c->d_attdone;   // re-arm the fused o-proj's arrival counters
-            dn.trace = tr(4);
-            dn.stamp = stamp;
-            if (skip & 24 || nl < 2 ||
-                !launch_ffn1(gu, dn, c->d_ffncnt + (size_t)l * 512, c->d_ffncnt + (size_t)((l + 1) % nl) * 512, c->fuse, s)) {
+            if (skip & 24 || nl < 2 || !launch_ffn1(gu, dn, fcnt, fcnt_next, c->fuse, s)) {
                 if (!(skip & 8)) launch_gemv(q8 ? EPI_SWIGLU_F32 : EPI_SWIGLU_F16, gu, s);
                 if (!(skip & 16)) launch_gemv(EPI_F32, dn, s);
                 else if (o_fused) (void)hipMemsetAsync(c->d_attdone, 0, 8 * 16 * 4, s);   // the skipped down-proj re-arms these
@@ -1288,7 +1307,8 @@ static double probe_bytes(const qasr_ctx *c, int B, int k) {
         double kv = 0;
         for (int b = 0; b < B; b++) kv += (double)(c->run_P[b] + k + 1) * KD * 2 * 2;
         const bool o_in = c->probe_o_fused;
-        return (QD + 2 * KD) * H * wb + (o_in ? H * QD * wb : 0.0) + kv + B * H * 4 * (o_in ? 3 : 1) + B * (QD + 2 * KD) * 4;
+        const double ffn = c->probe_layer_fused ? 3 * F * H * wb + B * H * 4 * 3 : 0.0;   // the layer launch's FFN
+        return (QD + 2 * KD) * H * wb + (o_in ? H * QD * wb : 0.0) + kv + B * H * 4 * (o_in ? 3 : 1) + B * (QD + 2 * KD) * 4 + ffn;
     }
     return 3 * F * H * wb + (c->probe_o_fused ? 0.0 : H * QD * wb) + B * H * 4 * 3;
 }

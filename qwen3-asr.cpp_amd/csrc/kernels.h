@@ -138,10 +138,14 @@ struct FuseCfg {
     int spl1 = 0;                       // batch-1 attention split: 0 = auto (64, or 128 from 1k keys)
     int poll_limit = 1 << 20;           // bounded waits: polls (s_sleep(4..8) apart) before giving up
     int fence = 0;                      // 1 = agent release before each arrival, acquire after each wait
+    int layer = 0;                      // batch 1: the whole decoder layer in one launch (layer1_kernel; measured slower)
+    int gu_delay = 16, dn_wdelay = 30, dn_delay = 8;   // layer launch: gate/up weight request, down weight request,
+                                                       // down first poll (s_sleep(8) units)
     int fa_exact_prefill = 1;           // prefill attention with ggml's CPU FA numerics (fa_exact.hip)
     int fa_exact_decode = -1;           // decode attention likewise: 1 on, 0 off (fp32 V accumulation), -1 = on for
                                         // Q8_0 models only (batch 1 exact skips the fused QKV + attention launch)
     int slots_ffn = 0, slots_qkv64 = 0, slots_qkv128 = 0;   // co-resident workgroups on this device
+    int slots_layer64 = 0, slots_layer128 = 0;
     unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
 };
 // co-resident workgroup capacity of the fused kernels on the current device
@@ -246,9 +250,21 @@ struct DecodeAttnArgs {
     unsigned int *err;                   // fused launch: sticky device error word (DevErr bits)
     int spl1;                            // batch <= 8: key split (0 = auto: 64, or 128 from 1k keys)
     unsigned long long *stamp;           // kernel-duration probe record or null
+    unsigned int qkv_need;               // fused launches: QKV-block arrivals per kv group (0 = 64)
     float *scores;                       // non-null (separate launch only): scores mode -- the splits write their
                                          // scaled scores [B][n_head][max_ctx] (+ the new K/V rows) and stop there
 };
+// Batch 1, the whole decoder layer in one launch (attention.hip layer1_kernel):
+// QKV (256 blocks) -> attention splits -> o-projection (128) -> gate/up (192)
+// -> down (128), each role waiting in-launch (bounded) on the previous one's
+// arrival counters; ocnt / fcnt: this layer's 32-shard o-proj / gate-up
+// arrival counters (16-word stride, zero on entry), *_next the next layer's
+// (re-armed here).  Returns 0 when not covered (the caller launches
+// qkv_attention1 + ffn1 or separate kernels), 1 when launched (dry: would be).
+int launch_layer1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs &o, const GemvArgs &gu, const GemvArgs &dn,
+                  unsigned int *ocnt, unsigned int *ocnt_next, unsigned int *fcnt, unsigned int *fcnt_next, const FuseCfg &cfg,
+                  hipStream_t s, bool dry);
+
 // the decode attention with ggml's CPU flash-attention numerics (fa_exact.hip),
 // after launch_decode_attention in scores mode: per (query head, sequence) the
 // keys in order with the fp16 V accumulator; reads scores, pos, vc, n_head,
