@@ -48,7 +48,9 @@ namespace qasr {
 
 #define PX_ROWS 16   // prefill query rows per workgroup
 #define PX_KC 128    // prefill keys per chunk
+#ifndef FX_B
 #define FX_B 16      // chain batch: keys whose V and weights are in registers together
+#endif
 
 // ggml_vec_mad_f16 on two dimensions packed in one dword: fp16(fma(v, vs, acc))
 __device__ __forceinline__ half2v fx_mad2(half2v acc, uint32_t v, float vs) {
@@ -229,7 +231,11 @@ typedef __attribute__((address_space(1))) void glb_void;
 #define PX_SCS (PX_KC + 4)   // score row stride (floats): the MFMA writes of 16 rows hit 16 banks
 #define PX_W 8               // waves per workgroup
 #define PX_R (PX_ROWS / PX_W)
-__global__ __launch_bounds__(64 * PX_W) void prefill_attn_exact_kernel(PrefillAttnArgs a) {
+#ifndef PX_MINW
+#define PX_MINW 1   // minimum waves per SIMD asked of the register allocator
+#endif
+template <bool F32S>   // fp32 Q / K scores (the aligner)
+__global__ __launch_bounds__(64 * PX_W, PX_MINW) void prefill_attn_exact_kernel(PrefillAttnArgs a) {
     __shared__ __attribute__((aligned(16))) float sc[PX_ROWS][PX_SCS];   // scores, then vs
     __shared__ __attribute__((aligned(16))) float msw[PX_ROWS][PX_SCS];
     __shared__ __attribute__((aligned(16))) uint32_t fl[PX_KC / FX_B][PX_ROWS];
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(64 * PX_W) void prefill_attn_exact_kernel(PrefillAt
             __builtin_amdgcn_global_load_lds((glb_void *)(vc + (long)(c0 + 4 * it + (lane >> 4)) * 128 + 8 * (lane & 15)),
                                              (lds_void *)(vsh + it * 256), 16, 0, 0);
         // (1) scores: 16-key tile t = wid
-        if (a.k32) {   // fp32 Q and K (the aligner): v_mfma_f32_16x16x4_f32, exact fp32 products
+        if constexpr (F32S) {   // fp32 Q and K (the aligner): v_mfma_f32_16x16x4_f32, exact fp32 products
             const int t = wid;
             if (t * 16 < n) {
                 // lane (row r = lane & 15, group g): dims 32 g .. 32 g + 31 of key r / query r
@@ -366,7 +372,8 @@ __global__ __launch_bounds__(64 * PX_W) void prefill_attn_exact_kernel(PrefillAt
 void launch_prefill_attention_exact(const PrefillAttnArgs &a, hipStream_t s) {
     if (a.n_seq <= 0 || a.max_len <= 0) return;
     dim3 grid((a.max_len + PX_ROWS - 1) / PX_ROWS, a.n_head, a.n_seq);
-    hipLaunchKernelGGL(prefill_attn_exact_kernel, grid, dim3(64 * PX_W), 0, s, a);
+    if (a.k32) hipLaunchKernelGGL(prefill_attn_exact_kernel<true>, grid, dim3(64 * PX_W), 0, s, a);
+    else hipLaunchKernelGGL(prefill_attn_exact_kernel<false>, grid, dim3(64 * PX_W), 0, s, a);
 }
 
 // ------------------------------------------------------------------- decode
