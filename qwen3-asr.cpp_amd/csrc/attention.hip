@@ -16,6 +16,7 @@
 // + a combine kernel.
 #include <algorithm>
 #include <cstdlib>
+#include <stdexcept>
 
 #include "dev_common.h"
 #include "kernels.h"
@@ -149,11 +150,239 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const float *__restrict__
     }
 }
 
+// ---------------------------------------------- encoder, fp16 MFMA, split operands
+// The same flash loop on v_mfma_f32_16x16x32_f16 with every fp32 operand split
+// into fp16 hi + lo parts (x = hi + lo to ~22 bits): S = Kh.Qh + Kh.Ql + Kl.Qh,
+// O += Vh.Ph + Vh.Pl + Vl.Ph (the lo.lo term, ~2^-22 relative, dropped).  The
+// products are exact and accumulate in fp32, so the scores and the output keep
+// fp32-level error (the reference's F32 mul_mat, src/audio_encoder.cpp:466-486)
+// at 3 f16 MFMAs where the fp32 path spends 8 f32 ones of 4x the cycles.
+// Q carries the score scale 1/8 and log2(e) (softmax by v_exp_f32); P is split
+// from p * 2^12 so its lo part stays a normal fp16 down to p ~ 2^-14 (the scale
+// is folded back with 1/l).  Two wave groups of four take alternate 64-key tiles
+// of the same 64 queries (two waves per SIMD on a one-block-per-CU grid) and
+// merge their (m, l, O) through LDS at the end.  LDS per group: K hi/lo
+// row-major [key][dim], V hi/lo transposed [dim][key'] with the keys permuted
+// into the MFMA k order of the P fragments (four consecutive keys stay
+// consecutive, so each staging thread writes 8-byte runs).
+#define EHS 72   // LDS row stride (halves) of the hi/lo tiles
+#define EH_GRP (4 * 64 * EHS)   // halves of one wave group's tiles
+
+__device__ __forceinline__ int eh_vpos(int key) {
+    // P.V k-step u takes S^T sub-tiles 2u, 2u+1; lane group g holds keys
+    // t*16 + 4g + i -> k index u*32 + 8g + 4*(t&1) + i
+    const int t = key >> 4, g = (key >> 2) & 3, i = key & 3;
+    return (t >> 1) * 32 + 8 * g + 4 * (t & 1) + i;
+}
+
+__global__ __launch_bounds__(512) void enc_attn_h_kernel(const float *__restrict__ qkv, const int *__restrict__ seg_start,
+                                                         const int *__restrict__ seg_len, int D, uint16_t *__restrict__ out,
+                                                         float *__restrict__ out32) {
+    __shared__ __attribute__((aligned(16))) f16 lds[2 * EH_GRP];
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int N = seg_len[b], r0 = seg_start[b];
+    const int qblk = blockIdx.x * 64;
+    if (qblk >= N) return;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int grp = wid >> 2, gtid = tid & 255;
+    const int g = lane >> 4, ql = lane & 15;
+    f16 *Kh = lds + grp * EH_GRP, *Kl = Kh + 64 * EHS, *Vh = Kh + 2 * 64 * EHS, *Vl = Kh + 3 * 64 * EHS;
+    const int ld = 3 * D;
+    const int q = qblk + (wid & 3) * 16 + ql;
+    const float qscale = 0.125f * 1.4426950408889634f;
+    // B operand of S^T = K Q^T, k-step s: lane holds Q[q][32s + 8g + j] * qscale
+    half8 qh[2], qlo[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
+        if (q < N) {
+            const float *qp = qkv + (long)(r0 + q) * ld + h * 64 + 32 * s + 8 * g;
+            a = *(const float4 *)qp;
+            c = *(const float4 *)(qp + 4);
+        }
+        const float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const float x = v[j] * qscale;
+            const f16 hi = (f16)x;
+            qh[s][j] = hi;
+            qlo[s][j] = (f16)(x - (float)hi);
+        }
+    }
+    floatx4 o[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++) o[d] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float m_run = -INFINITY, l_run = 0.0f;
+
+    // staging thread: keys 4*kq .. 4*kq+3 of the tile, dims c4 .. c4+3
+    const int kq = gtid >> 4, c4 = (gtid & 15) * 4;
+    float4 kpre[4], vpre[4];
+    auto fetch = [&](int kb) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int key = kb + 4 * kq + r;
+            kpre[r] = vpre[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (key < N) {
+                const float *rowp = qkv + (long)(r0 + key) * ld + h * 64 + c4;
+                kpre[r] = *(const float4 *)(rowp + D);
+                vpre[r] = *(const float4 *)(rowp + 2 * D);
+            }
+        }
+    };
+    const int ntile = (N + 63) >> 6;
+    const int niter = (ntile + 1) >> 1;
+    if (grp < ntile) fetch(grp * 64);
+    for (int it = 0; it < niter; it++) {
+        const int tile = 2 * it + grp;
+        const bool live = tile < ntile;   // the odd group's last tile may not exist
+        const int k0 = tile * 64;
+        __syncthreads();   // the previous tile's readers are done
+        if (live) {
+            const int vp = eh_vpos(4 * kq);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float kv[4] = {kpre[r].x, kpre[r].y, kpre[r].z, kpre[r].w};
+                half4 kh, kl;
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const f16 hk = (f16)kv[e];
+                    kh[e] = hk;
+                    kl[e] = (f16)(kv[e] - (float)hk);
+                }
+                *(half4 *)(Kh + (4 * kq + r) * EHS + c4) = kh;
+                *(half4 *)(Kl + (4 * kq + r) * EHS + c4) = kl;
+            }
+            const float vv[4][4] = {{vpre[0].x, vpre[0].y, vpre[0].z, vpre[0].w},
+                                    {vpre[1].x, vpre[1].y, vpre[1].z, vpre[1].w},
+                                    {vpre[2].x, vpre[2].y, vpre[2].z, vpre[2].w},
+                                    {vpre[3].x, vpre[3].y, vpre[3].z, vpre[3].w}};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                half4 vh, vl;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const f16 hv = (f16)vv[r][e];
+                    vh[r] = hv;
+                    vl[r] = (f16)(vv[r][e] - (float)hv);
+                }
+                *(half4 *)(Vh + (c4 + e) * EHS + vp) = vh;
+                *(half4 *)(Vl + (c4 + e) * EHS + vp) = vl;
+            }
+        }
+        __syncthreads();
+        if (!live) continue;
+        if (tile + 2 < ntile) fetch(k0 + 128);
+        floatx4 st[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            st[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const int off = (t * 16 + ql) * EHS + 32 * s + 8 * g;
+                const half8 ah = *(const half8 *)(Kh + off), al = *(const half8 *)(Kl + off);
+                st[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, qh[s], st[t], 0, 0, 0);
+                st[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, qlo[s], st[t], 0, 0, 0);
+                st[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, qh[s], st[t], 0, 0, 0);
+            }
+        }
+        // lane holds the scaled (log2-domain) S[q][key = k0 + t*16 + 4g + i]
+        if (k0 + 64 > N) {
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if (k0 + t * 16 + 4 * g + i >= N) st[t][i] = -INFINITY;
+        }
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) tmax = fmaxf(tmax, st[t][i]);
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float m_new = fmaxf(m_run, tmax);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        float psum = 0.0f;
+        half8 ph[2], pl[2];
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const float p = __builtin_amdgcn_exp2f(st[t][i] - m_new);
+                psum += p;
+                const float ps = p * 4096.0f;
+                const f16 hi = (f16)ps;
+                ph[t >> 1][4 * (t & 1) + i] = hi;
+                pl[t >> 1][4 * (t & 1) + i] = (f16)(ps - (float)hi);
+            }
+        psum += __shfl_xor(psum, 16, 64);
+        psum += __shfl_xor(psum, 32, 64);
+        l_run = l_run * alpha + psum;
+        m_run = m_new;
+#pragma unroll
+        for (int d = 0; d < 4; d++) o[d] *= alpha;
+        // O^T[d][q] += V^T[d][key'] P^T[key'][q]
+#pragma unroll
+        for (int d = 0; d < 4; d++)
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int off = (d * 16 + ql) * EHS + 32 * u + 8 * g;
+                const half8 ah = *(const half8 *)(Vh + off), al = *(const half8 *)(Vl + off);
+                o[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, ph[u], o[d], 0, 0, 0);
+                o[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, pl[u], o[d], 0, 0, 0);
+                o[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, ph[u], o[d], 0, 0, 0);
+            }
+    }
+    // merge the two groups: group 1 parks (m, l, O) in LDS, group 0 combines
+    __syncthreads();
+    float *park = (float *)lds;   // [4 waves][18][64 lanes]
+    if (grp == 1) {
+        float *pw = park + (wid & 3) * 18 * 64 + lane;
+        pw[0] = m_run;
+        pw[64] = l_run;
+#pragma unroll
+        for (int d = 0; d < 4; d++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) pw[(2 + 4 * d + i) * 64] = o[d][i];
+    }
+    __syncthreads();
+    if (grp == 1 || q >= N) return;
+    {
+        const float *pw = park + (wid & 3) * 18 * 64 + lane;
+        const float m1 = pw[0], l1 = pw[64];
+        const float m = fmaxf(m_run, m1);
+        const float a0 = __builtin_amdgcn_exp2f(m_run - m), a1 = __builtin_amdgcn_exp2f(m1 - m);
+        l_run = l_run * a0 + l1 * a1;
+#pragma unroll
+        for (int d = 0; d < 4; d++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) o[d][i] = o[d][i] * a0 + pw[(2 + 4 * d + i) * 64] * a1;
+    }
+    const float inv = (1.0f / l_run) * (1.0f / 4096.0f);
+    if (out32) {
+        float *dst = out32 + (long)(r0 + q) * D + h * 64;
+#pragma unroll
+        for (int d = 0; d < 4; d++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) dst[d * 16 + 4 * g + i] = o[d][i] * inv;
+    } else {
+        uint16_t *dst = out + (long)(r0 + q) * D + h * 64;
+#pragma unroll
+        for (int d = 0; d < 4; d++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) dst[d * 16 + 4 * g + i] = f_to_u16(o[d][i] * inv);
+    }
+}
+
 void launch_enc_attention(const float *qkv, const int *seg_start, const int *seg_len, int n_seg, int max_len, int D, int H,
-                          uint16_t *out, hipStream_t s, float *out32) {
+                          uint16_t *out, hipStream_t s, float *out32, bool f32_mfma) {
     if (n_seg <= 0 || max_len <= 0) return;
+    if (D != H * 64) throw std::runtime_error("encoder attention: head_dim must be 64");
     dim3 grid((max_len + 63) / 64, H, n_seg);
-    hipLaunchKernelGGL(enc_attn_kernel, grid, dim3(256), 0, s, qkv, seg_start, seg_len, D, out, out32);
+    if (f32_mfma)
+        hipLaunchKernelGGL(enc_attn_kernel, grid, dim3(256), 0, s, qkv, seg_start, seg_len, D, out, out32);
+    else
+        hipLaunchKernelGGL(enc_attn_h_kernel, grid, dim3(512), 0, s, qkv, seg_start, seg_len, D, out, out32);
 }
 
 // ===================================================== decoder q/k norm + RoPE

@@ -206,9 +206,17 @@ static const std::vector<FuseOption> &fuse_options() {
         {"dn_wdelay", "QASR_DN_WDELAY", &FuseCfg::dn_wdelay},
         {"dn_delay", "QASR_DN_DELAY", &FuseCfg::dn_delay},
         {"fa_exact_prefill", "QASR_FA_EXACT_PREFILL", &FuseCfg::fa_exact_prefill},
+        {"enc_attn_f32", "QASR_ENC_ATTN_F32", &FuseCfg::enc_attn_f32},
+        {"gemm_regs", "QASR_GEMM_REGS", &FuseCfg::gemm_regs},
         {"fa_exact_decode", "QASR_FA_EXACT_DECODE", &FuseCfg::fa_exact_decode},
     };
     return v;
+}
+
+// encoder / prefill GEMMs with the context's tile option
+static void launch_gemm_c(qasr_ctx *c, int amode, int epi, GemmArgs g, hipStream_t s) {
+    g.regs_staged = c->fuse.gemm_regs;
+    launch_gemm(amode, epi, g, s);
 }
 
 // the fused launches' sticky device error word: read (and cleared) after every
@@ -879,11 +887,11 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     // conv2: act1 (NHWC, H=64) -> act2 (NHWC, H=32)
     g.A = c->act1.as<uint16_t>(); g.W = m->conv2_w; g.ldw = 9 * C; g.M = r2; g.N = C; g.K = 9 * C;
     g.row_start = c->rs2.as<int>(); g.bias = m->conv2_b; g.out_f16 = c->act2.as<uint16_t>(); g.ldo16 = C;
-    launch_gemm(AM_CONV2, EPI_GELU_F16, g, s);
+    launch_gemm_c(c, AM_CONV2, EPI_GELU_F16, g, s);
     // conv3: act2 -> act3 rows ordered (chunk, w, h) so conv_out's A is dense
     g.A = c->act2.as<uint16_t>(); g.W = m->conv3_w; g.M = r3; g.row_start = c->rs3.as<int>(); g.bias = m->conv3_b;
     g.out_f16 = c->act3.as<uint16_t>();
-    launch_gemm(AM_CONV3, EPI_GELU_F16, g, s);
+    launch_gemm_c(c, AM_CONV3, EPI_GELU_F16, g, s);
     const bool q8 = m->q8;
     if (q8 && (rc = ensure_q8(c, N, std::max(16 * C, std::max(D, FF)), D))) return rc;
     // conv_out (no bias) + per-chunk sinusoidal PE (src/audio_encoder.cpp:147-149, :400-404)
@@ -894,7 +902,7 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
         gemm_q8(c, EPI_F32, o, nullptr, c->act3.as<uint16_t>(), 16 * C, C, m->conv_out_w, m->conv_out_d, s);
     } else {
         o.A = c->act3.as<uint16_t>(); o.lda = 16 * C; o.W = m->conv_out_w; o.ldw = 16 * C;
-        launch_gemm(AM_DENSE, EPI_F32, o, s);
+        launch_gemm_c(c, AM_DENSE, EPI_F32, o, s);
     }
     HIPCHK(hipGetLastError());
     if (c->profile_on) HIPCHK(hipEventRecord(c->ev[5], s));   // conv front-end | transformer
@@ -926,7 +934,7 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     auto linear = [&](int epi, GemmArgs g, const float *a32, const uint16_t *a16, int lda, const uint16_t *W, const uint16_t *Wd) {
         if (q8) { gemm_q8(c, epi, g, a32, a32 ? nullptr : a16, lda, 0, W, Wd, s); return; }
         g.A = a16; g.lda = lda; g.W = W; g.ldw = g.K;
-        launch_gemm(AM_DENSE, epi, g, s);
+        launch_gemm_c(c, AM_DENSE, epi, g, s);
     };
     for (int l = 0; l < hp.enc_layers; l++) {
         const EncLayer &L = m->enc[l];
@@ -935,7 +943,7 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
         q.M = N; q.N = 3 * D; q.K = D; q.bias = L.bqkv; q.out_f32 = c->eqkv.as<float>(); q.ldo = 3 * D;
         linear(EPI_F32, q, x32, xh, D, L.wqkv, L.wqkv_d);
         launch_enc_attention(c->eqkv.as<float>(), c->segs.as<int>(), c->segs.as<int>() + NS, NS, maxn, D, hp.enc_heads,
-                             c->eatt.as<uint16_t>(), s, x32);
+                             c->eatt.as<uint16_t>(), s, x32, c->fuse.enc_attn_f32 != 0);
         GemmArgs op{};
         op.M = N; op.N = D; op.K = D; op.bias = L.bo; op.res = x; op.ldr = D; op.out_f32 = x; op.ldo = D;
         linear(EPI_F32, op, x32, c->eatt.as<uint16_t>(), D, L.wo, L.wo_d);
@@ -1018,7 +1026,7 @@ static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const st
         GemmArgs q{};
         q.M = rows; q.N = QD + 2 * KD; q.K = H; q.out_f32 = c->pqkv.as<float>(); q.ldo = QD + 2 * KD;
         if (q8) gemm_q8(c, EPI_F32, q, x32, nullptr, H, 0, L.wqkv, L.wqkv_d, s);
-        else { q.A = xh; q.lda = H; q.W = L.wqkv; q.ldw = H; launch_gemm(AM_DENSE, EPI_F32, q, s); }
+        else { q.A = xh; q.lda = H; q.W = L.wqkv; q.ldw = H; launch_gemm_c(c, AM_DENSE, EPI_F32, q, s); }
         QkvPostArgs qa{};
         qa.qkv = c->pqkv.as<float>(); qa.rows = rows; qa.row_seq = d_seq; qa.row_pos = d_pos;
         qa.q_norm = L.q_norm; qa.k_norm = L.k_norm; qa.eps = hp.rms_eps; qa.rope = c->rope;
@@ -1037,7 +1045,7 @@ static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const st
         GemmArgs o{};
         o.M = rows; o.N = H; o.K = QD; o.res = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
         if (q8) gemm_q8(c, EPI_F32, o, x32, nullptr, QD, 0, L.wo, L.wo_d, s);
-        else { o.A = c->patt.as<uint16_t>(); o.lda = QD; o.W = L.wo; o.ldw = QD; launch_gemm(AM_DENSE, EPI_F32, o, s); }
+        else { o.A = c->patt.as<uint16_t>(); o.lda = QD; o.W = L.wo; o.ldw = QD; launch_gemm_c(c, AM_DENSE, EPI_F32, o, s); }
         launch_rmsnorm_f16(x, H, nullptr, rows, H, L.ffn_norm, hp.rms_eps, xh, s, x32);
         GemmArgs gu{};
         gu.M = rows; gu.N = 2 * F; gu.K = H;
@@ -1046,12 +1054,12 @@ static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const st
             gemm_q8(c, EPI_SWIGLU_F32, gu, x32, nullptr, H, 0, L.wgu, L.wgu_d, s);
         } else {
             gu.A = xh; gu.lda = H; gu.W = L.wgu; gu.ldw = H; gu.out_f16 = c->pact.as<uint16_t>(); gu.ldo16 = F;
-            launch_gemm(AM_DENSE, EPI_SWIGLU_F16, gu, s);
+            launch_gemm_c(c, AM_DENSE, EPI_SWIGLU_F16, gu, s);
         }
         GemmArgs dn{};
         dn.M = rows; dn.N = H; dn.K = F; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
         if (q8) gemm_q8(c, EPI_F32, dn, x32, nullptr, F, 0, L.wd, L.wd_d, s);
-        else { dn.A = c->pact.as<uint16_t>(); dn.lda = F; dn.W = L.wd; dn.ldw = F; launch_gemm(AM_DENSE, EPI_F32, dn, s); }
+        else { dn.A = c->pact.as<uint16_t>(); dn.lda = F; dn.W = L.wd; dn.ldw = F; launch_gemm_c(c, AM_DENSE, EPI_F32, dn, s); }
     }
     return 0;
 }
@@ -1079,7 +1087,7 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
         GemmArgs lm{};
         lm.A = xl; lm.lda = H; lm.W = m->embd; lm.ldw = H; lm.M = B; lm.N = hp.vocab; lm.K = H;
         lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
-        launch_gemm(AM_DENSE, EPI_ARGMAX, lm, s);
+        launch_gemm_c(c, AM_DENSE, EPI_ARGMAX, lm, s);
     }
     HIPCHK(hipMemsetAsync(c->d_step, 0, 4, s));
     launch_argmax_finish(c->d_amax, B, c->d_tok, c->d_hist, c->hist_cap, c->d_step, s);
@@ -1857,7 +1865,7 @@ static int align_classes(qasr_ctx *c, const float *pcm, int n, const std::vector
         GemmArgs g{};
         g.A = c->atx.as<uint16_t>(); g.lda = H; g.W = m->cls_w; g.ldw = H; g.M = NT; g.N = m->cls_rows; g.K = H;
         g.amax = c->aam.as<unsigned long long>(); g.n_valid = hp.classify_num;
-        launch_gemm(AM_DENSE, EPI_ARGMAX, g, s);
+        launch_gemm_c(c, AM_DENSE, EPI_ARGMAX, g, s);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(keys.data(), c->aam.p, (size_t)NT * 8, hipMemcpyDeviceToHost, s));
     }

@@ -240,10 +240,173 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     gemm_epilogue<BM, BN, EPI>(g, acc, m0, n0, wr, wc, lane);
 }
 
+// ---------------------------------------------------- LDS-DMA tiled GEMM
+// The same tile, fragments, swizzle and epilogue as gemm_kernel, but the
+// operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4: no staging
+// registers, no ds_write pass) through an NB-deep ring of stages (KS 32-deep
+// slabs each), NB - 1 stages in flight behind the one being multiplied; one raw
+// barrier per stage after a counted vmcnt (each wave waits only for its own
+// pieces of the stage it is about to read).  The swizzle is applied on the
+// source side: lane l of a 1-KiB piece lands at row l>>2, chunk position l&3,
+// and fetches chunk (l&3) ^ ((row>>1)&3) -- the position the fragment reads
+// expect.  Rows past M and conv taps in the padding fetch a global zero line
+// (LDS-DMA has no per-lane predicate).
+typedef __attribute__((address_space(3))) void lds_void_g;
+typedef __attribute__((address_space(1))) void glb_void_g;
+__device__ __attribute__((aligned(64))) uint32_t g_zero_line[16];
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int KS, int NB, int AMODE, int EPI>
+__global__ __launch_bounds__(256) void gemm_glds_kernel(GemmArgs g) {
+    constexpr int FM = BM / 32, FN = BN / 32;
+    constexpr int ROWS = BM + BN;
+    constexpr int SLAB = ROWS * 32;        // halves per 32-deep slab
+    constexpr int RG = ROWS / 16;          // 1-KiB pieces per slab
+    constexpr int NP = KS * RG;            // pieces per stage
+    constexpr int NW = (NP + 3) / 4;       // pieces per wave per stage (uniform: vmcnt counts)
+    constexpr int PAD = NW * 4 - NP;       // dummy pieces (zero line -> a scratch KiB) keep it uniform
+    static_assert(ROWS % 16 == 0, "16-row pieces");
+    static_assert(NB >= 2 && NB <= 4 && (NB - 2) * NW < 64, "ring depth");
+    constexpr int INFO = AMODE == AM_DENSE ? 0 : BM * 8;   // int4 row descriptors (conv modes)
+    constexpr int SCR = PAD ? 512 : 0;
+    __shared__ __attribute__((aligned(16))) uint16_t smem[NB * KS * SLAB + SCR + INFO];
+    int4 *rowinfo = (int4 *)(smem + NB * KS * SLAB + SCR);
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid >> 1, wc = wid & 1;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int M = g.M, K = g.K;
+
+    if constexpr (AMODE != AM_DENSE) {
+        for (int r = tid; r < BM; r += 256) {
+            const int row = m0 + r;
+            int4 info = make_int4(-1, 0, 0, 0);
+            if (row < M) {
+                const int c = find_chunk(g.row_start, g.n_chunks, row);
+                const ChunkDesc cd = g.chunks[c];
+                const int local = row - g.row_start[c];
+                int oh, ow, base, Win;
+                if constexpr (AMODE == AM_CONV2) {
+                    ow = local % cd.W2; oh = local / cd.W2; base = cd.row1; Win = cd.W1;
+                } else {
+                    oh = local % 16; ow = local / 16; base = cd.row2; Win = cd.W2;
+                }
+                info = make_int4(base, 2 * oh - 1, 2 * ow - 1, Win);
+            }
+            rowinfo[r] = info;
+        }
+        __syncthreads();
+    }
+
+    floatx4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int lrow = lane >> 2, lpos = lane & 3;
+    auto issue = [&](int k0, int buf) {
+        int tap = 0, kh = 0, kw = 0;
+        if constexpr (AMODE != AM_DENSE) {   // one 3x3 tap per stage (host: C % (32*KS) == 0)
+            tap = k0 / g.C;
+            kh = tap / 3;
+            kw = tap - kh * 3;
+        }
+#pragma unroll
+        for (int p = 0; p < NW; p++) {
+            const int i = wid + 4 * p;
+            if (PAD && i >= NP) {   // wave-uniform
+                __builtin_amdgcn_global_load_lds((glb_void_g *)g_zero_line, (lds_void_g *)(smem + NB * KS * SLAB), 16, 0, 0);
+                continue;
+            }
+            const int s = i / RG, rg = i - s * RG;
+            const int r = rg * 16 + lrow;
+            const int k = k0 + s * 32 + ((lpos ^ ((r >> 1) & 3)) << 3);
+            const uint16_t *src = (const uint16_t *)g_zero_line;
+            if (rg * 16 < BM) {
+                const int row = m0 + r;
+                if constexpr (AMODE == AM_DENSE) {
+                    if (row < M) src = g.A + (long)row * g.lda + k;
+                } else {
+                    const int4 ri = rowinfo[r];
+                    const int ih = ri.y + kh, iw = ri.z + kw;
+                    const int Hin = AMODE == AM_CONV2 ? 64 : 32;
+                    if (ri.x >= 0 && ih >= 0 && ih < Hin && iw >= 0 && iw < ri.w)
+                        src = g.A + ((long)(ri.x + ih * ri.w + iw) * g.C + (k - tap * g.C));
+                }
+            } else {
+                src = g.W + (long)(n0 + r - BM) * g.ldw + k;
+            }
+            __builtin_amdgcn_global_load_lds((glb_void_g *)src, (lds_void_g *)(smem + (buf * KS + s) * SLAB + rg * 512), 16, 0,
+                                             0);
+        }
+    };
+
+    const int nk = K / (32 * KS);
+#pragma unroll
+    for (int st = 0; st < NB - 1; st++)
+        if (st < nk) issue(st * 32 * KS, st);
+    int buf = 0;
+    for (int kt = 0; kt < nk; kt++) {
+        // this wave's pieces of stage kt have landed once at most the later
+        // stages' pieces are outstanding
+        const int ahead = nk - 1 - kt;
+        if constexpr (NB >= 4) {
+            if (ahead >= 2) wait_vm<2 * NW>();
+            else if (ahead == 1) wait_vm<NW>();
+            else wait_vm<0>();
+        } else if constexpr (NB == 3) {
+            if (ahead >= 1) wait_vm<NW>();
+            else wait_vm<0>();
+        } else {
+            wait_vm<0>();
+        }
+        asm volatile("s_barrier" ::: "memory");   // every wave's pieces landed; stage kt-1's readers done
+        if (kt + NB - 1 < nk) {
+            int nb = buf + NB - 1;
+            if (nb >= NB) nb -= NB;
+            issue((kt + NB - 1) * 32 * KS, nb);
+        }
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+            const uint16_t *sl = smem + (buf * KS + s) * SLAB;
+            half8 af[FM], bf[FN];
+            const int q = lane >> 4;
+#pragma unroll
+            for (int i = 0; i < FM; i++) {
+                const int r = wr * (BM / 2) + i * 16 + (lane & 15);
+                af[i] = *(const half8 *)(sl + r * 32 + ((q ^ ((r >> 1) & 3)) << 3));
+            }
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                const int r = BM + wc * (BN / 2) + j * 16 + (lane & 15);
+                bf[j] = *(const half8 *)(sl + r * 32 + ((q ^ ((r >> 1) & 3)) << 3));
+            }
+#pragma unroll
+            for (int i = 0; i < FM; i++)
+#pragma unroll
+                for (int j = 0; j < FN; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        if (++buf == NB) buf = 0;
+    }
+    gemm_epilogue<BM, BN, EPI>(g, acc, m0, n0, wr, wc, lane);
+}
+
 template <int BM, int BN, int KS, int AMODE, int EPI>
 static void run_gemm(const GemmArgs &g, hipStream_t s) {
     dim3 grid(g.N / BN, (g.M + BM - 1) / BM);
     hipLaunchKernelGGL((gemm_kernel<BM, BN, KS, AMODE, EPI>), grid, dim3(256), 0, s, g);
+}
+
+template <int BM, int BN, int KS, int NB, int AMODE, int EPI>
+static void run_glds(const GemmArgs &g, hipStream_t s) {
+    dim3 grid(g.N / BN, (g.M + BM - 1) / BM);
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, KS, NB, AMODE, EPI>), grid, dim3(256), 0, s, g);
 }
 
 template <int AMODE, int EPI>
@@ -254,7 +417,8 @@ static void dispatch_tiles(const GemmArgs &g, hipStream_t s) {
         if (wide && g.N == 480) {
             // all 480 output channels per block: the gathered A tile is read once
             // (N/96 = 5 re-reads of the im2col rows otherwise), W stays L2-resident
-            run_gemm<64, 480, 1, AMODE, EPI>(g, s);
+            if (g.regs_staged) run_gemm<64, 480, 1, AMODE, EPI>(g, s);
+            else run_glds<64, 480, 1, 2, AMODE, EPI>(g, s);
         } else if (g.N % 96 == 0 && g.C % 96 == 0) {
             if (g.M >= 4096) run_gemm<128, 96, 3, AMODE, EPI>(g, s);
             else run_gemm<64, 96, 3, AMODE, EPI>(g, s);
@@ -267,7 +431,9 @@ static void dispatch_tiles(const GemmArgs &g, hipStream_t s) {
         // clip) -> 64x64 with 4 slabs per stage for the narrow, deep
         // projections (N <= 1024), 96x64 for the wide ones (N >= 3072)
         const bool big = g.M >= 2048 && g.N % 128 == 0;
-        if (big && g.K % 64 == 0) {
+        if (big && !g.regs_staged) {   // LDS-DMA stages (tools/micro/glds_gemm_bench.hip: +5-10 %)
+            run_glds<128, 128, 1, 2, AMODE, EPI>(g, s);
+        } else if (big && g.K % 64 == 0) {
             if (g.K <= 1024) run_gemm<128, 128, 1, AMODE, EPI>(g, s);
             else run_gemm<128, 128, 2, AMODE, EPI>(g, s);
         } else if (!big && g.N <= 1024 && g.K % 128 == 0 && g.K >= 2048) {

@@ -72,6 +72,7 @@ struct GemmArgs {
     // Wd [N][K/32] (ggml block_q8_0 split into quants and scales)
     const int8_t *Aq; const float *Ad; int ldad;
     const int8_t *Wq; const uint16_t *Wd;
+    int regs_staged;                      // 1: register-staged tiles instead of the LDS-DMA ones (A/B option)
 };
 void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s);
 // decode-batch GEMM (gemm_skinny.hip): dense A, M <= 128, K % 128 == 0; returns
@@ -141,6 +142,8 @@ struct FuseCfg {
     int layer = 0;                      // batch 1: the whole decoder layer in one launch (layer1_kernel; measured slower)
     int gu_delay = 16, dn_wdelay = 30, dn_delay = 8;   // layer launch: gate/up weight request, down weight request,
                                                        // down first poll (s_sleep(8) units)
+    int enc_attn_f32 = 0;
+    int gemm_regs = 0;                  // encoder/prefill GEMMs on the register-staged tiles (gemm.hip)               // encoder attention on fp32 MFMA instead of split fp16 operands
     int fa_exact_prefill = 1;           // prefill attention with ggml's CPU FA numerics (fa_exact.hip)
     int fa_exact_decode = -1;           // decode attention likewise: 1 on, 0 off (fp32 V accumulation), -1 = on for
                                         // Q8_0 models only (batch 1 exact skips the fused QKV + attention launch)
@@ -170,10 +173,11 @@ void launch_rmsnorm_f16(const float *x, int ldx, const int *row_idx, int M, int 
 void launch_rmsnorm_q8(const float *x, int ldx, int M, int D, const float *w, float eps, int8_t *yq, float *yd, hipStream_t s);
 
 // ---------------------------------------------------------------- attention
-// encoder: full bidirectional fp32 attention per clip segment, head_dim 64.
+// encoder: full bidirectional attention per clip segment, head_dim 64, fp32-level
+// arithmetic (split fp16 operands on f16 MFMA, or fp32 MFMA when f32_mfma).
 // qkv fp32 [rows][3*D]; out fp16 [rows][D] (or fp32 out32 when non-null)
 void launch_enc_attention(const float *qkv, const int *seg_start, const int *seg_len, int n_seg, int max_len,
-                          int D, int H, uint16_t *out, hipStream_t s, float *out32 = nullptr);
+                          int D, int H, uint16_t *out, hipStream_t s, float *out32 = nullptr, bool f32_mfma = false);
 
 // rows of padding after the last K/V cache region: the exact-attention chains
 // (fa_exact.hip) load V a few batches ahead without clamping

@@ -106,6 +106,33 @@ def test_full_30s_batch_properties(full):
         assert c.transcribe([pcm], max_tokens=24, ignore_eos=True).tokens[0] == t
 
 
+def test_full_lds_dma_gemm_bit_identical(full):
+    """The LDS-DMA GEMM tiles (the default for >= 2048-row projections and the
+    implicit-GEMM convs) multiply the same fragments in the same k order as the
+    register-staged tiles (option gemm_regs): encoder features of 8 x 30 s
+    clips (3120 rows) and the batch's prefill logits (3240 rows) bit-identical,
+    and the batched features equal to a single clip's (small-M tiles)."""
+    m, _, _ = full
+    clips = [qasr.synth_pcm(15000 + i, 30 * SR) for i in range(8)]
+    cb = qasr.Context(m, max_batch=8, max_ctx=512)
+    try:
+        mels = cb.mel(clips)
+        out = {}
+        for regs in (1, 0):
+            cb.set_option("gemm_regs", regs)
+            f = cb.encode(mels)
+            ids, pos = m.build_prompt(f[0].shape[0])
+            lg, _ = cb.prefill([ids] * 8, f, [pos] * 8)
+            out[regs] = (f, lg)
+        single = cb.encode([mels[3]])[0]
+    finally:
+        cb.close()
+    for a, b in zip(out[0][0], out[1][0]):
+        assert np.array_equal(a, b)
+    assert np.array_equal(np.asarray(out[0][1]), np.asarray(out[1][1]))
+    assert np.array_equal(single, out[0][0][3])
+
+
 FUSE_KNOBS = {"QASR_FUSE_FFN": dict(fuse_ffn=0), "QASR_FUSE_QKV": dict(fuse_qkv=0, fuse_o=0), "QASR_FUSE_O": dict(fuse_o=0)}
 
 

@@ -84,6 +84,28 @@ def test_encode_matches_oracle(tiny, tiny_oracle, secs):
     assert mx <= 2e-2 and mean <= 1e-3, (mx, mean)
 
 
+@pytest.mark.parametrize("secs", [2.37, 12.3])
+def test_encoder_attention_paths_match_oracle(tiny, tiny_oracle, secs):
+    """Encoder attention on split fp16 operands (the default) and on fp32 MFMA
+    (option enc_attn_f32): both within the fp32 encoder bar of the oracle, the
+    split path no further from it than the fp32 one (the two differ by fp16
+    rounding flips of the attention output that feeds the o-projection)."""
+    _, c = tiny
+    mel = op.log_mel(qasr.synth_pcm(4100, int(secs * SR)))
+    o = tiny_oracle.encode(mel)
+    try:
+        c.set_option("enc_attn_f32", 1)
+        g32 = c.encode([mel])[0]
+    finally:
+        c.set_option("enc_attn_f32", 0)
+    g = c.encode([mel])[0]
+    mx, mean = _stats(g, o)
+    mx32, mean32 = _stats(g32, o)
+    assert mx <= 2e-2 and mean <= 1e-3, (mx, mean)
+    assert mx32 <= 2e-2 and mean32 <= 1e-3, (mx32, mean32)
+    assert mean <= 1.25 * mean32 + 1e-5 and mx <= 1.5 * mx32 + 1e-3, (mx, mean, mx32, mean32)
+
+
 def test_encode_batch_equals_single(tiny):
     _, c = tiny
     mels = [op.log_mel(qasr.synth_pcm(5000 + i, n)) for i, n in enumerate([SR, 3 * SR + 500, 2 * SR - 7])]
