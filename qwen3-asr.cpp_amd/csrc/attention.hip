@@ -641,10 +641,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     __shared__ float sc[2][SPL];
     __shared__ __attribute__((aligned(16))) float ored[DWAVES * 4][2][128];   // [wave x row][head][dim]
     __shared__ float cml[2][2];
-    __shared__ float wsp[2][32];         // combine: per-split weights of a pass
-    __shared__ float lsum[2];
     __shared__ int last;
-    __shared__ floatx4 stage[16 * 66];   // combine: passes of up to 16 splits x 2 heads x 33 float4
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
     const long blk = sp + (long)nsp * (g + (long)a.n_kv_head * b);   // dev-trace row
@@ -858,10 +855,10 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     mark(3);
     if (!last) return;
     // ---- last arriver: combine the partials of both heads (empty ones weigh 0).
-    //      Passes of up to 32 splits are staged through LDS with one burst of
-    //      16-B sc1 loads each (a per-split load loop would serialise ~nsp
-    //      memory latencies).  Wave h derives head h's split weights once
-    //      (lane = split); passes merge with the usual online rescale.
+    //      Thread (head hh, dim d) loads its dimension and the (m, l) pair of up
+    //      to 16 splits at a time with sc1 loads (all in flight together, one
+    //      memory latency per pass) and merges them in registers with the usual
+    //      online rescale: no LDS staging, no barrier.
     if (tid == 0) {
         __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if constexpr (FUSED)   // every split is past its wait: re-arm the 8 replicas
@@ -870,33 +867,30 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     const int hh = tid >> 7, d = tid & 127;
     float M = -INFINITY, L = 0.f, O = 0.f;
     for (int s0 = 0; s0 < nsp; s0 += 16) {
-        const int ns = min(16, nsp - s0), n4 = ns * 66;
-        const floatx4 *srcp = (const floatx4 *)(gpart + (long)s0 * 264);
-        floatx4 v[5];
-        ld_sc1_x4_burst5(srcp, tid, n4, v);
-        if (s0 == 0) mark(5);
-        __syncthreads();   // previous pass's readers are done with stage / wsp
+        const int ns = min(16, nsp - s0);
+        float ov[16];
+        unsigned long long ml[16];
 #pragma unroll
-        for (int j = 0; j < 5; j++)
-            if (tid + 256 * j < n4) stage[tid + 256 * j] = v[j];
-        __syncthreads();
-        const float *sf = (const float *)stage;
-        if (wid < 2) {
-            const float ms = lane < ns ? sf[(lane * 2 + wid) * 132 + 128] : -INFINITY;
-            const float ls = lane < ns ? sf[(lane * 2 + wid) * 132 + 129] : 0.f;
-            const float Mprev = s0 == 0 ? -INFINITY : cml[wid][0];   // running max of head wid
-            const float Mn = fmaxf(Mprev, wave_max(ms));
-            const float w = lane < ns ? expf(ms - Mn) : 0.f;
-            if (lane < 32) wsp[wid][lane] = w;
-            const float lp = wave_sum(ls * w);
-            if (lane == 0) { lsum[wid] = lp; cml[wid][0] = Mn; }
+        for (int u = 0; u < 16; u++) {
+            const float *pp = gpart + ((long)(s0 + min(u, ns - 1)) * 2 + hh) * 132;
+            ov[u] = __uint_as_float(__hip_atomic_load((const uint32_t *)(pp + d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            ml[u] = __hip_atomic_load((const unsigned long long *)(pp + 128), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        __syncthreads();
-        const float Mn = cml[hh][0];
+        if (s0 == 0) mark(5);
+        float Mn = M;
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+            if (u < ns) Mn = fmaxf(Mn, __uint_as_float((uint32_t)ml[u]));
         const float r = expf(M - Mn);   // first pass: exp(-inf) = 0 on L = O = 0
-        L = L * r + lsum[hh];
-        float op = 0.f;
-        for (int s2 = 0; s2 < ns; s2++) op = fmaf(wsp[hh][s2], sf[(s2 * 2 + hh) * 132 + d], op);
+        float lp = 0.f, op = 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+            if (u < ns) {
+                const float w = __expf(__uint_as_float((uint32_t)ml[u]) - Mn);
+                lp = fadd_rn(lp, fmul_rn(__uint_as_float((uint32_t)(ml[u] >> 32)), w));
+                op = fmaf(w, ov[u], op);
+            }
+        L = L * r + lp;
         O = O * r + op;
         M = Mn;
     }
@@ -995,13 +989,35 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
     if (lane == 0) o.out_f32[row] = fadd_rn(acc, res);
 }
 
+// Prefetch role: after pf_delay, plain 16-B loads over the given ranges (values
+// dropped) so the lines sit in the Infinity Cache when the next launch streams
+// them; nothing waits on these workgroups.
+__device__ __forceinline__ void prefetch_body(const DecodeAttnArgs a, int j) {
+    for (int i = 0; i < a.pf_delay; i++) __builtin_amdgcn_s_sleep(8);
+    const long n = a.pf_n0 + a.pf_n1, stride = (long)a.pf_blocks * 256;
+    constexpr int U = 12;
+    for (long c0 = (long)j * 256 + threadIdx.x; c0 < n; c0 += U * stride) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const long c = c0 + u * stride;
+            v[u] = u32x4{0u, 0u, 0u, 0u};
+            if (c < n) v[u] = c < a.pf_n0 ? ((const u32x4 *)a.pf0)[c] : ((const u32x4 *)a.pf1)[c - a.pf_n0];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) asm volatile("" ::"v"(v[u]));
+    }
+}
+
 template <int SPL>
 __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnArgs a, GemvArgs o) {
     constexpr int K = 1024, NT = 2, RPW = 2;
     stamp_start(a.stamp);
     if (blockIdx.x >= 512) {
         const int j = blockIdx.x - 512, nsp = a.grid_splits, nat = nsp * a.n_kv_head;   // grid_splits: this launch's splits
-        if (j >= nat) oproj1_body(o, a, j - nat);
+        const int nob = a.att_done ? 256 : 0;
+        if (j >= nat + nob) prefetch_body(a, j - nat - nob);
+        else if (j >= nat) oproj1_body(o, a, j - nat);
         else decode_attn_body<SPL, true>(a, j % nsp, j / nsp, 0, nsp);
         stamp_end(a.stamp);
         return;
@@ -1465,7 +1481,9 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     if (512 + ns * a.n_kv_head > slots) return 0;
     const bool with_o2 = with_o && fit_o;
     if (dry) return with_o2 ? 2 : 1;
-    const dim3 grid(512 + ns * a.n_kv_head + (with_o2 ? o->N / 4 : 0));
+    // prefetch workgroups wait on nothing: they need no co-residency
+    const int npf = a.pf0 && cfg.pf_blocks > 0 ? cfg.pf_blocks : 0;
+    const dim3 grid(512 + ns * a.n_kv_head + (with_o2 ? o->N / 4 : 0) + npf);
     // K/V delay ~2 us: measured optimum on MI355X (tools/job_delay.sh: 0 -> 236.3, 10 -> 232.0, 18 -> 240.3 ms decode)
     DecodeAttnArgs ad = a;
     ad.fuse_delay = cfg.qkv_delay;
@@ -1475,6 +1493,8 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     ad.err = cfg.err;
     ad.grid_splits = ns;   // the kernel's split count
     if (!with_o2) ad.att_done = nullptr;
+    ad.pf_blocks = npf;
+    ad.pf_delay = cfg.pf_delay;
     const GemvArgs oa = with_o2 ? *o : GemvArgs{};
     if (spl1 == 128) hipLaunchKernelGGL(qkv_attn1_kernel<128>, grid, dim3(256), 0, s, q, ad, oa);
     else hipLaunchKernelGGL(qkv_attn1_kernel<DSPLIT>, grid, dim3(256), 0, s, q, ad, oa);

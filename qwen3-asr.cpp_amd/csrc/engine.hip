@@ -208,6 +208,8 @@ static const std::vector<FuseOption> &fuse_options() {
         {"fa_exact_prefill", "QASR_FA_EXACT_PREFILL", &FuseCfg::fa_exact_prefill},
         {"enc_attn_f32", "QASR_ENC_ATTN_F32", &FuseCfg::enc_attn_f32},
         {"gemm_regs", "QASR_GEMM_REGS", &FuseCfg::gemm_regs},
+        {"pf_blocks", "QASR_PF_BLOCKS", &FuseCfg::pf_blocks},
+        {"pf_delay", "QASR_PF_DELAY", &FuseCfg::pf_delay},
         {"fa_exact_decode", "QASR_FA_EXACT_DECODE", &FuseCfg::fa_exact_decode},
     };
     return v;
@@ -1191,6 +1193,10 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         const bool exact = exact_decode(c);
         const bool fusable = skinny && B == 1 && !q8 && !skip && !exact;
         if (fusable) da.att_done = c->d_attdone;
+        if (fusable && c->fuse.pf_blocks > 0) {   // the layer's FFN weights -> Infinity Cache during the attention chain
+            da.pf0 = L.wgu; da.pf_n0 = (long)2 * F * H * 2 / 16;
+            da.pf1 = L.wd; da.pf_n1 = (long)H * F * 2 / 16;
+        }
         unsigned int *ocnt = c->d_ocnt + (size_t)l * 512, *ocnt_next = c->d_ocnt + (size_t)((l + 1) % nl) * 512;
         unsigned int *fcnt = c->d_ffncnt + (size_t)l * 512, *fcnt_next = c->d_ffncnt + (size_t)((l + 1) % nl) * 512;
         // the whole layer in one launch (decided without launching), else 0 = separate

@@ -142,8 +142,10 @@ struct FuseCfg {
     int layer = 0;                      // batch 1: the whole decoder layer in one launch (layer1_kernel; measured slower)
     int gu_delay = 16, dn_wdelay = 30, dn_delay = 8;   // layer launch: gate/up weight request, down weight request,
                                                        // down first poll (s_sleep(8) units)
-    int enc_attn_f32 = 0;
-    int gemm_regs = 0;                  // encoder/prefill GEMMs on the register-staged tiles (gemm.hip)               // encoder attention on fp32 MFMA instead of split fp16 operands
+    int enc_attn_f32 = 0;               // encoder attention on fp32 MFMA instead of split fp16 operands
+    int gemm_regs = 0;                  // encoder/prefill GEMMs on the register-staged tiles (gemm.hip)
+    int pf_blocks = 0, pf_delay = 30;   // batch 1: workgroups of the QKV launch that pull the layer's FFN weights
+                                        // into the Infinity Cache while the attention chain runs (s_sleep(8) units)
     int fa_exact_prefill = 1;           // prefill attention with ggml's CPU FA numerics (fa_exact.hip)
     int fa_exact_decode = -1;           // decode attention likewise: 1 on, 0 off (fp32 V accumulation), -1 = on for
                                         // Q8_0 models only (batch 1 exact skips the fused QKV + attention launch)
@@ -257,6 +259,9 @@ struct DecodeAttnArgs {
     unsigned int qkv_need;               // fused launches: QKV-block arrivals per kv group (0 = 64)
     float *scores;                       // non-null (separate launch only): scores mode -- the splits write their
                                          // scaled scores [B][n_head][max_ctx] (+ the new K/V rows) and stop there
+    const uint16_t *pf0, *pf1;           // fused launch: byte ranges pulled into the Infinity Cache (null: none)
+    long pf_n0, pf_n1;                   // their sizes in 16-B lines
+    int pf_blocks, pf_delay;
 };
 // Batch 1, the whole decoder layer in one launch (attention.hip layer1_kernel):
 // QKV (256 blocks) -> attention splits -> o-projection (128) -> gate/up (192)
