@@ -691,7 +691,26 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     // latencies in series).  The host sizes the grid to the context
     // (grid_splits, a 256-key bucket); a split past this sequence's end is
     // fully masked and publishes an empty partial (m = -inf, l = 0, O = 0).
-    if constexpr (FUSED) {
+    if (FUSED && a.gran) {
+        // granule hand-off: each lane polls its own two {value, tag} granules
+        // (sc1 loads) until both carry this step's tag -- the data arrives with
+        // its own flag, no drain / arrival count / second load (MI355X guide,
+        // hand-off table: data-tagged granules).  Bounded like the counter wait.
+        const uint32_t tag = ((uint32_t)a.pos[b] << 5) | (uint32_t)a.layer;
+        const unsigned long long *gp = a.gran + (src - raw) + lane;
+        unsigned long long v0 = 0, v1 = 0;
+        bool ok = false;
+        for (int it = 0; it < a.poll_limit; it++) {
+            v0 = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v1 = __hip_atomic_load(gp + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = (uint32_t)(v0 >> 32) == tag && (uint32_t)(v1 >> 32) == tag;
+            if (__all(ok)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_QKV_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        x0 = __uint_as_float((uint32_t)v0);
+        x1 = __uint_as_float((uint32_t)v1);
+    } else if constexpr (FUSED) {
         // wait for the kv group's 64 QKV workgroups (bounded: a lost arrival must
         // not hang the GPU), then read their write-through outputs with sc1 loads
         // A wait that runs out sets DEVERR_QKV_WAIT and the split still
@@ -1029,6 +1048,7 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
     // the block's 8 rows: q rows of heads 2g, 2g+1, then k, then v of group g
     const int rbase = loc < 32 ? grp * 256 + loc * 8 : loc < 48 ? QD + grp * 128 + (loc - 32) * 8 : QD + KD + grp * 128 + (loc - 48) * 8;
     const int row0 = rbase + wid * RPW;
+    const uint32_t gtag = a.gran ? ((uint32_t)a.pos[0] << 5) | (uint32_t)a.layer : 0u;
     half8 wv[RPW][NT];
 #pragma unroll
     for (int r = 0; r < RPW; r++)
@@ -1083,7 +1103,18 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
 #pragma unroll
             for (int e = 0; e < 8; e++) acc = fmaf((float)wv[r][t][e], xf[t][e], acc);
         acc = wave_sum(acc);
-        if (lane == 0) __hip_atomic_store((uint32_t *)(q.out_f32 + row0 + r), __float_as_uint(acc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.gran) {   // one 8-byte write-through {value, tag} store per output: the flag travels with the data
+            if (lane == 0)
+                __hip_atomic_store(a.gran + row0 + r, ((unsigned long long)gtag << 32) | __float_as_uint(acc), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else if (lane == 0) {
+            __hip_atomic_store((uint32_t *)(q.out_f32 + row0 + r), __float_as_uint(acc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (a.gran) {   // nothing to drain or count
+        if (q.trace && threadIdx.x == 0) q.trace[blockIdx.x * 8 + 1] = rt_now();
+        stamp_end(a.stamp);
+        return;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1177,6 +1208,7 @@ __device__ __forceinline__ void l1_qkv(const GemvArgs &q, const DecodeAttnArgs &
     const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
     const int rbase = loc < 16 ? grp * 256 + loc * 16 : loc < 24 ? QD + grp * 128 + (loc - 16) * 16 : QD + KD + grp * 128 + (loc - 24) * 16;
     const int row0 = rbase + wid * RPW;
+    const uint32_t gtag = a.gran ? ((uint32_t)a.pos[0] << 5) | (uint32_t)a.layer : 0u;
     half8 wv[RPW][NT];
 #pragma unroll
     for (int r = 0; r < RPW; r++)
@@ -1231,7 +1263,18 @@ __device__ __forceinline__ void l1_qkv(const GemvArgs &q, const DecodeAttnArgs &
 #pragma unroll
             for (int e = 0; e < 8; e++) acc = fmaf((float)wv[r][t][e], xf[t][e], acc);
         acc = wave_sum(acc);
-        if (lane == 0) __hip_atomic_store((uint32_t *)(q.out_f32 + row0 + r), __float_as_uint(acc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.gran) {   // one 8-byte write-through {value, tag} store per output: the flag travels with the data
+            if (lane == 0)
+                __hip_atomic_store(a.gran + row0 + r, ((unsigned long long)gtag << 32) | __float_as_uint(acc), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else if (lane == 0) {
+            __hip_atomic_store((uint32_t *)(q.out_f32 + row0 + r), __float_as_uint(acc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (a.gran) {   // nothing to drain or count
+        if (q.trace && threadIdx.x == 0) q.trace[blockIdx.x * 8 + 1] = rt_now();
+        stamp_end(a.stamp);
+        return;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -116,6 +116,8 @@ struct qasr_ctx {
     float *d_scores = nullptr;     // exact decode attention: [B][n_head][max_ctx] scaled scores
     unsigned int *d_counter = nullptr, *d_done = nullptr;
     unsigned int *d_qcnt = nullptr;   // fused batch-1 QKV + attention: QKV-block arrivals per kv group
+    unsigned long long *d_gran = nullptr;   // ... or its outputs as tagged granules (zeroed by every prefill)
+    bool qkv_in_gran = false;               // the captured step's last layer hands its QKV over in granules
     unsigned int *d_attdone = nullptr;   // fused batch-1 o-proj: combiner arrivals (8 replicas)
     unsigned int *d_ffncnt = nullptr;    // fused batch-1 FFN: gate/up arrivals, [layer][32 shards][16]
     unsigned int *d_ocnt = nullptr;      // batch-1 layer launch: o-proj arrivals, [layer][32 shards][16]
@@ -208,6 +210,7 @@ static const std::vector<FuseOption> &fuse_options() {
         {"fa_exact_prefill", "QASR_FA_EXACT_PREFILL", &FuseCfg::fa_exact_prefill},
         {"enc_attn_f32", "QASR_ENC_ATTN_F32", &FuseCfg::enc_attn_f32},
         {"gemm_regs", "QASR_GEMM_REGS", &FuseCfg::gemm_regs},
+        {"gran", "QASR_GRAN", &FuseCfg::gran},
         {"pf_blocks", "QASR_PF_BLOCKS", &FuseCfg::pf_blocks},
         {"pf_delay", "QASR_PF_DELAY", &FuseCfg::pf_delay},
         {"fa_exact_decode", "QASR_FA_EXACT_DECODE", &FuseCfg::fa_exact_decode},
@@ -692,6 +695,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_scores, (size_t)B * hp.n_head * max_ctx * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_qcnt, (size_t)hp.n_kv_head * 8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_attdone, (size_t)8 * 16 * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_gran, (size_t)(QD + 2 * KD) * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_ffncnt, (size_t)hp.dec_layers * 512 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_ocnt, (size_t)hp.dec_layers * 512 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_err, 4)) ||
@@ -706,6 +710,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     HIPCHK(hipMemset(c->d_qcnt, 0, (size_t)hp.n_kv_head * 8 * 16 * 4));
     HIPCHK(hipMemset(c->d_ocnt, 0, (size_t)hp.dec_layers * 512 * 4));
     HIPCHK(hipMemset(c->d_attdone, 0, (size_t)8 * 16 * 4));
+    HIPCHK(hipMemset(c->d_gran, 0, (size_t)(QD + 2 * KD) * 8));
     HIPCHK(hipMemset(c->d_ffncnt, 0, (size_t)hp.dec_layers * 512 * 4));
     HIPCHK(hipMemset(c->d_done, 0, 4));
     HIPCHK(hipMemset(c->d_err, 0, 4));
@@ -777,6 +782,15 @@ extern "C" int qasr_debug_read(qasr_ctx *c, const char *buffer, void *dst, int64
     else return fail(QASR_ERR_ARG, "unknown buffer '" + n + "'");
     if (bytes > cap) return fail(QASR_ERR_ARG, "read past the buffer");
     HIPCHK(hipSetDevice(c->m->device));
+    if (n == "qkv" && c->qkv_in_gran) {   // the last layer's QKV went out as {value, tag} granules (batch 1)
+        std::vector<unsigned long long> g(QD + 2 * KD);
+        HIPCHK(hipMemcpyAsync(g.data(), c->d_gran, g.size() * 8, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        std::vector<uint32_t> v(B * (QD + 2 * KD), 0u);
+        for (size_t i = 0; i < g.size(); i++) v[i] = (uint32_t)g[i];
+        memcpy(dst, v.data(), bytes);
+        return 0;
+    }
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;
@@ -1072,6 +1086,8 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
                        const std::vector<int> &audio_pos, const std::vector<int> &N, bool want_logits) {
     int rc;
     if ((rc = prefill_layers(c, ids, P, d_feats, audio_pos, N))) return rc;
+    // granule tags repeat across runs at the same positions: back to zero (no valid tag)
+    HIPCHK(hipMemsetAsync(c->d_gran, 0, (size_t)(c->m->hp.n_head + 2 * c->m->hp.n_kv_head) * 128 * 8, c->st));
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
     const int B = (int)P.size(), H = hp.hidden;
@@ -1209,9 +1225,12 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             c->probe_layer_fused = lfused;
         }
         if (ga) {
+            if (l == nl - 1) c->qkv_in_gran = false;
             if (lfused) {
                 (void)launch_layer1(q1, da, o, gu, dn, ocnt, ocnt_next, fcnt, fcnt_next, c->fuse, s, false);
             } else if (fmode) {
+                if (c->fuse.gran) { da.gran = c->d_gran; da.layer = l; }
+                if (l == nl - 1) c->qkv_in_gran = c->fuse.gran != 0;
                 (void)launch_qkv_attention1(q1, da, &o, c->fuse, s, false);
             } else {
                 if (skinny) {
@@ -1545,6 +1564,8 @@ extern "C" int qasr_prefill(qasr_ctx *c, const int32_t *ids, const int *P, const
 extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_past, int B, float *logits, int32_t *argmax) {
     if (!c || !tok || !n_past || B <= 0 || B > c->max_batch) return fail(QASR_ERR_ARG, "bad arguments");
     HIPCHK(hipSetDevice(c->m->device));
+    // a caller may repeat a position (same tag): no granule of an earlier call may match
+    HIPCHK(hipMemsetAsync(c->d_gran, 0, (size_t)(c->m->hp.n_head + 2 * c->m->hp.n_kv_head) * 128 * 8, c->st));
     std::vector<int> pos(B), nkv(B);
     for (int b = 0; b < B; b++) {
         if (n_past[b] < 0 || n_past[b] + 1 > c->max_ctx) return fail(QASR_ERR_ARG, "Context length exceeded");

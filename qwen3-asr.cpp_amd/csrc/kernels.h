@@ -144,6 +144,7 @@ struct FuseCfg {
                                                        // down first poll (s_sleep(8) units)
     int enc_attn_f32 = 0;               // encoder attention on fp32 MFMA instead of split fp16 operands
     int gemm_regs = 0;                  // encoder/prefill GEMMs on the register-staged tiles (gemm.hip)
+    int gran = 1;                       // batch 1: QKV -> attention hand-off by tagged granules (0 = arrival counters)
     int pf_blocks = 0, pf_delay = 30;   // batch 1: workgroups of the QKV launch that pull the layer's FFN weights
                                         // into the Infinity Cache while the attention chain runs (s_sleep(8) units)
     int fa_exact_prefill = 1;           // prefill attention with ggml's CPU FA numerics (fa_exact.hip)
@@ -259,6 +260,9 @@ struct DecodeAttnArgs {
     unsigned int qkv_need;               // fused launches: QKV-block arrivals per kv group (0 = 64)
     float *scores;                       // non-null (separate launch only): scores mode -- the splits write their
                                          // scaled scores [B][n_head][max_ctx] (+ the new K/V rows) and stop there
+    unsigned long long *gran;            // fused launch: QKV outputs as 8-byte {fp32 value, tag} granules the attention
+                                         // splits poll directly (no drain / arrival count); null = counters
+    int layer;                           // tag = (position << 5) | layer
     const uint16_t *pf0, *pf1;           // fused launch: byte ranges pulled into the Infinity Cache (null: none)
     long pf_n0, pf_n1;                   // their sizes in 16-B lines
     int pf_blocks, pf_delay;
