@@ -37,7 +37,18 @@ static double time_cfg(GemmArgs g, const std::vector<uint16_t *> &ws, hipStream_
     }
     const double us = best * 1e3 / NREP;
     const double bytes = (double)g.N * g.K * 2;
-    printf("  %-28s MT%d NT%d KW%d VAR%d  %7.2f us  %6.0f GB/s  grid %4dx%d\n", tag, MT, NT, KW, VAR, us, bytes / us * 1e-3, grid.x, grid.y);
+    // checksum of the last launch's output (same weights copy for every variant)
+    const size_t no = (size_t)g.M * (EPI == EPI_SWIGLU_F16 ? g.N / 2 : g.N);
+    double cs = 0;
+    if (EPI == EPI_SWIGLU_F16) {
+        std::vector<_Float16> h(no); CK(hipMemcpy(h.data(), g.out_f16, no * 2, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < no; i++) cs += (double)h[i] * (double)((i % 97) + 1);
+    } else {
+        std::vector<float> h(no); CK(hipMemcpy(h.data(), g.out_f32, no * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < no; i++) cs += (double)h[i] * (double)((i % 97) + 1);
+    }
+    printf("  %-28s MT%d NT%d KW%d VAR%d  %7.2f us  %6.0f GB/s  grid %4dx%d  sum %.9g\n", tag, MT, NT, KW, VAR, us, bytes / us * 1e-3, grid.x,
+           grid.y, cs);
     CK(hipGraphExecDestroy(ex)); CK(hipGraphDestroy(graph));
     return us;
 }
@@ -48,7 +59,13 @@ int main(int argc, char **argv) {
     Shape shapes[] = {{"qkv 4096x1024", 4096, 1024, EPI_F32}, {"o 1024x2048", 1024, 2048, EPI_F32},
                       {"gu 6144x1024 swiglu", 6144, 1024, EPI_SWIGLU_F16}, {"down 1024x3072", 1024, 3072, EPI_F32}};
     uint16_t *A; float *out, *res; uint16_t *out16;
-    CK(hipMalloc(&A, (size_t)128 * 4096 * 2)); CK(hipMemset(A, 0x11, (size_t)128 * 4096 * 2));
+    CK(hipMalloc(&A, (size_t)128 * 4096 * 2));
+    {
+        std::vector<_Float16> h((size_t)128 * 4096);
+        unsigned x = 777u;
+        for (auto &v : h) { x = x * 1664525u + 1013904223u; v = (_Float16)(((x >> 9) * (1.0f / 8388608.0f)) - 0.5f); }
+        CK(hipMemcpy(A, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    }
     CK(hipMalloc(&out, (size_t)128 * 8192 * 4)); CK(hipMalloc(&res, (size_t)128 * 8192 * 4)); CK(hipMalloc(&out16, (size_t)128 * 8192 * 2));
     CK(hipMemset(res, 0, (size_t)128 * 8192 * 4));
     printf("M = %d\n", M);
@@ -62,6 +79,11 @@ int main(int argc, char **argv) {
         g.out_f32 = out; g.ldo = sh.N; g.res = res; g.ldr = sh.N; g.out_f16 = out16; g.ldo16 = sh.N;
         printf("%s (%zu MB, %d copies)\n", sh.name, wb >> 20, NL);
         if (sh.epi == EPI_F32) {
+            time_cfg<4, 1, 8, EPI_F32, 0>(g, ws, s, "full");
+            time_cfg<4, 1, 8, EPI_F32, 4>(g, ws, s, "A via LDS-DMA");
+            time_cfg<1, 1, 8, EPI_F32, 0>(g, ws, s, "full");
+            time_cfg<1, 1, 8, EPI_F32, 4>(g, ws, s, "A via LDS-DMA");
+            time_cfg<2, 1, 8, EPI_F32, 4>(g, ws, s, "A via LDS-DMA");
             time_cfg<4, 1, 4, EPI_F32, 0>(g, ws, s, "full");
             time_cfg<4, 1, 4, EPI_F32, 1>(g, ws, s, "no A");
             time_cfg<4, 1, 4, EPI_F32, 2>(g, ws, s, "no W");
@@ -77,6 +99,9 @@ int main(int argc, char **argv) {
             time_cfg<4, 2, 4, EPI_F32, 0>(g, ws, s, "full");
         } else {
             time_cfg<4, 2, 4, EPI_SWIGLU_F16, 0>(g, ws, s, "full");
+            time_cfg<4, 2, 4, EPI_SWIGLU_F16, 4>(g, ws, s, "A via LDS-DMA");
+            time_cfg<2, 2, 4, EPI_SWIGLU_F16, 4>(g, ws, s, "A via LDS-DMA");
+            time_cfg<2, 2, 8, EPI_SWIGLU_F16, 4>(g, ws, s, "A via LDS-DMA");
             time_cfg<4, 2, 4, EPI_SWIGLU_F16, 1>(g, ws, s, "no A");
             time_cfg<4, 2, 4, EPI_SWIGLU_F16, 2>(g, ws, s, "no W");
             time_cfg<2, 2, 4, EPI_SWIGLU_F16, 0>(g, ws, s, "full");
