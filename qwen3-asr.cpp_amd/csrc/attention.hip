@@ -1032,8 +1032,9 @@ template <int SPL>
 __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnArgs a, GemvArgs o) {
     constexpr int K = 1024, NT = 2, RPW = 2;
     stamp_start(a.stamp);
-    if (blockIdx.x >= 512) {
-        const int j = blockIdx.x - 512, nsp = a.grid_splits, nat = nsp * a.n_kv_head;   // grid_splits: this launch's splits
+    const int nq = q.W ? 512 : 0;   // no QKV role: the previous FFN launch left the outputs in a.gran
+    if (blockIdx.x >= nq) {
+        const int j = blockIdx.x - nq, nsp = a.grid_splits, nat = nsp * a.n_kv_head;   // grid_splits: this launch's splits
         const int nob = a.att_done ? 256 : 0;
         if (j >= nat + nob) prefetch_body(a, j - nat - nob);
         else if (j >= nat) oproj1_body(o, a, j - nat);
@@ -1508,7 +1509,9 @@ int launch_layer1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs &o,
 // partials to combine, still >= 64 workgroups per 8 kv heads)
 static int split1(int spl1, int grid_splits) { return spl1 == 64 || spl1 == 128 ? spl1 : grid_splits >= 16 ? 128 : 64; }
 
-int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s, bool dry) {
+int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s, bool dry,
+                          bool no_qkv) {
+    if (no_qkv && !a.gran) return 0;
     if (!cfg.qkv || !cfg.err || a.B != 1 || !a.qcnt || q.M != 1 || q.K != 1024 || q.Wd || !q.norm_w || q.xh || q.bias || q.res ||
         a.out32 || a.outq || q.N != a.n_head * 128 + 2 * a.n_kv_head * 128 || a.n_head != 2 * a.n_kv_head || a.n_kv_head * 64 != 512)
         return 0;
@@ -1526,7 +1529,7 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     if (dry) return with_o2 ? 2 : 1;
     // prefetch workgroups wait on nothing: they need no co-residency
     const int npf = a.pf0 && cfg.pf_blocks > 0 ? cfg.pf_blocks : 0;
-    const dim3 grid(512 + ns * a.n_kv_head + (with_o2 ? o->N / 4 : 0) + npf);
+    const dim3 grid((no_qkv ? 0 : 512) + ns * a.n_kv_head + (with_o2 ? o->N / 4 : 0) + npf);
     // K/V delay ~2 us: measured optimum on MI355X (tools/job_delay.sh: 0 -> 236.3, 10 -> 232.0, 18 -> 240.3 ms decode)
     DecodeAttnArgs ad = a;
     ad.fuse_delay = cfg.qkv_delay;
@@ -1538,9 +1541,12 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     if (!with_o2) ad.att_done = nullptr;
     ad.pf_blocks = npf;
     ad.pf_delay = cfg.pf_delay;
+    if (no_qkv) ad.fuse_delay = 0;   // nothing to let ahead: the K/V stream starts at once
+    GemvArgs qa = q;
+    if (no_qkv) qa.W = nullptr;
     const GemvArgs oa = with_o2 ? *o : GemvArgs{};
-    if (spl1 == 128) hipLaunchKernelGGL(qkv_attn1_kernel<128>, grid, dim3(256), 0, s, q, ad, oa);
-    else hipLaunchKernelGGL(qkv_attn1_kernel<DSPLIT>, grid, dim3(256), 0, s, q, ad, oa);
+    if (spl1 == 128) hipLaunchKernelGGL(qkv_attn1_kernel<128>, grid, dim3(256), 0, s, qa, ad, oa);
+    else hipLaunchKernelGGL(qkv_attn1_kernel<DSPLIT>, grid, dim3(256), 0, s, qa, ad, oa);
     return with_o2 ? 2 : 1;
 }
 

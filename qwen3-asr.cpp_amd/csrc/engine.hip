@@ -121,6 +121,7 @@ struct qasr_ctx {
     unsigned int *d_attdone = nullptr;   // fused batch-1 o-proj: combiner arrivals (8 replicas)
     unsigned int *d_ffncnt = nullptr;    // fused batch-1 FFN: gate/up arrivals, [layer][32 shards][16]
     unsigned int *d_ocnt = nullptr;      // batch-1 layer launch: o-proj arrivals, [layer][32 shards][16]
+    unsigned int *d_dcnt = nullptr;      // batch-1 FFN launch with the next layer's QKV: down arrivals, [layer][32 shards][16]
     uint16_t *d_q = nullptr, *d_att = nullptr, *d_act = nullptr, *d_xh = nullptr;
     unsigned long long *d_amax = nullptr;
     int max_splits = 0, hist_cap = 0;
@@ -155,6 +156,7 @@ struct qasr_ctx {
     int probe_layer = 14;          // decoder layer whose groups probes 2 / 3 time
     bool probe_o_fused = false;    // the probed layer's o-projection runs inside the QKV launch
     bool probe_layer_fused = false;   // ... and its FFN too (layer1_kernel)
+    bool probe_qffn = false;          // the QKV projections run in the previous layer's FFN launch (FuseCfg::qkv_ffn)
     double probe_ms = 0.0, probe_bytes = 0.0, probe_dev_ms = 0.0;
     long probe_dev_n = 0;
     unsigned long long *d_pstamp = nullptr;   // per decode step: [32 min-starts | 32 max-ends] of the probed launches
@@ -214,6 +216,9 @@ static const std::vector<FuseOption> &fuse_options() {
         {"pf_blocks", "QASR_PF_BLOCKS", &FuseCfg::pf_blocks},
         {"pf_delay", "QASR_PF_DELAY", &FuseCfg::pf_delay},
         {"fa_exact_decode", "QASR_FA_EXACT_DECODE", &FuseCfg::fa_exact_decode},
+        {"qkv_ffn", "QASR_QKV_FFN", &FuseCfg::qkv_ffn},
+        {"qffn_delay", "QASR_QFFN_DELAY", &FuseCfg::qffn_delay},
+        {"qffn_poll_delay", "QASR_QFFN_POLL_DELAY", &FuseCfg::qffn_poll_delay},
     };
     return v;
 }
@@ -235,6 +240,7 @@ static int check_dev_err(qasr_ctx *c) {
     HIPCHK(hipMemsetAsync(c->d_err, 0, 4, c->st));
     HIPCHK(hipMemsetAsync(c->d_ffncnt, 0, (size_t)c->m->hp.dec_layers * 512 * 4, c->st));
     HIPCHK(hipMemsetAsync(c->d_ocnt, 0, (size_t)c->m->hp.dec_layers * 512 * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->d_dcnt, 0, (size_t)c->m->hp.dec_layers * 512 * 4, c->st));
     HIPCHK(hipMemsetAsync(c->d_qcnt, 0, (size_t)c->m->hp.n_kv_head * 8 * 16 * 4, c->st));
     HIPCHK(hipMemsetAsync(c->d_attdone, 0, (size_t)8 * 16 * 4, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
@@ -242,6 +248,7 @@ static int check_dev_err(qasr_ctx *c) {
     if (e & DEVERR_QKV_WAIT) what += " attention<-QKV";
     if (e & DEVERR_O_WAIT) what += " o-proj<-attention";
     if (e & DEVERR_FFN_WAIT) what += " down<-gate/up";
+    if (e & DEVERR_X_WAIT) what += " next-layer QKV<-down";
     return fail(QASR_ERR_DEVICE, "fused decode launch: an in-launch wait timed out (" + what.substr(1) +
                                      "); outputs of this call are invalid (another process or context sharing the GPU?)");
 }
@@ -698,6 +705,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_gran, (size_t)(QD + 2 * KD) * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_ffncnt, (size_t)hp.dec_layers * 512 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_ocnt, (size_t)hp.dec_layers * 512 * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_dcnt, (size_t)hp.dec_layers * 512 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_err, 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_pstamp, (size_t)max_ctx * kStampRec * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_logits, (size_t)B * hp.vocab * 4)) ||
@@ -709,6 +717,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     HIPCHK(hipMemset(c->d_counter, 0, (size_t)B * hp.n_kv_head * 4));
     HIPCHK(hipMemset(c->d_qcnt, 0, (size_t)hp.n_kv_head * 8 * 16 * 4));
     HIPCHK(hipMemset(c->d_ocnt, 0, (size_t)hp.dec_layers * 512 * 4));
+    HIPCHK(hipMemset(c->d_dcnt, 0, (size_t)hp.dec_layers * 512 * 4));
     HIPCHK(hipMemset(c->d_attdone, 0, (size_t)8 * 16 * 4));
     HIPCHK(hipMemset(c->d_gran, 0, (size_t)(QD + 2 * KD) * 8));
     HIPCHK(hipMemset(c->d_ffncnt, 0, (size_t)hp.dec_layers * 512 * 4));
@@ -1220,9 +1229,26 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         const bool lfused = fusable && nl >= 2 && launch_layer1(q1, da, o, gu, dn, ocnt, ocnt_next, fcnt, fcnt_next, c->fuse, s, true);
         const int fmode = lfused ? 0 : fusable ? launch_qkv_attention1(q1, da, &o, c->fuse, s, true) : 0;
         const bool o_fused = fmode == 2;
+        // layer l+1's rmsnorm + QKV in this layer's FFN launch (FuseCfg::qkv_ffn),
+        // its outputs in granules for layer l+1's attention launch: a decision
+        // from shapes and options only, so every layer's two launches agree
+        QkvNext qn{};
+        qn.dcnt = c->d_dcnt + (size_t)l * 512;
+        qn.dcnt_next = c->d_dcnt + (size_t)((l + 1) % nl) * 512;
+        qn.gran = c->d_gran;
+        qn.pos = c->d_pos;
+        qn.layer_next = l + 1;
+        if (l + 1 < nl) {
+            const DecLayer &Ln = m->dec[l + 1];
+            qn.q.x = x; qn.q.ldx = H; qn.q.norm_w = Ln.attn_norm; qn.q.eps = hp.rms_eps; qn.q.W = Ln.wqkv; qn.q.K = H;
+            qn.q.N = QD + 2 * KD; qn.q.M = 1; qn.q.ldo = QD + 2 * KD;
+        }
+        const bool qffn = fmode >= 1 && c->fuse.gran && c->fuse.qkv_ffn && nl >= 2 &&
+                          launch_ffn1(gu, dn, fcnt, fcnt_next, c->fuse, s, &qn, true);
         if (l == std::min(c->probe_layer, nl - 1)) {
             c->probe_o_fused = o_fused || lfused;
             c->probe_layer_fused = lfused;
+            c->probe_qffn = qffn;
         }
         if (ga) {
             if (l == nl - 1) c->qkv_in_gran = false;
@@ -1231,7 +1257,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             } else if (fmode) {
                 if (c->fuse.gran) { da.gran = c->d_gran; da.layer = l; }
                 if (l == nl - 1) c->qkv_in_gran = c->fuse.gran != 0;
-                (void)launch_qkv_attention1(q1, da, &o, c->fuse, s, false);
+                (void)launch_qkv_attention1(q1, da, &o, c->fuse, s, false, qffn && l > 0);
             } else {
                 if (skinny) {
                     if (!(skip & 1)) launch_gemv(EPI_F32, q1, s);
@@ -1261,7 +1287,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         if (skinny) {
             if (!o_fused && !(skip & 4)) launch_gemv(EPI_F32, o, s);
             if (o_fused) dn.zero8 = c->d_attdone;   // re-arm the fused o-proj's arrival counters
-            if (skip & 24 || nl < 2 || !launch_ffn1(gu, dn, fcnt, fcnt_next, c->fuse, s)) {
+            if (skip & 24 || nl < 2 || !launch_ffn1(gu, dn, fcnt, fcnt_next, c->fuse, s, qffn ? &qn : nullptr)) {
                 if (!(skip & 8)) launch_gemv(q8 ? EPI_SWIGLU_F32 : EPI_SWIGLU_F16, gu, s);
                 if (!(skip & 16)) launch_gemv(EPI_F32, dn, s);
                 else if (o_fused) (void)hipMemsetAsync(c->d_attdone, 0, 8 * 16 * 4, s);   // the skipped down-proj re-arms these
@@ -1341,9 +1367,14 @@ static double probe_bytes(const qasr_ctx *c, int B, int k) {
         for (int b = 0; b < B; b++) kv += (double)(c->run_P[b] + k + 1) * KD * 2 * 2;
         const bool o_in = c->probe_o_fused;
         const double ffn = c->probe_layer_fused ? 3 * F * H * wb + B * H * 4 * 3 : 0.0;   // the layer launch's FFN
-        return (QD + 2 * KD) * H * wb + (o_in ? H * QD * wb : 0.0) + kv + B * H * 4 * (o_in ? 3 : 1) + B * (QD + 2 * KD) * 4 + ffn;
+        // (the QKV projection left for the previous layer's FFN launch, FuseCfg::qkv_ffn)
+        const bool q_in = !(c->probe_qffn && std::min(c->probe_layer, step_layers(c) - 1) > 0);
+        return (q_in ? (QD + 2 * KD) * H * wb + B * H * 4 : 0.0) + (o_in ? H * QD * wb + B * H * 8 : 0.0) + kv +
+               B * (QD + 2 * KD) * (q_in ? 4 : 8) + ffn;
     }
-    return 3 * F * H * wb + (c->probe_o_fused ? 0.0 : H * QD * wb) + B * H * 4 * 3;
+    const bool qn = c->probe_qffn && std::min(c->probe_layer, step_layers(c) - 1) + 1 < step_layers(c);
+    return 3 * F * H * wb + (c->probe_o_fused ? 0.0 : H * QD * wb) + B * H * 4 * 3 +
+           (qn ? (QD + 2 * KD) * H * wb + B * H * 4 + B * (QD + 2 * KD) * 8 : 0.0);
 }
 
 static int capture(qasr_ctx *c, int B, bool want_logits, StepRange r, int splits, hipGraphExec_t *out) {

@@ -131,6 +131,7 @@ enum DevErr : unsigned {
     DEVERR_QKV_WAIT = 1u,    // attention split gave up on its kv group's QKV blocks
     DEVERR_O_WAIT = 2u,      // fused o-projection gave up on the attention combiners
     DEVERR_FFN_WAIT = 4u,    // fused down-projection gave up on the gate/up blocks
+    DEVERR_X_WAIT = 8u,      // the next layer's QKV blocks (FFN launch) gave up on the down blocks
 };
 struct FuseCfg {
     int ffn = 1, qkv = 1, o = 1;        // fused launches on/off
@@ -150,6 +151,10 @@ struct FuseCfg {
     int fa_exact_prefill = 1;           // prefill attention with ggml's CPU FA numerics (fa_exact.hip)
     int fa_exact_decode = -1;           // decode attention likewise: 1 on, 0 off (fp32 V accumulation), -1 = on for
                                         // Q8_0 models only (batch 1 exact skips the fused QKV + attention launch)
+    int qkv_ffn = 0;                    // batch 1: layer l+1's rmsnorm + QKV GEMV runs in layer l's FFN launch (its weights
+                                        // stream beside gate/up + down), the next launch is attention + o-proj only;
+                                        // bit-identical, measured slower (tools/job_qffn*.sh: decode 223 -> 246 ms)
+    int qffn_delay = 30, qffn_poll_delay = 10;   // ... its weight request / first poll (s_sleep(8) units, ~0.2 us)
     int slots_ffn = 0, slots_qkv64 = 0, slots_qkv128 = 0;   // co-resident workgroups on this device
     int slots_layer64 = 0, slots_layer128 = 0;
     unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
@@ -157,11 +162,20 @@ struct FuseCfg {
 // co-resident workgroup capacity of the fused kernels on the current device
 // (occupancy query x CUs); 0 = unknown (never fuse)
 void fused_slots(FuseCfg &cfg);
-// gemv.hip: batch-1 f16 gate/up + down in one launch; cnt = this layer's 32 x 16
-// words (zero on entry), cnt_next = the next layer's, re-armed here
-// (false = not covered)
+// the next decoder layer's QKV role of the batch-1 FFN launch (FuseCfg::qkv_ffn):
+// q = that layer's rmsnorm + QKV GemvArgs (x = this launch's down output;
+// q.W null: no QKV role, only the re-arm of dcnt_next); dcnt = this layer's 32 x
+// 16 down-arrival words (zero on entry), dcnt_next = the next layer's
+struct QkvNext {
+    GemvArgs q;
+    unsigned int *dcnt, *dcnt_next;
+    unsigned long long *gran; const int *pos; int layer_next;
+};
+// gemv.hip: batch-1 f16 gate/up + down (+ the next layer's QKV) in one launch;
+// cnt = this layer's 32 x 16 words (zero on entry), cnt_next = the next
+// layer's, re-armed here (false = not covered; dry: the decision only)
 bool launch_ffn1(const GemvArgs &gu, const GemvArgs &dn, unsigned int *cnt, unsigned int *cnt_next, const FuseCfg &cfg,
-                 hipStream_t s);
+                 hipStream_t s, const QkvNext *qn = nullptr, bool dry = false);
 
 // ---------------------------------------------------------------- norms
 // LayerNorm (ggml_norm + mul + add) fp32 [M][D] -> fp16 y, or fp32 y32 when
@@ -290,8 +304,10 @@ void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
 // (and, when o is the plain batch-1 o-projection, that too); returns 0 = not
 // taken, 1 = QKV + attention, 2 = QKV + attention + o-projection
 // dry = true: only the decision (nothing launched)
+// no_qkv: the QKV outputs are already in a.gran (the previous FFN launch ran
+// them, FuseCfg::qkv_ffn): the launch is the attention splits (+ o-projection)
 int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s,
-                          bool dry = false);
+                          bool dry = false, bool no_qkv = false);
 int decode_split_len();
 int decode_max_splits();
 
