@@ -670,6 +670,12 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     const int q4 = lane >> 4, c16 = lane & 15;
     constexpr int KPW = SPL / DWAVES / 4;   // V rows per lane (4 or 16)
     constexpr int TW = SPL / DWAVES / 16;   // 16-key MFMA tiles per wave (1 or 4)
+    // separate launches (decode batches, long kernels): keys past this
+    // sequence's position re-read its last row -- cache hits instead of HBM
+    // traffic for the masked tail of a short sequence in a batch whose grid
+    // covers the longest; the fused batch-1 launch keeps its K/V requests free
+    // of the dependent position load (see below)
+    const int kcap = FUSED ? a.max_ctx - 1 : min(a.pos[b], a.max_ctx - 1);
     // K in the v_mfma_f32_16x16x32_f16 B layout: tile t, step s -> key 16t + c16
     // of this wave's range, dims 32s + 8q4 .. +8 (16 rows x 64 B per load)
     half8 kk[TW][4], vv[KPW];
@@ -677,13 +683,13 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     for (int t = 0; t < TW; t++)
 #pragma unroll
         for (int s4 = 0; s4 < 4; s4++) {
-            const int key = min(k0 + wid * (SPL / DWAVES) + 16 * t + c16, a.max_ctx - 1);
+            const int key = min(k0 + wid * (SPL / DWAVES) + 16 * t + c16, kcap);
             kk[t][s4] = *(const half8 *)(kc + (long)key * 128 + 32 * s4 + 8 * q4);
         }
     if (!a.scores)   // scores mode reads no V
 #pragma unroll
         for (int i = 0; i < KPW; i++) {
-            const int key = min(k0 + wid * (SPL / DWAVES) + i * 4 + sub, a.max_ctx - 1);
+            const int key = min(k0 + wid * (SPL / DWAVES) + i * 4 + sub, kcap);
             vv[i] = *(const half8 *)(vc + (long)key * 128 + dl);
         }
     // No exit test on the position anywhere: with one, hipcc hoists the

@@ -484,13 +484,10 @@ __device__ __forceinline__ float fx_weights_reg(const float *src, int n, float &
     return S;
 }
 
-// grid (n_head, B), block 128: query head h of sequence b, wave w running
-// dimensions 64 w + lane; the two waves share nothing (each derives the
-// weights itself).
-__global__ __launch_bounds__(128) void decode_attn_exact_kernel(DecodeAttnArgs a) {
-    stamp_start(a.stamp);
-    const int h = blockIdx.x, b = blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+// query head h of sequence b, wave wid (0, 1) running dimensions 64 wid +
+// lane; the waves share nothing (each derives the weights itself)
+__device__ __forceinline__ void decode_attn_exact_body(const DecodeAttnArgs &a, const int h, const int b, const int wid) {
+    const int lane = threadIdx.x & 63;
     const int g = h / (a.n_head / a.n_kv_head);
     const int nkv = a.pos[b] + 1;
     const float *sg = a.scores + ((long)b * a.n_head + h) * a.max_ctx;
@@ -539,12 +536,35 @@ __global__ __launch_bounds__(128) void decode_attn_exact_kernel(DecodeAttnArgs a
     } else {
         a.out[e] = f_to_u16(ov);
     }
+}
+
+// grid (n_head, B), block 128: one query head per workgroup
+__global__ __launch_bounds__(128) void decode_attn_exact_kernel(DecodeAttnArgs a) {
+    stamp_start(a.stamp);
+    decode_attn_exact_body(a, blockIdx.x, blockIdx.y, threadIdx.x >> 6);
+    stamp_end(a.stamp);
+}
+
+// grid (n_head / 2, B), block 256: the two query heads 2x, 2x + 1 of one kv
+// group (GQA 2:1) in one workgroup -- waves 0/1 and 2/3 stream the same V^T
+// rows close together in time, so the second read is served by the CU's
+// caches instead of HBM (one head per workgroup read every V row twice from
+// memory: the Q8_0 batch-64 decode's largest kernel, memory-bound).  Same
+// per-wave arithmetic, so the outputs are bit-identical.
+__global__ __launch_bounds__(256) void decode_attn_exact_pair_kernel(DecodeAttnArgs a) {
+    stamp_start(a.stamp);
+    const int wid = threadIdx.x >> 6;
+    decode_attn_exact_body(a, 2 * blockIdx.x + (wid >> 1), blockIdx.y, wid & 1);
     stamp_end(a.stamp);
 }
 
 void launch_decode_attention_exact(const DecodeAttnArgs &a, hipStream_t s) {
     if (a.B <= 0) return;
-    hipLaunchKernelGGL(decode_attn_exact_kernel, dim3(a.n_head, a.B), dim3(128), 0, s, a);
+    // (measured on configs[2], Q8_0 64 x 30 s: decode 285.7 -> 267.2 ms, tools/job_fxpair.sh)
+    if (a.n_head % 2 == 0 && (a.n_head / a.n_kv_head) % 2 == 0)
+        hipLaunchKernelGGL(decode_attn_exact_pair_kernel, dim3(a.n_head / 2, a.B), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(decode_attn_exact_kernel, dim3(a.n_head, a.B), dim3(128), 0, s, a);
 }
 
 }  // namespace qasr
