@@ -956,6 +956,208 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeAttnArgs a) {
     stamp_end(a.stamp);
 }
 
+// ------------------------------------------ decode batches: one workgroup per sequence
+// decode_attn_kernel<256> needs 168 VGPRs (a whole split's K/V in flight in
+// registers), so 2 workgroups fit a CU: a batch-64 grid of 1024 splits ran in
+// two rounds with HBM idle through each round's score / publish / combine
+// tail (4.0 TB/s).  Here one workgroup takes one (kv group, sequence) and
+// walks that sequence's own keys in 64-key chunks, the next chunk's K/V
+// requested into a second register set before the current chunk's
+// arithmetic; each wave keeps its own online softmax (m, l, O) over its 16
+// keys of every chunk, so the loop has no barrier, no partial publish and no
+// drain -- the four waves merge once through LDS at the end.  Only keys below
+// the sequence's position are loaded (a short sequence in a batch streams
+// only its own context).  Numerics: fp16 Q.K products summed in fp32 on MFMA,
+// fp32 softmax and P.V as decode_attn_body; the merge order differs from the
+// split kernels (a few fp32 ulps).
+struct KvChunk {
+    half8 kk[4];   // K, v_mfma_f32_16x16x32_f16 B layout: key 16 wid + c16, dims 32 s4 + 8 q4
+    half8 vv[4];   // V rows 16 wid + 4 i + sub, dims dl .. dl + 8
+};
+
+__device__ __forceinline__ void kvc_issue(const uint16_t *kc, const uint16_t *vc, int c0, int kcap, bool want_v, KvChunk &r) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int sub = lane >> 4, dl = (lane & 15) * 8, q4 = lane >> 4, c16 = lane & 15;
+    const int kk = min(c0 + 16 * wid + c16, kcap);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; s4++) r.kk[s4] = *(const half8 *)(kc + (long)kk * 128 + 32 * s4 + 8 * q4);
+    if (want_v)
+#pragma unroll
+        for (int i = 0; i < 4; i++) r.vv[i] = *(const half8 *)(vc + (long)min(c0 + 16 * wid + 4 * i + sub, kcap) * 128 + dl);
+}
+
+struct SeqSt {
+    float m0, m1, l0, l1;   // running max / sum per head (uniform in the wave)
+    float o0[8], o1[8];     // this lane's partial O (its keys 4 i + sub, dims dl .. dl + 8)
+};
+
+// one 64-key chunk for this wave (keys c0 + 16 wid .. + 15)
+__device__ __forceinline__ void kvc_step(const DecodeAttnArgs &a, const half8 *qa, const uint16_t *knew, const uint16_t *vnew,
+                                         int c0, int pos, const KvChunk &r, SeqSt &st, float *sdst) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int q4 = lane >> 4, c16 = lane & 15, sub = lane >> 4, dl = (lane & 15) * 8;
+    const int key = c0 + 16 * wid + c16;
+    half8 kt[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; s4++) kt[s4] = key == pos ? *(const half8 *)&knew[32 * s4 + 8 * q4] : r.kk[s4];
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s4 = 0; s4 < 4; s4++) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(qa[s4], kt[s4], acc, 0, 0, 0);
+    // lanes 0-15 (q4 = 0): S[head r][key c16] in acc[r]
+    const bool ok = q4 == 0 && key <= pos;
+    const float s0 = ok ? acc[0] * a.scale : -INFINITY, s1 = ok ? acc[1] * a.scale : -INFINITY;
+    if (sdst) {   // scores mode (front half of the exact attention, fa_exact.hip)
+        if (ok) {
+            sdst[key] = s0;
+            sdst[(long)a.max_ctx + key] = s1;
+        }
+        return;
+    }
+    const float c0m = wave_max(s0), c1m = wave_max(s1);
+    const float M0 = fmaxf(st.m0, c0m), M1 = fmaxf(st.m1, c1m);
+    const float r0 = M0 == -INFINITY ? 1.f : expf(st.m0 - M0), r1 = M1 == -INFINITY ? 1.f : expf(st.m1 - M1);
+    const float p0 = ok ? expf(s0 - M0) : 0.f, p1 = ok ? expf(s1 - M1) : 0.f;
+    st.l0 = st.l0 * r0 + wave_sum(p0);
+    st.l1 = st.l1 * r1 + wave_sum(p1);
+    st.m0 = M0;
+    st.m1 = M1;
+#pragma unroll
+    for (int e = 0; e < 8; e++) { st.o0[e] *= r0; st.o1[e] *= r1; }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int kl = 4 * i + sub;   // this lane's key of row i (lane kl of the score row holds its p)
+        const float q0 = __shfl(p0, kl, 64), q1 = __shfl(p1, kl, 64);
+        const half8 vr = c0 + 16 * wid + kl == pos ? *(const half8 *)&vnew[dl] : r.vv[i];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            const float v = (float)vr[e];
+            st.o0[e] = fmaf(v, q0, st.o0[e]);
+            st.o1[e] = fmaf(v, q1, st.o1[e]);
+        }
+    }
+}
+
+// grid (n_kv_head, B): kv group g of sequence b, both of its query heads
+__global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) {
+    __shared__ __attribute__((aligned(16))) uint16_t qs[2][128];
+    __shared__ __attribute__((aligned(16))) uint16_t knew[128];
+    __shared__ __attribute__((aligned(16))) uint16_t vnew[128];
+    __shared__ float wst[4][2][2];                                  // per wave: (m, l) per head
+    __shared__ __attribute__((aligned(16))) float wo[4][2][128];   // per wave: O per head
+    stamp_start(a.stamp);
+    const int g = blockIdx.x, b = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
+    const int q4 = lane >> 4, c16 = lane & 15, sub = lane >> 4, dl = (lane & 15) * 8;
+    const long cbase = ((long)b * a.n_kv_head + g) * a.max_ctx;
+    uint16_t *kc = a.kc + cbase * 128, *vc = a.vc + cbase * 128;
+    const int pos = a.pos[b], nkv = pos + 1, kcap = min(pos, a.max_ctx - 1);
+    const bool want_v = !a.scores;
+    KvChunk A, B;
+    kvc_issue(kc, vc, 0, kcap, want_v, A);
+    // ---- the token's q / k / v: rms norm * weight + NEOX RoPE (decode_attn_body), new K/V row to the caches
+    {
+        const float *raw = a.qkv + (long)b * (QD + 2 * KD);
+        const float *src = wid < 2 ? raw + (2 * g + wid) * 128 : raw + QD + (wid - 2) * KD + g * 128;
+        const float x0 = src[lane], x1 = src[lane + 64];
+        const float *nw = wid < 2 ? a.q_norm : a.k_norm;
+        const float2 cs = *(const float2 *)(a.rope + ((long)pos * 64 + lane) * 2);
+        if (wid < 3) {
+            const double ss = wave_sum_d((double)(x0 * x0) + (double)(x1 * x1));
+            const float scale = 1.0f / sqrtf((float)(ss / 128.0) + a.eps);
+            const float y0 = fmul_rn(fmul_rn(x0, scale), nw[lane]), y1 = fmul_rn(fmul_rn(x1, scale), nw[lane + 64]);
+            const uint16_t r0 = f_to_u16(y0 * cs.x - y1 * cs.y), r1 = f_to_u16(y0 * cs.y + y1 * cs.x);
+            if (wid < 2) {
+                qs[wid][lane] = r0;
+                qs[wid][lane + 64] = r1;
+            } else {
+                knew[lane] = r0; knew[lane + 64] = r1;
+                kc[(long)pos * 128 + lane] = r0;
+                kc[(long)pos * 128 + lane + 64] = r1;
+            }
+        } else {
+            const uint16_t v0 = f_to_u16(x0), v1 = f_to_u16(x1);
+            vnew[lane] = v0; vnew[lane + 64] = v1;
+            vc[(long)pos * 128 + lane] = v0;
+            vc[(long)pos * 128 + lane + 64] = v1;
+            uint16_t *t = a.vt + ((long)b * a.n_kv_head + g) * 128 * vt_ctx(a.max_ctx);
+            t[vt_index(pos, lane)] = v0;
+            t[vt_index(pos, lane + 64)] = v1;
+        }
+    }
+    __syncthreads();
+    half8 qa[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; s4++)
+        qa[s4] = c16 < 2 ? *(const half8 *)&qs[c16][32 * s4 + 8 * q4] : half8{0, 0, 0, 0, 0, 0, 0, 0};
+    float *sdst = a.scores ? a.scores + ((long)b * a.n_head + 2 * g) * a.max_ctx : nullptr;
+    SeqSt st;
+    st.m0 = st.m1 = -INFINITY;
+    st.l0 = st.l1 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; e++) { st.o0[e] = 0.f; st.o1[e] = 0.f; }
+    for (int c0 = 0; c0 < nkv; c0 += 128) {   // two chunks a trip, each prefetching the other set
+        if (c0 + 64 < nkv) kvc_issue(kc, vc, c0 + 64, kcap, want_v, B);
+        kvc_step(a, qa, knew, vnew, c0, pos, A, st, sdst);
+        if (c0 + 64 >= nkv) break;
+        if (c0 + 128 < nkv) kvc_issue(kc, vc, c0 + 128, kcap, want_v, A);
+        kvc_step(a, qa, knew, vnew, c0 + 64, pos, B, st, sdst);
+    }
+    if (sdst) { stamp_end(a.stamp); return; }
+    // ---- merge: lanes of equal dl hold partial O over their keys (sub = 0..3): sum over sub, then over waves
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        st.o0[e] += __shfl_xor(st.o0[e], 16, 64);
+        st.o0[e] += __shfl_xor(st.o0[e], 32, 64);
+        st.o1[e] += __shfl_xor(st.o1[e], 16, 64);
+        st.o1[e] += __shfl_xor(st.o1[e], 32, 64);
+    }
+    if (sub == 0) {
+        *(floatx4 *)&wo[wid][0][dl] = floatx4{st.o0[0], st.o0[1], st.o0[2], st.o0[3]};
+        *(floatx4 *)&wo[wid][0][dl + 4] = floatx4{st.o0[4], st.o0[5], st.o0[6], st.o0[7]};
+        *(floatx4 *)&wo[wid][1][dl] = floatx4{st.o1[0], st.o1[1], st.o1[2], st.o1[3]};
+        *(floatx4 *)&wo[wid][1][dl + 4] = floatx4{st.o1[4], st.o1[5], st.o1[6], st.o1[7]};
+    }
+    if (lane == 0) {
+        wst[wid][0][0] = st.m0; wst[wid][0][1] = st.l0;
+        wst[wid][1][0] = st.m1; wst[wid][1][1] = st.l1;
+    }
+    __syncthreads();
+    const int hh = tid >> 7, d = tid & 127;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; w++) M = fmaxf(M, wst[w][hh][0]);
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const float mw = wst[w][hh][0];
+        const float f = mw == -INFINITY ? 0.f : expf(mw - M);
+        L = fmaf(wst[w][hh][1], f, L);
+        O = fmaf(wo[w][hh][d], f, O);
+    }
+    const float inv = L > 0.f ? 1.0f / L : 0.f;
+    const float v = O * inv;
+    const long e = (long)b * QD + (2 * g + hh) * 128 + d;
+    if (a.outq) {   // quantised for the Q8_0 o-proj: a 32-block = 32 lanes of one wave
+        float am = fabsf(v);
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+        a.outq[e] = q8_quant(v, am);
+        if ((d & 31) == 0) a.outd[e >> 5] = q8_scale(am);
+    } else if (a.out32) a.out32[e] = v;
+    else a.out[e] = f_to_u16(v);
+    stamp_end(a.stamp);
+}
+
+int decode_stream_slots() {
+    int nb = 0, dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(decode_attn_seq_kernel), 256, 0) !=
+            hipSuccess)
+        return 0;
+    return nb * cus;
+}
+
 // ------------------------------------------------- batch 1: QKV + attention
 // One launch for the batch-1 QKV projection and the attention it feeds.
 // Blocks [0, 512): the QKV GEMV (gemv1_kernel's arithmetic, K = 1024, 2 rows
@@ -1565,6 +1767,9 @@ void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {
         } else {
             hipLaunchKernelGGL(decode_attn_kernel<DSPLIT>, dim3(a.grid_splits, a.n_kv_head, a.B), dim3(256), 0, s, a);
         }
+    } else if (a.stream_blocks > 0 && a.n_head == 2 * a.n_kv_head && a.n_kv_head * a.B >= a.stream_blocks / 2) {
+        // batches that give every CU a sequence or more: one workgroup per (kv group, sequence)
+        hipLaunchKernelGGL(decode_attn_seq_kernel, dim3(a.n_kv_head, a.B), dim3(256), 0, s, a);
     } else {   // batches: longer splits (fewer workgroups and partials per sequence)
         static const int spl = [] { const char *e = getenv("QASR_ATT_SPL"); return e ? atoi(e) : 256; }();
         if (spl == 128) {
@@ -1592,6 +1797,7 @@ void fused_slots(FuseCfg &cfg) {
     cfg.slots_ffn = fused_slots_ffn();
     cfg.slots_layer64 = slots_of(reinterpret_cast<const void *>(layer1_kernel<DSPLIT>));
     cfg.slots_layer128 = slots_of(reinterpret_cast<const void *>(layer1_kernel<128>));
+    cfg.slots_stream = decode_stream_slots();
 }
 
 int decode_split_len() { return DSPLIT; }

@@ -217,6 +217,7 @@ static const std::vector<FuseOption> &fuse_options() {
         {"pf_delay", "QASR_PF_DELAY", &FuseCfg::pf_delay},
         {"fa_exact_decode", "QASR_FA_EXACT_DECODE", &FuseCfg::fa_exact_decode},
         {"qkv_ffn", "QASR_QKV_FFN", &FuseCfg::qkv_ffn},
+        {"att_stream", "QASR_ATT_STREAM", &FuseCfg::att_stream},
         {"qffn_delay", "QASR_QFFN_DELAY", &FuseCfg::qffn_delay},
         {"qffn_poll_delay", "QASR_QFFN_POLL_DELAY", &FuseCfg::qffn_poll_delay},
     };
@@ -1185,6 +1186,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         da.trace = tr(1);
         da.qcnt = c->d_qcnt;
         da.spl1 = c->fuse.spl1;
+        da.stream_blocks = !skinny && c->fuse.att_stream ? c->fuse.slots_stream : 0;
         da.stamp = stamp;
         GemvArgs o{};
         if (skinny) {

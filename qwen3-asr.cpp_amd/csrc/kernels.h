@@ -157,6 +157,8 @@ struct FuseCfg {
     int qffn_delay = 30, qffn_poll_delay = 10;   // ... its weight request / first poll (s_sleep(8) units, ~0.2 us)
     int slots_ffn = 0, slots_qkv64 = 0, slots_qkv128 = 0;   // co-resident workgroups on this device
     int slots_layer64 = 0, slots_layer128 = 0;
+    int att_stream = 1;                 // decode batches: streamed attention splits (decode_attn_stream_kernel)
+    int slots_stream = 0;               // ... its co-resident workgroups on this device
     unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
 };
 // co-resident workgroup capacity of the fused kernels on the current device
@@ -280,6 +282,8 @@ struct DecodeAttnArgs {
     const uint16_t *pf0, *pf1;           // fused launch: byte ranges pulled into the Infinity Cache (null: none)
     long pf_n0, pf_n1;                   // their sizes in 16-B lines
     int pf_blocks, pf_delay;
+    int stream_blocks;                   // decode batches (B > 8): grid of decode_attn_stream_kernel, which loops over the
+                                         // 128-key splits with the next one's K/V in flight (0 = one workgroup per split)
 };
 // Batch 1, the whole decoder layer in one launch (attention.hip layer1_kernel):
 // QKV (256 blocks) -> attention splits -> o-projection (128) -> gate/up (192)

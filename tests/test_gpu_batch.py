@@ -1,5 +1,7 @@
 """GPU: the decode-batch kernels (B > 8: gemm_skinny_kernel / gemm_skinny_q8_kernel
-row blocks and K-split waves, 256-key attention splits, the skinny LM head with
+row blocks and K-split waves, the attention -- one workgroup per (kv group,
+sequence) streaming that sequence's keys (decode_attn_seq_kernel) once the
+batch fills the CUs, 256-key splits below that --, the skinny LM head with
 argmax, Q8_0 quantisation fused into the norm and the attention combiner) at
 the batch sizes the bench runs.
 
@@ -80,3 +82,40 @@ def test_decode_long_context_splits(B, gpu, tiny_gguf, tiny_oracle):
         tol = 1e-2 * float(np.abs(ref).max())
         for b in range(B):
             assert np.abs(outs[s][b] - ref).max() <= tol, (s, b, np.abs(outs[s][b] - ref).max(), tol)
+
+
+@pytest.mark.parametrize("path", ["f16", "q8"])
+def test_decode_batch_ragged_contexts(path, gpu, tiny_gguf, tiny_q8_gguf, tiny_oracle, tiny_q8_oracle):
+    """a batch of 40 rows with two different prompts (2.1 s and 9.7 s clips,
+    alternating): each sequence attends over its own context only (the
+    per-sequence attention loads keys up to its own position); rows of the same
+    clip bit-identical, row 0 / row 1 against the oracle"""
+    q8 = path == "q8"
+    om = tiny_q8_oracle if q8 else tiny_oracle
+    m = qasr.Model(tiny_q8_gguf if q8 else tiny_gguf)
+    B, steps = 40, 3
+    fs = [om.encode(op.log_mel(qasr.synth_pcm(9300 + k, int(sec * SR)))) for k, sec in enumerate((2.1, 9.7))]
+    pr = [m.build_prompt(f.shape[0]) for f in fs]
+    c = qasr.Context(m, max_batch=B, max_ctx=max(len(p[0]) for p in pr) + steps + 8)
+    try:
+        _, am = c.prefill([pr[b % 2][0] for b in range(B)], [fs[b % 2] for b in range(B)], [pr[b % 2][1] for b in range(B)],
+                          want_logits=False)
+        tok0 = [int(am[0]), int(am[1])]
+        toks, out = [tok0[b % 2] for b in range(B)], []
+        for s in range(steps):
+            lg, am = c.decode_step(toks, [len(pr[b % 2][0]) + s for b in range(B)])
+            out.append(lg)
+            toks = [int(am[b % 2]) for b in range(B)]
+    finally:
+        c.close()
+        m.close()
+    for lg in out:
+        for b in range(2, B):
+            assert np.array_equal(lg[b], lg[b % 2]), b
+    for k in range(2):
+        ids, pos = pr[k]
+        dec = op.OracleDecoder(om, len(ids) + steps + 8)
+        dec.forward(ids, 0, fs[k], pos)
+        ref = dec.forward([tok0[k]], len(ids))
+        tol = (2e-2 if q8 else 1e-2) * float(np.abs(ref).max())
+        assert np.abs(out[0][k] - ref).max() <= tol, (k, np.abs(out[0][k] - ref).max(), tol)
