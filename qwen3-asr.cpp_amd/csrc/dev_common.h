@@ -149,3 +149,49 @@ __device__ __forceinline__ void q8_scale_acc(floatx4 &acc, float dw, floatx4 dx,
     const floatx2 a23 = __builtin_elementwise_fma(s23, c23, floatx2{acc[2], acc[3]});
     acc = floatx4{a01[0], a01[1], a23[0], a23[1]};
 }
+
+// ggml_rms_norm (+ mul by w) of one D-wide fp32 row by one wave: lane owns
+// columns 4 lane + 256 i (v[i]); sum of fp32 squares in double, scale =
+// 1/sqrtf(mean + eps).  Output: fp16 y, fp32 y32, or Q8_0 (yq int8 + yd fp32
+// block scales, a 32-block = 8 lanes) -- row `row` of a D-wide output.
+// Shared by rmsnorm_kernel and the skinny GEMM's fused post-norm, so both give
+// the same bits.
+template <int D>
+__device__ __forceinline__ void rms_row(const float4 *v, const float *__restrict__ w, float eps, long row,
+                                        uint16_t *__restrict__ y, float *__restrict__ y32, int8_t *__restrict__ yq,
+                                        float *__restrict__ yd) {
+    constexpr int PER = D / 256;
+    const int lane = threadIdx.x & 63;
+    float4 wv[PER];
+#pragma unroll
+    for (int i = 0; i < PER; i++) wv[i] = *(const float4 *)(w + 4 * lane + 256 * i);
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < PER; i++)
+        s += ((double)fmul_rn(v[i].x, v[i].x) + (double)fmul_rn(v[i].y, v[i].y)) +
+             ((double)fmul_rn(v[i].z, v[i].z) + (double)fmul_rn(v[i].w, v[i].w));
+    s = wave_sum_d(s);
+    const float mean = (float)(s / D);
+    const float scale = 1.0f / sqrtf(mean + eps);
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+        const float4 t = make_float4(fmul_rn(fmul_rn(v[i].x, scale), wv[i].x), fmul_rn(fmul_rn(v[i].y, scale), wv[i].y),
+                                     fmul_rn(fmul_rn(v[i].z, scale), wv[i].z), fmul_rn(fmul_rn(v[i].w, scale), wv[i].w));
+        const long o = row * D + 4 * lane + 256 * i;
+        if (yq) {
+            float am = fmaxf(fmaxf(fabsf(t.x), fabsf(t.y)), fmaxf(fabsf(t.z), fabsf(t.w)));
+            am = fmaxf(am, __shfl_xor(am, 1, 64));
+            am = fmaxf(am, __shfl_xor(am, 2, 64));
+            am = fmaxf(am, __shfl_xor(am, 4, 64));
+            const uint32_t u = (uint32_t)(uint8_t)q8_quant(t.x, am) | (uint32_t)(uint8_t)q8_quant(t.y, am) << 8 |
+                               (uint32_t)(uint8_t)q8_quant(t.z, am) << 16 | (uint32_t)(uint8_t)q8_quant(t.w, am) << 24;
+            *(uint32_t *)(yq + o) = u;
+            if ((lane & 7) == 0) yd[row * (D / 32) + lane / 8 + 8 * i] = q8_scale(am);
+        } else if (y32) {
+            *(float4 *)(y32 + o) = t;
+        } else {
+            const uint32_t lo = f_to_u16(t.x) | ((uint32_t)f_to_u16(t.y) << 16), hi = f_to_u16(t.z) | ((uint32_t)f_to_u16(t.w) << 16);
+            *(uint2 *)(y + o) = make_uint2(lo, hi);
+        }
+    }
+}

@@ -155,41 +155,10 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float *__restrict__ 
     constexpr int PER = D / 256;
     const int src = row_idx ? row_idx[row] : row;
     const float *xr = x + (long)src * ldx;
-    float4 v[PER], wv[PER];
+    float4 v[PER];
 #pragma unroll
-    for (int i = 0; i < PER; i++) {
-        v[i] = *(const float4 *)(xr + 4 * lane + 256 * i);
-        wv[i] = *(const float4 *)(w + 4 * lane + 256 * i);
-    }
-    double s = 0.0;
-#pragma unroll
-    for (int i = 0; i < PER; i++)
-        s += ((double)fmul_rn(v[i].x, v[i].x) + (double)fmul_rn(v[i].y, v[i].y)) +
-             ((double)fmul_rn(v[i].z, v[i].z) + (double)fmul_rn(v[i].w, v[i].w));
-    s = wave_sum_d(s);
-    const float mean = (float)(s / D);
-    const float scale = 1.0f / sqrtf(mean + eps);
-#pragma unroll
-    for (int i = 0; i < PER; i++) {
-        const float4 t = make_float4(fmul_rn(fmul_rn(v[i].x, scale), wv[i].x), fmul_rn(fmul_rn(v[i].y, scale), wv[i].y),
-                                     fmul_rn(fmul_rn(v[i].z, scale), wv[i].z), fmul_rn(fmul_rn(v[i].w, scale), wv[i].w));
-        const long o = (long)row * D + 4 * lane + 256 * i;
-        if (yq) {
-            float am = fmaxf(fmaxf(fabsf(t.x), fabsf(t.y)), fmaxf(fabsf(t.z), fabsf(t.w)));
-            am = fmaxf(am, __shfl_xor(am, 1, 64));
-            am = fmaxf(am, __shfl_xor(am, 2, 64));
-            am = fmaxf(am, __shfl_xor(am, 4, 64));
-            const uint32_t u = (uint32_t)(uint8_t)q8_quant(t.x, am) | (uint32_t)(uint8_t)q8_quant(t.y, am) << 8 |
-                               (uint32_t)(uint8_t)q8_quant(t.z, am) << 16 | (uint32_t)(uint8_t)q8_quant(t.w, am) << 24;
-            *(uint32_t *)(yq + o) = u;
-            if ((lane & 7) == 0) yd[(long)row * (D / 32) + lane / 8 + 8 * i] = q8_scale(am);
-        } else if (y32) {
-            *(float4 *)(y32 + o) = t;
-        } else {
-            const uint32_t lo = f_to_u16(t.x) | ((uint32_t)f_to_u16(t.y) << 16), hi = f_to_u16(t.z) | ((uint32_t)f_to_u16(t.w) << 16);
-            *(uint2 *)(y + o) = make_uint2(lo, hi);
-        }
-    }
+    for (int i = 0; i < PER; i++) v[i] = *(const float4 *)(xr + 4 * lane + 256 * i);
+    rms_row<D>(v, w, eps, row, y, y32, yq, yd);
 }
 
 static void rmsnorm_any(const float *x, int ldx, const int *row_idx, int M, int D, const float *w, float eps, uint16_t *y,

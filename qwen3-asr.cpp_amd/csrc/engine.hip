@@ -109,6 +109,8 @@ struct qasr_ctx {
     DevBuf q8a, q8d, x32;          // Q8_0 models: quantised activations (int8 + scales), fp32 layer inputs
     float *d_att32 = nullptr, *d_act32 = nullptr;   // Q8_0 decode: fp32 attention output / SwiGLU output
     int8_t *d_q8a = nullptr; float *d_q8d = nullptr, *d_x32 = nullptr;   // Q8_0 batched (B > 8) decode, graph-fixed
+    int8_t *d_q8n = nullptr; float *d_q8nd = nullptr;   // ... the RMS-normed layer inputs (QKV, gate/up), quantised
+    unsigned int *d_ncnt = nullptr;                     // decode batches: fused post-norm row-block counters [8][16]
     // fixed decode state (sized by max_batch)
     int32_t *d_tok = nullptr, *d_hist = nullptr;
     int *d_pos = nullptr, *d_nkv = nullptr, *d_slot = nullptr, *d_step = nullptr;
@@ -218,6 +220,7 @@ static const std::vector<FuseOption> &fuse_options() {
         {"fa_exact_decode", "QASR_FA_EXACT_DECODE", &FuseCfg::fa_exact_decode},
         {"qkv_ffn", "QASR_QKV_FFN", &FuseCfg::qkv_ffn},
         {"att_stream", "QASR_ATT_STREAM", &FuseCfg::att_stream},
+        {"post_norm", "QASR_POST_NORM", &FuseCfg::post_norm},
         {"qffn_delay", "QASR_QFFN_DELAY", &FuseCfg::qffn_delay},
         {"qffn_poll_delay", "QASR_QFFN_POLL_DELAY", &FuseCfg::qffn_poll_delay},
     };
@@ -336,6 +339,14 @@ static int upload(qasr_ctx *c, DevBuf &b, const std::vector<T> &v) {
 // A Q8_0 linear layer: quantise the activation rows (fp32 a32 or fp16 a16,
 // optional conv_out gather) into c->q8a / c->q8d, then the int8 block GEMM.
 // g carries M, N, K and the epilogue.
+// a projection asked for the fused post-norm (GemmArgs.post_w) that the
+// skinny GEMM did not take: the separate norm launch instead
+static void post_norm_fallback(const GemmArgs &g, hipStream_t s) {
+    if (!g.post_w) return;
+    if (g.post_yq) launch_rmsnorm_q8(g.out_f32, g.ldo, g.M, g.N, g.post_w, g.post_eps, g.post_yq, g.post_yd, s);
+    else launch_rmsnorm_f16(g.out_f32, g.ldo, nullptr, g.M, g.N, g.post_w, g.post_eps, g.post_y, s);
+}
+
 static void gemm_q8(qasr_ctx *c, int epi, GemmArgs g, const float *a32, const uint16_t *a16, int lda, int gather_C,
                     const uint16_t *W, const uint16_t *Wd, hipStream_t s, int8_t *qa = nullptr, float *qd = nullptr,
                     bool decode = false) {
@@ -345,14 +356,18 @@ static void gemm_q8(qasr_ctx *c, int epi, GemmArgs g, const float *a32, const ui
     g.Wq = (const int8_t *)W; g.ldw = g.K; g.Wd = Wd;
     if (decode && launch_gemm_skinny_q8(epi, g, s)) return;
     launch_gemm_q8(epi, g, s);
+    post_norm_fallback(g, s);
 }
 
 // decode batches: activations already quantised into d_q8a / d_q8d by the
 // producing kernel (rmsnorm_q8, the attention combiner)
-static void gemm_q8_pre(qasr_ctx *c, int epi, GemmArgs g, const uint16_t *W, const uint16_t *Wd, hipStream_t s) {
-    g.Aq = c->d_q8a; g.lda = g.K; g.Ad = c->d_q8d; g.ldad = g.K / 32;
+static void gemm_q8_pre(qasr_ctx *c, int epi, GemmArgs g, const uint16_t *W, const uint16_t *Wd, hipStream_t s,
+                        const int8_t *qa = nullptr, const float *qd = nullptr) {
+    g.Aq = qa ? qa : c->d_q8a; g.lda = g.K; g.Ad = qa ? qd : c->d_q8d; g.ldad = g.K / 32;
     g.Wq = (const int8_t *)W; g.ldw = g.K; g.Wd = Wd;
-    if (!launch_gemm_skinny_q8(epi, g, s)) launch_gemm_q8(epi, g, s);
+    if (launch_gemm_skinny_q8(epi, g, s)) return;
+    launch_gemm_q8(epi, g, s);
+    post_norm_fallback(g, s);
 }
 
 static int ensure_q8(qasr_ctx *c, size_t rows, size_t kmax, size_t x32_cols) {
@@ -698,6 +713,9 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_q8a, (size_t)B * std::max(QD, std::max(hp.hidden, hp.dec_ffn)))) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_q8d, (size_t)B * std::max(QD, std::max(hp.hidden, hp.dec_ffn)) / 32 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_x32, (size_t)B * std::max(QD, std::max(hp.hidden, hp.dec_ffn)) * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_q8n, (size_t)B * hp.hidden)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_q8nd, (size_t)B * hp.hidden / 32 * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_ncnt, (size_t)8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_part, (size_t)B * hp.n_kv_head * c->max_splits * 2 * 132 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_counter, (size_t)B * hp.n_kv_head * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_scores, (size_t)B * hp.n_head * max_ctx * 4)) ||
@@ -719,6 +737,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     HIPCHK(hipMemset(c->d_qcnt, 0, (size_t)hp.n_kv_head * 8 * 16 * 4));
     HIPCHK(hipMemset(c->d_ocnt, 0, (size_t)hp.dec_layers * 512 * 4));
     HIPCHK(hipMemset(c->d_dcnt, 0, (size_t)hp.dec_layers * 512 * 4));
+    HIPCHK(hipMemset(c->d_ncnt, 0, (size_t)8 * 16 * 4));
     HIPCHK(hipMemset(c->d_attdone, 0, (size_t)8 * 16 * 4));
     HIPCHK(hipMemset(c->d_gran, 0, (size_t)(QD + 2 * KD) * 8));
     HIPCHK(hipMemset(c->d_ffncnt, 0, (size_t)hp.dec_layers * 512 * 4));
@@ -1133,7 +1152,9 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
 // decode-batch projections: the weight-streaming skinny GEMM where it takes
 // the shape, the tiled GEMM otherwise
 static void dec_gemm(int epi, const GemmArgs &g, hipStream_t s) {
-    if (!launch_gemm_skinny(epi, g, s)) launch_gemm(AM_DENSE, epi, g, s);
+    if (launch_gemm_skinny(epi, g, s)) return;
+    launch_gemm(AM_DENSE, epi, g, s);
+    post_norm_fallback(g, s);
 }
 
 // Launch groups of one decode step, in stream order (decoder cut at nl layers):
@@ -1166,6 +1187,13 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
     unsigned long long *stamp = r.hi - r.lo == 1 ? c->cur_stamp : nullptr;
     if (r.in(0) && !skinny) launch_embed(c->d_tok, B, m->embd, H, nullptr, nullptr, x, s);
     const int skip = c->dev_skip;   // profiling only (QASR_DEV_SKIP): drop kernels to price them
+    // decode batches: the RMS norms fused into the o / down projections that
+    // produce x (GemmArgs.post_w): shape-only decisions, equal for every layer
+    const bool post_o = !skinny && c->fuse.post_norm && skinny_post_ok(m->q8, B, QD, H);
+    const bool post_d = !skinny && c->fuse.post_norm && skinny_post_ok(m->q8, B, F, H);
+    auto set_post = [&](GemmArgs &g, const float *w, uint16_t *y, int8_t *yq, float *yd) {
+        g.post_w = w; g.post_eps = hp.rms_eps; g.post_y = y; g.post_yq = yq; g.post_yd = yd; g.post_cnt = c->d_ncnt;
+    };
     if (c->d_trace && r.in(0)) (void)hipMemsetAsync(c->d_trace, 0, 6 * 4096 * 8 * 8, s);
     for (int l = 0; l < nl; l++) {
         const bool ga = r.in(1 + 2 * l), gb = r.in(2 + 2 * l);
@@ -1266,11 +1294,12 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
                 } else {
                     GemmArgs q{};
                     q.M = B; q.N = QD + 2 * KD; q.K = H; q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
+                    const bool normed = l > 0 && post_d;   // the previous layer's down projection normalised x
                     if (q8) {
-                        launch_rmsnorm_q8(x, H, B, H, L.attn_norm, hp.rms_eps, c->d_q8a, c->d_q8d, s);
-                        gemm_q8_pre(c, EPI_F32, q, L.wqkv, L.wqkv_d, s);
+                        if (!normed) launch_rmsnorm_q8(x, H, B, H, L.attn_norm, hp.rms_eps, c->d_q8n, c->d_q8nd, s);
+                        gemm_q8_pre(c, EPI_F32, q, L.wqkv, L.wqkv_d, s, c->d_q8n, c->d_q8nd);
                     } else {
-                        launch_rmsnorm_f16(x, H, nullptr, B, H, L.attn_norm, hp.rms_eps, c->d_xh, s);
+                        if (!normed) launch_rmsnorm_f16(x, H, nullptr, B, H, L.attn_norm, hp.rms_eps, c->d_xh, s);
                         q.A = c->d_xh; q.lda = H; q.W = L.wqkv; q.ldw = H; dec_gemm(EPI_F32, q, s);
                     }
                 }
@@ -1297,24 +1326,31 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         } else if (q8) {
             GemmArgs ob{};
             ob.M = B; ob.N = H; ob.K = QD; ob.res = x; ob.ldr = H; ob.out_f32 = x; ob.ldo = H;
+            if (post_o) set_post(ob, L.ffn_norm, nullptr, c->d_q8n, c->d_q8nd);
             gemm_q8_pre(c, EPI_F32, ob, L.wo, L.wo_d, s);
-            launch_rmsnorm_q8(x, H, B, H, L.ffn_norm, hp.rms_eps, c->d_q8a, c->d_q8d, s);
+            if (!post_o) launch_rmsnorm_q8(x, H, B, H, L.ffn_norm, hp.rms_eps, c->d_q8n, c->d_q8nd, s);
             GemmArgs gu{};
             gu.M = B; gu.N = 2 * F; gu.K = H; gu.out_f32 = c->d_x32; gu.ldo = F;
-            gemm_q8_pre(c, EPI_SWIGLU_F32, gu, L.wgu, L.wgu_d, s);
+            gemm_q8_pre(c, EPI_SWIGLU_F32, gu, L.wgu, L.wgu_d, s, c->d_q8n, c->d_q8nd);
             GemmArgs dn{};
             dn.M = B; dn.N = H; dn.K = F; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
+            if (post_d) {   // the next layer's attention norm (Q8_0), or the final norm of the (f16) LM head
+                if (l + 1 < nl) set_post(dn, m->dec[l + 1].attn_norm, nullptr, c->d_q8n, c->d_q8nd);
+                else set_post(dn, m->out_norm, c->d_xh, nullptr, nullptr);
+            }
             gemm_q8(c, EPI_F32, dn, c->d_x32, nullptr, F, 0, L.wd, L.wd_d, s, c->d_q8a, c->d_q8d, true);
         } else {
             GemmArgs ob{};
             ob.A = c->d_att; ob.lda = QD; ob.W = L.wo; ob.ldw = QD; ob.M = B; ob.N = H; ob.K = QD; ob.res = x; ob.ldr = H; ob.out_f32 = x; ob.ldo = H;
+            if (post_o) set_post(ob, L.ffn_norm, c->d_xh, nullptr, nullptr);
             dec_gemm(EPI_F32, ob, s);
-            launch_rmsnorm_f16(x, H, nullptr, B, H, L.ffn_norm, hp.rms_eps, c->d_xh, s);
+            if (!post_o) launch_rmsnorm_f16(x, H, nullptr, B, H, L.ffn_norm, hp.rms_eps, c->d_xh, s);
             GemmArgs gu{};
             gu.A = c->d_xh; gu.lda = H; gu.W = L.wgu; gu.ldw = H; gu.M = B; gu.N = 2 * F; gu.K = H; gu.out_f16 = c->d_act; gu.ldo16 = F;
             dec_gemm(EPI_SWIGLU_F16, gu, s);
             GemmArgs dn{};
             dn.A = c->d_act; dn.lda = F; dn.W = L.wd; dn.ldw = F; dn.M = B; dn.N = H; dn.K = F; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
+            if (post_d) set_post(dn, l + 1 < nl ? m->dec[l + 1].attn_norm : m->out_norm, c->d_xh, nullptr, nullptr);
             dec_gemm(EPI_F32, dn, s);
         }
     }
@@ -1329,7 +1365,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             launch_gemv(EPI_ARGMAX, lm, s);
         } else {
             launch_fill_u64(c->d_amax, B, 0ull, s);
-            launch_rmsnorm_f16(x, H, nullptr, B, H, m->out_norm, hp.rms_eps, c->d_xh, s);
+            if (!(post_d && nl > 0)) launch_rmsnorm_f16(x, H, nullptr, B, H, m->out_norm, hp.rms_eps, c->d_xh, s);
             GemmArgs lm{};
             lm.A = c->d_xh; lm.lda = H; lm.W = m->embd; lm.ldw = H; lm.M = B; lm.N = hp.vocab; lm.K = H;
             lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;

@@ -73,7 +73,17 @@ struct GemmArgs {
     const int8_t *Aq; const float *Ad; int ldad;
     const int8_t *Wq; const uint16_t *Wd;
     int regs_staged;                      // 1: register-staged tiles instead of the LDS-DMA ones (A/B option)
+    // decode batches (skinny EPI_F32, N = 1024, + residual): the row block's
+    // last column-tile workgroup RMS-normalises its finished output rows with
+    // rmsnorm_kernel's arithmetic (dev_common.h rms_row) into post_y (fp16) or
+    // post_yq / post_yd (Q8_0) -- the next projection's input, instead of a
+    // separate rmsnorm launch; post_cnt: per row block arrival counters
+    // (16-word stride, zero at rest)
+    const float *post_w; float post_eps; uint16_t *post_y; int8_t *post_yq; float *post_yd; unsigned int *post_cnt;
 };
+// the skinny decode-batch GEMM takes an EPI_F32 projection of this shape with
+// the fused post-norm (launch_gemm_skinny / _q8 with post_w set)
+bool skinny_post_ok(bool q8, int M, int K, int N);
 void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s);
 // decode-batch GEMM (gemm_skinny.hip): dense A, M <= 128, K % 128 == 0; returns
 // false (nothing launched) for shapes it does not take.  QASR_SKINNY=0 disables.
@@ -157,7 +167,10 @@ struct FuseCfg {
     int qffn_delay = 30, qffn_poll_delay = 10;   // ... its weight request / first poll (s_sleep(8) units, ~0.2 us)
     int slots_ffn = 0, slots_qkv64 = 0, slots_qkv128 = 0;   // co-resident workgroups on this device
     int slots_layer64 = 0, slots_layer128 = 0;
-    int att_stream = 1;                 // decode batches: streamed attention splits (decode_attn_stream_kernel)
+    int att_stream = 1;                 // decode batches: one workgroup per (kv group, sequence) (decode_attn_seq_kernel)
+    int post_norm = 0;                  // decode batches: RMS norms fused into the producing o / down projections
+                                        // (last arriver per row block); bit-identical, measured slower (64 x 30 s decode
+                                        // f16 203.6 -> 208.9 ms, Q8_0 266.5 -> 275.0: tools/job_postnorm.sh)
     int slots_stream = 0;               // ... its co-resident workgroups on this device
     unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
 };
