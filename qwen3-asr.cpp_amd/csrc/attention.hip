@@ -1771,8 +1771,7 @@ void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {
         // batches that give every CU a sequence or more: one workgroup per (kv group, sequence)
         hipLaunchKernelGGL(decode_attn_seq_kernel, dim3(a.n_kv_head, a.B), dim3(256), 0, s, a);
     } else {   // batches: longer splits (fewer workgroups and partials per sequence)
-        static const int spl = [] { const char *e = getenv("QASR_ATT_SPL"); return e ? atoi(e) : 256; }();
-        if (spl == 128) {
+        if (a.spl_batch == 128) {
             const int g2 = (a.grid_splits * DSPLIT + 127) / 128;
             hipLaunchKernelGGL(decode_attn_kernel<128>, dim3(g2, a.n_kv_head, a.B), dim3(256), 0, s, a);
         } else {

@@ -221,6 +221,8 @@ static const std::vector<FuseOption> &fuse_options() {
         {"qkv_ffn", "QASR_QKV_FFN", &FuseCfg::qkv_ffn},
         {"att_stream", "QASR_ATT_STREAM", &FuseCfg::att_stream},
         {"post_norm", "QASR_POST_NORM", &FuseCfg::post_norm},
+        {"skinny", "QASR_SKINNY", &FuseCfg::skinny},
+        {"att_spl", "QASR_ATT_SPL", &FuseCfg::att_spl},
         {"qffn_delay", "QASR_QFFN_DELAY", &FuseCfg::qffn_delay},
         {"qffn_poll_delay", "QASR_QFFN_POLL_DELAY", &FuseCfg::qffn_poll_delay},
     };
@@ -354,6 +356,7 @@ static void gemm_q8(qasr_ctx *c, int epi, GemmArgs g, const float *a32, const ui
     launch_quantize_q8(a32, a16, lda, g.M, g.K, gather_C, qa, qd, s);
     g.Aq = qa; g.lda = g.K; g.Ad = qd; g.ldad = g.K / 32;
     g.Wq = (const int8_t *)W; g.ldw = g.K; g.Wd = Wd;
+    g.no_skinny = !c->fuse.skinny;
     if (decode && launch_gemm_skinny_q8(epi, g, s)) return;
     launch_gemm_q8(epi, g, s);
     post_norm_fallback(g, s);
@@ -365,6 +368,7 @@ static void gemm_q8_pre(qasr_ctx *c, int epi, GemmArgs g, const uint16_t *W, con
                         const int8_t *qa = nullptr, const float *qd = nullptr) {
     g.Aq = qa ? qa : c->d_q8a; g.lda = g.K; g.Ad = qa ? qd : c->d_q8d; g.ldad = g.K / 32;
     g.Wq = (const int8_t *)W; g.ldw = g.K; g.Wd = Wd;
+    g.no_skinny = !c->fuse.skinny;
     if (launch_gemm_skinny_q8(epi, g, s)) return;
     launch_gemm_q8(epi, g, s);
     post_norm_fallback(g, s);
@@ -1151,7 +1155,8 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
 
 // decode-batch projections: the weight-streaming skinny GEMM where it takes
 // the shape, the tiled GEMM otherwise
-static void dec_gemm(int epi, const GemmArgs &g, hipStream_t s) {
+static void dec_gemm(qasr_ctx *c, int epi, GemmArgs g, hipStream_t s) {
+    g.no_skinny = !c->fuse.skinny;
     if (launch_gemm_skinny(epi, g, s)) return;
     launch_gemm(AM_DENSE, epi, g, s);
     post_norm_fallback(g, s);
@@ -1189,8 +1194,8 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
     const int skip = c->dev_skip;   // profiling only (QASR_DEV_SKIP): drop kernels to price them
     // decode batches: the RMS norms fused into the o / down projections that
     // produce x (GemmArgs.post_w): shape-only decisions, equal for every layer
-    const bool post_o = !skinny && c->fuse.post_norm && skinny_post_ok(m->q8, B, QD, H);
-    const bool post_d = !skinny && c->fuse.post_norm && skinny_post_ok(m->q8, B, F, H);
+    const bool post_o = !skinny && c->fuse.post_norm && c->fuse.skinny && skinny_post_ok(m->q8, B, QD, H);
+    const bool post_d = !skinny && c->fuse.post_norm && c->fuse.skinny && skinny_post_ok(m->q8, B, F, H);
     auto set_post = [&](GemmArgs &g, const float *w, uint16_t *y, int8_t *yq, float *yd) {
         g.post_w = w; g.post_eps = hp.rms_eps; g.post_y = y; g.post_yq = yq; g.post_yd = yd; g.post_cnt = c->d_ncnt;
     };
@@ -1215,6 +1220,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         da.qcnt = c->d_qcnt;
         da.spl1 = c->fuse.spl1;
         da.stream_blocks = !skinny && c->fuse.att_stream ? c->fuse.slots_stream : 0;
+        da.spl_batch = c->fuse.att_spl;
         da.stamp = stamp;
         GemvArgs o{};
         if (skinny) {
@@ -1300,7 +1306,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
                         gemm_q8_pre(c, EPI_F32, q, L.wqkv, L.wqkv_d, s, c->d_q8n, c->d_q8nd);
                     } else {
                         if (!normed) launch_rmsnorm_f16(x, H, nullptr, B, H, L.attn_norm, hp.rms_eps, c->d_xh, s);
-                        q.A = c->d_xh; q.lda = H; q.W = L.wqkv; q.ldw = H; dec_gemm(EPI_F32, q, s);
+                        q.A = c->d_xh; q.lda = H; q.W = L.wqkv; q.ldw = H; dec_gemm(c, EPI_F32, q, s);
                     }
                 }
                 da.att_done = nullptr;
@@ -1343,15 +1349,15 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             GemmArgs ob{};
             ob.A = c->d_att; ob.lda = QD; ob.W = L.wo; ob.ldw = QD; ob.M = B; ob.N = H; ob.K = QD; ob.res = x; ob.ldr = H; ob.out_f32 = x; ob.ldo = H;
             if (post_o) set_post(ob, L.ffn_norm, c->d_xh, nullptr, nullptr);
-            dec_gemm(EPI_F32, ob, s);
+            dec_gemm(c, EPI_F32, ob, s);
             if (!post_o) launch_rmsnorm_f16(x, H, nullptr, B, H, L.ffn_norm, hp.rms_eps, c->d_xh, s);
             GemmArgs gu{};
             gu.A = c->d_xh; gu.lda = H; gu.W = L.wgu; gu.ldw = H; gu.M = B; gu.N = 2 * F; gu.K = H; gu.out_f16 = c->d_act; gu.ldo16 = F;
-            dec_gemm(EPI_SWIGLU_F16, gu, s);
+            dec_gemm(c, EPI_SWIGLU_F16, gu, s);
             GemmArgs dn{};
             dn.A = c->d_act; dn.lda = F; dn.W = L.wd; dn.ldw = F; dn.M = B; dn.N = H; dn.K = F; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
             if (post_d) set_post(dn, l + 1 < nl ? m->dec[l + 1].attn_norm : m->out_norm, c->d_xh, nullptr, nullptr);
-            dec_gemm(EPI_F32, dn, s);
+            dec_gemm(c, EPI_F32, dn, s);
         }
     }
     if (r.in(1 + 2 * nl)) {
@@ -1369,7 +1375,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             GemmArgs lm{};
             lm.A = c->d_xh; lm.lda = H; lm.W = m->embd; lm.ldw = H; lm.M = B; lm.N = hp.vocab; lm.K = H;
             lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
-            dec_gemm(EPI_ARGMAX, lm, s);
+            dec_gemm(c, EPI_ARGMAX, lm, s);
         }
     }
     if (r.in(2 + 2 * nl) && !skinny) {   // bookkeeping (fused into the LM-head GEMV at batch <= 8)

@@ -460,19 +460,14 @@ static void skinny_mt(const GemmArgs &g, hipStream_t s) {
     else run_skinny<MTMAX >= 4 ? 4 : 1, NT, KW, EPI>(g, s);
 }
 
-static bool skinny_off() {
-    static const bool off = [] { const char *e = getenv("QASR_SKINNY"); return e && e[0] == '0'; }();
-    return off;
-}
-
 // the o / down projections of a decode batch (<1, 1, 8> tiles, N = 1024): the
 // shapes launch_gemm_skinny / _q8 take with the fused post-norm
 bool skinny_post_ok(bool q8, int M, int K, int N) {
-    return !skinny_off() && M > 8 && M <= 128 && K % 128 == 0 && (q8 ? K % 16 == 0 : K % 8 == 0) && N == 1024;
+    return M > 8 && M <= 128 && K % 128 == 0 && (q8 ? K % 16 == 0 : K % 8 == 0) && N == 1024;
 }
 
 bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s) {
-    const bool off = skinny_off();
+    const bool off = g.no_skinny != 0;
     if (g.post_w && (epi != EPI_F32 || !skinny_post_ok(false, g.M, g.K, g.N) || !g.post_cnt || g.ldo != 1024)) return false;
     if (off || g.M <= 0 || g.M > 128 || g.K % 128 != 0 || g.lda % 8 != 0 || g.ldw % 8 != 0) return false;
     switch (epi) {
@@ -503,7 +498,7 @@ bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s) {
 }
 
 bool launch_gemm_skinny_q8(int epi, const GemmArgs &g, hipStream_t s) {
-    const bool off = skinny_off();
+    const bool off = g.no_skinny != 0;
     if (g.post_w && (epi != EPI_F32 || !skinny_post_ok(true, g.M, g.K, g.N) || !g.post_cnt || g.ldo != 1024)) return false;
     if (off || g.M <= 0 || g.M > 128 || g.K % 128 != 0 || g.lda % 16 != 0 || g.ldw % 16 != 0 || g.ldad % 4 != 0) return false;
     switch (epi) {

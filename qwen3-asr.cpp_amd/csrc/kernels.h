@@ -80,13 +80,14 @@ struct GemmArgs {
     // separate rmsnorm launch; post_cnt: per row block arrival counters
     // (16-word stride, zero at rest)
     const float *post_w; float post_eps; uint16_t *post_y; int8_t *post_yq; float *post_yd; unsigned int *post_cnt;
+    int no_skinny;                        // 1: launch_gemm_skinny / _q8 decline (per-context option skinny = 0)
 };
 // the skinny decode-batch GEMM takes an EPI_F32 projection of this shape with
 // the fused post-norm (launch_gemm_skinny / _q8 with post_w set)
 bool skinny_post_ok(bool q8, int M, int K, int N);
 void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s);
 // decode-batch GEMM (gemm_skinny.hip): dense A, M <= 128, K % 128 == 0; returns
-// false (nothing launched) for shapes it does not take.  QASR_SKINNY=0 disables.
+// false (nothing launched) for shapes it does not take, or when g.no_skinny.
 bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s);
 // the same for Q8_0 weights (Aq/Ad quantised activations, Wq/Wd): EPI_F32, EPI_SWIGLU_F32
 bool launch_gemm_skinny_q8(int epi, const GemmArgs &g, hipStream_t s);
@@ -168,6 +169,8 @@ struct FuseCfg {
     int slots_ffn = 0, slots_qkv64 = 0, slots_qkv128 = 0;   // co-resident workgroups on this device
     int slots_layer64 = 0, slots_layer128 = 0;
     int att_stream = 1;                 // decode batches: one workgroup per (kv group, sequence) (decode_attn_seq_kernel)
+    int skinny = 1;                     // decode batches: the weight-streaming skinny GEMMs (0 = tiled GEMMs)
+    int att_spl = 256;                  // decode batches on the split attention kernels: keys per split (128 or 256)
     int post_norm = 0;                  // decode batches: RMS norms fused into the producing o / down projections
                                         // (last arriver per row block); bit-identical, measured slower (64 x 30 s decode
                                         // f16 203.6 -> 208.9 ms, Q8_0 266.5 -> 275.0: tools/job_postnorm.sh)
@@ -295,8 +298,9 @@ struct DecodeAttnArgs {
     const uint16_t *pf0, *pf1;           // fused launch: byte ranges pulled into the Infinity Cache (null: none)
     long pf_n0, pf_n1;                   // their sizes in 16-B lines
     int pf_blocks, pf_delay;
-    int stream_blocks;                   // decode batches (B > 8): grid of decode_attn_stream_kernel, which loops over the
-                                         // 128-key splits with the next one's K/V in flight (0 = one workgroup per split)
+    int stream_blocks;                   // decode batches (B > 8): co-resident workgroups of decode_attn_seq_kernel (one per
+                                         // kv group and sequence, taken once the batch fills them; 0 = split kernels)
+    int spl_batch;                       // decode batches on the split kernels: 128- or 256-key splits (FuseCfg::att_spl)
 };
 // Batch 1, the whole decoder layer in one launch (attention.hip layer1_kernel):
 // QKV (256 blocks) -> attention splits -> o-projection (128) -> gate/up (192)
