@@ -588,7 +588,14 @@ template <int EPI>
 static void dispatch_q8(const GemmArgs &g, hipStream_t s) {
     const bool big = g.M >= 2048 && g.N % 128 == 0;
     if (g.K % 128 == 0) {
-        if (big) run_gemm_q8<128, 128, 2, EPI>(g, s);   // (KS 4: 82 KB of LDS, one workgroup a CU: prefill 152 -> 306 ms)
+        // large M: 128 x 64 tiles (4 x 2 fragments a wave).  With 128 x 128 the 64
+        // fp32 accumulators a wave did not fit beside the MFMA results and every
+        // block's scaling shuttled them through AGPRs (~10 v_accvgpr moves per
+        // MFMA on top of the 8 scaling ops): configs[2] prefill 152.6 -> 121.6 ms,
+        // encode 80.6 -> 64.3 (64 x 64: 130.3 / 67.4, 64 x 128: 122.5 / 65.2;
+        // 128 x 128 with 128-wide K stages: 306 ms, one workgroup a CU)
+        if (big && g.N % 64 == 0) run_gemm_q8<128, 64, 2, EPI>(g, s);
+        else if (big) run_gemm_q8<128, 128, 2, EPI>(g, s);
         else run_gemm_q8<64, 64, 4, EPI>(g, s);
     } else {
         run_gemm_q8<64, 64, 1, EPI>(g, s);
