@@ -594,6 +594,7 @@ static void dispatch_q8(const GemmArgs &g, hipStream_t s) {
         // MFMA on top of the 8 scaling ops): configs[2] prefill 152.6 -> 121.6 ms,
         // encode 80.6 -> 64.3 (64 x 64: 130.3 / 67.4, 64 x 128: 122.5 / 65.2;
         // 128 x 128 with 128-wide K stages: 306 ms, one workgroup a CU)
+        // (128 x 64 with 128-wide K stages: 162.1 ms; 96 x 64: 129.7)
         if (big && g.N % 64 == 0) run_gemm_q8<128, 64, 2, EPI>(g, s);
         else if (big) run_gemm_q8<128, 128, 2, EPI>(g, s);
         else run_gemm_q8<64, 64, 4, EPI>(g, s);
