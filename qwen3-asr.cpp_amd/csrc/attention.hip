@@ -633,6 +633,12 @@ __device__ __forceinline__ void ld_sc1_x4_4(const uint16_t *p, u32x4 *v) {
         : "memory");
 }
 
+// a K/V cache row piece: read once per step by one CU -- nontemporal when
+// DecodeAttnArgs.kv_nt (MI355X_MICROARCH.md nt-weights), else default policy
+__device__ __forceinline__ half8 kv_load(const uint16_t *p, int nt) {
+    return nt ? __builtin_nontemporal_load((const half8 *)p) : *(const half8 *)p;
+}
+
 template <int SPL, bool FUSED>
 __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const int sp, const int g, const int b, const int nsp) {
     __shared__ __attribute__((aligned(16))) uint16_t qs[2][128];
@@ -684,13 +690,13 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
 #pragma unroll
         for (int s4 = 0; s4 < 4; s4++) {
             const int key = min(k0 + wid * (SPL / DWAVES) + 16 * t + c16, kcap);
-            kk[t][s4] = *(const half8 *)(kc + (long)key * 128 + 32 * s4 + 8 * q4);
+            kk[t][s4] = kv_load(kc + (long)key * 128 + 32 * s4 + 8 * q4, a.kv_nt);
         }
     if (!a.scores)   // scores mode reads no V
 #pragma unroll
         for (int i = 0; i < KPW; i++) {
             const int key = min(k0 + wid * (SPL / DWAVES) + i * 4 + sub, kcap);
-            vv[i] = *(const half8 *)(vc + (long)key * 128 + dl);
+            vv[i] = kv_load(vc + (long)key * 128 + dl, a.kv_nt);
         }
     // No exit test on the position anywhere: with one, hipcc hoists the
     // dependent pos load and the test in front of the K/V requests (two memory
@@ -975,15 +981,16 @@ struct KvChunk {
     half8 vv[4];   // V rows 16 wid + 4 i + sub, dims dl .. dl + 8
 };
 
-__device__ __forceinline__ void kvc_issue(const uint16_t *kc, const uint16_t *vc, int c0, int kcap, bool want_v, KvChunk &r) {
+__device__ __forceinline__ void kvc_issue(const uint16_t *kc, const uint16_t *vc, int c0, int kcap, bool want_v, KvChunk &r,
+                                          bool nt) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int sub = lane >> 4, dl = (lane & 15) * 8, q4 = lane >> 4, c16 = lane & 15;
     const int kk = min(c0 + 16 * wid + c16, kcap);
 #pragma unroll
-    for (int s4 = 0; s4 < 4; s4++) r.kk[s4] = *(const half8 *)(kc + (long)kk * 128 + 32 * s4 + 8 * q4);
+    for (int s4 = 0; s4 < 4; s4++) r.kk[s4] = kv_load(kc + (long)kk * 128 + 32 * s4 + 8 * q4, nt);
     if (want_v)
 #pragma unroll
-        for (int i = 0; i < 4; i++) r.vv[i] = *(const half8 *)(vc + (long)min(c0 + 16 * wid + 4 * i + sub, kcap) * 128 + dl);
+        for (int i = 0; i < 4; i++) r.vv[i] = kv_load(vc + (long)min(c0 + 16 * wid + 4 * i + sub, kcap) * 128 + dl, nt);
 }
 
 struct SeqSt {
@@ -1054,7 +1061,7 @@ __global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) 
     const int pos = a.pos[b], nkv = pos + 1, kcap = min(pos, a.max_ctx - 1);
     const bool want_v = !a.scores;
     KvChunk A, B;
-    kvc_issue(kc, vc, 0, kcap, want_v, A);
+    kvc_issue(kc, vc, 0, kcap, want_v, A, a.kv_nt);
     // ---- the token's q / k / v: rms norm * weight + NEOX RoPE (decode_attn_body), new K/V row to the caches
     {
         const float *raw = a.qkv + (long)b * (QD + 2 * KD);
@@ -1097,10 +1104,10 @@ __global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) 
 #pragma unroll
     for (int e = 0; e < 8; e++) { st.o0[e] = 0.f; st.o1[e] = 0.f; }
     for (int c0 = 0; c0 < nkv; c0 += 128) {   // two chunks a trip, each prefetching the other set
-        if (c0 + 64 < nkv) kvc_issue(kc, vc, c0 + 64, kcap, want_v, B);
+        if (c0 + 64 < nkv) kvc_issue(kc, vc, c0 + 64, kcap, want_v, B, a.kv_nt);
         kvc_step(a, qa, knew, vnew, c0, pos, A, st, sdst);
         if (c0 + 64 >= nkv) break;
-        if (c0 + 128 < nkv) kvc_issue(kc, vc, c0 + 128, kcap, want_v, A);
+        if (c0 + 128 < nkv) kvc_issue(kc, vc, c0 + 128, kcap, want_v, A, a.kv_nt);
         kvc_step(a, qa, knew, vnew, c0 + 64, pos, B, st, sdst);
     }
     if (sdst) { stamp_end(a.stamp); return; }

@@ -223,6 +223,7 @@ static const std::vector<FuseOption> &fuse_options() {
         {"post_norm", "QASR_POST_NORM", &FuseCfg::post_norm},
         {"skinny", "QASR_SKINNY", &FuseCfg::skinny},
         {"att_spl", "QASR_ATT_SPL", &FuseCfg::att_spl},
+        {"kv_nt", "QASR_KV_NT", &FuseCfg::kv_nt},
         {"qffn_delay", "QASR_QFFN_DELAY", &FuseCfg::qffn_delay},
         {"qffn_poll_delay", "QASR_QFFN_POLL_DELAY", &FuseCfg::qffn_poll_delay},
     };
@@ -1221,6 +1222,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         da.spl1 = c->fuse.spl1;
         da.stream_blocks = !skinny && c->fuse.att_stream ? c->fuse.slots_stream : 0;
         da.spl_batch = c->fuse.att_spl;
+        da.kv_nt = c->fuse.kv_nt;
         da.stamp = stamp;
         GemvArgs o{};
         if (skinny) {

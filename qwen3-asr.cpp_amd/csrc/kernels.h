@@ -171,6 +171,8 @@ struct FuseCfg {
     int att_stream = 1;                 // decode batches: one workgroup per (kv group, sequence) (decode_attn_seq_kernel)
     int skinny = 1;                     // decode batches: the weight-streaming skinny GEMMs (0 = tiled GEMMs)
     int att_spl = 256;                  // decode batches on the split attention kernels: keys per split (128 or 256)
+    int kv_nt = 1;                      // decode attention: K/V cache rows loaded nontemporal (read once per step by one
+                                        // CU; tools/job_kvnt.sh: configs[1] neutral, 64 x 30 s decode 205.0 -> 202.1 ms)
     int post_norm = 0;                  // decode batches: RMS norms fused into the producing o / down projections
                                         // (last arriver per row block); bit-identical, measured slower (64 x 30 s decode
                                         // f16 203.6 -> 208.9 ms, Q8_0 266.5 -> 275.0: tools/job_postnorm.sh)
@@ -301,6 +303,7 @@ struct DecodeAttnArgs {
     int stream_blocks;                   // decode batches (B > 8): co-resident workgroups of decode_attn_seq_kernel (one per
                                          // kv group and sequence, taken once the batch fills them; 0 = split kernels)
     int spl_batch;                       // decode batches on the split kernels: 128- or 256-key splits (FuseCfg::att_spl)
+    int kv_nt;                           // K/V cache loads nontemporal (FuseCfg::kv_nt)
 };
 // Batch 1, the whole decoder layer in one launch (attention.hip layer1_kernel):
 // QKV (256 blocks) -> attention splits -> o-projection (128) -> gate/up (192)
