@@ -128,7 +128,7 @@ def cpu_baseline(model_path: str, secs: float, tok_rate: float, threads: int, fu
 
 def pmc_traffic(kernel_prefix: str):
     """HBM bytes per launch of the roofline kernel from the newest committed
-    rocprofv3 PMC summary (profiles/<round>/summary.json, tools/job_prof.sh:
+    rocprofv3 PMC summary (profiles/<round>/summary.json, tools/profile_round.sh:
     separate FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH x2 correction)."""
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")), reverse=True):

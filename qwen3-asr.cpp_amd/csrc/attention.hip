@@ -1745,7 +1745,7 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     // prefetch workgroups wait on nothing: they need no co-residency
     const int npf = a.pf0 && cfg.pf_blocks > 0 ? cfg.pf_blocks : 0;
     const dim3 grid((no_qkv ? 0 : 512) + ns * a.n_kv_head + (with_o2 ? o->N / 4 : 0) + npf);
-    // K/V delay ~2 us: measured optimum on MI355X (tools/job_delay.sh: 0 -> 236.3, 10 -> 232.0, 18 -> 240.3 ms decode)
+    // K/V delay ~2 us: measured optimum on MI355X (round-1 delay sweep: 0 -> 236.3, 10 -> 232.0, 18 -> 240.3 ms decode)
     DecodeAttnArgs ad = a;
     ad.fuse_delay = cfg.qkv_delay;
     ad.oproj_delay = cfg.o_delay;

@@ -560,7 +560,7 @@ __global__ __launch_bounds__(256) void decode_attn_exact_pair_kernel(DecodeAttnA
 
 void launch_decode_attention_exact(const DecodeAttnArgs &a, hipStream_t s) {
     if (a.B <= 0) return;
-    // (measured on configs[2], Q8_0 64 x 30 s: decode 285.7 -> 267.2 ms, tools/job_fxpair.sh)
+    // (measured on configs[2], Q8_0 64 x 30 s: decode 285.7 -> 267.2 ms, tools/experiments.sh fxpair)
     if (a.n_head % 2 == 0 && (a.n_head / a.n_kv_head) % 2 == 0)
         hipLaunchKernelGGL(decode_attn_exact_pair_kernel, dim3(a.n_head / 2, a.B), dim3(256), 0, s, a);
     else

@@ -489,7 +489,7 @@ bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s) {
         case EPI_ARGMAX:
             if (g.N % 64 != 0) return false;
             // (64-row x 128-column tiles and 4 K waves measured 136-186 us against
-            // 139 for this one at batch 64: tools/job_lmh.sh)
+            // 139 for this one at batch 64: tools/experiments.sh lmh)
             skinny_mt<4, 4, 2, EPI_ARGMAX>(g, s);
             return true;
         default:

@@ -452,7 +452,7 @@ bool launch_ffn1(const GemvArgs &g, const GemvArgs &d, unsigned int *cnt, unsign
     if (grid > cfg.slots_ffn) return false;   // down blocks wait on gate/up blocks: all must be resident
     if (dry) return true;
     // delays in s_sleep(8) units (~0.2 us): down weights requested ~3 us after the
-    // gate/up ones, first poll ~1 us later (tools/job_ffn3.sh, 92 s decode:
+    // gate/up ones, first poll ~1 us later (round-1 delay sweep, 92 s decode:
     // unfused 224.8 ms; 12/4 217.9, 14/4 208.2 (x3), 16/4 210.0, 14/2 210.8, 14/6 210.0, 20/6 221.0)
     FfnCtl c{cnt, cnt_next, cfg.err, cfg.ffn_wdelay, cfg.ffn_delay, cfg.poll_limit, cfg.fence};
     GemvArgs q{};

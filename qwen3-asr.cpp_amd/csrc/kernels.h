@@ -164,7 +164,7 @@ struct FuseCfg {
                                         // Q8_0 models only (batch 1 exact skips the fused QKV + attention launch)
     int qkv_ffn = 0;                    // batch 1: layer l+1's rmsnorm + QKV GEMV runs in layer l's FFN launch (its weights
                                         // stream beside gate/up + down), the next launch is attention + o-proj only;
-                                        // bit-identical, measured slower (tools/job_qffn*.sh: decode 223 -> 246 ms)
+                                        // bit-identical, measured slower (tools/experiments.sh qffn / qffn2: decode 223 -> 246 ms)
     int qffn_delay = 30, qffn_poll_delay = 10;   // ... its weight request / first poll (s_sleep(8) units, ~0.2 us)
     int slots_ffn = 0, slots_qkv64 = 0, slots_qkv128 = 0;   // co-resident workgroups on this device
     int slots_layer64 = 0, slots_layer128 = 0;
@@ -172,10 +172,10 @@ struct FuseCfg {
     int skinny = 1;                     // decode batches: the weight-streaming skinny GEMMs (0 = tiled GEMMs)
     int att_spl = 256;                  // decode batches on the split attention kernels: keys per split (128 or 256)
     int kv_nt = 1;                      // decode attention: K/V cache rows loaded nontemporal (read once per step by one
-                                        // CU; tools/job_kvnt.sh: configs[1] neutral, 64 x 30 s decode 205.0 -> 202.1 ms)
+                                        // CU; tools/experiments.sh kvnt: configs[1] neutral, 64 x 30 s decode 205.0 -> 202.1 ms)
     int post_norm = 0;                  // decode batches: RMS norms fused into the producing o / down projections
                                         // (last arriver per row block); bit-identical, measured slower (64 x 30 s decode
-                                        // f16 203.6 -> 208.9 ms, Q8_0 266.5 -> 275.0: tools/job_postnorm.sh)
+                                        // f16 203.6 -> 208.9 ms, Q8_0 266.5 -> 275.0: tools/experiments.sh postnorm)
     int slots_stream = 0;               // ... its co-resident workgroups on this device
     unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
 };
