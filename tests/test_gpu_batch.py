@@ -148,3 +148,40 @@ def test_decode_batch_fused_post_norm_bit_identical(path, gpu, tiny_gguf, tiny_q
         m.close()
     for a, b in zip(*out):
         assert np.array_equal(a, b), float(np.abs(a - b).max())
+
+
+@pytest.mark.parametrize("B", [1, 48])
+def test_decode_kv_nt_bit_identical_and_attention_kernels_agree(B, gpu, tiny_gguf, tiny_oracle):
+    """kv_nt (K/V cache rows loaded nontemporal, default on) reads the same
+    bytes: bit-identical decode-step logits with it off.  At B = 48 also the
+    split-K batch attention (att_stream = 0) against the per-sequence kernel:
+    different merge order, so equal within the oracle tolerance, and both
+    against the oracle."""
+    m = qasr.Model(tiny_gguf)
+    rng = np.random.default_rng(9)
+    ids = [int(t) for t in rng.integers(0, 151643, 300)]
+    toks = [int(t) for t in rng.integers(0, 151643, 3)]
+    runs = {}
+    try:
+        for cfg in ((1, 1), (0, 1), (1, 0)):
+            if B == 1 and cfg[1] == 0:
+                continue
+            c = qasr.Context(m, max_batch=B, max_ctx=320)
+            c.set_option("kv_nt", cfg[0])
+            c.set_option("att_stream", cfg[1])
+            try:
+                c.prefill([ids] * B, want_logits=False)
+                runs[cfg] = [c.decode_step([t] * B, [len(ids) + s] * B)[0].copy() for s, t in enumerate(toks)]
+            finally:
+                c.close()
+    finally:
+        m.close()
+    for a, b in zip(runs[(1, 1)], runs[(0, 1)]):
+        assert np.array_equal(a, b)
+    dec = op.OracleDecoder(tiny_oracle, 320)
+    dec.forward(ids, 0)
+    for s, t in enumerate(toks):
+        ref = dec.forward([t], len(ids) + s)
+        tol = 1e-2 * float(np.abs(ref).max())
+        for cfg, out in runs.items():
+            assert np.abs(out[s][0] - ref).max() <= tol, (cfg, s)
