@@ -16,6 +16,7 @@
 #   qffn       next-layer QKV in the FFN launch (qkv_ffn): targeted tests, then decode A/B and delay sweep
 #   qffn2      attention launch without its QKV role: device traces and 64-key splits
 #   stream     streamed batch attention splits (att_stream) vs one workgroup per split
+#   seq3       per-sequence batch attention with three K/V register sets: tests + 64 x 30 s lines
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -164,7 +165,17 @@ for st in 1 0; do
   done
 done
 ;;
+seq3)
+timeout -k 10 300 python -u -m pytest tests/test_gpu_batch.py -x -q --timeout 240 --timeout-method thread > gpurun_out/s3_t.log 2>&1
+rc=$?; tail -2 gpurun_out/s3_t.log; [ $rc -ne 0 ] && exit $rc
+for r in 1 2; do
+  for q in "" "--q8"; do
+    timeout -k 10 200 python bench.py --batch 64 --seconds 30 --steps 2 --warmup 1 --no-cpu-baseline --no-probe $q > gpurun_out/s3_b.log 2>&1 || exit 1
+    python3 -c "import json; d=json.loads([l for l in open('gpurun_out/s3_b.log') if l.startswith('{')][-1]); print('seq3 $q', d['value'], d['stage_ms_per_step_rank0']['decode'])"
+  done
+done
+;;
 *)
-sed -n 2,20p "$0"; exit 2
+sed -n 2,21p "$0"; exit 2
 ;;
 esac
