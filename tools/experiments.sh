@@ -17,6 +17,7 @@
 #   qffn2      attention launch without its QKV role: device traces and 64-key splits
 #   stream     streamed batch attention splits (att_stream) vs one workgroup per split
 #   seq3       per-sequence batch attention with three K/V register sets: tests + 64 x 30 s lines
+#   conv1lds   conv1 with the GELU table in LDS: encoder tests + encode times (configs[1], 64 x 30 s)
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -175,7 +176,17 @@ for r in 1 2; do
   done
 done
 ;;
+conv1lds)
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_q8.py tests/test_hf_anchor.py tests/test_gpu_aligner.py -x -q --timeout 300 --timeout-method thread > gpurun_out/c1_t.log 2>&1
+rc=$?; tail -2 gpurun_out/c1_t.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python -u -m pytest tests/test_gpu_full.py -x -q --timeout 300 --timeout-method thread -k "encode or configs1" > gpurun_out/c1_t2.log 2>&1
+rc=$?; tail -2 gpurun_out/c1_t2.log; [ $rc -ne 0 ] && exit $rc
+for a in "" "--batch 64 --seconds 30"; do
+  timeout -k 10 200 python bench.py $a --steps 2 --warmup 1 --no-cpu-baseline --no-probe > gpurun_out/c1_b.log 2>&1 || exit 1
+  python3 -c "import json; d=json.loads([l for l in open('gpurun_out/c1_b.log') if l.startswith('{')][-1]); print('conv1lds $a', d['value'], d['stage_ms_per_step_rank0'])"
+done
+;;
 *)
-sed -n 2,21p "$0"; exit 2
+sed -n 2,22p "$0"; exit 2
 ;;
 esac
