@@ -18,6 +18,7 @@
 #   stream     streamed batch attention splits (att_stream) vs one workgroup per split
 #   seq3       per-sequence batch attention with three K/V register sets: tests + 64 x 30 s lines
 #   conv1lds   conv1 with the GELU table in LDS: encoder tests + encode times (configs[1], 64 x 30 s)
+#   delays     batch-1 fused-launch delays (qkv_delay, o_delay, ffn_wdelay) re-swept on configs[1]
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -186,7 +187,15 @@ for a in "" "--batch 64 --seconds 30"; do
   python3 -c "import json; d=json.loads([l for l in open('gpurun_out/c1_b.log') if l.startswith('{')][-1]); print('conv1lds $a', d['value'], d['stage_ms_per_step_rank0'])"
 done
 ;;
+delays)
+for cfg in "10 20 14" "6 20 14" "14 20 14" "10 14 14" "10 26 14" "10 20 10" "10 20 18" "10 20 14" \
+           "10 24 14" "10 28 14" "10 32 14" "10 36 14" "6 26 14" "6 28 14" "10 26 14"; do
+  set -- $cfg
+  QASR_FUSE_DELAY=$1 QASR_FUSE_ODELAY=$2 QASR_FFN_WDELAY=$3 timeout -k 10 150 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe > gpurun_out/dl_b.log 2>&1 || exit 1
+  python3 -c "import json; d=json.loads([l for l in open('gpurun_out/dl_b.log') if l.startswith('{')][-1]); print('qkv_delay=$1 o_delay=$2 ffn_wdelay=$3', d['value'], d['stage_ms_per_step_rank0']['decode'])"
+done
+;;
 *)
-sed -n 2,22p "$0"; exit 2
+sed -n 2,23p "$0"; exit 2
 ;;
 esac
