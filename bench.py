@@ -53,6 +53,7 @@ def parse():
                          "takes the fused QKV + attention launch); default: the engine's (exact for Q8_0 only)")
     ap.add_argument("--cpu-threads", type=int, default=4, help="reference's effective ggml thread count")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--probe-stride", type=int, default=8, help="probe every k-th decode step (roofline)")
     ap.add_argument("--q8", action="store_true", help="Q8_0 synthetic model (configs[2] weights)")
     ap.add_argument("--pipeline", choices=("asr", "align"), default="asr",
                     help="align: configs[4] transcribe + ForcedAligner on every clip (src/main.cpp:416-500)")
@@ -370,6 +371,10 @@ def main():
             align_all()
     if not args.no_probe:
         ctx.set_option("probe_layer", args.probe_layer)
+        # every 8th decode step probed (HIP events + device clock around the
+        # group, live in the timed region); the others replay the whole-step
+        # graph -- probing every step cost ~3 % of the step time
+        ctx.set_option("probe_stride", args.probe_stride)
         ctx.set_probe(2)   # the dominant kernel: layer probe_layer's QKV + attention (+ o-proj) launch
     barrier()
     t0 = time.perf_counter()

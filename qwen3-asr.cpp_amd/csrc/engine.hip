@@ -156,6 +156,8 @@ struct qasr_ctx {
     // kernel probe: HIP-event timing of one decode-step kernel inside qasr_run
     int probe = 0;                 // 0 off, 1 LM head, 2 layer QKV + attention, 3 layer FFN
     int probe_layer = 14;          // decoder layer whose groups probes 2 / 3 time
+    int probe_stride = 1;          // probe decode steps k with k % probe_stride == 0 (the others replay the whole-step
+                                   // graph: the probed step's split graphs and eager group cost ~3 % of a step)
     bool probe_o_fused = false;    // the probed layer's o-projection runs inside the QKV launch
     bool probe_layer_fused = false;   // ... and its FFN too (layer1_kernel)
     bool probe_qffn = false;          // the QKV projections run in the previous layer's FFN launch (FuseCfg::qkv_ffn)
@@ -768,6 +770,11 @@ extern "C" int qasr_ctx_set_option(qasr_ctx *c, const char *name, int value) {
         c->graph_probe_group = -1;
         return 0;
     }
+    if (n == "probe_stride") {
+        if (value < 1) return fail(QASR_ERR_ARG, "probe_stride must be >= 1");
+        c->probe_stride = value;
+        return 0;
+    }
     if (n == "dec_layers") {
         if (value < 0 || value > c->m->hp.dec_layers) return fail(QASR_ERR_ARG, "dec_layers out of range");
         c->dbg_layers = value;
@@ -795,6 +802,7 @@ extern "C" int qasr_ctx_get_option(const qasr_ctx *c, const char *name, int *val
     const std::string n = name;
     if (n == "dec_layers") { *value = c->dbg_layers; return 0; }
     if (n == "probe_layer") { *value = c->probe_layer; return 0; }
+    if (n == "probe_stride") { *value = c->probe_stride; return 0; }
     if (n == "slots_ffn") { *value = c->fuse.slots_ffn; return 0; }
     if (n == "slots_qkv") { *value = std::min(c->fuse.slots_qkv64, c->fuse.slots_qkv128); return 0; }
     for (const auto &o : fuse_options())
@@ -1473,7 +1481,7 @@ static int launch_step(qasr_ctx *c, int B, int k) {
     qasr_ctx::StepGraphs *gs = nullptr;
     int rc;
     if (!c->eager && (rc = step_graphs(c, splits, &gs))) return rc;
-    if (!c->probe) {
+    if (!c->probe || k % c->probe_stride != 0) {
         if (c->eager) decode_step_kernels(c, B, c->graph_logits, kWholeStep, splits);
         else HIPCHK(hipGraphLaunch(gs->full, c->st));
         return 0;
@@ -1520,7 +1528,7 @@ static int probe_collect(qasr_ctx *c, int B, int nsteps) {
         c->probe_dev_ms += (double)(t1 - t0) * 1e-5;
         c->probe_dev_n++;
     }
-    for (int k = 0; k < nsteps; k++) {
+    for (int k = 0; k < nsteps; k += c->probe_stride) {   // (steps between strides left no records)
         float ms = 0.f;
         HIPCHK(hipEventElapsedTime(&ms, c->pev[2 * k], c->pev[2 * k + 1]));
         c->probe_ms += ms;

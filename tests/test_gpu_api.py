@@ -129,3 +129,25 @@ def test_bench_utterance_driver(gpu):
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')][-1])
     assert line["scaling"] == "strong" and line["n_gpus"] == 1 and line["config"]["utterances"] == 24
     assert line["value"] > 0 and line["decode_tokens_per_s"] > 0
+
+
+def test_probe_stride_samples_steps(gpu, tiny_gguf):
+    """the bench's roofline probe (qasr_set_probe) with probe_stride = 4 times
+    every 4th decode step only (HIP events and the device-clock record), and
+    the whole-step graph replays in between give the same tokens"""
+    m = qasr.Model(tiny_gguf)
+    c = qasr.Context(m, max_batch=1, max_ctx=256)
+    try:
+        pcm = qasr.synth_pcm(7700, 2 * 16000)
+        ref = c.transcribe([pcm], max_tokens=13, ignore_eos=True).tokens
+        c.set_option("probe_stride", 4)
+        assert c.get_option("probe_stride") == 4
+        c.set_probe(2)
+        got = c.transcribe([pcm], max_tokens=13, ignore_eos=True).tokens
+        ms, n, nbytes = c.get_probe()
+        c.set_probe(0)
+    finally:
+        c.close()
+        m.close()
+    assert got == ref
+    assert n == 3 and ms > 0 and nbytes > 0   # decode steps 0, 4, 8 of the 12
