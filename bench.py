@@ -164,7 +164,7 @@ def profiled_mfma():
 
 
 def roofline_entry(kind: int, batch: int, total_ms: float, n: int, bytes_per_launch: float, dev_ms: float, dev_n: int,
-                   layer: int, exact: bool = False, qffn: bool = False) -> dict:
+                   layer: int, exact: bool = False) -> dict:
     """HBM roofline of one probed launch group: algorithmic bytes per launch
     (engine.hip probe_bytes: weights + the layer's K/V rows at each step's
     n_kv, averaged over the probed steps) / its mean duration.  Both clocks of
@@ -181,17 +181,12 @@ def roofline_entry(kind: int, batch: int, total_ms: float, n: int, bytes_per_lau
         kname = ("decode layer QKV GEMV + decode_attn_exact_kernel (ggml fp16-accumulating attention), "
                  "first start to last end" if b1 else "decode layer QKV projection + exact attention (kernel group)")
         prefix = None
-    elif kind == 2 and qffn and b1:
-        kname = ("qkv_attn1_kernel without its QKV role (batch 1: split-K attention + o-proj, one launch; the layer's "
-                 "rmsnorm + QKV GEMV ran in the previous layer's FFN launch)")
-        prefix = "void qasr::qkv_attn1_kernel<"
     elif kind == 2:
         kname = ("qkv_attn1_kernel (batch 1: rmsnorm + QKV GEMV + split-K attention + o-proj, one launch)" if b1 else
                  "decode layer QKV projection + attention (kernel group)")
         prefix = "void qasr::qkv_attn1_kernel<" if b1 else None
     elif kind == 3:
-        kname = ("ffn1_kernel (batch 1: rmsnorm + gate/up SwiGLU + down + residual" +
-                 (" + the next layer's rmsnorm + QKV GEMV" if qffn else "") + ", one launch)") if b1 else \
+        kname = "ffn1_kernel (batch 1: rmsnorm + gate/up SwiGLU + down + residual, one launch)" if b1 else \
             "decode layer FFN (kernel group)"
         prefix = "void qasr::ffn1_kernel<" if b1 else None
     else:
@@ -440,9 +435,8 @@ def main():
     if probe and probe[1]:
         # `roofline` = the decode launch with the larger time (both run once per
         # layer per step); the other one and the LM head go to roofline_other
-        qffn = bool(ctx.get_option("qkv_ffn")) and args.batch == 1 and not exact
-        ents = {2: roofline_entry(2, args.batch, *probe, args.probe_layer, exact, qffn)}
-        ents.update({k: roofline_entry(k, args.batch, *v, args.probe_layer, exact, qffn) for k, v in extra.items() if v[1]})
+        ents = {2: roofline_entry(2, args.batch, *probe, args.probe_layer, exact)}
+        ents.update({k: roofline_entry(k, args.batch, *v, args.probe_layer, exact) for k, v in extra.items() if v[1]})
         top = max((k for k in ents if k != 1), key=lambda k: ents[k]["avg_launch_us"])
         out["roofline"] = ents.pop(top)
         out["roofline_other"] = list(ents.values())

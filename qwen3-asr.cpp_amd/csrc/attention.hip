@@ -708,7 +708,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
         // (sc1 loads) until both carry this step's tag -- the data arrives with
         // its own flag, no drain / arrival count / second load (MI355X guide,
         // hand-off table: data-tagged granules).  Bounded like the counter wait.
-        const uint32_t tag = ((uint32_t)a.pos[b] << 5) | (uint32_t)a.layer;
+        const uint32_t tag = gran_tag(a.pos[b], a.layer);
         const unsigned long long *gp = a.gran + (src - raw) + lane;
         unsigned long long v0 = 0, v1 = 0;
         bool ok = false;
@@ -1223,36 +1223,13 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
     if (lane == 0) o.out_f32[row] = fadd_rn(acc, res);
 }
 
-// Prefetch role: after pf_delay, plain 16-B loads over the given ranges (values
-// dropped) so the lines sit in the Infinity Cache when the next launch streams
-// them; nothing waits on these workgroups.
-__device__ __forceinline__ void prefetch_body(const DecodeAttnArgs a, int j) {
-    for (int i = 0; i < a.pf_delay; i++) __builtin_amdgcn_s_sleep(8);
-    const long n = a.pf_n0 + a.pf_n1, stride = (long)a.pf_blocks * 256;
-    constexpr int U = 12;
-    for (long c0 = (long)j * 256 + threadIdx.x; c0 < n; c0 += U * stride) {
-        u32x4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const long c = c0 + u * stride;
-            v[u] = u32x4{0u, 0u, 0u, 0u};
-            if (c < n) v[u] = c < a.pf_n0 ? ((const u32x4 *)a.pf0)[c] : ((const u32x4 *)a.pf1)[c - a.pf_n0];
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) asm volatile("" ::"v"(v[u]));
-    }
-}
-
 template <int SPL>
 __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnArgs a, GemvArgs o) {
     constexpr int K = 1024, NT = 2, RPW = 2;
     stamp_start(a.stamp);
-    const int nq = q.W ? 512 : 0;   // no QKV role: the previous FFN launch left the outputs in a.gran
-    if (blockIdx.x >= nq) {
-        const int j = blockIdx.x - nq, nsp = a.grid_splits, nat = nsp * a.n_kv_head;   // grid_splits: this launch's splits
-        const int nob = a.att_done ? 256 : 0;
-        if (j >= nat + nob) prefetch_body(a, j - nat - nob);
-        else if (j >= nat) oproj1_body(o, a, j - nat);
+    if (blockIdx.x >= 512) {
+        const int j = blockIdx.x - 512, nsp = a.grid_splits, nat = nsp * a.n_kv_head;   // grid_splits: this launch's splits
+        if (j >= nat) oproj1_body(o, a, j - nat);
         else decode_attn_body<SPL, true>(a, j % nsp, j / nsp, 0, nsp);
         stamp_end(a.stamp);
         return;
@@ -1264,7 +1241,7 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
     // the block's 8 rows: q rows of heads 2g, 2g+1, then k, then v of group g
     const int rbase = loc < 32 ? grp * 256 + loc * 8 : loc < 48 ? QD + grp * 128 + (loc - 32) * 8 : QD + KD + grp * 128 + (loc - 48) * 8;
     const int row0 = rbase + wid * RPW;
-    const uint32_t gtag = a.gran ? ((uint32_t)a.pos[0] << 5) | (uint32_t)a.layer : 0u;
+    const uint32_t gtag = a.gran ? gran_tag(a.pos[0], a.layer) : 0u;
     half8 wv[RPW][NT];
 #pragma unroll
     for (int r = 0; r < RPW; r++)
@@ -1345,388 +1322,11 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
     stamp_end(a.stamp);
 }
 
-static int split1(int spl1, int grid_splits);
-// ------------------------------------------ batch 1: the whole decoder layer
-// One launch per layer: QKV GEMV -> attention splits -> o-projection ->
-// gate/up (SwiGLU) -> down, every role a range of workgroups that waits
-// in-launch (bounded polls, the sticky error word) on the previous role's
-// write-through outputs and arrival counters.  What it buys over the
-// qkv_attn1 + ffn1 pair: the FFN weights (18.9 MB) are requested while the
-// attention's score / combine chain runs instead of after a kernel boundary.
-// Fewer, wider workgroups per role than the two-launch kernels (the whole grid
-// must be co-resident at 4 workgroups per CU): QKV 16 rows (4 per wave),
-// o-proj and down 8 rows (2 per wave), gate/up 16 SwiGLU outputs (4 per
-// wave) -- every row's arithmetic is gemv1_kernel's, so the results are
-// bit-identical to the separate launches.
-struct LayerCtl {
-    unsigned int *ocnt, *ocnt_next;   // o-proj arrivals, 32 shards x 16 words: this layer's, the next layer's
-    unsigned int *fcnt, *fcnt_next;   // gate/up arrivals, likewise
-    int gu_delay, dn_wdelay, dn_delay;
-};
-#define L1_QKV 256
-#define L1_O 128
-#define L1_GU 192
-#define L1_DN 128
-
-__device__ __forceinline__ void l1_sc1_x4_6(const uint16_t *p, u32x4 *v) {   // act (3072 halves) as gemv.hip
-    asm volatile(
-        "global_load_dwordx4 %0, %6, off sc1\n\t"
-        "global_load_dwordx4 %1, %6, off offset:1024 sc1\n\t"
-        "global_load_dwordx4 %2, %6, off offset:2048 sc1\n\t"
-        "global_load_dwordx4 %3, %6, off offset:3072 sc1\n\t"
-        "global_load_dwordx4 %4, %7, off sc1\n\t"
-        "global_load_dwordx4 %5, %7, off offset:1024 sc1\n\t"
-        "s_waitcnt vmcnt(0)"
-        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5])
-        : "v"(p), "v"(p + 2048)
-        : "memory");
-}
-__device__ __forceinline__ float l1_silu(float g) { return g / (1.0f + expf(-g)); }
-// wave 0 polls 32 shards (lane s: shard s) until each holds `need`; false on timeout
-__device__ __forceinline__ bool l1_wait32(const unsigned int *cnt, unsigned need, int delay, const DecodeAttnArgs &a) {
-    __shared__ int ready;
-    const int lane = threadIdx.x & 63;
-    if (threadIdx.x < 64) {
-        for (int i = 0; i < delay; i++) __builtin_amdgcn_s_sleep(8);
-        int ok = 0;
-        for (int it = 0; it < a.poll_limit; it++) {
-            const unsigned v = lane < 32 ? __hip_atomic_load(cnt + lane * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
-            if (__all(v >= need)) { ok = 1; break; }
-            __builtin_amdgcn_s_sleep(4);
-        }
-        if (a.fence) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (lane == 0) ready = ok;
-    }
-    __syncthreads();
-    return ready != 0;
-}
-// every wave drained its write-through stores: one arrival
-__device__ __forceinline__ void l1_arrive(unsigned int *cnt, const DecodeAttnArgs &a) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (a.fence && threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    if (a.fence) __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// QKV: block b serves kv group b / 32 (its 256 q rows in 16 blocks, 128 k rows
-// in 8, 128 v rows in 8); 4 rows a wave
-__device__ __forceinline__ void l1_qkv(const GemvArgs &q, const DecodeAttnArgs &a, int b) {
-    constexpr int K = 1024, NT = 2, RPW = 4;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int grp = b >> 5, loc = b & 31;
-    const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
-    const int rbase = loc < 16 ? grp * 256 + loc * 16 : loc < 24 ? QD + grp * 128 + (loc - 16) * 16 : QD + KD + grp * 128 + (loc - 24) * 16;
-    const int row0 = rbase + wid * RPW;
-    const uint32_t gtag = a.gran ? ((uint32_t)a.pos[0] << 5) | (uint32_t)a.layer : 0u;
-    half8 wv[RPW][NT];
-#pragma unroll
-    for (int r = 0; r < RPW; r++)
-#pragma unroll
-        for (int t = 0; t < NT; t++)
-            wv[r][t] = __builtin_nontemporal_load((const half8 *)(q.W + (long)(row0 + r) * K + t * 512 + lane * 8));
-    float xf[NT][8];
-    if (q.embd_ids) {   // layer 0: x = token_embd[id]
-        const uint16_t *er = q.embd + (long)q.embd_ids[0] * K;
-#pragma unroll
-        for (int t = 0; t < NT; t++) {
-            const half8 h = *(const half8 *)(er + t * 512 + lane * 8);
-#pragma unroll
-            for (int e = 0; e < 8; e++) xf[t][e] = (float)h[e];
-        }
-        if (q.x_store && b == 0 && wid == 0)   // write-through: the o-proj adds it as its residual
-#pragma unroll
-            for (int t = 0; t < NT; t++)
-#pragma unroll
-                for (int e = 0; e < 8; e++)
-                    __hip_atomic_store((uint32_t *)(q.x_store + t * 512 + lane * 8 + e), __float_as_uint(xf[t][e]), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-#pragma unroll
-        for (int t = 0; t < NT; t++) {
-            const float4 u = *(const float4 *)(q.x + t * 512 + lane * 8);
-            const float4 v = *(const float4 *)(q.x + t * 512 + lane * 8 + 4);
-            xf[t][0] = u.x; xf[t][1] = u.y; xf[t][2] = u.z; xf[t][3] = u.w;
-            xf[t][4] = v.x; xf[t][5] = v.y; xf[t][6] = v.z; xf[t][7] = v.w;
-        }
-    }
-    double ss = 0.0;   // ggml_rms_norm: double sum of fp32 squares
-#pragma unroll
-    for (int t = 0; t < NT; t++)
-#pragma unroll
-        for (int e = 0; e < 8; e++) ss += (double)(xf[t][e] * xf[t][e]);
-    ss = wave_sum_d(ss);
-    const float scale = 1.0f / sqrtf((float)(ss / K) + q.eps);
-#pragma unroll
-    for (int t = 0; t < NT; t++) {
-        const float4 u = *(const float4 *)(q.norm_w + t * 512 + lane * 8);
-        const float4 v = *(const float4 *)(q.norm_w + t * 512 + lane * 8 + 4);
-        const float w[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int e = 0; e < 8; e++) xf[t][e] = (float)f2h(fmul_rn(fmul_rn(xf[t][e], scale), w[e]));
-    }
-#pragma unroll
-    for (int r = 0; r < RPW; r++) {
-        float acc = 0.f;
-#pragma unroll
-        for (int t = 0; t < NT; t++)
-#pragma unroll
-            for (int e = 0; e < 8; e++) acc = fmaf((float)wv[r][t][e], xf[t][e], acc);
-        acc = wave_sum(acc);
-        if (a.gran) {   // one 8-byte write-through {value, tag} store per output: the flag travels with the data
-            if (lane == 0)
-                __hip_atomic_store(a.gran + row0 + r, ((unsigned long long)gtag << 32) | __float_as_uint(acc), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        } else if (lane == 0) {
-            __hip_atomic_store((uint32_t *)(q.out_f32 + row0 + r), __float_as_uint(acc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    if (a.gran) {   // nothing to drain or count
-        if (q.trace && threadIdx.x == 0) q.trace[blockIdx.x * 8 + 1] = rt_now();
-        stamp_end(a.stamp);
-        return;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (a.fence && threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    if (a.fence) __syncthreads();
-    if (threadIdx.x < 8)   // one lane per replica of the group's counter
-        __hip_atomic_fetch_add(a.qcnt + (grp * 8 + threadIdx.x) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// o-projection: rows 8 j + 2 wid + r (K = 2048), + residual; x rows leave
-// write-through, one arrival per block on o-proj shard j % 32
-__device__ __forceinline__ void l1_oproj(const GemvArgs &o, const DecodeAttnArgs &a, const LayerCtl &c, int j) {
-    constexpr int K = 2048, NT = 4, RPW = 2;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int row0 = j * 8 + wid * RPW;
-    for (int i = 0; i < a.oproj_delay; i++) __builtin_amdgcn_s_sleep(8);
-    half8 wv[RPW][NT];
-#pragma unroll
-    for (int r = 0; r < RPW; r++)
-#pragma unroll
-        for (int t = 0; t < NT; t++) wv[r][t] = __builtin_nontemporal_load((const half8 *)(o.W + (long)(row0 + r) * K + t * 512 + lane * 8));
-    __shared__ int oready;
-    if (threadIdx.x == 0) {
-        int ok = 0;
-        for (int it = 0; it < a.poll_limit; it++) {
-            if (__hip_atomic_load(a.att_done + (j & 7) * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)a.n_kv_head) {
-                ok = 1;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(4);
-        }
-        if (a.fence) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (!ok) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_O_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        oready = ok;
-    }
-    __syncthreads();
-    if (oready) {   // (a timed-out block still arrives: the error is reported, the waits behind it end)
-        u32x4 xv[NT];
-        ld_sc1_x4_4(o.xh + lane * 8, xv);
-#pragma unroll
-        for (int r = 0; r < RPW; r++) {
-            const float res = __uint_as_float(__hip_atomic_load((const uint32_t *)(o.res + row0 + r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            float acc = 0.f;
-#pragma unroll
-            for (int t = 0; t < NT; t++) {
-                const half8 h = __builtin_bit_cast(half8, xv[t]);
-#pragma unroll
-                for (int e = 0; e < 8; e++) acc = fmaf((float)wv[r][t][e], (float)h[e], acc);
-            }
-            acc = wave_sum(acc);
-            if (lane == 0)
-                __hip_atomic_store((uint32_t *)(o.out_f32 + row0 + r), __float_as_uint(fadd_rn(acc, res)), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    l1_arrive(c.ocnt + (j & 31) * 16, a);
-}
-
-// gate/up: SwiGLU outputs 16 j + 4 wid + u (16-row interleave as ffn1_kernel)
-__device__ __forceinline__ void l1_gateup(const GemvArgs &g, const DecodeAttnArgs &a, const LayerCtl &c, int j) {
-    constexpr int K = 1024, NT = 2, OPW = 4;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int o0 = j * 16 + wid * OPW;
-    for (int i = 0; i < c.gu_delay; i++) __builtin_amdgcn_s_sleep(8);   // the QKV and K/V streams go first
-    half8 wv[OPW][2][NT];
-#pragma unroll
-    for (int u = 0; u < OPW; u++)
-#pragma unroll
-        for (int q = 0; q < 2; q++)
-#pragma unroll
-            for (int t = 0; t < NT; t++) {
-                const int o = o0 + u;
-                wv[u][q][t] = __builtin_nontemporal_load((const half8 *)(g.W + (32L * (o >> 4) + (o & 15) + 16 * q) * K + t * 512 + lane * 8));
-            }
-    const bool ok = l1_wait32(c.ocnt, L1_O / 32, 0, a);
-    if (!ok && threadIdx.x == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_O_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (j == 0 && threadIdx.x < 32) {   // every o-proj block is past its wait: re-arm its counters, and the next layer's
-        c.fcnt_next[threadIdx.x * 16] = 0u;
-        c.ocnt_next[threadIdx.x * 16] = 0u;
-        if (threadIdx.x < 8) __hip_atomic_store(a.att_done + threadIdx.x * 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    float xf[NT][8];
-    {
-        u32x4 xv[2 * NT];   // x (fp32, written this launch): sc1 loads
-        const uint32_t *xp = (const uint32_t *)g.x + lane * 8;
-        asm volatile(
-            "global_load_dwordx4 %0, %4, off sc1\n\t"
-            "global_load_dwordx4 %1, %4, off offset:16 sc1\n\t"
-            "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\t"
-            "global_load_dwordx4 %3, %4, off offset:2064 sc1\n\t"
-            "s_waitcnt vmcnt(0)"
-            : "=&v"(xv[0]), "=&v"(xv[1]), "=&v"(xv[2]), "=&v"(xv[3])
-            : "v"(xp)
-            : "memory");
-#pragma unroll
-        for (int t = 0; t < NT; t++)
-#pragma unroll
-            for (int e = 0; e < 8; e++) xf[t][e] = __uint_as_float(xv[2 * t + (e >> 2)][e & 3]);
-    }
-    double ss = 0.0;
-#pragma unroll
-    for (int t = 0; t < NT; t++)
-#pragma unroll
-        for (int e = 0; e < 8; e++) ss += (double)(xf[t][e] * xf[t][e]);
-    ss = wave_sum_d(ss);
-    const float scale = 1.0f / sqrtf((float)(ss / K) + g.eps);
-#pragma unroll
-    for (int t = 0; t < NT; t++) {
-        const float4 u = *(const float4 *)(g.norm_w + t * 512 + lane * 8);
-        const float4 v = *(const float4 *)(g.norm_w + t * 512 + lane * 8 + 4);
-        const float w[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int e = 0; e < 8; e++) xf[t][e] = (float)f2h(fmul_rn(fmul_rn(xf[t][e], scale), w[e]));
-    }
-    __shared__ uint16_t outs[16];
-#pragma unroll
-    for (int u = 0; u < OPW; u++) {
-        float acc[2];
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            acc[q] = 0.f;
-#pragma unroll
-            for (int t = 0; t < NT; t++)
-#pragma unroll
-                for (int e = 0; e < 8; e++) acc[q] = fmaf((float)wv[u][q][t][e], xf[t][e], acc[q]);
-            acc[q] = wave_sum(acc[q]);
-        }
-        if (lane == 0) outs[wid * OPW + u] = f_to_u16(l1_silu(acc[0]) * acc[1]);
-    }
-    __syncthreads();
-    if (threadIdx.x < 8)   // 16 fp16 outputs as 8 write-through dwords
-        __hip_atomic_store((uint32_t *)(g.out_f16 + j * 16) + threadIdx.x,
-                           (uint32_t)outs[2 * threadIdx.x] | ((uint32_t)outs[2 * threadIdx.x + 1] << 16), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    l1_arrive(c.fcnt + (j & 31) * 16, a);
-}
-
-// down: rows 8 j + 2 wid + r (K = 3072), + residual (x as the o-proj left it)
-__device__ __forceinline__ void l1_down(const GemvArgs &d, const DecodeAttnArgs &a, const LayerCtl &c, int j) {
-    constexpr int F = 3072, NTD = 6, RPW = 2;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int row0 = j * 8 + wid * RPW;
-    for (int i = 0; i < c.dn_wdelay; i++) __builtin_amdgcn_s_sleep(8);
-    half8 wv[RPW][NTD];
-#pragma unroll
-    for (int r = 0; r < RPW; r++)
-#pragma unroll
-        for (int t = 0; t < NTD; t++) wv[r][t] = __builtin_nontemporal_load((const half8 *)(d.W + (long)(row0 + r) * F + t * 512 + lane * 8));
-    const bool ok = l1_wait32(c.fcnt, L1_GU / 32, c.dn_delay, a);
-    if (!ok) {
-        if (threadIdx.x == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_FFN_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;   // reported through the error word; x keeps the o-proj's rows
-    }
-    u32x4 xv[NTD];
-    l1_sc1_x4_6(d.xh + lane * 8, xv);
-#pragma unroll
-    for (int r = 0; r < RPW; r++) {
-        const float res = __uint_as_float(__hip_atomic_load((const uint32_t *)(d.res + row0 + r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        float acc = 0.f;
-#pragma unroll
-        for (int t = 0; t < NTD; t++) {
-            const half8 h = __builtin_bit_cast(half8, xv[t]);
-#pragma unroll
-            for (int e = 0; e < 8; e++) acc = fmaf((float)wv[r][t][e], (float)h[e], acc);
-        }
-        acc = wave_sum(acc);
-        if (lane == 0) d.out_f32[row0 + r] = fadd_rn(acc, res);
-    }
-}
-
-template <int SPL>
-__global__ __launch_bounds__(256) void layer1_kernel(GemvArgs q, DecodeAttnArgs a, GemvArgs o, GemvArgs gu, GemvArgs dn, LayerCtl c) {
-    stamp_start(a.stamp);
-    int b = blockIdx.x;
-    const int nsp = a.grid_splits, nat = nsp * a.n_kv_head;
-    if (b < L1_QKV) {
-        l1_qkv(q, a, b);
-    } else if ((b -= L1_QKV) < nat) {
-        decode_attn_body<SPL, true>(a, b % nsp, b / nsp, 0, nsp);
-    } else if ((b -= nat) < L1_O) {
-        l1_oproj(o, a, c, b);
-    } else if ((b -= L1_O) < L1_GU) {
-        l1_gateup(gu, a, c, b);
-    } else {
-        l1_down(dn, a, c, b - L1_GU);
-    }
-    stamp_end(a.stamp);
-}
-
-int launch_layer1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs &o, const GemvArgs &gu, const GemvArgs &dn,
-                  unsigned int *ocnt, unsigned int *ocnt_next, unsigned int *fcnt, unsigned int *fcnt_next, const FuseCfg &cfg,
-                  hipStream_t s, bool dry) {
-    if (!cfg.layer || !cfg.qkv || !cfg.o || !cfg.ffn || !cfg.err || a.B != 1 || !a.qcnt || !a.att_done || !ocnt || !ocnt_next ||
-        ocnt == ocnt_next || !fcnt || !fcnt_next || fcnt == fcnt_next)
-        return 0;
-    // shapes: the plain f16 batch-1 layer of the 0.6B decoder
-    if (q.M != 1 || q.K != 1024 || q.Wd || !q.norm_w || q.xh || q.bias || q.res || a.out32 || a.outq ||
-        q.N != a.n_head * 128 + 2 * a.n_kv_head * 128 || a.n_head != 2 * a.n_kv_head || a.n_kv_head != 8)
-        return 0;
-    if (o.M != 1 || o.K != 2048 || o.N != 1024 || o.xh != a.out || !o.res || o.Wd || o.bias || o.norm_w)
-        return 0;
-    if (gu.M != 1 || gu.Wd || gu.K != 1024 || gu.N != 3072 || !gu.x || gu.xh || !gu.norm_w || gu.embd_ids || !gu.out_f16 ||
-        dn.M != 1 || dn.Wd || dn.K != 3072 || dn.N != 1024 || dn.xh != gu.out_f16 || !dn.res || dn.bias || dn.norm_w || !dn.out_f32)
-        return 0;
-    const int spl1 = split1(cfg.spl1, a.grid_splits);
-    const int ns = (a.grid_splits * DSPLIT + spl1 - 1) / spl1;
-    const int grid = L1_QKV + ns * a.n_kv_head + L1_O + L1_GU + L1_DN;
-    if (grid > (spl1 == 128 ? cfg.slots_layer128 : cfg.slots_layer64)) return 0;   // every block co-resident
-    if (dry) return 1;
-    DecodeAttnArgs ad = a;
-    ad.fuse_delay = cfg.qkv_delay;
-    ad.oproj_delay = cfg.o_delay;
-    ad.poll_limit = cfg.poll_limit;
-    ad.fence = cfg.fence;
-    ad.err = cfg.err;
-    ad.grid_splits = ns;
-    ad.qkv_need = L1_QKV / a.n_kv_head;
-    const LayerCtl c{ocnt, ocnt_next, fcnt, fcnt_next, cfg.gu_delay, cfg.dn_wdelay, cfg.dn_delay};
-    if (spl1 == 128) hipLaunchKernelGGL(layer1_kernel<128>, dim3(grid), dim3(256), 0, s, q, ad, o, gu, dn, c);
-    else hipLaunchKernelGGL(layer1_kernel<DSPLIT>, dim3(grid), dim3(256), 0, s, q, ad, o, gu, dn, c);
-    return 1;
-}
-
 // batch <= 8 key split: cfg 64 / 128, else 128 from 1k keys (half the
 // partials to combine, still >= 64 workgroups per 8 kv heads)
 static int split1(int spl1, int grid_splits) { return spl1 == 64 || spl1 == 128 ? spl1 : grid_splits >= 16 ? 128 : 64; }
 
-int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s, bool dry,
-                          bool no_qkv) {
-    if (no_qkv && !a.gran) return 0;
+int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s, bool dry) {
     if (!cfg.qkv || !cfg.err || a.B != 1 || !a.qcnt || q.M != 1 || q.K != 1024 || q.Wd || !q.norm_w || q.xh || q.bias || q.res ||
         a.out32 || a.outq || q.N != a.n_head * 128 + 2 * a.n_kv_head * 128 || a.n_head != 2 * a.n_kv_head || a.n_kv_head * 64 != 512)
         return 0;
@@ -1742,9 +1342,7 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     if (512 + ns * a.n_kv_head > slots) return 0;
     const bool with_o2 = with_o && fit_o;
     if (dry) return with_o2 ? 2 : 1;
-    // prefetch workgroups wait on nothing: they need no co-residency
-    const int npf = a.pf0 && cfg.pf_blocks > 0 ? cfg.pf_blocks : 0;
-    const dim3 grid((no_qkv ? 0 : 512) + ns * a.n_kv_head + (with_o2 ? o->N / 4 : 0) + npf);
+    const dim3 grid(512 + ns * a.n_kv_head + (with_o2 ? o->N / 4 : 0));
     // K/V delay ~2 us: measured optimum on MI355X (round-1 delay sweep: 0 -> 236.3, 10 -> 232.0, 18 -> 240.3 ms decode)
     DecodeAttnArgs ad = a;
     ad.fuse_delay = cfg.qkv_delay;
@@ -1754,11 +1352,7 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     ad.err = cfg.err;
     ad.grid_splits = ns;   // the kernel's split count
     if (!with_o2) ad.att_done = nullptr;
-    ad.pf_blocks = npf;
-    ad.pf_delay = cfg.pf_delay;
-    if (no_qkv) ad.fuse_delay = 0;   // nothing to let ahead: the K/V stream starts at once
-    GemvArgs qa = q;
-    if (no_qkv) qa.W = nullptr;
+    const GemvArgs qa = q;
     const GemvArgs oa = with_o2 ? *o : GemvArgs{};
     if (spl1 == 128) hipLaunchKernelGGL(qkv_attn1_kernel<128>, grid, dim3(256), 0, s, qa, ad, oa);
     else hipLaunchKernelGGL(qkv_attn1_kernel<DSPLIT>, grid, dim3(256), 0, s, qa, ad, oa);
@@ -1801,8 +1395,6 @@ void fused_slots(FuseCfg &cfg) {
     cfg.slots_qkv64 = slots_of(reinterpret_cast<const void *>(qkv_attn1_kernel<DSPLIT>));
     cfg.slots_qkv128 = slots_of(reinterpret_cast<const void *>(qkv_attn1_kernel<128>));
     cfg.slots_ffn = fused_slots_ffn();
-    cfg.slots_layer64 = slots_of(reinterpret_cast<const void *>(layer1_kernel<DSPLIT>));
-    cfg.slots_layer128 = slots_of(reinterpret_cast<const void *>(layer1_kernel<128>));
     cfg.slots_stream = decode_stream_slots();
 }
 

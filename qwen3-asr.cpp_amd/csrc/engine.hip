@@ -110,7 +110,6 @@ struct qasr_ctx {
     float *d_att32 = nullptr, *d_act32 = nullptr;   // Q8_0 decode: fp32 attention output / SwiGLU output
     int8_t *d_q8a = nullptr; float *d_q8d = nullptr, *d_x32 = nullptr;   // Q8_0 batched (B > 8) decode, graph-fixed
     int8_t *d_q8n = nullptr; float *d_q8nd = nullptr;   // ... the RMS-normed layer inputs (QKV, gate/up), quantised
-    unsigned int *d_ncnt = nullptr;                     // decode batches: fused post-norm row-block counters [8][16]
     // fixed decode state (sized by max_batch)
     int32_t *d_tok = nullptr, *d_hist = nullptr;
     int *d_pos = nullptr, *d_nkv = nullptr, *d_slot = nullptr, *d_step = nullptr;
@@ -122,8 +121,6 @@ struct qasr_ctx {
     bool qkv_in_gran = false;               // the captured step's last layer hands its QKV over in granules
     unsigned int *d_attdone = nullptr;   // fused batch-1 o-proj: combiner arrivals (8 replicas)
     unsigned int *d_ffncnt = nullptr;    // fused batch-1 FFN: gate/up arrivals, [layer][32 shards][16]
-    unsigned int *d_ocnt = nullptr;      // batch-1 layer launch: o-proj arrivals, [layer][32 shards][16]
-    unsigned int *d_dcnt = nullptr;      // batch-1 FFN launch with the next layer's QKV: down arrivals, [layer][32 shards][16]
     uint16_t *d_q = nullptr, *d_att = nullptr, *d_act = nullptr, *d_xh = nullptr;
     unsigned long long *d_amax = nullptr;
     int max_splits = 0, hist_cap = 0;
@@ -159,8 +156,6 @@ struct qasr_ctx {
     int probe_stride = 1;          // probe decode steps k with k % probe_stride == 0 (the others replay the whole-step
                                    // graph: the probed step's split graphs and eager group cost ~3 % of a step)
     bool probe_o_fused = false;    // the probed layer's o-projection runs inside the QKV launch
-    bool probe_layer_fused = false;   // ... and its FFN too (layer1_kernel)
-    bool probe_qffn = false;          // the QKV projections run in the previous layer's FFN launch (FuseCfg::qkv_ffn)
     double probe_ms = 0.0, probe_bytes = 0.0, probe_dev_ms = 0.0;
     long probe_dev_n = 0;
     unsigned long long *d_pstamp = nullptr;   // per decode step: [32 min-starts | 32 max-ends] of the probed launches
@@ -205,29 +200,20 @@ struct FuseOption {
 static const std::vector<FuseOption> &fuse_options() {
     static const std::vector<FuseOption> v = {
         {"fuse_ffn", "QASR_FUSE_FFN", &FuseCfg::ffn},          {"fuse_qkv", "QASR_FUSE_QKV", &FuseCfg::qkv},
-        {"fuse_o", "QASR_FUSE_O", &FuseCfg::o},                {"ffn_delay", "QASR_FFN_DELAY", &FuseCfg::ffn_delay},
+        {"fuse_o", "QASR_FUSE_O", &FuseCfg::o},
+        {"ffn_delay", "QASR_FFN_DELAY", &FuseCfg::ffn_delay},
         {"ffn_wdelay", "QASR_FFN_WDELAY", &FuseCfg::ffn_wdelay}, {"qkv_delay", "QASR_FUSE_DELAY", &FuseCfg::qkv_delay},
         {"o_delay", "QASR_FUSE_ODELAY", &FuseCfg::o_delay},    {"att_spl1", "QASR_ATT_SPL1", &FuseCfg::spl1},
         {"poll_limit", "QASR_POLL_LIMIT", &FuseCfg::poll_limit}, {"handoff_fence", "QASR_HANDOFF_FENCE", &FuseCfg::fence},
-        {"fuse_layer", "QASR_FUSE_LAYER", &FuseCfg::layer},
-        {"gu_delay", "QASR_GU_DELAY", &FuseCfg::gu_delay},
-        {"dn_wdelay", "QASR_DN_WDELAY", &FuseCfg::dn_wdelay},
-        {"dn_delay", "QASR_DN_DELAY", &FuseCfg::dn_delay},
         {"fa_exact_prefill", "QASR_FA_EXACT_PREFILL", &FuseCfg::fa_exact_prefill},
         {"enc_attn_f32", "QASR_ENC_ATTN_F32", &FuseCfg::enc_attn_f32},
         {"gemm_regs", "QASR_GEMM_REGS", &FuseCfg::gemm_regs},
         {"gran", "QASR_GRAN", &FuseCfg::gran},
-        {"pf_blocks", "QASR_PF_BLOCKS", &FuseCfg::pf_blocks},
-        {"pf_delay", "QASR_PF_DELAY", &FuseCfg::pf_delay},
         {"fa_exact_decode", "QASR_FA_EXACT_DECODE", &FuseCfg::fa_exact_decode},
-        {"qkv_ffn", "QASR_QKV_FFN", &FuseCfg::qkv_ffn},
         {"att_stream", "QASR_ATT_STREAM", &FuseCfg::att_stream},
-        {"post_norm", "QASR_POST_NORM", &FuseCfg::post_norm},
         {"skinny", "QASR_SKINNY", &FuseCfg::skinny},
         {"att_spl", "QASR_ATT_SPL", &FuseCfg::att_spl},
         {"kv_nt", "QASR_KV_NT", &FuseCfg::kv_nt},
-        {"qffn_delay", "QASR_QFFN_DELAY", &FuseCfg::qffn_delay},
-        {"qffn_poll_delay", "QASR_QFFN_POLL_DELAY", &FuseCfg::qffn_poll_delay},
     };
     return v;
 }
@@ -236,6 +222,17 @@ static const std::vector<FuseOption> &fuse_options() {
 static void launch_gemm_c(qasr_ctx *c, int amode, int epi, GemmArgs g, hipStream_t s) {
     g.regs_staged = c->fuse.gemm_regs;
     launch_gemm(amode, epi, g, s);
+}
+
+// every arrival counter of the fused launches back to rest (zero), on the
+// context stream: after an option change and after a wait that gave up
+static int reset_counters(qasr_ctx *c) {
+    const Hparams &hp = c->m->hp;
+    HIPCHK(hipMemsetAsync(c->d_ffncnt, 0, (size_t)hp.dec_layers * 512 * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->d_qcnt, 0, (size_t)hp.n_kv_head * 8 * 16 * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->d_attdone, 0, (size_t)8 * 16 * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->d_counter, 0, (size_t)c->max_batch * hp.n_kv_head * 4, c->st));
+    return 0;
 }
 
 // the fused launches' sticky device error word: read (and cleared) after every
@@ -247,17 +244,13 @@ static int check_dev_err(qasr_ctx *c) {
     if (!e) return 0;
     // a wait that gave up can leave late arrivals in the counters: back to rest
     HIPCHK(hipMemsetAsync(c->d_err, 0, 4, c->st));
-    HIPCHK(hipMemsetAsync(c->d_ffncnt, 0, (size_t)c->m->hp.dec_layers * 512 * 4, c->st));
-    HIPCHK(hipMemsetAsync(c->d_ocnt, 0, (size_t)c->m->hp.dec_layers * 512 * 4, c->st));
-    HIPCHK(hipMemsetAsync(c->d_dcnt, 0, (size_t)c->m->hp.dec_layers * 512 * 4, c->st));
-    HIPCHK(hipMemsetAsync(c->d_qcnt, 0, (size_t)c->m->hp.n_kv_head * 8 * 16 * 4, c->st));
-    HIPCHK(hipMemsetAsync(c->d_attdone, 0, (size_t)8 * 16 * 4, c->st));
+    const int rc = reset_counters(c);
+    if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->st));
     std::string what;
     if (e & DEVERR_QKV_WAIT) what += " attention<-QKV";
     if (e & DEVERR_O_WAIT) what += " o-proj<-attention";
     if (e & DEVERR_FFN_WAIT) what += " down<-gate/up";
-    if (e & DEVERR_X_WAIT) what += " next-layer QKV<-down";
     return fail(QASR_ERR_DEVICE, "fused decode launch: an in-launch wait timed out (" + what.substr(1) +
                                      "); outputs of this call are invalid (another process or context sharing the GPU?)");
 }
@@ -344,14 +337,6 @@ static int upload(qasr_ctx *c, DevBuf &b, const std::vector<T> &v) {
 // A Q8_0 linear layer: quantise the activation rows (fp32 a32 or fp16 a16,
 // optional conv_out gather) into c->q8a / c->q8d, then the int8 block GEMM.
 // g carries M, N, K and the epilogue.
-// a projection asked for the fused post-norm (GemmArgs.post_w) that the
-// skinny GEMM did not take: the separate norm launch instead
-static void post_norm_fallback(const GemmArgs &g, hipStream_t s) {
-    if (!g.post_w) return;
-    if (g.post_yq) launch_rmsnorm_q8(g.out_f32, g.ldo, g.M, g.N, g.post_w, g.post_eps, g.post_yq, g.post_yd, s);
-    else launch_rmsnorm_f16(g.out_f32, g.ldo, nullptr, g.M, g.N, g.post_w, g.post_eps, g.post_y, s);
-}
-
 static void gemm_q8(qasr_ctx *c, int epi, GemmArgs g, const float *a32, const uint16_t *a16, int lda, int gather_C,
                     const uint16_t *W, const uint16_t *Wd, hipStream_t s, int8_t *qa = nullptr, float *qd = nullptr,
                     bool decode = false) {
@@ -362,7 +347,6 @@ static void gemm_q8(qasr_ctx *c, int epi, GemmArgs g, const float *a32, const ui
     g.no_skinny = !c->fuse.skinny;
     if (decode && launch_gemm_skinny_q8(epi, g, s)) return;
     launch_gemm_q8(epi, g, s);
-    post_norm_fallback(g, s);
 }
 
 // decode batches: activations already quantised into d_q8a / d_q8d by the
@@ -374,7 +358,6 @@ static void gemm_q8_pre(qasr_ctx *c, int epi, GemmArgs g, const uint16_t *W, con
     g.no_skinny = !c->fuse.skinny;
     if (launch_gemm_skinny_q8(epi, g, s)) return;
     launch_gemm_q8(epi, g, s);
-    post_norm_fallback(g, s);
 }
 
 static int ensure_q8(qasr_ctx *c, size_t rows, size_t kmax, size_t x32_cols) {
@@ -722,7 +705,6 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_x32, (size_t)B * std::max(QD, std::max(hp.hidden, hp.dec_ffn)) * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_q8n, (size_t)B * hp.hidden)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_q8nd, (size_t)B * hp.hidden / 32 * 4)) ||
-        (rc = dev_alloc(c.get(), (void **)&c->d_ncnt, (size_t)8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_part, (size_t)B * hp.n_kv_head * c->max_splits * 2 * 132 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_counter, (size_t)B * hp.n_kv_head * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_scores, (size_t)B * hp.n_head * max_ctx * 4)) ||
@@ -730,8 +712,6 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_attdone, (size_t)8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_gran, (size_t)(QD + 2 * KD) * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_ffncnt, (size_t)hp.dec_layers * 512 * 4)) ||
-        (rc = dev_alloc(c.get(), (void **)&c->d_ocnt, (size_t)hp.dec_layers * 512 * 4)) ||
-        (rc = dev_alloc(c.get(), (void **)&c->d_dcnt, (size_t)hp.dec_layers * 512 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_err, 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_pstamp, (size_t)max_ctx * kStampRec * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_logits, (size_t)B * hp.vocab * 4)) ||
@@ -742,9 +722,6 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     HIPCHK(hipMemcpy(c->d_slot, slots.data(), B * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(c->d_counter, 0, (size_t)B * hp.n_kv_head * 4));
     HIPCHK(hipMemset(c->d_qcnt, 0, (size_t)hp.n_kv_head * 8 * 16 * 4));
-    HIPCHK(hipMemset(c->d_ocnt, 0, (size_t)hp.dec_layers * 512 * 4));
-    HIPCHK(hipMemset(c->d_dcnt, 0, (size_t)hp.dec_layers * 512 * 4));
-    HIPCHK(hipMemset(c->d_ncnt, 0, (size_t)8 * 16 * 4));
     HIPCHK(hipMemset(c->d_attdone, 0, (size_t)8 * 16 * 4));
     HIPCHK(hipMemset(c->d_gran, 0, (size_t)(QD + 2 * KD) * 8));
     HIPCHK(hipMemset(c->d_ffncnt, 0, (size_t)hp.dec_layers * 512 * 4));
@@ -787,10 +764,8 @@ extern "C" int qasr_ctx_set_option(qasr_ctx *c, const char *name, int value) {
             c->fuse.*(o.field) = value;
             c->drop_graphs();   // captured steps hold the old launch configuration
             HIPCHK(hipSetDevice(c->m->device));   // arrival counters back to rest
-            HIPCHK(hipMemsetAsync(c->d_ffncnt, 0, (size_t)c->m->hp.dec_layers * 512 * 4, c->st));
-    HIPCHK(hipMemsetAsync(c->d_ocnt, 0, (size_t)c->m->hp.dec_layers * 512 * 4, c->st));
-            HIPCHK(hipMemsetAsync(c->d_qcnt, 0, (size_t)c->m->hp.n_kv_head * 8 * 16 * 4, c->st));
-            HIPCHK(hipMemsetAsync(c->d_attdone, 0, (size_t)8 * 16 * 4, c->st));
+            const int rc = reset_counters(c);
+            if (rc) return rc;
             HIPCHK(hipStreamSynchronize(c->st));
             return 0;
         }
@@ -1168,7 +1143,6 @@ static void dec_gemm(qasr_ctx *c, int epi, GemmArgs g, hipStream_t s) {
     g.no_skinny = !c->fuse.skinny;
     if (launch_gemm_skinny(epi, g, s)) return;
     launch_gemm(AM_DENSE, epi, g, s);
-    post_norm_fallback(g, s);
 }
 
 // Launch groups of one decode step, in stream order (decoder cut at nl layers):
@@ -1201,13 +1175,6 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
     unsigned long long *stamp = r.hi - r.lo == 1 ? c->cur_stamp : nullptr;
     if (r.in(0) && !skinny) launch_embed(c->d_tok, B, m->embd, H, nullptr, nullptr, x, s);
     const int skip = c->dev_skip;   // profiling only (QASR_DEV_SKIP): drop kernels to price them
-    // decode batches: the RMS norms fused into the o / down projections that
-    // produce x (GemmArgs.post_w): shape-only decisions, equal for every layer
-    const bool post_o = !skinny && c->fuse.post_norm && c->fuse.skinny && skinny_post_ok(m->q8, B, QD, H);
-    const bool post_d = !skinny && c->fuse.post_norm && c->fuse.skinny && skinny_post_ok(m->q8, B, F, H);
-    auto set_post = [&](GemmArgs &g, const float *w, uint16_t *y, int8_t *yq, float *yd) {
-        g.post_w = w; g.post_eps = hp.rms_eps; g.post_y = y; g.post_yq = yq; g.post_yd = yd; g.post_cnt = c->d_ncnt;
-    };
     if (c->d_trace && r.in(0)) (void)hipMemsetAsync(c->d_trace, 0, 6 * 4096 * 8 * 8, s);
     for (int l = 0; l < nl; l++) {
         const bool ga = r.in(1 + 2 * l), gb = r.in(2 + 2 * l);
@@ -1264,58 +1231,28 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         const bool exact = exact_decode(c);
         const bool fusable = skinny && B == 1 && !q8 && !skip && !exact;
         if (fusable) da.att_done = c->d_attdone;
-        if (fusable && c->fuse.pf_blocks > 0) {   // the layer's FFN weights -> Infinity Cache during the attention chain
-            da.pf0 = L.wgu; da.pf_n0 = (long)2 * F * H * 2 / 16;
-            da.pf1 = L.wd; da.pf_n1 = (long)H * F * 2 / 16;
-        }
-        unsigned int *ocnt = c->d_ocnt + (size_t)l * 512, *ocnt_next = c->d_ocnt + (size_t)((l + 1) % nl) * 512;
         unsigned int *fcnt = c->d_ffncnt + (size_t)l * 512, *fcnt_next = c->d_ffncnt + (size_t)((l + 1) % nl) * 512;
-        // the whole layer in one launch (decided without launching), else 0 = separate
-        // launches, 1 = QKV + attention, 2 = + o-projection
-        const bool lfused = fusable && nl >= 2 && launch_layer1(q1, da, o, gu, dn, ocnt, ocnt_next, fcnt, fcnt_next, c->fuse, s, true);
-        const int fmode = lfused ? 0 : fusable ? launch_qkv_attention1(q1, da, &o, c->fuse, s, true) : 0;
+        // 0 = separate launches, 1 = QKV + attention in one launch, 2 = + o-projection
+        const int fmode = fusable ? launch_qkv_attention1(q1, da, &o, c->fuse, s, true) : 0;
         const bool o_fused = fmode == 2;
-        // layer l+1's rmsnorm + QKV in this layer's FFN launch (FuseCfg::qkv_ffn),
-        // its outputs in granules for layer l+1's attention launch: a decision
-        // from shapes and options only, so every layer's two launches agree
-        QkvNext qn{};
-        qn.dcnt = c->d_dcnt + (size_t)l * 512;
-        qn.dcnt_next = c->d_dcnt + (size_t)((l + 1) % nl) * 512;
-        qn.gran = c->d_gran;
-        qn.pos = c->d_pos;
-        qn.layer_next = l + 1;
-        if (l + 1 < nl) {
-            const DecLayer &Ln = m->dec[l + 1];
-            qn.q.x = x; qn.q.ldx = H; qn.q.norm_w = Ln.attn_norm; qn.q.eps = hp.rms_eps; qn.q.W = Ln.wqkv; qn.q.K = H;
-            qn.q.N = QD + 2 * KD; qn.q.M = 1; qn.q.ldo = QD + 2 * KD;
-        }
-        const bool qffn = fmode >= 1 && c->fuse.gran && c->fuse.qkv_ffn && nl >= 2 &&
-                          launch_ffn1(gu, dn, fcnt, fcnt_next, c->fuse, s, &qn, true);
-        if (l == std::min(c->probe_layer, nl - 1)) {
-            c->probe_o_fused = o_fused || lfused;
-            c->probe_layer_fused = lfused;
-            c->probe_qffn = qffn;
-        }
+        if (l == std::min(c->probe_layer, nl - 1)) c->probe_o_fused = o_fused;
         if (ga) {
             if (l == nl - 1) c->qkv_in_gran = false;
-            if (lfused) {
-                (void)launch_layer1(q1, da, o, gu, dn, ocnt, ocnt_next, fcnt, fcnt_next, c->fuse, s, false);
-            } else if (fmode) {
+            if (fmode) {
                 if (c->fuse.gran) { da.gran = c->d_gran; da.layer = l; }
                 if (l == nl - 1) c->qkv_in_gran = c->fuse.gran != 0;
-                (void)launch_qkv_attention1(q1, da, &o, c->fuse, s, false, qffn && l > 0);
+                (void)launch_qkv_attention1(q1, da, &o, c->fuse, s, false);
             } else {
                 if (skinny) {
                     if (!(skip & 1)) launch_gemv(EPI_F32, q1, s);
                 } else {
                     GemmArgs q{};
                     q.M = B; q.N = QD + 2 * KD; q.K = H; q.out_f32 = c->d_qkv; q.ldo = QD + 2 * KD;
-                    const bool normed = l > 0 && post_d;   // the previous layer's down projection normalised x
                     if (q8) {
-                        if (!normed) launch_rmsnorm_q8(x, H, B, H, L.attn_norm, hp.rms_eps, c->d_q8n, c->d_q8nd, s);
+                        launch_rmsnorm_q8(x, H, B, H, L.attn_norm, hp.rms_eps, c->d_q8n, c->d_q8nd, s);
                         gemm_q8_pre(c, EPI_F32, q, L.wqkv, L.wqkv_d, s, c->d_q8n, c->d_q8nd);
                     } else {
-                        if (!normed) launch_rmsnorm_f16(x, H, nullptr, B, H, L.attn_norm, hp.rms_eps, c->d_xh, s);
+                        launch_rmsnorm_f16(x, H, nullptr, B, H, L.attn_norm, hp.rms_eps, c->d_xh, s);
                         q.A = c->d_xh; q.lda = H; q.W = L.wqkv; q.ldw = H; dec_gemm(c, EPI_F32, q, s);
                     }
                 }
@@ -1330,11 +1267,11 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
                 }
             }
         }
-        if (!gb || lfused) continue;   // (the layer launch ran the o-projection and the FFN)
+        if (!gb) continue;
         if (skinny) {
             if (!o_fused && !(skip & 4)) launch_gemv(EPI_F32, o, s);
             if (o_fused) dn.zero8 = c->d_attdone;   // re-arm the fused o-proj's arrival counters
-            if (skip & 24 || nl < 2 || !launch_ffn1(gu, dn, fcnt, fcnt_next, c->fuse, s, qffn ? &qn : nullptr)) {
+            if (skip & 24 || nl < 2 || !launch_ffn1(gu, dn, fcnt, fcnt_next, c->fuse, s)) {
                 if (!(skip & 8)) launch_gemv(q8 ? EPI_SWIGLU_F32 : EPI_SWIGLU_F16, gu, s);
                 if (!(skip & 16)) launch_gemv(EPI_F32, dn, s);
                 else if (o_fused) (void)hipMemsetAsync(c->d_attdone, 0, 8 * 16 * 4, s);   // the skipped down-proj re-arms these
@@ -1342,31 +1279,24 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         } else if (q8) {
             GemmArgs ob{};
             ob.M = B; ob.N = H; ob.K = QD; ob.res = x; ob.ldr = H; ob.out_f32 = x; ob.ldo = H;
-            if (post_o) set_post(ob, L.ffn_norm, nullptr, c->d_q8n, c->d_q8nd);
             gemm_q8_pre(c, EPI_F32, ob, L.wo, L.wo_d, s);
-            if (!post_o) launch_rmsnorm_q8(x, H, B, H, L.ffn_norm, hp.rms_eps, c->d_q8n, c->d_q8nd, s);
+            launch_rmsnorm_q8(x, H, B, H, L.ffn_norm, hp.rms_eps, c->d_q8n, c->d_q8nd, s);
             GemmArgs gu{};
             gu.M = B; gu.N = 2 * F; gu.K = H; gu.out_f32 = c->d_x32; gu.ldo = F;
             gemm_q8_pre(c, EPI_SWIGLU_F32, gu, L.wgu, L.wgu_d, s, c->d_q8n, c->d_q8nd);
             GemmArgs dn{};
             dn.M = B; dn.N = H; dn.K = F; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
-            if (post_d) {   // the next layer's attention norm (Q8_0), or the final norm of the (f16) LM head
-                if (l + 1 < nl) set_post(dn, m->dec[l + 1].attn_norm, nullptr, c->d_q8n, c->d_q8nd);
-                else set_post(dn, m->out_norm, c->d_xh, nullptr, nullptr);
-            }
             gemm_q8(c, EPI_F32, dn, c->d_x32, nullptr, F, 0, L.wd, L.wd_d, s, c->d_q8a, c->d_q8d, true);
         } else {
             GemmArgs ob{};
             ob.A = c->d_att; ob.lda = QD; ob.W = L.wo; ob.ldw = QD; ob.M = B; ob.N = H; ob.K = QD; ob.res = x; ob.ldr = H; ob.out_f32 = x; ob.ldo = H;
-            if (post_o) set_post(ob, L.ffn_norm, c->d_xh, nullptr, nullptr);
             dec_gemm(c, EPI_F32, ob, s);
-            if (!post_o) launch_rmsnorm_f16(x, H, nullptr, B, H, L.ffn_norm, hp.rms_eps, c->d_xh, s);
+            launch_rmsnorm_f16(x, H, nullptr, B, H, L.ffn_norm, hp.rms_eps, c->d_xh, s);
             GemmArgs gu{};
             gu.A = c->d_xh; gu.lda = H; gu.W = L.wgu; gu.ldw = H; gu.M = B; gu.N = 2 * F; gu.K = H; gu.out_f16 = c->d_act; gu.ldo16 = F;
             dec_gemm(c, EPI_SWIGLU_F16, gu, s);
             GemmArgs dn{};
             dn.A = c->d_act; dn.lda = F; dn.W = L.wd; dn.ldw = F; dn.M = B; dn.N = H; dn.K = F; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
-            if (post_d) set_post(dn, l + 1 < nl ? m->dec[l + 1].attn_norm : m->out_norm, c->d_xh, nullptr, nullptr);
             dec_gemm(c, EPI_F32, dn, s);
         }
     }
@@ -1381,7 +1311,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             launch_gemv(EPI_ARGMAX, lm, s);
         } else {
             launch_fill_u64(c->d_amax, B, 0ull, s);
-            if (!(post_d && nl > 0)) launch_rmsnorm_f16(x, H, nullptr, B, H, m->out_norm, hp.rms_eps, c->d_xh, s);
+            launch_rmsnorm_f16(x, H, nullptr, B, H, m->out_norm, hp.rms_eps, c->d_xh, s);
             GemmArgs lm{};
             lm.A = c->d_xh; lm.lda = H; lm.W = m->embd; lm.ldw = H; lm.M = B; lm.N = hp.vocab; lm.K = H;
             lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
@@ -1420,15 +1350,9 @@ static double probe_bytes(const qasr_ctx *c, int B, int k) {
         double kv = 0;
         for (int b = 0; b < B; b++) kv += (double)(c->run_P[b] + k + 1) * KD * 2 * 2;
         const bool o_in = c->probe_o_fused;
-        const double ffn = c->probe_layer_fused ? 3 * F * H * wb + B * H * 4 * 3 : 0.0;   // the layer launch's FFN
-        // (the QKV projection left for the previous layer's FFN launch, FuseCfg::qkv_ffn)
-        const bool q_in = !(c->probe_qffn && std::min(c->probe_layer, step_layers(c) - 1) > 0);
-        return (q_in ? (QD + 2 * KD) * H * wb + B * H * 4 : 0.0) + (o_in ? H * QD * wb + B * H * 8 : 0.0) + kv +
-               B * (QD + 2 * KD) * (q_in ? 4 : 8) + ffn;
+        return (QD + 2 * KD) * H * wb + B * H * 4 + (o_in ? H * QD * wb + B * H * 8 : 0.0) + kv + B * (QD + 2 * KD) * 4;
     }
-    const bool qn = c->probe_qffn && std::min(c->probe_layer, step_layers(c) - 1) + 1 < step_layers(c);
-    return 3 * F * H * wb + (c->probe_o_fused ? 0.0 : H * QD * wb) + B * H * 4 * 3 +
-           (qn ? (QD + 2 * KD) * H * wb + B * H * 4 + B * (QD + 2 * KD) * 8 : 0.0);
+    return 3 * F * H * wb + (c->probe_o_fused ? 0.0 : H * QD * wb) + B * H * 4 * 3;
 }
 
 static int capture(qasr_ctx *c, int B, bool want_logits, StepRange r, int splits, hipGraphExec_t *out) {

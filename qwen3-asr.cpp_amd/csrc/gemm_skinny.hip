@@ -29,49 +29,6 @@ __device__ __forceinline__ float silu_s(float g) { return g / (1.0f + expf(-g));
 // Residual prefetch: epilogue element e -> (tile, row in tile, column in
 // tile); the residual values a thread adds are requested at kernel entry, so
 // their latency hides under the K loop.
-// four 16-B sc1 loads of one 1024-wide fp32 row (lane: columns 4 lane + 256 i)
-__device__ __forceinline__ void ld_sc1_row1024(const float *p, float4 *v) {
-    floatx4 a, b, c, d;
-    asm volatile(
-        "global_load_dwordx4 %0, %4, off sc1\n\t"
-        "global_load_dwordx4 %1, %4, off offset:1024 sc1\n\t"
-        "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\t"
-        "global_load_dwordx4 %3, %4, off offset:3072 sc1\n\t"
-        "s_waitcnt vmcnt(0)"
-        : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
-        : "v"(p)
-        : "memory");
-    v[0] = make_float4(a[0], a[1], a[2], a[3]);
-    v[1] = make_float4(b[0], b[1], b[2], b[3]);
-    v[2] = make_float4(c[0], c[1], c[2], c[3]);
-    v[3] = make_float4(d[0], d[1], d[2], d[3]);
-}
-
-// fused post-norm (GemmArgs.post_w): this workgroup's outputs went out
-// write-through; every wave drains, one lane counts the workgroup into its row
-// block's counter, and the last of the row block's gridDim.x column tiles
-// (told by its add's return value) reads the finished rows with sc1 loads and
-// normalises them, one wave a row (MI355X_MICROARCH.md hand-off table, row 1)
-template <int MT, int KW>
-__device__ __forceinline__ void skinny_post_norm(const GemmArgs &g, int m0, int tid) {
-    __shared__ int last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    unsigned int *cnt = g.post_cnt + blockIdx.y * 16;
-    if (tid == 0) last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // back to rest
-    const int wid = tid >> 6, lane = tid & 63;
-    for (int r = wid; r < 16 * MT; r += KW) {
-        const int row = m0 + r;
-        if (row >= g.M) break;
-        float4 v[4];
-        ld_sc1_row1024(g.out_f32 + (long)row * g.ldo + 4 * lane, v);
-        rms_row<1024>(v, g.post_w, g.post_eps, row, g.post_y, nullptr, g.post_yq, g.post_yd);
-    }
-}
-
 template <int MT, int NT, int KW, int EPI>
 struct SkinnyEpi {
     static constexpr int NTILE = MT * NT;
@@ -136,16 +93,10 @@ struct SkinnyEpi {
                         g.out_f16[(long)row * g.ldo16 + col] = f_to_u16(v);
                     } else {
                         if (g.res) v = fadd_rn(v, resv[k]);
-                        if (g.post_w)   // read back by the row block's last workgroup: write-through
-                            __hip_atomic_store((uint32_t *)(g.out_f32 + (long)row * g.ldo + col), __float_as_uint(v), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                        else
-                            g.out_f32[(long)row * g.ldo + col] = v;
+                        g.out_f32[(long)row * g.ldo + col] = v;
                     }
                 }
             }
-            if constexpr (EPI == EPI_F32)
-                if (g.post_w) skinny_post_norm<MT, KW>(g, m0, tid);
             if constexpr (EPI == EPI_ARGMAX) {
                 __syncthreads();
                 if (tid < MT * 16 && m0 + tid < M) atomicMax(g.amax + m0 + tid, rmax[tid]);
@@ -460,15 +411,8 @@ static void skinny_mt(const GemmArgs &g, hipStream_t s) {
     else run_skinny<MTMAX >= 4 ? 4 : 1, NT, KW, EPI>(g, s);
 }
 
-// the o / down projections of a decode batch (<1, 1, 8> tiles, N = 1024): the
-// shapes launch_gemm_skinny / _q8 take with the fused post-norm
-bool skinny_post_ok(bool q8, int M, int K, int N) {
-    return M > 8 && M <= 128 && K % 128 == 0 && (q8 ? K % 16 == 0 : K % 8 == 0) && N == 1024;
-}
-
 bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s) {
     const bool off = g.no_skinny != 0;
-    if (g.post_w && (epi != EPI_F32 || !skinny_post_ok(false, g.M, g.K, g.N) || !g.post_cnt || g.ldo != 1024)) return false;
     if (off || g.M <= 0 || g.M > 128 || g.K % 128 != 0 || g.lda % 8 != 0 || g.ldw % 8 != 0) return false;
     switch (epi) {
         case EPI_F32:
@@ -499,7 +443,6 @@ bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s) {
 
 bool launch_gemm_skinny_q8(int epi, const GemmArgs &g, hipStream_t s) {
     const bool off = g.no_skinny != 0;
-    if (g.post_w && (epi != EPI_F32 || !skinny_post_ok(true, g.M, g.K, g.N) || !g.post_cnt || g.ldo != 1024)) return false;
     if (off || g.M <= 0 || g.M > 128 || g.K % 128 != 0 || g.lda % 16 != 0 || g.ldw % 16 != 0 || g.ldad % 4 != 0) return false;
     switch (epi) {
         case EPI_F32:

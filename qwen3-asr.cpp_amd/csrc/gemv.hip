@@ -201,116 +201,13 @@ struct FfnCtl {
     unsigned int *cnt, *cnt_next;   // this layer's 32 arrival shards (16-word stride), the next layer's
     unsigned int *err;              // sticky device error word
     int wdelay, delay, poll_limit, fence;
-    // the next layer's QKV role (launch_ffn1 with qn): the down blocks store x
-    // write-through and count into dcnt (32 shards), the QKV blocks wait there
-    unsigned int *dcnt, *dcnt_next; // this layer's down arrivals, the next layer's (re-armed here)
-    unsigned long long *gran;       // QKV outputs of layer `layer_next` as {fp32, tag} granules
-    const int *pos;                 // tag = (pos[0] << 5) | layer_next
-    int layer_next, qdelay, qpoll_delay;
 };
 
-// ---- the next decoder layer's rmsnorm + QKV GEMV inside the FFN launch: block
-// j serves kv group j / 32 (its 256 q rows in 16 blocks, 128 k rows in 8, 128
-// v rows in 8), 4 rows a wave (gemv1_kernel's arithmetic, K = 1024).  Its
-// weights are requested at launch start (after qdelay), so the 8.4 MB stream
-// runs beside gate/up and down instead of after a kernel boundary; it waits for
-// every down block (32 shards of 8), reads x with sc1 loads and hands its
-// outputs to the next launch's attention splits as tagged granules.
-__device__ __forceinline__ void ffn1_qkv_next(const GemvArgs &q, const GemvArgs &d, const FfnCtl &c, int j) {
-    constexpr int K = 1024, NT = 2, RPW = 4, QD = 2048, KD = 1024;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int grp = j >> 5, loc = j & 31;
-    const int rbase = loc < 16 ? grp * 256 + loc * 16 : loc < 24 ? QD + grp * 128 + (loc - 16) * 16 : QD + KD + grp * 128 + (loc - 24) * 16;
-    const int row0 = rbase + wid * RPW;
-    for (int i = 0; i < c.qdelay; i++) __builtin_amdgcn_s_sleep(8);
-    half8 wv[RPW][NT];
-#pragma unroll
-    for (int r = 0; r < RPW; r++)
-#pragma unroll
-        for (int t = 0; t < NT; t++)
-            wv[r][t] = __builtin_nontemporal_load((const half8 *)(q.W + (long)(row0 + r) * K + t * 512 + lane * 8));
-    const uint32_t gtag = ((uint32_t)c.pos[0] << 5) | (uint32_t)c.layer_next;
-    float nw[NT][8];
-#pragma unroll
-    for (int t = 0; t < NT; t++) {
-        const float4 u = *(const float4 *)(q.norm_w + t * 512 + lane * 8);
-        const float4 v = *(const float4 *)(q.norm_w + t * 512 + lane * 8 + 4);
-        nw[t][0] = u.x; nw[t][1] = u.y; nw[t][2] = u.z; nw[t][3] = u.w;
-        nw[t][4] = v.x; nw[t][5] = v.y; nw[t][6] = v.z; nw[t][7] = v.w;
-    }
-    __shared__ int qready;
-    if (wid == 0) {   // lane s polls shard s; every shard holds 256 / 32 down arrivals when x is complete
-        for (int i = 0; i < c.qpoll_delay; i++) __builtin_amdgcn_s_sleep(8);
-        int ok = 0;
-        for (int it = 0; it < c.poll_limit; it++) {
-            const unsigned v = lane < 32 ? __hip_atomic_load(c.dcnt + lane * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
-            if (__all(v >= 8u)) { ok = 1; break; }
-            __builtin_amdgcn_s_sleep(4);
-        }
-        if (c.fence) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (lane == 0) {
-            qready = ok;
-            if (!ok) __hip_atomic_fetch_or(c.err, (unsigned)DEVERR_X_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    __syncthreads();
-    if (!qready) return;   // reported through the error word; the attention splits then time out too
-    float xf[NT][8];
-    {
-        u32x4 xv[2 * NT];   // x (fp32, written write-through by this launch's down blocks): sc1 loads
-        const uint32_t *xp = (const uint32_t *)d.out_f32 + lane * 8;
-        asm volatile(
-            "global_load_dwordx4 %0, %4, off sc1\n\t"
-            "global_load_dwordx4 %1, %4, off offset:16 sc1\n\t"
-            "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\t"
-            "global_load_dwordx4 %3, %4, off offset:2064 sc1\n\t"
-            "s_waitcnt vmcnt(0)"
-            : "=&v"(xv[0]), "=&v"(xv[1]), "=&v"(xv[2]), "=&v"(xv[3])
-            : "v"(xp)
-            : "memory");
-#pragma unroll
-        for (int t = 0; t < NT; t++)
-#pragma unroll
-            for (int e = 0; e < 8; e++) xf[t][e] = __uint_as_float(xv[2 * t + (e >> 2)][e & 3]);
-    }
-    double ss = 0.0;   // ggml_rms_norm: double sum of fp32 squares
-#pragma unroll
-    for (int t = 0; t < NT; t++)
-#pragma unroll
-        for (int e = 0; e < 8; e++) ss += (double)(xf[t][e] * xf[t][e]);
-    ss = wave_sum_d(ss);
-    const float scale = 1.0f / sqrtf((float)(ss / K) + q.eps);
-#pragma unroll
-    for (int t = 0; t < NT; t++)
-#pragma unroll
-        for (int e = 0; e < 8; e++) xf[t][e] = (float)f2h(fmul_rn(fmul_rn(xf[t][e], scale), nw[t][e]));
-#pragma unroll
-    for (int r = 0; r < RPW; r++) {
-        float acc = 0.f;
-#pragma unroll
-        for (int t = 0; t < NT; t++)
-#pragma unroll
-            for (int e = 0; e < 8; e++) acc = fmaf((float)wv[r][t][e], xf[t][e], acc);
-        acc = wave_sum(acc);
-        if (lane == 0)   // one 8-byte write-through {value, tag} store per output
-            __hip_atomic_store(c.gran + row0 + r, ((unsigned long long)gtag << 32) | __float_as_uint(acc), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
 template <int K, int F>
-__global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, GemvArgs q, FfnCtl c) {
-    constexpr int NT = K / 512, NTD = F / 512, NGU = F / 4, NDN = K / 4;
+__global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, FfnCtl c) {
+    constexpr int NT = K / 512, NTD = F / 512, NGU = F / 4;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     stamp_start(g.stamp);
-    if (blockIdx.x >= NGU + NDN) {   // ---- the next layer's QKV (launch_ffn1 with qn)
-        ffn1_qkv_next(q, d, c, blockIdx.x - NGU - NDN);
-        stamp_end(g.stamp);
-        return;
-    }
     if (blockIdx.x >= NGU) {   // ---- down projection
         const int j = blockIdx.x - NGU, row = j * 4 + wid;
         if (d.trace && threadIdx.x == 0) d.trace[j * 8] = rt_now();
@@ -353,20 +250,7 @@ __global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, GemvA
             for (int e = 0; e < 8; e++) acc = fmaf((float)wv[t][e], (float)h[e], acc);
         }
         acc = wave_sum(acc);
-        if (c.dcnt) {   // the next layer's QKV blocks read x in this launch: write-through, drained, counted
-            if (lane == 0)
-                __hip_atomic_store((uint32_t *)(d.out_f32 + row), __float_as_uint(fadd_rn(acc, res)), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (c.fence && threadIdx.x == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            if (threadIdx.x == 0) __hip_atomic_fetch_add(c.dcnt + (j & 31) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else if (lane == 0) {
-            d.out_f32[row] = fadd_rn(acc, res);
-        }
+        if (lane == 0) d.out_f32[row] = fadd_rn(acc, res);
         if (d.trace && threadIdx.x == 0) d.trace[j * 8 + 1] = rt_now();
         stamp_end(g.stamp);
         return;
@@ -375,7 +259,6 @@ __global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, GemvA
     if (g.trace && threadIdx.x == 0) g.trace[blockIdx.x * 8] = rt_now();
     if (blockIdx.x == 0 && threadIdx.x < 32) {   // re-arm: the next layer's shards and the fused o-proj's counters
         c.cnt_next[threadIdx.x * 16] = 0u;
-        if (c.dcnt_next) c.dcnt_next[threadIdx.x * 16] = 0u;
         if (d.zero8 && threadIdx.x < 8) d.zero8[threadIdx.x * 16] = 0u;
     }
     const int o = blockIdx.x * 4 + wid;
@@ -439,34 +322,19 @@ __global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, GemvA
 // the plain batch-1 f16 FFN (K = 1024, F = 3072) in one launch when every
 // block is co-resident; false = not covered (two launch_gemv calls instead)
 bool launch_ffn1(const GemvArgs &g, const GemvArgs &d, unsigned int *cnt, unsigned int *cnt_next, const FuseCfg &cfg,
-                 hipStream_t s, const QkvNext *qn, bool dry) {
+                 hipStream_t s, bool dry) {
     if (!cfg.ffn || !cfg.err || !cnt || !cnt_next || cnt_next == cnt || g.M != 1 || d.M != 1 || g.Wd || d.Wd || g.K != 1024 ||
         g.N != 3072 || !g.x || g.xh || !g.norm_w || g.embd_ids || !g.out_f16 || d.K != 3072 || d.N != 1024 || d.xh != g.out_f16 ||
         !d.res || d.bias || d.norm_w || !d.out_f32)
         return false;
-    if (qn && (!qn->gran || !qn->pos || !qn->dcnt_next || qn->dcnt_next == qn->dcnt || qn->layer_next < 0 || qn->layer_next > 31 ||
-               (qn->q.W && (qn->q.M != 1 || qn->q.Wd || qn->q.K != 1024 || qn->q.N != 4096 || !qn->q.norm_w || !qn->dcnt))))
-        return false;
-    const bool with_q = qn && qn->q.W;
-    const int grid = 3072 / 4 + 1024 / 4 + (qn ? 256 : 0);   // (the dry decision is the one with the QKV role)
+    const int grid = 3072 / 4 + 1024 / 4;
     if (grid > cfg.slots_ffn) return false;   // down blocks wait on gate/up blocks: all must be resident
     if (dry) return true;
     // delays in s_sleep(8) units (~0.2 us): down weights requested ~3 us after the
     // gate/up ones, first poll ~1 us later (round-1 delay sweep, 92 s decode:
     // unfused 224.8 ms; 12/4 217.9, 14/4 208.2 (x3), 16/4 210.0, 14/2 210.8, 14/6 210.0, 20/6 221.0)
-    FfnCtl c{cnt, cnt_next, cfg.err, cfg.ffn_wdelay, cfg.ffn_delay, cfg.poll_limit, cfg.fence};
-    GemvArgs q{};
-    if (qn) {
-        c.dcnt = with_q ? qn->dcnt : nullptr;
-        c.dcnt_next = qn->dcnt_next;
-        c.gran = qn->gran;
-        c.pos = qn->pos;
-        c.layer_next = qn->layer_next;
-        c.qdelay = cfg.qffn_delay;
-        c.qpoll_delay = cfg.qffn_poll_delay;
-        if (with_q) q = qn->q;
-    }
-    hipLaunchKernelGGL((ffn1_kernel<1024, 3072>), dim3(3072 / 4 + 1024 / 4 + (with_q ? 256 : 0)), dim3(256), 0, s, g, d, q, c);
+    const FfnCtl c{cnt, cnt_next, cfg.err, cfg.ffn_wdelay, cfg.ffn_delay, cfg.poll_limit, cfg.fence};
+    hipLaunchKernelGGL((ffn1_kernel<1024, 3072>), dim3(grid), dim3(256), 0, s, g, d, c);
     return true;
 }
 

@@ -73,18 +73,8 @@ struct GemmArgs {
     const int8_t *Aq; const float *Ad; int ldad;
     const int8_t *Wq; const uint16_t *Wd;
     int regs_staged;                      // 1: register-staged tiles instead of the LDS-DMA ones (A/B option)
-    // decode batches (skinny EPI_F32, N = 1024, + residual): the row block's
-    // last column-tile workgroup RMS-normalises its finished output rows with
-    // rmsnorm_kernel's arithmetic (dev_common.h rms_row) into post_y (fp16) or
-    // post_yq / post_yd (Q8_0) -- the next projection's input, instead of a
-    // separate rmsnorm launch; post_cnt: per row block arrival counters
-    // (16-word stride, zero at rest)
-    const float *post_w; float post_eps; uint16_t *post_y; int8_t *post_yq; float *post_yd; unsigned int *post_cnt;
     int no_skinny;                        // 1: launch_gemm_skinny / _q8 decline (per-context option skinny = 0)
 };
-// the skinny decode-batch GEMM takes an EPI_F32 projection of this shape with
-// the fused post-norm (launch_gemm_skinny / _q8 with post_w set)
-bool skinny_post_ok(bool q8, int M, int K, int N);
 void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s);
 // decode-batch GEMM (gemm_skinny.hip): dense A, M <= 128, K % 128 == 0; returns
 // false (nothing launched) for shapes it does not take, or when g.no_skinny.
@@ -142,7 +132,6 @@ enum DevErr : unsigned {
     DEVERR_QKV_WAIT = 1u,    // attention split gave up on its kv group's QKV blocks
     DEVERR_O_WAIT = 2u,      // fused o-projection gave up on the attention combiners
     DEVERR_FFN_WAIT = 4u,    // fused down-projection gave up on the gate/up blocks
-    DEVERR_X_WAIT = 8u,      // the next layer's QKV blocks (FFN launch) gave up on the down blocks
 };
 struct FuseCfg {
     int ffn = 1, qkv = 1, o = 1;        // fused launches on/off
@@ -152,51 +141,29 @@ struct FuseCfg {
     int spl1 = 0;                       // batch-1 attention split: 0 = auto (64, or 128 from 1k keys)
     int poll_limit = 1 << 20;           // bounded waits: polls (s_sleep(4..8) apart) before giving up
     int fence = 0;                      // 1 = agent release before each arrival, acquire after each wait
-    int layer = 0;                      // batch 1: the whole decoder layer in one launch (layer1_kernel; measured slower)
-    int gu_delay = 16, dn_wdelay = 30, dn_delay = 8;   // layer launch: gate/up weight request, down weight request,
-                                                       // down first poll (s_sleep(8) units)
     int enc_attn_f32 = 0;               // encoder attention on fp32 MFMA instead of split fp16 operands
     int gemm_regs = 0;                  // encoder/prefill GEMMs on the register-staged tiles (gemm.hip)
     int gran = 1;                       // batch 1: QKV -> attention hand-off by tagged granules (0 = arrival counters)
-    int pf_blocks = 0, pf_delay = 30;   // batch 1: workgroups of the QKV launch that pull the layer's FFN weights
-                                        // into the Infinity Cache while the attention chain runs (s_sleep(8) units)
     int fa_exact_prefill = 1;           // prefill attention with ggml's CPU FA numerics (fa_exact.hip)
     int fa_exact_decode = -1;           // decode attention likewise: 1 on, 0 off (fp32 V accumulation), -1 = on for
                                         // Q8_0 models only (batch 1 exact skips the fused QKV + attention launch)
-    int qkv_ffn = 0;                    // batch 1: layer l+1's rmsnorm + QKV GEMV runs in layer l's FFN launch (its weights
-                                        // stream beside gate/up + down), the next launch is attention + o-proj only;
-                                        // bit-identical, measured slower (tools/experiments.sh qffn / qffn2: decode 223 -> 246 ms)
-    int qffn_delay = 30, qffn_poll_delay = 10;   // ... its weight request / first poll (s_sleep(8) units, ~0.2 us)
     int slots_ffn = 0, slots_qkv64 = 0, slots_qkv128 = 0;   // co-resident workgroups on this device
-    int slots_layer64 = 0, slots_layer128 = 0;
     int att_stream = 1;                 // decode batches: one workgroup per (kv group, sequence) (decode_attn_seq_kernel)
     int skinny = 1;                     // decode batches: the weight-streaming skinny GEMMs (0 = tiled GEMMs)
     int att_spl = 256;                  // decode batches on the split attention kernels: keys per split (128 or 256)
     int kv_nt = 1;                      // decode attention: K/V cache rows loaded nontemporal (read once per step by one
                                         // CU; tools/experiments.sh kvnt: configs[1] neutral, 64 x 30 s decode 205.0 -> 202.1 ms)
-    int post_norm = 0;                  // decode batches: RMS norms fused into the producing o / down projections
-                                        // (last arriver per row block); bit-identical, measured slower (64 x 30 s decode
-                                        // f16 203.6 -> 208.9 ms, Q8_0 266.5 -> 275.0: tools/experiments.sh postnorm)
     int slots_stream = 0;               // ... its co-resident workgroups on this device
     unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
 };
 // co-resident workgroup capacity of the fused kernels on the current device
 // (occupancy query x CUs); 0 = unknown (never fuse)
 void fused_slots(FuseCfg &cfg);
-// the next decoder layer's QKV role of the batch-1 FFN launch (FuseCfg::qkv_ffn):
-// q = that layer's rmsnorm + QKV GemvArgs (x = this launch's down output;
-// q.W null: no QKV role, only the re-arm of dcnt_next); dcnt = this layer's 32 x
-// 16 down-arrival words (zero on entry), dcnt_next = the next layer's
-struct QkvNext {
-    GemvArgs q;
-    unsigned int *dcnt, *dcnt_next;
-    unsigned long long *gran; const int *pos; int layer_next;
-};
-// gemv.hip: batch-1 f16 gate/up + down (+ the next layer's QKV) in one launch;
-// cnt = this layer's 32 x 16 words (zero on entry), cnt_next = the next
-// layer's, re-armed here (false = not covered; dry: the decision only)
+// gemv.hip: batch-1 f16 gate/up + down in one launch; cnt = this layer's
+// 32 x 16 words (zero on entry), cnt_next = the next layer's, re-armed here
+// (false = not covered; dry: the decision only)
 bool launch_ffn1(const GemvArgs &gu, const GemvArgs &dn, unsigned int *cnt, unsigned int *cnt_next, const FuseCfg &cfg,
-                 hipStream_t s, const QkvNext *qn = nullptr, bool dry = false);
+                 hipStream_t s, bool dry = false);
 
 // ---------------------------------------------------------------- norms
 // LayerNorm (ggml_norm + mul + add) fp32 [M][D] -> fp16 y, or fp32 y32 when
@@ -263,6 +230,12 @@ void launch_prefill_attention(const PrefillAttnArgs &a, hipStream_t s);
 // keys in order per query row, fp16 V accumulator rounded after every key
 void launch_prefill_attention_exact(const PrefillAttnArgs &a, hipStream_t s);
 
+// tag of a batch-1 hand-off granule {value, tag} (DecodeAttnArgs.gran): the
+// step's position and the layer.  Never 0, the value the granule buffers are
+// reset to before every call, so a granule not yet written this step can
+// never match (position 0 at layer 0 included).
+__host__ __device__ inline uint32_t gran_tag(int pos, int layer) { return ((uint32_t)(pos + 1) << 5) | (uint32_t)layer; }
+
 // decoder single-token attention, fused: q/k RMSNorm + RoPE, fp16 KV-cache
 // write of the new token and split-KV flash decoding (64-key splits); the last
 // arriving split of each kv group combines the partials and writes out.
@@ -297,26 +270,12 @@ struct DecodeAttnArgs {
                                          // scaled scores [B][n_head][max_ctx] (+ the new K/V rows) and stop there
     unsigned long long *gran;            // fused launch: QKV outputs as 8-byte {fp32 value, tag} granules the attention
                                          // splits poll directly (no drain / arrival count); null = counters
-    int layer;                           // tag = (position << 5) | layer
-    const uint16_t *pf0, *pf1;           // fused launch: byte ranges pulled into the Infinity Cache (null: none)
-    long pf_n0, pf_n1;                   // their sizes in 16-B lines
-    int pf_blocks, pf_delay;
+    int layer;                           // granule tag = gran_tag(position, layer)
     int stream_blocks;                   // decode batches (B > 8): co-resident workgroups of decode_attn_seq_kernel (one per
                                          // kv group and sequence, taken once the batch fills them; 0 = split kernels)
     int spl_batch;                       // decode batches on the split kernels: 128- or 256-key splits (FuseCfg::att_spl)
     int kv_nt;                           // K/V cache loads nontemporal (FuseCfg::kv_nt)
 };
-// Batch 1, the whole decoder layer in one launch (attention.hip layer1_kernel):
-// QKV (256 blocks) -> attention splits -> o-projection (128) -> gate/up (192)
-// -> down (128), each role waiting in-launch (bounded) on the previous one's
-// arrival counters; ocnt / fcnt: this layer's 32-shard o-proj / gate-up
-// arrival counters (16-word stride, zero on entry), *_next the next layer's
-// (re-armed here).  Returns 0 when not covered (the caller launches
-// qkv_attention1 + ffn1 or separate kernels), 1 when launched (dry: would be).
-int launch_layer1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs &o, const GemvArgs &gu, const GemvArgs &dn,
-                  unsigned int *ocnt, unsigned int *ocnt_next, unsigned int *fcnt, unsigned int *fcnt_next, const FuseCfg &cfg,
-                  hipStream_t s, bool dry);
-
 // the decode attention with ggml's CPU flash-attention numerics (fa_exact.hip),
 // after launch_decode_attention in scores mode: per (query head, sequence) the
 // keys in order with the fp16 V accumulator; reads scores, pos, vc, n_head,
@@ -329,10 +288,8 @@ void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
 // (and, when o is the plain batch-1 o-projection, that too); returns 0 = not
 // taken, 1 = QKV + attention, 2 = QKV + attention + o-projection
 // dry = true: only the decision (nothing launched)
-// no_qkv: the QKV outputs are already in a.gran (the previous FFN launch ran
-// them, FuseCfg::qkv_ffn): the launch is the attention splits (+ o-projection)
 int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s,
-                          bool dry = false, bool no_qkv = false);
+                          bool dry = false);
 int decode_split_len();
 int decode_max_splits();
 

@@ -121,35 +121,6 @@ def test_decode_batch_ragged_contexts(path, gpu, tiny_gguf, tiny_q8_gguf, tiny_o
         assert np.abs(out[0][k] - ref).max() <= tol, (k, np.abs(out[0][k] - ref).max(), tol)
 
 
-@pytest.mark.parametrize("path", ["f16", "q8"])
-def test_decode_batch_fused_post_norm_bit_identical(path, gpu, tiny_gguf, tiny_q8_gguf):
-    """option post_norm (the RMS norms computed by the last workgroup of each row
-    block of the o / down projections instead of separate launches; off by
-    default, measured slower) gives bit-identical decode-step logits"""
-    m = qasr.Model(tiny_q8_gguf if path == "q8" else tiny_gguf)
-    B, steps = 48, 3
-    rng = np.random.default_rng(5)
-    ids = [int(t) for t in rng.integers(0, 151643, 40)]
-    out = []
-    try:
-        for pn in (0, 1):
-            c = qasr.Context(m, max_batch=B, max_ctx=64)
-            c.set_option("post_norm", pn)
-            try:
-                c.prefill([ids] * B, want_logits=False)
-                lgs = []
-                for s in range(steps):
-                    lg, _ = c.decode_step([int(ids[s])] * B, [len(ids) + s] * B)
-                    lgs.append(lg.copy())
-                out.append(lgs)
-            finally:
-                c.close()
-    finally:
-        m.close()
-    for a, b in zip(*out):
-        assert np.array_equal(a, b), float(np.abs(a - b).max())
-
-
 @pytest.mark.parametrize("B", [1, 48])
 def test_decode_kv_nt_bit_identical_and_attention_kernels_agree(B, gpu, tiny_gguf, tiny_oracle):
     """kv_nt (K/V cache rows loaded nontemporal, default on) reads the same

@@ -133,8 +133,7 @@ def test_full_lds_dma_gemm_bit_identical(full):
     assert np.array_equal(single, out[0][0][3])
 
 
-FUSE_KNOBS = {"QASR_FUSE_FFN": dict(fuse_ffn=0), "QASR_FUSE_QKV": dict(fuse_qkv=0, fuse_o=0), "QASR_FUSE_O": dict(fuse_o=0),
-              "QASR_QKV_FFN": dict(qkv_ffn=0)}
+FUSE_KNOBS = {"QASR_FUSE_FFN": dict(fuse_ffn=0), "QASR_FUSE_QKV": dict(fuse_qkv=0, fuse_o=0), "QASR_FUSE_O": dict(fuse_o=0)}
 
 
 def _step_state(c, ids, feats, pos, tok=1234):
@@ -160,9 +159,6 @@ def test_full_fused_launches_match_separate(full, knob):
         feats = c1.encode(c1.mel([pcm]))[0]
         ids, pos = m.build_prompt(feats.shape[0])
         r_f = c1.transcribe([pcm], max_tokens=24, ignore_eos=True)
-        if knob == "QASR_QKV_FFN":   # an off-by-default fusion: switch it on for the first run
-            c1.set_option("qkv_ffn", 1)
-            r_f = c1.transcribe([pcm], max_tokens=24, ignore_eos=True)
         lg_f, st_f = _step_state(c1, ids, feats, pos)
         for k, v in FUSE_KNOBS[knob].items():
             c1.set_option(k, v)
@@ -180,31 +176,6 @@ def test_full_fused_launches_match_separate(full, knob):
     assert np.abs(lg_f - lo).max() <= 1e-2 * float(np.abs(lo).max())
 
 
-def test_full_layer_launch_matches_two_launches(full):
-    """the whole-layer launch (fuse_layer = 1: QKV, attention, o-proj, gate/up
-    and down as roles of one launch, tools/sweep_layer.sh measured it slower
-    than the default two launches) gives bit-identical decode-step logits and
-    the same greedy tokens"""
-    m, _, _ = full
-    c1 = qasr.Context(m, max_batch=1, max_ctx=512)
-    c1.set_option("fa_exact_decode", 0)
-    try:
-        pcm = qasr.synth_pcm(14100, 3 * SR)
-        feats = c1.encode(c1.mel([pcm]))[0]
-        ids, pos = m.build_prompt(feats.shape[0])
-        r_2 = c1.transcribe([pcm], max_tokens=24, ignore_eos=True)
-        lg_2, st_2 = _step_state(c1, ids, feats, pos)
-        c1.set_option("fuse_layer", 1)
-        r_1 = c1.transcribe([pcm], max_tokens=24, ignore_eos=True)
-        lg_1, st_1 = _step_state(c1, ids, feats, pos)
-    finally:
-        c1.close()
-    assert r_1.tokens == r_2.tokens
-    assert np.array_equal(lg_1, lg_2), float(np.abs(lg_1 - lg_2).max())
-    for k in st_1:
-        assert np.array_equal(st_1[k], st_2[k]), k
-
-
 def test_full_fused_launches_long_context(full):
     """80 s clip (prompt ~1.06k tokens: 128-key attention splits, 10 per kv
     group): fused and separate launches give the same 24 greedy tokens and
@@ -218,7 +189,7 @@ def test_full_fused_launches_long_context(full):
         feats = c1.encode(c1.mel([pcm]))[0]
         ids, pos = m.build_prompt(feats.shape[0])
         lg_f, _ = _step_state(c1, ids, feats, pos)
-        for k in ("fuse_layer", "fuse_ffn", "fuse_qkv", "fuse_o", "qkv_ffn"):
+        for k in ("fuse_ffn", "fuse_qkv", "fuse_o"):
             c1.set_option(k, 0)
         r_s = c1.transcribe([pcm], max_tokens=24, ignore_eos=True)
         lg_s, _ = _step_state(c1, ids, feats, pos)
@@ -239,8 +210,7 @@ def test_full_fused_wait_timeout_is_an_error(full):
         assert c1.get_option("slots_ffn") >= 1024 + 256 and c1.get_option("slots_qkv") >= 512 + 8 * 4 + 256
         pcm = qasr.synth_pcm(14000, 2 * SR)
         ref = c1.transcribe([pcm], max_tokens=4, ignore_eos=True).tokens
-        for k, v in (("poll_limit", 1), ("ffn_delay", 0), ("ffn_wdelay", 0), ("qkv_delay", 0), ("o_delay", 0), ("gu_delay", 0),
-                     ("dn_wdelay", 0), ("dn_delay", 0), ("qffn_delay", 0), ("qffn_poll_delay", 0)):
+        for k, v in (("poll_limit", 1), ("ffn_delay", 0), ("ffn_wdelay", 0), ("qkv_delay", 0), ("o_delay", 0)):
             c1.set_option(k, v)
         with pytest.raises(qasr.QasrError, match="timed out"):
             c1.transcribe([pcm], max_tokens=4, ignore_eos=True)
