@@ -49,8 +49,8 @@ def parse():
     ap.add_argument("--cpu-sample-seconds", type=float, default=10.0)
     ap.add_argument("--probe-layer", type=int, default=14, help="decoder layer whose fused launches are probed")
     ap.add_argument("--fa-exact-decode", type=int, default=None, choices=(0, 1),
-                    help="decode attention numerics: 1 = ggml's fp16 V accumulation, 0 = fp32 accumulation (batch 1 "
-                         "takes the fused QKV + attention launch); default: the engine's (exact for Q8_0 only)")
+                    help="decode attention numerics: 1 = ggml's fp16 V accumulation (the engine default; batch 1 f16: the "
+                         "fused launch's chain role), 0 = fp32 accumulation (split-K)")
     ap.add_argument("--cpu-threads", type=int, default=4, help="reference's effective ggml thread count")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--probe-stride", type=int, default=8, help="probe every k-th decode step (roofline)")
@@ -178,9 +178,9 @@ def roofline_entry(kind: int, batch: int, total_ms: float, n: int, bytes_per_lau
     achieved = bytes_per_launch / avg_s / 1e9
     b1 = batch == 1
     if kind == 2 and exact:
-        kname = ("decode layer QKV GEMV + decode_attn_exact_kernel (ggml fp16-accumulating attention), "
-                 "first start to last end" if b1 else "decode layer QKV projection + exact attention (kernel group)")
-        prefix = None
+        kname = ("qkv_attn1_kernel (batch 1: rmsnorm + QKV GEMV + attention scores + ggml fp16-V chain + o-proj, one launch)"
+                 if b1 else "decode layer QKV projection + exact attention (kernel group)")
+        prefix = "void qasr::qkv_attn1_kernel<" if b1 else None
     elif kind == 2:
         kname = ("qkv_attn1_kernel (batch 1: rmsnorm + QKV GEMV + split-K attention + o-proj, one launch)" if b1 else
                  "decode layer QKV projection + attention (kernel group)")
@@ -359,7 +359,7 @@ def main():
     if args.fa_exact_decode is not None:
         ctx.set_option("fa_exact_decode", args.fa_exact_decode)
     fx = ctx.get_option("fa_exact_decode")
-    exact = fx > 0 or (fx < 0 and args.q8)
+    exact = fx != 0
     for _ in range(args.warmup):
         ctx.run(ntok, ignore_eos=True)
         if actx:
@@ -428,7 +428,9 @@ def main():
         "config": {"workload": workload(args, ntok, bool(actx)), "clips_per_gpu": args.batch,
                    "clip_seconds": args.seconds, "decode_tokens": ntok, "parallelism": f"dp{N} (utterance sharding)"},
         "decode_tokens_per_s": round(N * args.batch * ntok * args.steps / dt, 2),
-        "decode_attention": "fp16 V accumulation per key (ggml CPU flash-attention numerics)" if exact else
+        "decode_attention": ("fp16 V accumulation per key (ggml CPU flash-attention numerics" +
+                             ("; chain role of the fused QKV + attention + o-proj launch)" if args.batch == 1 and not args.q8
+                              else ")")) if exact else
                             "fp32 V accumulation (split-K)",
         "stage_ms_per_step_rank0": {k: round(v / args.steps, 3) for k, v in tm.items()},
     }

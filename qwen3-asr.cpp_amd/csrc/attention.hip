@@ -19,6 +19,7 @@
 #include <stdexcept>
 
 #include "dev_common.h"
+#include "fx_chain.h"
 #include "kernels.h"
 
 namespace qasr {
@@ -692,12 +693,19 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
             const int key = min(k0 + wid * (SPL / DWAVES) + 16 * t + c16, kcap);
             kk[t][s4] = kv_load(kc + (long)key * 128 + 32 * s4 + 8 * q4, a.kv_nt);
         }
-    if (!a.scores)   // scores mode reads no V
+    if (FUSED && a.fx) {   // exact attention: no V here; this split's keys' V^T rows -> this XCD's L2 for the chain
+        if (a.fx_vpf) {
+            const uint16_t *vt = a.vt + ((long)b * a.n_kv_head + g) * 128 * vt_ctx(a.max_ctx) + (long)(k0 / 8) * 1024;
+#pragma unroll
+            for (int i = 0; i < KPW; i++) vv[i] = *(const half8 *)(vt + (long)(i * 256 + tid) * 8);
+        }
+    } else if (!a.scores) {   // scores mode reads no V
 #pragma unroll
         for (int i = 0; i < KPW; i++) {
             const int key = min(k0 + wid * (SPL / DWAVES) + i * 4 + sub, kcap);
             vv[i] = kv_load(vc + (long)key * 128 + dl, a.kv_nt);
         }
+    }
     // No exit test on the position anywhere: with one, hipcc hoists the
     // dependent pos load and the test in front of the K/V requests (two memory
     // latencies in series).  The host sizes the grid to the context
@@ -811,6 +819,23 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     }
     __syncthreads();
     mark(6);
+    if constexpr (FUSED) {
+        if (a.fx) {   // exact attention: the scaled scores to the kv group's chain workgroup, one {fp32, tag} granule each
+            const uint32_t tag = gran_tag(pos, a.layer);
+            if (tid < 2 * SPL) {
+                const int hh = tid / SPL, j = tid - hh * SPL;
+                if (k0 + j < k1)
+                    __hip_atomic_store(a.sgran + (long)(2 * g + hh) * a.max_ctx + k0 + j,
+                                       ((unsigned long long)tag << 32) | __float_as_uint(sc[hh][j]), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (a.fx_vpf)
+#pragma unroll
+                for (int i = 0; i < KPW; i++) asm volatile("" ::"v"(vv[i]));   // (the V^T pull has landed)
+            mark(3);
+            return;
+        }
+    }
     if constexpr (!FUSED) {
         if (a.scores) {   // front half of the exact attention (fa_exact.hip): this split's scaled scores
             float *dst = a.scores + ((long)b * a.n_head + 2 * g) * a.max_ctx + k0;
@@ -1223,14 +1248,157 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
     if (lane == 0) o.out_f32[row] = fadd_rn(acc, res);
 }
 
+// Chain role of the fused exact attention (DecodeAttnArgs.fx): one workgroup
+// per kv group g, wave w running query head 2g + w / 2, dimensions 64 (w % 2)
+// + lane, with ggml's CPU flash-attention numerics (fx_chain.h; the same
+// arithmetic as fa_exact.hip's decode_attn_exact_kernel, so the two launches
+// are bit-identical).  V^T of keys below the position comes from the cache
+// (earlier steps' rows; the first 128 keys requested at entry); the new key's
+// v from its QKV granule.  The two heads' scores arrive as granules from the
+// splits, gathered per DX_KC-key chunk into LDS (every thread polls its own
+// 16-B granule pairs, bounded); each wave derives the chunk's weights from
+// LDS into registers and runs the chain.  The output goes to the o-projection
+// role as the split-K combiners' does (write-through, drained, att_done).
+// eight 16-B sc1 loads at base + off[u] bytes (base uniform: the SGPR-pair
+// address form, so the offsets cost one VGPR each), drained in the same asm
+// block (no copy of an output can be scheduled before the data has landed)
+__device__ __forceinline__ void ld_sc1_x4_8(const void *base, const uint32_t *off, u32x4 *v) {
+    asm volatile(
+        "global_load_dwordx4 %0, %8, %16 sc1\n\t"
+        "global_load_dwordx4 %1, %9, %16 sc1\n\t"
+        "global_load_dwordx4 %2, %10, %16 sc1\n\t"
+        "global_load_dwordx4 %3, %11, %16 sc1\n\t"
+        "global_load_dwordx4 %4, %12, %16 sc1\n\t"
+        "global_load_dwordx4 %5, %13, %16 sc1\n\t"
+        "global_load_dwordx4 %6, %14, %16 sc1\n\t"
+        "global_load_dwordx4 %7, %15, %16 sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+        : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]), "v"(off[7]), "s"(base)
+        : "memory");
+}
+__device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const int g) {
+    __shared__ __attribute__((aligned(16))) float fsc[2][DX_KC / DX_B * FX_ST];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int hh = wid >> 1, wu = __builtin_amdgcn_readfirstlane(wid & 1);
+    const int d = 64 * wu + lane, loff = 8 * lane;
+    const uint16_t *vt = a.vt + (long)g * 128 * vt_ctx(a.max_ctx) + 64 * wu * 8;   // batch 1: slot 0; the wave's key block 0
+    const int pos = a.pos[0], nkv = pos + 1;
+    const uint32_t tag = gran_tag(pos, a.layer);
+    const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
+    // the new key's v (this lane's dimension): its QKV granule, cast to fp16 as the cache write is
+    uint16_t vnew = 0;
+    {
+        const unsigned long long *gp = a.gran + QD + KD + g * 128 + d;
+        unsigned long long v = 0;
+        bool ok = false;
+        for (int it = 0; it < a.poll_limit; it++) {
+            v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = (uint32_t)(v >> 32) == tag;
+            if (__all(ok)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_QKV_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        vnew = f_to_u16(__uint_as_float((uint32_t)v));
+    }
+    for (int i = 0; i < a.fx_delay; i++) __builtin_amdgcn_s_sleep(8);
+    // one chunk: the launch is taken only while n_kv <= DX_KC (launch_qkv_attention1)
+    const int n = nkv, np = (n + 1) >> 1;
+    // (1) the score granules of both heads -> LDS: thread tid takes the 16-B
+    //     pairs q = tid + 256 (u / 2) of head u % 2, all in flight together
+    {
+        const unsigned long long *gb = a.sgran + (long)(2 * g) * a.max_ctx;   // uniform
+        uint32_t go[DX_KC / 256];
+#pragma unroll
+        for (int u = 0; u < DX_KC / 256; u++) {
+            const int q = tid + 256 * (u >> 1);
+            go[u] = q < np ? (uint32_t)(((u & 1) * a.max_ctx + 2 * q) * 8) : 0u;
+        }
+        u32x4 gv[DX_KC / 256];
+        bool ok = false;
+        for (int it = 0; it < a.poll_limit; it++) {
+            ld_sc1_x4_8(gb, go, gv);
+            ok = true;
+#pragma unroll
+            for (int u = 0; u < DX_KC / 256; u++) {
+                const int q = tid + 256 * (u >> 1);
+                if (q < np) ok = ok && gv[u][1] == tag && (2 * q + 1 >= n || gv[u][3] == tag);
+            }
+            if (__syncthreads_and(ok)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok && tid == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_SCORE_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int u = 0; u < DX_KC / 256; u++) {
+            const int q = tid + 256 * (u >> 1), j = 2 * q;   // even: both keys in one 32-key row
+            if (q < np)
+                *(float2 *)&fsc[u & 1][(j >> 5) * FX_ST + (j & 31)] = make_float2(__uint_as_float(gv[u][0]), __uint_as_float(gv[u][2]));
+        }
+    }
+    __syncthreads();
+    // (2) the weights of this wave's head (both waves of a head compute the
+    //     same), written back over the scores; (3) the chain, weights from LDS
+    float M = -INFINITY, S;
+    unsigned long long flags;
+    {
+        float w[DX_B], wl;   // (wl: unused here)
+        float *row = fsc[hh] + lane * FX_ST;   // this lane's 32 keys
+        S = fx_weights_reg([&](int j) { return row[j & 31]; }, n, M, w, flags, wl);
+        __syncthreads();   // every wave has read its scores
+        if ((wid & 1) == 0)
+#pragma unroll
+            for (int i = 0; i < DX_B; i += 4) *(floatx4 *)&row[i] = floatx4{w[i], w[i + 1], w[i + 2], w[i + 3]};
+    }
+    __syncthreads();
+    // the new key (n - 1) takes vnew: its batch on the slow path
+    flags |= 1ull << ((n - 1) / DX_B);
+    f16 acc = 0;
+    {
+        u32x4 va[DX_Q / 8], vb[DX_Q / 8];
+        floatx4 wa, wb;
+        fx_loadQ(va, vt, loff, 0);
+        fx_w8(fsc[hh], 0, wa, wb);
+        for (int j0 = 0; j0 < n; j0 += 2 * DX_Q) {
+            fx_loadQ(vb, vt, loff, j0 + DX_Q);
+            fx_step1_lds(va, j0, n, fsc[hh], flags, acc, n - 1, vnew, wa, wb);
+            fx_loadQ(va, vt, loff, j0 + 2 * DX_Q);
+            fx_step1_lds(vb, j0 + DX_Q, n, fsc[hh], flags, acc, n - 1, vnew, wa, wb);
+        }
+    }
+    // ggml: VKQ32 = fp32(VKQ16) * (1 / S); fp16 for the o-projection
+    const float ov = (float)acc * (S == 0.0f ? 0.0f : 1.0f / S);
+    const uint32_t h16 = f_to_u16(ov);
+    const uint32_t hn = __shfl_xor(h16, 1, 64);
+    uint16_t *out = a.out + (2 * g + hh) * 128 + d;
+    if (a.att_done) {   // the o-proj blocks of this launch read it: write-through pairs, drained, one arrival per replica
+        if ((lane & 1) == 0) __hip_atomic_store((uint32_t *)out, h16 | (hn << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (a.fence && tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (a.fence) __syncthreads();
+        if (tid < 8) __hip_atomic_fetch_add(a.att_done + tid * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        *out = (uint16_t)h16;
+    }
+}
+
 template <int SPL>
 __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnArgs a, GemvArgs o) {
     constexpr int K = 1024, NT = 2, RPW = 2;
     stamp_start(a.stamp);
     if (blockIdx.x >= 512) {
+        // splits (kv group j % n_kv_head: blocks b and b + 8 share an XCD under
+        // round-robin placement, so a group's splits and its chain workgroup
+        // share one L2 -- speed only), the chain workgroups (exact attention),
+        // the o-projection
         const int j = blockIdx.x - 512, nsp = a.grid_splits, nat = nsp * a.n_kv_head;   // grid_splits: this launch's splits
-        if (j >= nat) oproj1_body(o, a, j - nat);
-        else decode_attn_body<SPL, true>(a, j % nsp, j / nsp, 0, nsp);
+        const int nfx = a.fx ? a.n_kv_head : 0;
+        if (j >= nat + nfx) oproj1_body(o, a, j - nat - nfx);
+        else if (j >= nat) fx1_chain_body(a, j - nat);
+        else decode_attn_body<SPL, true>(a, j / a.n_kv_head, j % a.n_kv_head, 0, nsp);
         stamp_end(a.stamp);
         return;
     }
@@ -1337,12 +1505,16 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
                         !o->Wd && !o->bias && !o->norm_w && o->xh == a.out;
     // every block of the launch must be co-resident (blocks wait on earlier
     // ones): fall back to separate launches for contexts that would not fit
+    // (exact attention: n_kv_head chain workgroups too; they read the new v
+    // from its granule, so the fused exact path needs the granule hand-off)
+    if (a.fx && (!a.gran || !a.sgran || a.max_ctx % 2 || ns * spl1 > DX_KC)) return 0;   // (one chain chunk)
+    const int nfx = a.fx ? a.n_kv_head : 0;
     const int slots = spl1 == 128 ? cfg.slots_qkv128 : cfg.slots_qkv64;
-    const bool fit_o = 512 + ns * a.n_kv_head + 256 <= slots;
-    if (512 + ns * a.n_kv_head > slots) return 0;
+    const bool fit_o = 512 + ns * a.n_kv_head + nfx + 256 <= slots;
+    if (512 + ns * a.n_kv_head + nfx > slots) return 0;
     const bool with_o2 = with_o && fit_o;
     if (dry) return with_o2 ? 2 : 1;
-    const dim3 grid(512 + ns * a.n_kv_head + (with_o2 ? o->N / 4 : 0));
+    const dim3 grid(512 + ns * a.n_kv_head + nfx + (with_o2 ? o->N / 4 : 0));
     // K/V delay ~2 us: measured optimum on MI355X (round-1 delay sweep: 0 -> 236.3, 10 -> 232.0, 18 -> 240.3 ms decode)
     DecodeAttnArgs ad = a;
     ad.fuse_delay = cfg.qkv_delay;
@@ -1351,6 +1523,8 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     ad.fence = cfg.fence;
     ad.err = cfg.err;
     ad.grid_splits = ns;   // the kernel's split count
+    ad.fx_delay = cfg.fx_delay;
+    ad.fx_vpf = cfg.fx_vpf;
     if (!with_o2) ad.att_done = nullptr;
     const GemvArgs qa = q;
     const GemvArgs oa = with_o2 ? *o : GemvArgs{};

@@ -118,6 +118,7 @@ struct qasr_ctx {
     unsigned int *d_counter = nullptr, *d_done = nullptr;
     unsigned int *d_qcnt = nullptr;   // fused batch-1 QKV + attention: QKV-block arrivals per kv group
     unsigned long long *d_gran = nullptr;   // ... or its outputs as tagged granules (zeroed by every prefill)
+    unsigned long long *d_sgran = nullptr;  // ... exact attention: the splits' scores as granules [n_head][max_ctx] (zeroed likewise)
     bool qkv_in_gran = false;               // the captured step's last layer hands its QKV over in granules
     unsigned int *d_attdone = nullptr;   // fused batch-1 o-proj: combiner arrivals (8 replicas)
     unsigned int *d_ffncnt = nullptr;    // fused batch-1 FFN: gate/up arrivals, [layer][32 shards][16]
@@ -210,6 +211,8 @@ static const std::vector<FuseOption> &fuse_options() {
         {"gemm_regs", "QASR_GEMM_REGS", &FuseCfg::gemm_regs},
         {"gran", "QASR_GRAN", &FuseCfg::gran},
         {"fa_exact_decode", "QASR_FA_EXACT_DECODE", &FuseCfg::fa_exact_decode},
+        {"fx_delay", "QASR_FX_DELAY", &FuseCfg::fx_delay},
+        {"fx_vpf", "QASR_FX_VPF", &FuseCfg::fx_vpf},
         {"att_stream", "QASR_ATT_STREAM", &FuseCfg::att_stream},
         {"skinny", "QASR_SKINNY", &FuseCfg::skinny},
         {"att_spl", "QASR_ATT_SPL", &FuseCfg::att_spl},
@@ -251,6 +254,7 @@ static int check_dev_err(qasr_ctx *c) {
     if (e & DEVERR_QKV_WAIT) what += " attention<-QKV";
     if (e & DEVERR_O_WAIT) what += " o-proj<-attention";
     if (e & DEVERR_FFN_WAIT) what += " down<-gate/up";
+    if (e & DEVERR_SCORE_WAIT) what += " chain<-scores";
     return fail(QASR_ERR_DEVICE, "fused decode launch: an in-launch wait timed out (" + what.substr(1) +
                                      "); outputs of this call are invalid (another process or context sharing the GPU?)");
 }
@@ -268,14 +272,14 @@ static std::mutex &device_lock(int device) {
 }
 // decode attention with ggml's fp16 V accumulation (fa_exact.hip)?
 static bool exact_decode(const qasr_ctx *c) {
-    return c->fuse.fa_exact_decode > 0 || (c->fuse.fa_exact_decode < 0 && c->m->q8);
+    return c->fuse.fa_exact_decode != 0;
 }
 // V^T cache elements of one layer
 static size_t layer_vt(const qasr_ctx *c) {
     return (size_t)c->max_batch * c->m->hp.n_kv_head * 128 * vt_ctx(c->max_ctx);
 }
 static bool takes_fused(const qasr_ctx *c, int B) {
-    return B == 1 && !c->m->q8 && (c->fuse.ffn || (c->fuse.qkv && !exact_decode(c)));
+    return B == 1 && !c->m->q8 && (c->fuse.ffn || c->fuse.qkv);
 }
 
 // a roctx range for the lifetime of the object (rocprofv3 --marker-trace)
@@ -711,6 +715,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_qcnt, (size_t)hp.n_kv_head * 8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_attdone, (size_t)8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_gran, (size_t)(QD + 2 * KD) * 8)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_sgran, (size_t)hp.n_head * max_ctx * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_ffncnt, (size_t)hp.dec_layers * 512 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_err, 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_pstamp, (size_t)max_ctx * kStampRec * 8)) ||
@@ -724,6 +729,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     HIPCHK(hipMemset(c->d_qcnt, 0, (size_t)hp.n_kv_head * 8 * 16 * 4));
     HIPCHK(hipMemset(c->d_attdone, 0, (size_t)8 * 16 * 4));
     HIPCHK(hipMemset(c->d_gran, 0, (size_t)(QD + 2 * KD) * 8));
+    HIPCHK(hipMemset(c->d_sgran, 0, (size_t)hp.n_head * max_ctx * 8));
     HIPCHK(hipMemset(c->d_ffncnt, 0, (size_t)hp.dec_layers * 512 * 4));
     HIPCHK(hipMemset(c->d_done, 0, 4));
     HIPCHK(hipMemset(c->d_err, 0, 4));
@@ -1105,6 +1111,7 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
     if ((rc = prefill_layers(c, ids, P, d_feats, audio_pos, N))) return rc;
     // granule tags repeat across runs at the same positions: back to zero (no valid tag)
     HIPCHK(hipMemsetAsync(c->d_gran, 0, (size_t)(c->m->hp.n_head + 2 * c->m->hp.n_kv_head) * 128 * 8, c->st));
+    HIPCHK(hipMemsetAsync(c->d_sgran, 0, (size_t)c->m->hp.n_head * c->max_ctx * 8, c->st));
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
     const int B = (int)P.size(), H = hp.hidden;
@@ -1229,8 +1236,14 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             dn.stamp = stamp;
         }
         const bool exact = exact_decode(c);
-        const bool fusable = skinny && B == 1 && !q8 && !skip && !exact;
+        const bool fusable = skinny && B == 1 && !q8 && !skip;
         if (fusable) da.att_done = c->d_attdone;
+        if (fusable && exact && c->fuse.gran) {   // ggml's attention numerics as the fused launch's chain role
+            da.fx = 1;
+            da.sgran = c->d_sgran;
+            da.gran = c->d_gran;   // (the fused decision needs the granule hand-off)
+            da.layer = l;
+        }
         unsigned int *fcnt = c->d_ffncnt + (size_t)l * 512, *fcnt_next = c->d_ffncnt + (size_t)((l + 1) % nl) * 512;
         // 0 = separate launches, 1 = QKV + attention in one launch, 2 = + o-projection
         const int fmode = fusable ? launch_qkv_attention1(q1, da, &o, c->fuse, s, true) : 0;
@@ -1575,6 +1588,7 @@ extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_pa
     HIPCHK(hipSetDevice(c->m->device));
     // a caller may repeat a position (same tag): no granule of an earlier call may match
     HIPCHK(hipMemsetAsync(c->d_gran, 0, (size_t)(c->m->hp.n_head + 2 * c->m->hp.n_kv_head) * 128 * 8, c->st));
+    HIPCHK(hipMemsetAsync(c->d_sgran, 0, (size_t)c->m->hp.n_head * c->max_ctx * 8, c->st));
     std::vector<int> pos(B), nkv(B);
     for (int b = 0; b < B; b++) {
         if (n_past[b] < 0 || n_past[b] + 1 > c->max_ctx) return fail(QASR_ERR_ARG, "Context length exceeded");

@@ -42,6 +42,7 @@
 // dimensions 62 -- a wave issues a VALU instruction every ~5 cycles, and
 // more waves per SIMD do not slow each other.
 #include "dev_common.h"
+#include "fx_chain.h"
 #include "kernels.h"
 
 namespace qasr {
@@ -63,36 +64,6 @@ __device__ __forceinline__ half2v fx_mad2(half2v acc, uint32_t v, float vs) {
 __device__ __forceinline__ half2v fx_scale2(half2v acc, float ms) {
     return __builtin_convertvector((floatx2){(float)acc.x * ms, (float)acc.y * ms}, half2v);
 }
-// one value: the conversion in asm (a scalar fptrunc would fold into mixlo)
-__device__ __forceinline__ f16 fx_cvt(float f) {
-    f16 h;
-    asm("v_cvt_f16_f32 %0, %1" : "=v"(h) : "v"(f));
-    return h;
-}
-__device__ __forceinline__ f16 fx_mad1(f16 acc, uint16_t v, float vs) {
-    return fx_cvt(fmaf((float)__builtin_bit_cast(f16, v), vs, (float)acc));
-}
-
-// DPP lane move with -inf where the source lane is out of range or its row
-// is masked off (bound_ctrl off: the lane keeps the -inf of `old`)
-template <int CTRL, int ROWS>
-__device__ __forceinline__ float dpp_ninf(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, -INFINITY), __builtin_bit_cast(int, v),
-                                                                 CTRL, ROWS, 0xF, false));
-}
-// inclusive prefix maximum over the 64 lanes, all in VALU DPP: Hillis-Steele
-// in each 16-lane row (row_shr 1, 2, 4, 8), then row_bcast:15 (each row's
-// last lane into the next row) and row_bcast:31 (lane 31 into rows 2, 3)
-__device__ __forceinline__ float wave_scan_max(float x) {
-    x = fmaxf(x, dpp_ninf<0x111, 0xF>(x));
-    x = fmaxf(x, dpp_ninf<0x112, 0xF>(x));
-    x = fmaxf(x, dpp_ninf<0x114, 0xF>(x));
-    x = fmaxf(x, dpp_ninf<0x118, 0xF>(x));
-    x = fmaxf(x, dpp_ninf<0x142, 0xA>(x));
-    x = fmaxf(x, dpp_ninf<0x143, 0xC>(x));
-    return x;
-}
-
 // Weights of n keys (n <= KPL * 64) of one row, one wave: src[j] = the scaled
 // score (src may be sc itself), sc[j] = vs_j on return, ms[j] = ms_j (1 where no new
 // maximum; a masked key (-inf) gives vs = 0, ms = 1 -- ggml skips it, and a
@@ -387,101 +358,22 @@ void launch_prefill_attention_exact(const PrefillAttnArgs &a, hipStream_t s) {
 // of exposed latency), V prefetched through a four-slot register ring (the
 // loop-carried wait counts came out vmcnt(0)) or an LDS-DMA ring (~60 cycles
 // of issue per 1 KiB piece).
-#define DX_B 32    // keys per lane of the weights = keys sharing one fast/slow decision
-#define DX_Q 64    // keys of V per register buffer (two in turn)
-__device__ __forceinline__ uint16_t fx_elem(const u32x4 *v, int i) {   // key i of the step (i constant)
-    const uint32_t w = v[i >> 3][(i >> 1) & 3];
-    return (uint16_t)((i & 1) ? (w >> 16) : (w & 0xffffu));
-}
-__device__ __forceinline__ float fx_lane(float x, int l) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
-}
-// keys [j0, j0 + DX_Q) of the chunk from registers v; w / m: the weights
-// registers (key 32 L + i in lane L, element i); flags: bit L = a new maximum
-// among lane L's keys
-__device__ __forceinline__ void fx_step1(const u32x4 *v, int j0, int n, const float *w, const float *m,
-                                         unsigned long long flags, f16 &acc) {
-#pragma unroll
-    for (int bq = 0; bq < DX_Q / DX_B; bq++) {
-        const int jb = j0 + bq * DX_B;
-        const int L = jb / DX_B;
-        const int nb = min(DX_B, n - jb);
-        if (nb == DX_B && !((flags >> L) & 1ull)) {
-#pragma unroll
-            for (int i = 0; i < DX_B; i++) acc = fx_mad1(acc, fx_elem(v, bq * DX_B + i), fx_lane(w[i], L));
-        } else if (nb > 0) {
-#pragma unroll
-            for (int i = 0; i < DX_B; i++) {
-                if (i < nb) {
-                    acc = fx_cvt((float)acc * fx_lane(m[i], L));   // ms = 1: exact
-                    acc = fx_mad1(acc, fx_elem(v, bq * DX_B + i), fx_lane(w[i], L));
-                }
-            }
-        }
-    }
-}
-__device__ __forceinline__ void fx_loadQ(u32x4 *v, const uint16_t *__restrict__ vt, int loff, int j0) {
-#pragma unroll
-    for (int i = 0; i < DX_Q / 8; i++) v[i] = *(const u32x4 *)(vt + (long)(j0 / 8 + i) * 1024 + loff);
-}
-// vt: the wave's key block 0 of the chunk (uniform: the loads take a scalar
-// base and the lane offset loff = 8 lane, kernels.h vt_index: 1024 halves
-// per block; the region carries read-ahead slack).  Two register buffers in
+//
+// keys [0, n) of one (head, sequence): the V^T rows of the wave's 64
+// dimensions from vt (its key block 0, uniform), two register buffers in
 // turn, the next step's loads issued before the current step's arithmetic --
-// unconditionally (slack), so the wait counts stay exact.
-__device__ __forceinline__ void fx_chain1(const uint16_t *__restrict__ vt, int loff, int n, const float *w, const float *m,
+// unconditionally (vt_ctx carries read-ahead slack), so the wait counts stay
+// exact.  c0: the first key of the current weights chunk.
+__device__ __forceinline__ void fx_chain1(const uint16_t *__restrict__ vt, int loff, int c0, int n, const float *w,
                                           unsigned long long flags, f16 &acc) {
     u32x4 va[DX_Q / 8], vb[DX_Q / 8];
-    fx_loadQ(va, vt, loff, 0);
+    fx_loadQ(va, vt, loff, c0);
     for (int j0 = 0; j0 < n; j0 += 2 * DX_Q) {
-        fx_loadQ(vb, vt, loff, j0 + DX_Q);
-        fx_step1(va, j0, n, w, m, flags, acc);
-        fx_loadQ(va, vt, loff, j0 + 2 * DX_Q);
-        fx_step1(vb, j0 + DX_Q, n, w, m, flags, acc);
+        fx_loadQ(vb, vt, loff, c0 + j0 + DX_Q);
+        fx_step1(va, j0, n, w, flags, acc);
+        fx_loadQ(va, vt, loff, c0 + j0 + 2 * DX_Q);
+        fx_step1(vb, j0 + DX_Q, n, w, flags, acc);
     }
-}
-
-// The weights of a chunk's n keys (n <= 64 DX_B) for one wave, in registers:
-// lane L's keys 32 L + i -> w[i] = vs, m[i] = ms; flags bit L = a new maximum
-// among them.  M: running maximum (in/out); returns this chunk's S at the new
-// maximum (per lane a sequential S = S * ms + vs as ggml, the lanes combined
-// in fp32).
-__device__ __forceinline__ float fx_weights_reg(const float *src, int n, float &M, float *w, float *m,
-                                                unsigned long long &flags) {
-    const int lane = threadIdx.x & 63;
-    float lm = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < DX_B; i++) {
-        const int j = lane * DX_B + i;
-        w[i] = j < n ? src[j] : -INFINITY;   // the score, replaced by vs below
-    }
-#pragma unroll
-    for (int i = 0; i < DX_B; i++) lm = fmaxf(lm, w[i]);
-    const float inc = wave_scan_max(lm);
-    float Mp = fmaxf(M, dpp_ninf<0x138, 0xF>(inc));
-    const float Mn = fmaxf(M, lane_f(inc, 63));
-    float Sl = 0.0f;
-    bool nm = false;
-#pragma unroll
-    for (int i = 0; i < DX_B; i++) {
-        const float s = w[i];
-        float m1 = 1.0f, v1 = 0.0f;
-        if (s > Mp) {   // new maximum: ms = expf(Mold - M) (0 before the first key), vs = 1
-            m1 = expf(Mp - s);
-            v1 = 1.0f;
-            Mp = s;
-            nm = true;
-        } else if (s != -INFINITY) {
-            v1 = expf(s - Mp);
-        }
-        Sl = Sl * m1 + v1;
-        w[i] = v1;
-        m[i] = m1;
-    }
-    const float S = wave_sum(Mp == -INFINITY ? 0.0f : Sl * expf(Mp - Mn));
-    flags = __ballot(nm);
-    M = Mn;
-    return S;
 }
 
 // query head h of sequence b, wave wid (0, 1) running dimensions 64 wid +
@@ -500,17 +392,18 @@ __device__ __forceinline__ void decode_attn_exact_body(const DecodeAttnArgs &a, 
     unsigned long long tsum[4] = {0, 0, 0, 0};
     FX_CLK(tk0);
 #endif
-    for (int c0 = 0; c0 < nkv; c0 += 64 * DX_B) {
+    for (int c0 = 0; c0 < nkv; c0 += DX_KC) {
         FX_CLK(ta);
-        const int n = min(64 * DX_B, nkv - c0);
-        float w[DX_B], m[DX_B];
+        const int n = min(DX_KC, nkv - c0);
+        float w[DX_B], wl;
         unsigned long long flags;
         const float Mold = M;
-        const float Sc = fx_weights_reg(sg + c0, n, M, w, m, flags);
+        const float *sc = sg + c0;
+        const float Sc = fx_weights_reg([&](int j) { return sc[j]; }, n, M, w, flags, wl);
         S = (Mold == -INFINITY ? 0.0f : S * expf(Mold - M)) + Sc;
         FX_CLK(tb);
         FX_ADD(0, tb - ta);
-        fx_chain1(vcol + (long)c0 * 128, 8 * lane, n, w, m, flags, acc);
+        fx_chain1(vcol, 8 * lane, c0, n, w, flags, acc);
         FX_CLK(tc);
         FX_ADD(1, tc - tb);
     }

@@ -1,0 +1,216 @@
+// fx_chain.h -- the decode-step chain of ggml's CPU flash attention, shared by
+// the separate exact decode kernels (fa_exact.hip) and the batch-1 fused
+// launch (attention.hip qkv_attn1_kernel, chain role).
+//
+// ggml_flash_attn_ext on the CPU backend (src/text_decoder.cpp:534-540;
+// SURVEY.md §8(a) viii) walks one query row's keys in order: s = q.k * scale;
+// a new maximum rescales the fp16 V accumulator (ggml_vec_scale_f16: y =
+// fp16(fp32(y) * ms)), every key adds v * vs (ggml_vec_mad_f16: y =
+// fp16(fma(fp32(v), vs, fp32(y)))), and S = S * ms + vs in fp32.  Each
+// (query, head, dimension) is one sequential chain; here one dimension a lane,
+// V from the V^T cache (kernels.h vt_index: 8 keys of a dimension per 16-B
+// load), the key's weight an SGPR operand (v_readlane) of v_fma_mix_f32.
+//
+// Weights are kept one register per key: w = vs where the key is not a new
+// maximum, w = -ms where it is (vs = 1 there; ms in [0, 1), the first key's
+// ms = exp(-inf) = 0 is stored as -0.0f) -- the sign bit tells the two apart,
+// so a chunk's weights cost 32 VGPRs instead of 64.
+#pragma once
+#include "dev_common.h"
+
+namespace qasr {
+
+#define DX_B 32    // keys per lane of the weights = keys sharing one fast/slow decision
+#define DX_Q 64    // keys of V per register buffer (two in turn)
+#define DX_KC (64 * DX_B)   // keys per weights chunk (one wave: 64 lanes x DX_B)
+
+// one value: the conversion in asm (a scalar fptrunc of an fma would fold
+// into v_fma_mixlo_f16, which rounds once instead of fp32-then-fp16)
+__device__ __forceinline__ f16 fx_cvt(float f) {
+    f16 h;
+    asm("v_cvt_f16_f32 %0, %1" : "=v"(h) : "v"(f));
+    return h;
+}
+// ggml_vec_mad_f16 on one value: fp16(fma(v, vs, acc)), the fma rounded to fp32
+__device__ __forceinline__ f16 fx_mad1(f16 acc, uint16_t v, float vs) {
+    return fx_cvt(fmaf((float)__builtin_bit_cast(f16, v), vs, (float)acc));
+}
+
+// DPP lane move with -inf where the source lane is out of range or its row
+// is masked off (bound_ctrl off: the lane keeps the -inf of `old`)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_ninf(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, -INFINITY), __builtin_bit_cast(int, v),
+                                                                 CTRL, ROWS, 0xF, false));
+}
+// inclusive prefix maximum over the 64 lanes, all in VALU DPP: Hillis-Steele
+// in each 16-lane row (row_shr 1, 2, 4, 8), then row_bcast:15 (each row's
+// last lane into the next row) and row_bcast:31 (lane 31 into rows 2, 3)
+__device__ __forceinline__ float wave_scan_max(float x) {
+    x = fmaxf(x, dpp_ninf<0x111, 0xF>(x));
+    x = fmaxf(x, dpp_ninf<0x112, 0xF>(x));
+    x = fmaxf(x, dpp_ninf<0x114, 0xF>(x));
+    x = fmaxf(x, dpp_ninf<0x118, 0xF>(x));
+    x = fmaxf(x, dpp_ninf<0x142, 0xA>(x));
+    x = fmaxf(x, dpp_ninf<0x143, 0xC>(x));
+    return x;
+}
+
+__device__ __forceinline__ uint16_t fx_elem(const u32x4 *v, int i) {   // key i of the buffer (i constant)
+    const uint32_t w = v[i >> 3][(i >> 1) & 3];
+    return (uint16_t)((i & 1) ? (w >> 16) : (w & 0xffffu));
+}
+__device__ __forceinline__ float fx_lane(float x, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+}
+// one key of the slow path, branch-free: w signed as above (uniform), so
+// ms = 1 and vs = w, or ms = -w and vs = 1 -- the scale is exact where ms = 1
+// (an fp16 value times 1), and a zero weight (keys past the chunk) leaves the
+// accumulator unchanged (fma(v, 0, acc) = acc for finite v)
+__device__ __forceinline__ f16 fx_key_slow(f16 acc, uint16_t v, float w) {
+    const bool nm = __builtin_signbit(w);
+    acc = fx_cvt((float)acc * (nm ? -w : 1.0f));
+    return fx_mad1(acc, v, nm ? 1.0f : w);
+}
+
+// keys [j0, min(j0 + DX_Q, n)) of the chunk (relative to its first key) from
+// registers v, in 32-key batches.  w: the weights registers (key 32 L + i in lane L, element i;
+// zero past the chunk's keys); flags: bit L = lane L's batch takes the slow
+// path (a new maximum among its keys, keys past the chunk, or key `last`) --
+// the others take two VALU instructions a key.  Key `last` (relative to the
+// chunk; -1: none) takes vnew instead of its V^T element (the fused launch's
+// new key, whose cache row is being written by another workgroup).
+__device__ __forceinline__ void fx_step1(const u32x4 *v, int j0, int n, const float *w, unsigned long long flags, f16 &acc,
+                                         int last = -1, uint16_t vnew = 0) {
+#pragma unroll
+    for (int bq = 0; bq < DX_Q / DX_B; bq++) {
+        const int jb = j0 + bq * DX_B;
+        const int L = jb / DX_B;
+        if (jb >= n) break;
+        if (!((flags >> L) & 1ull)) {
+#pragma unroll
+            for (int i = 0; i < DX_B; i++) acc = fx_mad1(acc, fx_elem(v, bq * DX_B + i), fx_lane(w[i], L));
+        } else {
+#pragma unroll
+            for (int i = 0; i < DX_B; i++) {
+                const uint16_t e = fx_elem(v, bq * DX_B + i);
+                acc = fx_key_slow(acc, jb + i == last ? vnew : e, fx_lane(w[i], L));
+            }
+        }
+    }
+}
+// fx_step1 with the weights in LDS instead of registers (the fused launch's
+// chain role): ws = the head's signed weights, FX_ST floats per 32-key row
+// (row L = lane L's keys of fx_weights_reg).  Per 8 keys the weights arrive
+// as two uniform ds_read_b128 (VGPR operands of v_fma_mix_f32), requested one
+// group ahead; the fast path of a group is one inline-asm block of the
+// chain's 16 instructions -- the compiler neither hoists the next groups'
+// loads above it (the "memory" clobber) nor interleaves anything into it, so
+// the role's register use stays bounded (compiler-scheduled, the unrolled
+// 64-key step held up to 190 VGPRs).  The arithmetic is fx_mad1's:
+// v_fma_mix_f32 (fp16 v and accumulator, fp32 weight, one fp32 rounding),
+// then v_cvt_f16_f32 (RNE).
+#define FX_ST 36   // LDS floats per 32-key row: the 64 rows' 16-B reads of fx_weights_reg hit distinct banks
+#define FX_MIX(VI, W, SEL) "v_fma_mix_f32 %0, " VI ", " W ", %1 op_sel:[" SEL ",0,0] op_sel_hi:[1,0,1]\n\t"
+#define FX_CVT "s_nop 0\n\tv_cvt_f16_f32 %1, %0\n\t"
+__device__ __forceinline__ void fx8_fast(f16 &acc, const u32x4 v, const floatx4 wa, const floatx4 wb) {
+    float t;
+    asm volatile(FX_MIX("%2", "%6", "0") FX_CVT FX_MIX("%2", "%7", "1") FX_CVT FX_MIX("%3", "%8", "0") FX_CVT
+                 FX_MIX("%3", "%9", "1") FX_CVT FX_MIX("%4", "%10", "0") FX_CVT FX_MIX("%4", "%11", "1") FX_CVT
+                 FX_MIX("%5", "%12", "0") FX_CVT FX_MIX("%5", "%13", "1") FX_CVT
+                 : "=&v"(t), "+v"(acc)
+                 : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(wa[0]), "v"(wa[1]), "v"(wa[2]), "v"(wa[3]), "v"(wb[0]),
+                   "v"(wb[1]), "v"(wb[2]), "v"(wb[3])
+                 : "memory");
+}
+#undef FX_MIX
+#undef FX_CVT
+// the slow path of 8 keys (fx_key_slow each; key `last` (relative to the
+// group; -1: none) takes vnew)
+__device__ __forceinline__ void fx8_slow(f16 &acc, const u32x4 v, const floatx4 wa, const floatx4 wb, int last, uint16_t vnew) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint32_t d = v[i >> 1];
+        const uint16_t e = (i & 1) ? (uint16_t)(d >> 16) : (uint16_t)(d & 0xffffu);
+        acc = fx_key_slow(acc, i == last ? vnew : e, i < 4 ? wa[i] : wb[i - 4]);
+    }
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void fx_w8(const float *ws, int k, floatx4 &wa, floatx4 &wb) {   // weights of keys k .. k + 7
+    const float *p = ws + (k >> 5) * FX_ST + (k & 31);
+    wa = *(const floatx4 *)p;
+    wb = *(const floatx4 *)(p + 4);
+}
+// keys [j0, min(j0 + DX_Q, n)) from registers v (8 keys per u32x4);
+// wa / wb: the weights of keys j0 .. j0 + 7 on entry, of j0 + DX_Q .. on exit
+__device__ __forceinline__ void fx_step1_lds(const u32x4 *v, int j0, int n, const float *ws, unsigned long long flags, f16 &acc,
+                                             int last, uint16_t vnew, floatx4 &wa, floatx4 &wb) {
+#pragma unroll
+    for (int g8 = 0; g8 < DX_Q / 8; g8++) {
+        const int k = j0 + 8 * g8;
+        if (k >= n) break;
+        floatx4 na, nb;
+        fx_w8(ws, k + 8, na, nb);   // (row padding / the next row: in bounds of the chunk's LDS image)
+        if ((flags >> (k / DX_B)) & 1ull) fx8_slow(acc, v[g8], wa, wb, last - k, vnew);
+        else fx8_fast(acc, v[g8], wa, wb);
+        wa = na;
+        wb = nb;
+    }
+}
+
+// DX_Q keys of V from key block j0 / 8 (vt: the wave's key block 0, uniform;
+// loff = 8 lane: kernels.h vt_index, 1024 halves per block)
+__device__ __forceinline__ void fx_loadQ(u32x4 *v, const uint16_t *__restrict__ vt, int loff, int j0) {
+#pragma unroll
+    for (int i = 0; i < DX_Q / 8; i++) v[i] = *(const u32x4 *)(vt + (long)(j0 / 8 + i) * 1024 + loff);
+}
+
+// The weights of a chunk's n keys (n <= DX_KC) for one wave, in registers:
+// lane L's keys 32 L + i -> w[i] (signed as above; 0 past n); flags bit L =
+// lane L's batch takes the slow path (fx_step1).  src(j) = the scaled score of key j (-inf: masked, vs =
+// 0, ms = 1).  M: running maximum (in/out).  Returns this chunk's S at the new
+// maximum (per lane a sequential S = S * ms + vs as ggml, the lanes combined
+// in fp32).  wlast: the weight of key n - 1 (uniform).
+template <class Src>
+__device__ __forceinline__ float fx_weights_reg(Src src, int n, float &M, float *w, unsigned long long &flags, float &wlast) {
+    const int lane = threadIdx.x & 63;
+    float lm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < DX_B; i++) {
+        const int j = lane * DX_B + i;
+        w[i] = j < n ? src(j) : -INFINITY;   // the score, replaced by the weight below
+    }
+#pragma unroll
+    for (int i = 0; i < DX_B; i++) lm = fmaxf(lm, w[i]);
+    const float inc = wave_scan_max(lm);
+    float Mp = fmaxf(M, dpp_ninf<0x138, 0xF>(inc));   // wave_shr:1 -> the exclusive prefix (lane 0: -inf)
+    const float Mn = fmaxf(M, lane_f(inc, 63));
+    bool nm = false;
+#pragma unroll
+    for (int i = 0; i < DX_B; i++) {
+        const float s = w[i];
+        if (s > Mp) {   // new maximum: ms = expf(Mold - M) (0 before the first key), vs = 1
+            w[i] = -expf(Mp - s);
+            Mp = s;
+            nm = true;
+        } else {
+            w[i] = s != -INFINITY ? expf(s - Mp) : 0.0f;
+        }
+    }
+    // the lane's sequential S = S * ms + vs, (ms, vs) recovered from the signed
+    // weight (a second pass: the first keeps only w[] live)
+    float Sl = 0.0f, wl = 0.0f;
+#pragma unroll
+    for (int i = 0; i < DX_B; i++) {
+        const float x = w[i];
+        Sl = __builtin_signbit(x) ? fadd_rn(fmul_rn(Sl, -x), 1.0f) : fadd_rn(fmul_rn(Sl, 1.0f), x);
+        if (lane * DX_B + i == n - 1) wl = x;
+    }
+    const float S = wave_sum(Mp == -INFINITY ? 0.0f : Sl * expf(Mp - Mn));
+    flags = __ballot(nm || (lane + 1) * DX_B > n);   // (a batch with keys past n: the slow path, zero weights)
+    wlast = lane_f(wl, (n - 1) / DX_B);
+    M = Mn;
+    return S;
+}
+
+}  // namespace qasr

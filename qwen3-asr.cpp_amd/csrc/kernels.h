@@ -132,6 +132,7 @@ enum DevErr : unsigned {
     DEVERR_QKV_WAIT = 1u,    // attention split gave up on its kv group's QKV blocks
     DEVERR_O_WAIT = 2u,      // fused o-projection gave up on the attention combiners
     DEVERR_FFN_WAIT = 4u,    // fused down-projection gave up on the gate/up blocks
+    DEVERR_SCORE_WAIT = 8u,  // fused exact attention: the chain gave up on the splits' score granules
 };
 struct FuseCfg {
     int ffn = 1, qkv = 1, o = 1;        // fused launches on/off
@@ -145,8 +146,10 @@ struct FuseCfg {
     int gemm_regs = 0;                  // encoder/prefill GEMMs on the register-staged tiles (gemm.hip)
     int gran = 1;                       // batch 1: QKV -> attention hand-off by tagged granules (0 = arrival counters)
     int fa_exact_prefill = 1;           // prefill attention with ggml's CPU FA numerics (fa_exact.hip)
-    int fa_exact_decode = -1;           // decode attention likewise: 1 on, 0 off (fp32 V accumulation), -1 = on for
-                                        // Q8_0 models only (batch 1 exact skips the fused QKV + attention launch)
+    int fa_exact_decode = 1;            // decode attention likewise: 1 on (every model and batch; batch 1 f16 in the
+                                        // fused launch's chain role), 0 off (fp32 V accumulation, split-K)
+    int fx_delay = 0, fx_vpf = 1;       // batch-1 fused exact attention: chain first-poll delay (s_sleep(8) units),
+                                        // V^T pulled into L2 by the splits
     int slots_ffn = 0, slots_qkv64 = 0, slots_qkv128 = 0;   // co-resident workgroups on this device
     int att_stream = 1;                 // decode batches: one workgroup per (kv group, sequence) (decode_attn_seq_kernel)
     int skinny = 1;                     // decode batches: the weight-streaming skinny GEMMs (0 = tiled GEMMs)
@@ -275,6 +278,15 @@ struct DecodeAttnArgs {
                                          // kv group and sequence, taken once the batch fills them; 0 = split kernels)
     int spl_batch;                       // decode batches on the split kernels: 128- or 256-key splits (FuseCfg::att_spl)
     int kv_nt;                           // K/V cache loads nontemporal (FuseCfg::kv_nt)
+    // batch-1 fused launch with ggml's fp16-accumulating attention (fx = 1,
+    // needs gran): the splits publish their scaled scores as {fp32, tag}
+    // granules in sgran [n_head][max_ctx]; one chain workgroup per kv group
+    // runs fx_chain.h's chain for both query heads and hands the output to the
+    // o-projection role (att_done)
+    int fx;
+    unsigned long long *sgran;
+    int fx_delay;                        // chain workgroups: first score poll after fx_delay x ~0.2 us
+    int fx_vpf;                          // splits pull their keys' V^T rows into their XCD's L2 for the chain
 };
 // the decode attention with ggml's CPU flash-attention numerics (fa_exact.hip),
 // after launch_decode_attention in scores mode: per (query head, sequence) the

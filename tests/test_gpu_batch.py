@@ -127,7 +127,8 @@ def test_decode_kv_nt_bit_identical_and_attention_kernels_agree(B, gpu, tiny_ggu
     bytes: bit-identical decode-step logits with it off.  At B = 48 also the
     split-K batch attention (att_stream = 0) against the per-sequence kernel:
     different merge order, so equal within the oracle tolerance, and both
-    against the oracle."""
+    against the oracle.  Both are the fp32-accumulating attention (option
+    fa_exact_decode = 0), so the oracle runs its QO_FA_V_F32 switch."""
     m = qasr.Model(tiny_gguf)
     rng = np.random.default_rng(9)
     ids = [int(t) for t in rng.integers(0, 151643, 300)]
@@ -140,6 +141,7 @@ def test_decode_kv_nt_bit_identical_and_attention_kernels_agree(B, gpu, tiny_ggu
             c = qasr.Context(m, max_batch=B, max_ctx=320)
             c.set_option("kv_nt", cfg[0])
             c.set_option("att_stream", cfg[1])
+            c.set_option("fa_exact_decode", 0)
             try:
                 c.prefill([ids] * B, want_logits=False)
                 runs[cfg] = [c.decode_step([t] * B, [len(ids) + s] * B)[0].copy() for s, t in enumerate(toks)]
@@ -149,7 +151,7 @@ def test_decode_kv_nt_bit_identical_and_attention_kernels_agree(B, gpu, tiny_ggu
         m.close()
     for a, b in zip(runs[(1, 1)], runs[(0, 1)]):
         assert np.array_equal(a, b)
-    dec = op.OracleDecoder(tiny_oracle, 320)
+    dec = op.OracleDecoder(tiny_oracle, 320, op.OracleModel.FA_V_F32)
     dec.forward(ids, 0)
     for s, t in enumerate(toks):
         ref = dec.forward([t], len(ids) + s)
