@@ -12,8 +12,10 @@
  *           GGUFLoader::load              src/gguf_loader.cpp:17-53)
  *   qasr_ctx_create / qasr_ctx_free
  *       <- TextDecoder::init_kv_cache     src/text_decoder.cpp:337-386
- *   qasr_mel
+ *   qasr_mel, qasr_mel_engine_run
  *       <- log_mel_spectrogram            src/mel_spectrogram.h:53-55 / .cpp:484-628
+ *   qasr_mel_filters
+ *       <- generate_mel_filters           src/mel_spectrogram.h:42-43 / .cpp:352-395
  *   qasr_encode, qasr_encode_conv
  *       <- AudioEncoder::encode           src/audio_encoder.h:27 / .cpp:312-601
  *          AudioEncoder::encode_conv_only src/audio_encoder.h:30
@@ -130,6 +132,19 @@ int qasr_prefill(qasr_ctx *c, const int32_t *ids, const int *P, const float *fea
 /* One decode step for B sequences at positions n_past[b] (token tok[b]). */
 int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_past, int B,
                      float *logits, int32_t *argmax);
+
+/* ---- standalone log-mel (no model) ----------------------------------------- */
+/* log_mel_spectrogram of src/mel_spectrogram.h:53-55 without a model: an
+ * engine keeps the DFT / window tables and a filterbank on one device and runs
+ * the context's mel kernels.  filters: [128][201] (NULL: the built-in
+ * generate_mel_filters values); mel_out: [128][qasr_mel_frames(n)].  One
+ * engine per host thread. */
+typedef struct qasr_mel_engine qasr_mel_engine;
+int qasr_mel_engine_create(int device, qasr_mel_engine **out);
+void qasr_mel_engine_free(qasr_mel_engine *e);
+int qasr_mel_engine_run(qasr_mel_engine *e, const float *pcm, int n, const float *filters, float *mel_out);
+/* host: generate_mel_filters(128, 400, 16000) (src/mel_spectrogram.cpp:352-395) -> out[128][201] */
+int qasr_mel_filters(float *out);
 
 /* ---- whole path ----------------------------------------------------------- */
 /* Stage PCM into device HBM (one H2D copy); qasr_run then works from HBM.

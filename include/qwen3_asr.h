@@ -10,27 +10,13 @@
 #include <string>
 #include <vector>
 
+#include "audio_encoder.h"
+#include "audio_injection.h"
+#include "mel_spectrogram.h"
 #include "qasr_capi.h"
+#include "text_decoder.h"
 
 namespace qwen3_asr {
-
-// src/text_decoder.h:15-31
-struct text_decoder_config {
-    int32_t vocab_size = 151936;
-    int32_t hidden_size = 1024;
-    int32_t n_decoder_layers = 28;
-    int32_t n_attention_heads = 16;
-    int32_t n_key_value_heads = 8;
-    int32_t intermediate_size = 3072;
-    int32_t head_dim = 128;
-    float rms_norm_eps = 1e-6f;
-    float rope_theta = 1000000.0f;
-    int32_t pad_token_id = 151643;
-    int32_t eos_token_id = 151645;
-    int32_t audio_start_token_id = 151669;
-    int32_t audio_end_token_id = 151670;
-    int32_t audio_pad_token_id = 151676;
-};
 
 // src/qwen3_asr.h:15-34
 struct transcribe_params {

@@ -1525,6 +1525,105 @@ extern "C" int qasr_mel(qasr_ctx *c, const float *const *pcm, const int *n, int 
     return 0;
 }
 
+// ---------------------------------------------------- standalone log-mel
+// log_mel_spectrogram of the component API (include/mel_spectrogram.h,
+// src/mel_spectrogram.h:53-55) takes no model: an engine holds the DFT /
+// window tables and a filterbank on one device and runs the same mel kernels
+// as a context (launch_mel, csrc/mel.hip).
+struct qasr_mel_engine {
+    int device = 0;
+    hipStream_t st = nullptr;
+    double2 *tw = nullptr;
+    double *hann = nullptr;
+    float *filt = nullptr;        // [128][201], the last filterbank run with
+    std::vector<float> filt_host; // ... its host copy (re-uploaded when a call brings other values)
+    float *pcm = nullptr, *out = nullptr;
+    double *tmp = nullptr;
+    unsigned long long *cmax = nullptr;
+    MelClip *clip = nullptr;
+    int2 *blocks = nullptr;
+    size_t pcm_cap = 0, out_cap = 0, tmp_cap = 0, blk_cap = 0;
+    ~qasr_mel_engine() {
+        (void)hipSetDevice(device);
+        for (void *p : {(void *)tw, (void *)hann, (void *)filt, (void *)pcm, (void *)out, (void *)tmp, (void *)cmax, (void *)clip,
+                        (void *)blocks})
+            if (p) (void)hipFree(p);
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+
+static int grow(void **p, size_t &cap, size_t bytes) {
+    if (bytes <= cap && *p) return 0;
+    if (*p) HIPCHK(hipFree(*p));
+    *p = nullptr;
+    cap = std::max<size_t>(bytes + bytes / 4, 4096);
+    HIPCHK(hipMalloc(p, cap));
+    return 0;
+}
+
+extern "C" int qasr_mel_filters(float *out) {
+    if (!out) return fail(QASR_ERR_ARG, "bad arguments");
+    std::vector<float> f;
+    mel_filters(f);
+    memcpy(out, f.data(), f.size() * 4);
+    return 0;
+}
+
+extern "C" int qasr_mel_engine_create(int device, qasr_mel_engine **out) {
+    if (!out) return fail(QASR_ERR_ARG, "bad arguments");
+    *out = nullptr;
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return fail(QASR_ERR_DEVICE, "no such HIP device");
+    std::unique_ptr<qasr_mel_engine> e(new qasr_mel_engine());
+    e->device = device;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
+    std::vector<double> tw, hn;
+    dft_twiddles(tw);
+    hann_window(hn);
+    mel_filters(e->filt_host);
+    HIPCHK(hipMalloc((void **)&e->tw, tw.size() * 8));
+    HIPCHK(hipMalloc((void **)&e->hann, hn.size() * 8));
+    HIPCHK(hipMalloc((void **)&e->filt, e->filt_host.size() * 4));
+    HIPCHK(hipMalloc((void **)&e->cmax, 8));
+    HIPCHK(hipMalloc((void **)&e->clip, sizeof(MelClip)));
+    HIPCHK(hipMemcpy(e->tw, tw.data(), tw.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->hann, hn.data(), hn.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->filt, e->filt_host.data(), e->filt_host.size() * 4, hipMemcpyHostToDevice));
+    *out = e.release();
+    return 0;
+}
+
+extern "C" void qasr_mel_engine_free(qasr_mel_engine *e) { delete e; }
+
+extern "C" int qasr_mel_engine_run(qasr_mel_engine *e, const float *pcm, int n, const float *filters, float *mel_out) {
+    if (!e || n < 0 || (n > 0 && !pcm) || (mel_frames(n) > 0 && !mel_out)) return fail(QASR_ERR_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(e->device));
+    const int TF = n / 160 + 1, T = TF - 1;
+    if (filters && memcmp(filters, e->filt_host.data(), e->filt_host.size() * 4) != 0) {
+        memcpy(e->filt_host.data(), filters, e->filt_host.size() * 4);
+        HIPCHK(hipMemcpyAsync(e->filt, e->filt_host.data(), e->filt_host.size() * 4, hipMemcpyHostToDevice, e->st));
+    }
+    std::vector<int2> blocks;
+    for (int f = 0; f < TF; f += mel_frames_per_block()) blocks.push_back(make_int2(0, f));
+    const MelClip clip{0, n, TF, 0, 0};
+    int rc;
+    if ((rc = grow((void **)&e->pcm, e->pcm_cap, std::max<size_t>((size_t)n, 1) * 4)) ||
+        (rc = grow((void **)&e->tmp, e->tmp_cap, (size_t)128 * TF * 8)) ||
+        (rc = grow((void **)&e->out, e->out_cap, std::max<size_t>((size_t)128 * T, 1) * 4)) ||
+        (rc = grow((void **)&e->blocks, e->blk_cap, blocks.size() * sizeof(int2))))
+        return rc;
+    if (n) HIPCHK(hipMemcpyAsync(e->pcm, pcm, (size_t)n * 4, hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipMemcpyAsync(e->clip, &clip, sizeof clip, hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipMemcpyAsync(e->blocks, blocks.data(), blocks.size() * sizeof(int2), hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipMemsetAsync(e->cmax, 0, 8, e->st));
+    launch_mel(e->pcm, e->clip, 1, e->blocks, (int)blocks.size(), e->tw, e->hann, e->filt, e->tmp, e->cmax, e->out, e->st);
+    HIPCHK(hipGetLastError());
+    if (T > 0) HIPCHK(hipMemcpyAsync(mel_out, e->out, (size_t)128 * T * 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));   // (the host vectors above go out of scope)
+    return 0;
+}
+
 static int encode_common(qasr_ctx *c, const float *mel, const int *T, int B, float *outp, bool conv_only) {
     if (!c || !mel || !T || B <= 0 || !outp) return fail(QASR_ERR_ARG, "bad arguments");
     HIPCHK(hipSetDevice(c->m->device));

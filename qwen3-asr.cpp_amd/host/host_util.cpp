@@ -104,8 +104,8 @@ Hparams read_hparams(const GGUFFile &f) {
 static float hz_to_mel(float hz) { return 2595.0f * log10f(1.0f + hz / 700.0f); }
 static float mel_to_hz(float mel) { return 700.0f * (powf(10.0f, mel / 2595.0f) - 1.0f); }
 
-void mel_filters(std::vector<float> &f) {
-    const int n_mels = 128, n_fft = 400, sr = 16000, nb = 201;
+void mel_filters(std::vector<float> &f, int n_mels, int n_fft, int sr) {
+    const int nb = 1 + n_fft / 2;
     f.assign((size_t)n_mels * nb, 0.0f);
     const float mel_min = hz_to_mel(0.0f), mel_max = hz_to_mel(sr / 2.0f);
     std::vector<float> hz(n_mels + 2), bins(n_mels + 2);

@@ -34,7 +34,7 @@ Hparams read_hparams(const GGUFFile &f);
 
 // ---- precomputed tables (computed on the host exactly as the reference) ----
 // src/mel_spectrogram.cpp:361-415
-void mel_filters(std::vector<float> &f /*[128][201]*/);
+void mel_filters(std::vector<float> &f /*[n_mels][1 + n_fft/2]*/, int n_mels = 128, int n_fft = 400, int sr = 16000);
 // src/audio_encoder.cpp:12-22 (positions 0..n_ctx-1)
 void sinusoidal_pe(std::vector<float> &pe, int n_ctx, int d_model);
 // ggml_table_gelu_f16 (ggml tanh-GELU fp16 table)

@@ -50,6 +50,17 @@ def tiny_gguf(built, tmp_path_factory):
 
 
 @pytest.fixture(scope="session")
+def full_f16_gguf(built, tmp_path_factory):
+    """the Qwen3-ASR-0.6B-shaped synthetic f16 GGUF (seed 42), or $QASR_MODEL"""
+    import qasr
+    if os.environ.get("QASR_MODEL"):
+        return os.environ["QASR_MODEL"]
+    p = str(tmp_path_factory.mktemp("full") / "full-f16.gguf")
+    qasr.write_synthetic_gguf(p, "full", 42, 1)
+    return p
+
+
+@pytest.fixture(scope="session")
 def tiny_oracle(tiny_gguf):
     import oracle_py as op
     op.set_threads(min(8, os.cpu_count() or 1))

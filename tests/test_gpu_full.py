@@ -25,10 +25,8 @@ def _err(g, o):
 
 
 @pytest.fixture(scope="module")
-def full(gpu, tmp_path_factory):
-    p = os.environ.get("QASR_MODEL") or str(tmp_path_factory.mktemp("full") / "full-f16.gguf")
-    if not os.environ.get("QASR_MODEL"):
-        qasr.write_synthetic_gguf(p, "full", 42, 1)
+def full(gpu, full_f16_gguf):
+    p = full_f16_gguf
     m = qasr.Model(p)
     c = qasr.Context(m, max_batch=4, max_ctx=1536)
     op.set_threads(min(16, os.cpu_count() or 1))
