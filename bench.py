@@ -429,8 +429,8 @@ def main():
                    "clip_seconds": args.seconds, "decode_tokens": ntok, "parallelism": f"dp{N} (utterance sharding)"},
         "decode_tokens_per_s": round(N * args.batch * ntok * args.steps / dt, 2),
         "decode_attention": ("fp16 V accumulation per key (ggml CPU flash-attention numerics" +
-                             ("; chain role of the fused QKV + attention + o-proj launch)" if args.batch == 1 and not args.q8
-                              else ")")) if exact else
+                             ("; chain role of the fused QKV + attention + o-proj launch)" if ctx.get_option("fused_exact")
+                              else "; separate scores + chain kernels)")) if exact else
                             "fp32 V accumulation (split-K)",
         "stage_ms_per_step_rank0": {k: round(v / args.steps, 3) for k, v in tm.items()},
     }

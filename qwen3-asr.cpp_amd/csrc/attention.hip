@@ -694,7 +694,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
             kk[t][s4] = kv_load(kc + (long)key * 128 + 32 * s4 + 8 * q4, a.kv_nt);
         }
     if (FUSED && a.fx) {   // exact attention: no V here; this split's keys' V^T rows -> this XCD's L2 for the chain
-        if (a.fx_vpf) {
+        if (a.fx_vpf & 1) {
             const uint16_t *vt = a.vt + ((long)b * a.n_kv_head + g) * 128 * vt_ctx(a.max_ctx) + (long)(k0 / 8) * 1024;
 #pragma unroll
             for (int i = 0; i < KPW; i++) vv[i] = *(const half8 *)(vt + (long)(i * 256 + tid) * 8);
@@ -825,11 +825,11 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
             if (tid < 2 * SPL) {
                 const int hh = tid / SPL, j = tid - hh * SPL;
                 if (k0 + j < k1)
-                    __hip_atomic_store(a.sgran + (long)(2 * g + hh) * a.max_ctx + k0 + j,
+                    __hip_atomic_store(a.sgran + (long)(2 * g + hh) * sgran_ld(a.max_ctx) + k0 + j,
                                        ((unsigned long long)tag << 32) | __float_as_uint(sc[hh][j]), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (a.fx_vpf)
+            if (a.fx_vpf & 1)
 #pragma unroll
                 for (int i = 0; i < KPW; i++) asm volatile("" ::"v"(vv[i]));   // (the V^T pull has landed)
             mark(3);
@@ -1283,36 +1283,42 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
     const int hh = wid >> 1, wu = __builtin_amdgcn_readfirstlane(wid & 1);
     const int d = 64 * wu + lane, loff = 8 * lane;
     const uint16_t *vt = a.vt + (long)g * 128 * vt_ctx(a.max_ctx) + 64 * wu * 8;   // batch 1: slot 0; the wave's key block 0
+    // dev trace (QASR_DEV_TRACE): rows 4000 + g of the attention kernel's table:
+    // [start, v ready, scores gathered, weights done, chain done, published]
+    // (v ready comes after the weights: the new v is polled last)
+    auto mark = [&](int slot) {
+        if (a.trace && tid == 0) a.trace[(4000L + g) * 8 + slot] = rt_now();
+    };
+    mark(0);
     const int pos = a.pos[0], nkv = pos + 1;
     const uint32_t tag = gran_tag(pos, a.layer);
     const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
-    // the new key's v (this lane's dimension): its QKV granule, cast to fp16 as the cache write is
-    uint16_t vnew = 0;
-    {
-        const unsigned long long *gp = a.gran + QD + KD + g * 128 + d;
-        unsigned long long v = 0;
-        bool ok = false;
-        for (int it = 0; it < a.poll_limit; it++) {
-            v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ok = (uint32_t)(v >> 32) == tag;
-            if (__all(ok)) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_QKV_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        vnew = f_to_u16(__uint_as_float((uint32_t)v));
+    // V^T of the wave's 64 dimensions -> this CU's L2 while the scores are
+    // computed: wave w pulls the key blocks kb = w / 2 (mod 2), so the four
+    // waves cover their two dimension halves once; LDS-DMA pieces (no
+    // register destination) into the wave's own 1 KiB of fsc, contents unused
+    // (the first gather poll below drains them: its vmcnt(0) and barrier).
+    // Without it the chain's V^T loads were HBM misses one 64-key buffer
+    // ahead: ~40 cycles a key instead of ~12 (device trace, layer 14).
+    if (a.fx_vpf & 2) {
+        typedef __attribute__((address_space(3))) void lds_void_c;
+        typedef __attribute__((address_space(1))) void glb_void_c;
+        lds_void_c *dst = (lds_void_c *)((float *)fsc + wid * 256);
+        for (int kb = hh; kb * 8 < nkv; kb += 2)
+            __builtin_amdgcn_global_load_lds((glb_void_c *)(vt + (long)kb * 1024 + loff), dst, 16, 0, 0);
     }
-    for (int i = 0; i < a.fx_delay; i++) __builtin_amdgcn_s_sleep(8);
     // one chunk: the launch is taken only while n_kv <= DX_KC (launch_qkv_attention1)
     const int n = nkv, np = (n + 1) >> 1;
     // (1) the score granules of both heads -> LDS: thread tid takes the 16-B
     //     pairs q = tid + 256 (u / 2) of head u % 2, all in flight together
     {
-        const unsigned long long *gb = a.sgran + (long)(2 * g) * a.max_ctx;   // uniform
+        const int ld = sgran_ld(a.max_ctx);
+        const unsigned long long *gb = a.sgran + (long)(2 * g) * ld;   // uniform
         uint32_t go[DX_KC / 256];
 #pragma unroll
         for (int u = 0; u < DX_KC / 256; u++) {
             const int q = tid + 256 * (u >> 1);
-            go[u] = q < np ? (uint32_t)(((u & 1) * a.max_ctx + 2 * q) * 8) : 0u;
+            go[u] = q < np ? (uint32_t)(((u & 1) * ld + 2 * q) * 8) : 0u;
         }
         u32x4 gv[DX_KC / 256];
         bool ok = false;
@@ -1336,35 +1342,107 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         }
     }
     __syncthreads();
-    // (2) the weights of this wave's head (both waves of a head compute the
-    //     same), written back over the scores; (3) the chain, weights from LDS
-    float M = -INFINITY, S;
+    mark(2);
+    // (2) the weights of this wave's head, fx_weights_reg's arithmetic split
+    //     over the head's two waves: both read the lane's 32 scores and take
+    //     the maxima (a lane's batch holds a new maximum iff its maximum beats
+    //     the exclusive prefix), wave wu computes the expf of keys 16 wu ..
+    //     16 wu + 15 of every lane and writes them back over the scores.  The
+    //     new key n - 1 gets weight 0 in LDS (a no-op for the chain loop, which
+    //     reads the cache row another workgroup is writing) and its weight in
+    //     fwl, applied once after the loop with vnew -- the same sequence of
+    //     operations as fa_exact.hip's chain, so both launches agree bit for bit
+    __shared__ float fwl[2];
+    float M, S;
     unsigned long long flags;
     {
-        float w[DX_B], wl;   // (wl: unused here)
         float *row = fsc[hh] + lane * FX_ST;   // this lane's 32 keys
-        S = fx_weights_reg([&](int j) { return row[j & 31]; }, n, M, w, flags, wl);
-        __syncthreads();   // every wave has read its scores
-        if ((wid & 1) == 0)
+        float sv[DX_B];
 #pragma unroll
-            for (int i = 0; i < DX_B; i += 4) *(floatx4 *)&row[i] = floatx4{w[i], w[i + 1], w[i + 2], w[i + 3]};
+        for (int i = 0; i < DX_B; i += 4) {
+            const floatx4 r = *(const floatx4 *)&row[i];
+#pragma unroll
+            for (int e = 0; e < 4; e++) sv[i + e] = lane * DX_B + i + e < n ? r[e] : -INFINITY;
+        }
+        float lm = -INFINITY, lh = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < DX_B / 2; i++) lh = fmaxf(lh, sv[i]);
+#pragma unroll
+        for (int i = DX_B / 2; i < DX_B; i++) lm = fmaxf(lm, sv[i]);
+        lm = fmaxf(lm, lh);
+        const float inc = wave_scan_max(lm);
+        const float Mp0 = dpp_ninf<0x138, 0xF>(inc);   // exclusive prefix (lane 0: -inf; the chunk is the first)
+        M = lane_f(inc, 63);
+        flags = __ballot(lm > Mp0);
+        float Mq = wu ? fmaxf(Mp0, lh) : Mp0;
+        float x[DX_B / 2];
+#pragma unroll
+        for (int i = 0; i < DX_B / 2; i++) {
+            const float sc = wu ? sv[DX_B / 2 + i] : sv[i];
+            const bool gt = sc > Mq;
+            const float e = expf(gt ? Mq - sc : sc - Mq);
+            x[i] = gt ? -e : (sc != -INFINITY ? e : 0.0f);
+            Mq = fmaxf(Mq, sc);
+        }
+        __syncthreads();   // both waves have read their scores
+#pragma unroll
+        for (int i = 0; i < DX_B / 2; i += 4) *(floatx4 *)&row[16 * wu + i] = floatx4{x[i], x[i + 1], x[i + 2], x[i + 3]};
+        const int kl = n - 1;
+        if (lane == (kl >> 5) && wu == ((kl >> 4) & 1)) {   // (its own store above: ordered)
+            fwl[hh] = row[kl & 31];
+            row[kl & 31] = 0.0f;
+        }
+        __syncthreads();
+        // the lane's sequential S = S * ms + vs over its 32 weights (key n - 1
+        // read as 0 is S * 1 + 0 = S: its own term, the lane's last, goes after)
+        const float wl = fwl[hh];
+        float Sl = 0.0f;
+#pragma unroll
+        for (int i = 0; i < DX_B; i += 4) {
+            const floatx4 r = *(const floatx4 *)&row[i];
+#pragma unroll
+            for (int e = 0; e < 4; e++) Sl = __builtin_signbit(r[e]) ? fadd_rn(fmul_rn(Sl, -r[e]), 1.0f) : fadd_rn(fmul_rn(Sl, 1.0f), r[e]);
+        }
+        if (lane == (kl >> 5)) Sl = __builtin_signbit(wl) ? fadd_rn(fmul_rn(Sl, -wl), 1.0f) : fadd_rn(fmul_rn(Sl, 1.0f), wl);
+        const float Ml = fmaxf(Mp0, lm);
+        S = wave_sum(Ml == -INFINITY ? 0.0f : Sl * expf(Ml - M));
     }
-    __syncthreads();
-    // the new key (n - 1) takes vnew: its batch on the slow path
-    flags |= 1ull << ((n - 1) / DX_B);
+    mark(3);
+    // the new key's v (this lane's dimension): its QKV granule, cast to fp16 as
+    // the cache write is (long published by now: polled after the weights)
+    uint16_t vnew = 0;
+    {
+        const unsigned long long *gp = a.gran + QD + KD + g * 128 + d;
+        unsigned long long v = 0;
+        bool ok = false;
+        for (int it = 0; it < a.poll_limit; it++) {
+            v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = (uint32_t)(v >> 32) == tag;
+            if (__all(ok)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_QKV_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        vnew = f_to_u16(__uint_as_float((uint32_t)v));
+    }
+    mark(1);
     f16 acc = 0;
     {
+        // keys 0 .. n - 2 from V^T (the loop may run into key n - 1 and past n:
+        // zero weights), then the new key
+        const int nl = n - 1;
         u32x4 va[DX_Q / 8], vb[DX_Q / 8];
         floatx4 wa, wb;
         fx_loadQ(va, vt, loff, 0);
         fx_w8(fsc[hh], 0, wa, wb);
-        for (int j0 = 0; j0 < n; j0 += 2 * DX_Q) {
+        for (int j0 = 0; j0 < nl; j0 += 2 * DX_Q) {
             fx_loadQ(vb, vt, loff, j0 + DX_Q);
-            fx_step1_lds(va, j0, n, fsc[hh], flags, acc, n - 1, vnew, wa, wb);
+            fx_step1_lds(va, j0, nl, fsc[hh], flags, acc, wa, wb);
             fx_loadQ(va, vt, loff, j0 + 2 * DX_Q);
-            fx_step1_lds(vb, j0 + DX_Q, n, fsc[hh], flags, acc, n - 1, vnew, wa, wb);
+            fx_step1_lds(vb, j0 + DX_Q, nl, fsc[hh], flags, acc, wa, wb);
         }
+        acc = fx_key_slow(acc, vnew, fwl[hh]);
     }
+    mark(4);
     // ggml: VKQ32 = fp32(VKQ16) * (1 / S); fp16 for the o-projection
     const float ov = (float)acc * (S == 0.0f ? 0.0f : 1.0f / S);
     const uint32_t h16 = f_to_u16(ov);
@@ -1383,6 +1461,7 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
     } else {
         *out = (uint16_t)h16;
     }
+    mark(5);
 }
 
 template <int SPL>
@@ -1507,7 +1586,7 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     // ones): fall back to separate launches for contexts that would not fit
     // (exact attention: n_kv_head chain workgroups too; they read the new v
     // from its granule, so the fused exact path needs the granule hand-off)
-    if (a.fx && (!a.gran || !a.sgran || a.max_ctx % 2 || ns * spl1 > DX_KC)) return 0;   // (one chain chunk)
+    if (a.fx && (!a.gran || !a.sgran || ns * spl1 > DX_KC)) return 0;   // (one chain chunk)
     const int nfx = a.fx ? a.n_kv_head : 0;
     const int slots = spl1 == 128 ? cfg.slots_qkv128 : cfg.slots_qkv64;
     const bool fit_o = 512 + ns * a.n_kv_head + nfx + 256 <= slots;

@@ -157,6 +157,9 @@ struct qasr_ctx {
     int probe_stride = 1;          // probe decode steps k with k % probe_stride == 0 (the others replay the whole-step
                                    // graph: the probed step's split graphs and eager group cost ~3 % of a step)
     bool probe_o_fused = false;    // the probed layer's o-projection runs inside the QKV launch
+    int last_fmode = 0, last_fx = 0;   // the last emitted decode step, layer 0: fused launch mode (0 separate, 1 QKV +
+                                       // attention, 2 + o-proj) and whether its attention was the chain role (options
+                                       // "fused_mode" / "fused_exact", read-only)
     double probe_ms = 0.0, probe_bytes = 0.0, probe_dev_ms = 0.0;
     long probe_dev_n = 0;
     unsigned long long *d_pstamp = nullptr;   // per decode step: [32 min-starts | 32 max-ends] of the probed launches
@@ -715,7 +718,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_qcnt, (size_t)hp.n_kv_head * 8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_attdone, (size_t)8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_gran, (size_t)(QD + 2 * KD) * 8)) ||
-        (rc = dev_alloc(c.get(), (void **)&c->d_sgran, (size_t)hp.n_head * max_ctx * 8)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_sgran, (size_t)hp.n_head * sgran_ld(max_ctx) * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_ffncnt, (size_t)hp.dec_layers * 512 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_err, 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_pstamp, (size_t)max_ctx * kStampRec * 8)) ||
@@ -729,7 +732,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     HIPCHK(hipMemset(c->d_qcnt, 0, (size_t)hp.n_kv_head * 8 * 16 * 4));
     HIPCHK(hipMemset(c->d_attdone, 0, (size_t)8 * 16 * 4));
     HIPCHK(hipMemset(c->d_gran, 0, (size_t)(QD + 2 * KD) * 8));
-    HIPCHK(hipMemset(c->d_sgran, 0, (size_t)hp.n_head * max_ctx * 8));
+    HIPCHK(hipMemset(c->d_sgran, 0, (size_t)hp.n_head * sgran_ld(max_ctx) * 8));
     HIPCHK(hipMemset(c->d_ffncnt, 0, (size_t)hp.dec_layers * 512 * 4));
     HIPCHK(hipMemset(c->d_done, 0, 4));
     HIPCHK(hipMemset(c->d_err, 0, 4));
@@ -785,6 +788,8 @@ extern "C" int qasr_ctx_get_option(const qasr_ctx *c, const char *name, int *val
     if (n == "probe_layer") { *value = c->probe_layer; return 0; }
     if (n == "probe_stride") { *value = c->probe_stride; return 0; }
     if (n == "slots_ffn") { *value = c->fuse.slots_ffn; return 0; }
+    if (n == "fused_mode") { *value = c->last_fmode; return 0; }
+    if (n == "fused_exact") { *value = c->last_fx; return 0; }
     if (n == "slots_qkv") { *value = std::min(c->fuse.slots_qkv64, c->fuse.slots_qkv128); return 0; }
     for (const auto &o : fuse_options())
         if (n == o.name) { *value = c->fuse.*(o.field); return 0; }
@@ -1111,7 +1116,7 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
     if ((rc = prefill_layers(c, ids, P, d_feats, audio_pos, N))) return rc;
     // granule tags repeat across runs at the same positions: back to zero (no valid tag)
     HIPCHK(hipMemsetAsync(c->d_gran, 0, (size_t)(c->m->hp.n_head + 2 * c->m->hp.n_kv_head) * 128 * 8, c->st));
-    HIPCHK(hipMemsetAsync(c->d_sgran, 0, (size_t)c->m->hp.n_head * c->max_ctx * 8, c->st));
+    HIPCHK(hipMemsetAsync(c->d_sgran, 0, (size_t)c->m->hp.n_head * sgran_ld(c->max_ctx) * 8, c->st));
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
     const int B = (int)P.size(), H = hp.hidden;
@@ -1249,6 +1254,10 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         const int fmode = fusable ? launch_qkv_attention1(q1, da, &o, c->fuse, s, true) : 0;
         const bool o_fused = fmode == 2;
         if (l == std::min(c->probe_layer, nl - 1)) c->probe_o_fused = o_fused;
+        if (l == 0) {
+            c->last_fmode = fmode;
+            c->last_fx = fmode && da.fx;
+        }
         if (ga) {
             if (l == nl - 1) c->qkv_in_gran = false;
             if (fmode) {
@@ -1687,7 +1696,7 @@ extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_pa
     HIPCHK(hipSetDevice(c->m->device));
     // a caller may repeat a position (same tag): no granule of an earlier call may match
     HIPCHK(hipMemsetAsync(c->d_gran, 0, (size_t)(c->m->hp.n_head + 2 * c->m->hp.n_kv_head) * 128 * 8, c->st));
-    HIPCHK(hipMemsetAsync(c->d_sgran, 0, (size_t)c->m->hp.n_head * c->max_ctx * 8, c->st));
+    HIPCHK(hipMemsetAsync(c->d_sgran, 0, (size_t)c->m->hp.n_head * sgran_ld(c->max_ctx) * 8, c->st));
     std::vector<int> pos(B), nkv(B);
     for (int b = 0; b < B; b++) {
         if (n_past[b] < 0 || n_past[b] + 1 > c->max_ctx) return fail(QASR_ERR_ARG, "Context length exceeded");

@@ -112,7 +112,11 @@ __device__ __forceinline__ void fx_step1(const u32x4 *v, int j0, int n, const fl
 // then v_cvt_f16_f32 (RNE).
 #define FX_ST 36   // LDS floats per 32-key row: the 64 rows' 16-B reads of fx_weights_reg hit distinct banks
 #define FX_MIX(VI, W, SEL) "v_fma_mix_f32 %0, " VI ", " W ", %1 op_sel:[" SEL ",0,0] op_sel_hi:[1,0,1]\n\t"
-#define FX_CVT "s_nop 0\n\tv_cvt_f16_f32 %1, %0\n\t"
+// (no wait state between the mix and the convert: the hardware interlocks the
+// dependency; tools/micro/chain_asm.hip: bit-identical, 13.1 cycles a key
+// against 17.1 with an s_nop 0 -- the padding hipcc adds in front of an asm
+// statement that reads a just-written VGPR)
+#define FX_CVT "v_cvt_f16_f32 %1, %0\n\t"
 __device__ __forceinline__ void fx8_fast(f16 &acc, const u32x4 v, const floatx4 wa, const floatx4 wb) {
     float t;
     asm volatile(FX_MIX("%2", "%6", "0") FX_CVT FX_MIX("%2", "%7", "1") FX_CVT FX_MIX("%3", "%8", "0") FX_CVT
@@ -125,33 +129,48 @@ __device__ __forceinline__ void fx8_fast(f16 &acc, const u32x4 v, const floatx4 
 }
 #undef FX_MIX
 #undef FX_CVT
-// the slow path of 8 keys (fx_key_slow each; key `last` (relative to the
-// group; -1: none) takes vnew)
-__device__ __forceinline__ void fx8_slow(f16 &acc, const u32x4 v, const floatx4 wa, const floatx4 wb, int last, uint16_t vnew) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const uint32_t d = v[i >> 1];
-        const uint16_t e = (i & 1) ? (uint16_t)(d >> 16) : (uint16_t)(d & 0xffffu);
-        acc = fx_key_slow(acc, i == last ? vnew : e, i < 4 ? wa[i] : wb[i - 4]);
-    }
-    asm volatile("" ::: "memory");
+// the slow path of 8 keys as one asm block too (fx_key_slow's arithmetic:
+// the sign of w selects ms = -w, vs = 1 or ms = 1, vs = w; the scale is
+// fp16(fp32(acc) * ms), exact where ms = 1), so the chain loop stays a few
+// hundred bytes of straight code per group -- with the slow path as compiler
+// code between the fast blocks the fused launch's chain ran 21 us instead of
+// 12 at 1.37k keys (device trace; instruction fetch over ~30 KB of loop)
+#define FX_SLOW1(VI, W, SEL)                                                   \
+    "v_cmp_gt_i32 vcc, 0, " W "\n\t"                                         \
+    "v_cndmask_b32_e64 %2, 1.0, -" W ", vcc\n\t"                              \
+    "v_cndmask_b32_e64 %3, " W ", 1.0, vcc\n\t"                               \
+    "v_cvt_f32_f16 %0, %1\n\t"                                                \
+    "v_mul_f32 %0, %0, %2\n\t"                                                \
+    "v_cvt_f16_f32 %1, %0\n\t"                                                \
+    "v_fma_mix_f32 %0, " VI ", %3, %1 op_sel:[" SEL ",0,0] op_sel_hi:[1,0,1]\n\t" \
+    "v_cvt_f16_f32 %1, %0\n\t"
+__device__ __forceinline__ void fx8_slow(f16 &acc, const u32x4 v, const floatx4 wa, const floatx4 wb) {
+    float t, ms, vs;
+    asm volatile(FX_SLOW1("%4", "%8", "0") FX_SLOW1("%4", "%9", "1") FX_SLOW1("%5", "%10", "0") FX_SLOW1("%5", "%11", "1")
+                 FX_SLOW1("%6", "%12", "0") FX_SLOW1("%6", "%13", "1") FX_SLOW1("%7", "%14", "0") FX_SLOW1("%7", "%15", "1")
+                 : "=&v"(t), "+v"(acc), "=&v"(ms), "=&v"(vs)
+                 : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(wa[0]), "v"(wa[1]), "v"(wa[2]), "v"(wa[3]), "v"(wb[0]),
+                   "v"(wb[1]), "v"(wb[2]), "v"(wb[3])
+                 : "vcc", "memory");
 }
+#undef FX_SLOW1
 __device__ __forceinline__ void fx_w8(const float *ws, int k, floatx4 &wa, floatx4 &wb) {   // weights of keys k .. k + 7
     const float *p = ws + (k >> 5) * FX_ST + (k & 31);
     wa = *(const floatx4 *)p;
     wb = *(const floatx4 *)(p + 4);
 }
-// keys [j0, min(j0 + DX_Q, n)) from registers v (8 keys per u32x4);
+// keys [j0, min(j0 + DX_Q, n)) in groups of 8 from registers v (8 keys per
+// u32x4; the last group may run past n: those keys carry zero weights);
 // wa / wb: the weights of keys j0 .. j0 + 7 on entry, of j0 + DX_Q .. on exit
 __device__ __forceinline__ void fx_step1_lds(const u32x4 *v, int j0, int n, const float *ws, unsigned long long flags, f16 &acc,
-                                             int last, uint16_t vnew, floatx4 &wa, floatx4 &wb) {
+                                             floatx4 &wa, floatx4 &wb) {
 #pragma unroll
     for (int g8 = 0; g8 < DX_Q / 8; g8++) {
         const int k = j0 + 8 * g8;
         if (k >= n) break;
         floatx4 na, nb;
         fx_w8(ws, k + 8, na, nb);   // (row padding / the next row: in bounds of the chunk's LDS image)
-        if ((flags >> (k / DX_B)) & 1ull) fx8_slow(acc, v[g8], wa, wb, last - k, vnew);
+        if ((flags >> (k / DX_B)) & 1ull) fx8_slow(acc, v[g8], wa, wb);
         else fx8_fast(acc, v[g8], wa, wb);
         wa = na;
         wb = nb;
@@ -185,17 +204,18 @@ __device__ __forceinline__ float fx_weights_reg(Src src, int n, float &M, float 
     const float inc = wave_scan_max(lm);
     float Mp = fmaxf(M, dpp_ninf<0x138, 0xF>(inc));   // wave_shr:1 -> the exclusive prefix (lane 0: -inf)
     const float Mn = fmaxf(M, lane_f(inc, 63));
+    // one expf per key, branch-free (lanes diverge on where the maxima fall):
+    // a new maximum gives ms = expf(Mold - M) (0 before the first key), stored
+    // negated (its vs = 1); any other key vs = expf(s - M)
     bool nm = false;
 #pragma unroll
     for (int i = 0; i < DX_B; i++) {
         const float s = w[i];
-        if (s > Mp) {   // new maximum: ms = expf(Mold - M) (0 before the first key), vs = 1
-            w[i] = -expf(Mp - s);
-            Mp = s;
-            nm = true;
-        } else {
-            w[i] = s != -INFINITY ? expf(s - Mp) : 0.0f;
-        }
+        const bool gt = s > Mp;
+        const float e = expf(gt ? Mp - s : s - Mp);
+        w[i] = gt ? -e : (s != -INFINITY ? e : 0.0f);
+        Mp = fmaxf(Mp, s);
+        nm = nm || gt;
     }
     // the lane's sequential S = S * ms + vs, (ms, vs) recovered from the signed
     // weight (a second pass: the first keeps only w[] live)

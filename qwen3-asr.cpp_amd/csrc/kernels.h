@@ -148,8 +148,8 @@ struct FuseCfg {
     int fa_exact_prefill = 1;           // prefill attention with ggml's CPU FA numerics (fa_exact.hip)
     int fa_exact_decode = 1;            // decode attention likewise: 1 on (every model and batch; batch 1 f16 in the
                                         // fused launch's chain role), 0 off (fp32 V accumulation, split-K)
-    int fx_delay = 0, fx_vpf = 1;       // batch-1 fused exact attention: chain first-poll delay (s_sleep(8) units),
-                                        // V^T pulled into L2 by the splits
+    int fx_delay = 0, fx_vpf = 2;       // batch-1 fused exact attention: chain first-poll delay (unused), V^T pulled
+                                        // into L2 ahead of the chain (DecodeAttnArgs.fx_vpf bits)
     int slots_ffn = 0, slots_qkv64 = 0, slots_qkv128 = 0;   // co-resident workgroups on this device
     int att_stream = 1;                 // decode batches: one workgroup per (kv group, sequence) (decode_attn_seq_kernel)
     int skinny = 1;                     // decode batches: the weight-streaming skinny GEMMs (0 = tiled GEMMs)
@@ -233,6 +233,8 @@ void launch_prefill_attention(const PrefillAttnArgs &a, hipStream_t s);
 // keys in order per query row, fp16 V accumulator rounded after every key
 void launch_prefill_attention_exact(const PrefillAttnArgs &a, hipStream_t s);
 
+// row stride (granules) of the fused exact attention's score granules
+__host__ __device__ inline int sgran_ld(int max_ctx) { return (max_ctx + 63) / 64 * 64; }
 // tag of a batch-1 hand-off granule {value, tag} (DecodeAttnArgs.gran): the
 // step's position and the layer.  Never 0, the value the granule buffers are
 // reset to before every call, so a granule not yet written this step can
@@ -284,9 +286,10 @@ struct DecodeAttnArgs {
     // runs fx_chain.h's chain for both query heads and hands the output to the
     // o-projection role (att_done)
     int fx;
-    unsigned long long *sgran;
+    unsigned long long *sgran;           // row stride sgran_ld(max_ctx) (16-B aligned granule pairs)
     int fx_delay;                        // chain workgroups: first score poll after fx_delay x ~0.2 us
-    int fx_vpf;                          // splits pull their keys' V^T rows into their XCD's L2 for the chain
+    int fx_vpf;                          // bit 0: the splits pull their keys' V^T rows into their XCD's L2 for the
+                                         // chain; bit 1: the chain workgroups pull their own (LDS-DMA, while waiting)
 };
 // the decode attention with ggml's CPU flash-attention numerics (fa_exact.hip),
 // after launch_decode_attention in scores mode: per (query head, sequence) the

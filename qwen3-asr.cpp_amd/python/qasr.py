@@ -16,7 +16,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libqasr.so")
+LIB_PATH = os.environ.get("QASR_LIB_OVERRIDE") or os.path.join(PKG_DIR, "libqasr.so")   # (override: diagnostic builds only)
 
 EXPORTS = [
     "qasr_last_error", "qasr_version", "qasr_device_count",

@@ -194,7 +194,7 @@ def test_full_decode_from_position_zero(full):
     must not match the zeroed buffers -- bit-identical to the separate launches
     and within the bar of the oracle"""
     m, _, om = full
-    c1 = qasr.Context(m, max_batch=1, max_ctx=256)
+    c1 = qasr.Context(m, max_batch=1, max_ctx=257)   # (odd: the score-granule rows are padded)
     try:
         out = {}
         for fused in (1, 0):
@@ -204,6 +204,7 @@ def test_full_decode_from_position_zero(full):
             for k, tok in enumerate([151644, 8948, 198]):
                 lg, _ = c1.decode_step([tok], [k])
                 lgs.append(lg[0].copy())
+                assert c1.get_option("fused_exact") == fused and c1.get_option("fused_mode") == 2 * fused
             out[fused] = lgs
     finally:
         c1.close()
@@ -325,6 +326,7 @@ def test_full_configs1_92s(full):
     errs = []
     for k in range(1, 16):
         lg, am = c.decode_step([toks[k - 1]], [len(ids) + k - 1])
+        assert c.get_option("fused_exact") == 1
         errs.append(_err(lg[0], lo[k]))
     print("configs[1] decode steps (abs, rel):", [(round(a_, 4), round(r_, 5)) for a_, r_ in errs])
     assert max(r_ for _, r_ in errs) <= 1e-2, errs

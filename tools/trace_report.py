@@ -9,6 +9,9 @@ NAMES = ["qkv_gemv", "attention", "oproj_gemv", "gateup_gemv", "down_gemv"]
 
 def main(path):
     t = np.fromfile(path, dtype=np.uint64).reshape(6, 4096, 8).astype(np.int64)
+    ch = t[1][4000:4016]
+    ch = ch[ch[:, 0] > 0]
+    t[1][4000:4016] = 0
     live = [t[k][t[k][:, 0] > 0] for k in range(5)]
     t0 = min(int(x[:, 0].min()) for x in live if len(x))
     us = lambda v: (v - t0) / 100.0
@@ -17,7 +20,14 @@ def main(path):
         if not len(x):
             continue
         st = x[:, 0]
-        if k == 1:
+        if k == 1 and len(ch):   # fused exact attention: split blocks (scores) + chain workgroups
+            print(f"{NAMES[k]:12s} split blocks {len(x):4d} start {us(st.min()):7.2f}..{us(st.max()):7.2f}  "
+                  f"scores published max {us(x[:, 3].max()):7.2f}")
+            lab = ["start", "v ready", "scores gathered", "weights", "chain", "published"]
+            print(f"{'':12s} chain wgs {len(ch)}: " + "  ".join(f"{lab[i]} {us(np.median(ch[:, i])):6.2f}/{us(ch[:, i].max()):6.2f}"
+                                                             for i in range(6)))
+            e = ch[:, 5].max()
+        elif k == 1:
             kv, rdy, cnt = x[:, 1], x[:, 2], x[:, 3]
             lastb = x[x[:, 4] > 0]
             print(f"{NAMES[k]:12s} blocks {len(x):4d} start {us(st.min()):7.2f}..{us(st.max()):7.2f}  "
