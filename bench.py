@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--q8", action="store_true", help="Q8_0 synthetic model (configs[2] weights)")
     ap.add_argument("--pipeline", choices=("asr", "align"), default="asr",
                     help="align: configs[4] transcribe + ForcedAligner on every clip (src/main.cpp:416-500)")
+    ap.add_argument("--queue", choices=("dynamic", "static"), default="dynamic",
+                    help="--utterances: a shared work queue feeding each GPU's continuous-batching stream (dynamic), "
+                         "or the static longest-first shards in fixed batches (static)")
     ap.add_argument("--utterances", type=int, default=0,
                     help="configs[3]/[4]: a fixed set of N seeded utterances of U[--utt-min, --utt-max] s sharded "
                          "longest-first over the ranks (strong scaling); a step = one pass over the set")
@@ -89,37 +92,49 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(model_path: str, secs: float, tok_rate: float, threads: int, full_secs: float, full_tok: int):
-    """Oracle (C restatement of the reference CPU path, ggml numerics) on a
-    bounded sample, at the reference's effective thread count (4: ggml's
+    """Oracle (C restatement of the reference CPU path, ggml numerics) timed
+    on configs[0]'s own workload -- one 30 s clip, its 105-token budget, no
+    extrapolation -- at the reference's effective thread count (4: ggml's
     default; mel single-threaded as the reference) and at
-    every core this process may use.  The configs[1] figure is extrapolated
-    per stage from the sample: mel / encoder / prefill x (full / sample
-    seconds), decode x (full / sample tokens)."""
+    every core this process may use (the GPU box's lease: OMP_NUM_THREADS),
+    plus the shorter `secs` sample with its per-stage extrapolation to the
+    bench's own clip (configs[1])."""
     import oracle_py as op
-    n = int(secs * 16000)
-    pcm = qasr.synth_pcm(1000, n)
-    ntok = int(math.ceil(tok_rate * secs))
     om = op.OracleModel(model_path)
     allc = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 10 ** 6))
-    runs = {}
-    for th in sorted({threads, allc}):
+
+    def timed(clip_s, th):
+        n = int(clip_s * 16000)
+        ntok = int(math.ceil(tok_rate * clip_s))
         op.set_threads(th)
         t0 = time.perf_counter()
-        _, t = om.transcribe(pcm, max_tokens=ntok, ignore_eos=True)
+        _, t = om.transcribe(qasr.synth_pcm(1000, n), max_tokens=ntok, ignore_eos=True)
         dt = time.perf_counter() - t0
+        return dt, t, ntok
+
+    c0 = {}   # configs[0]: 30 s, measured
+    for th in sorted({threads, allc}):
+        dt, t, ntok = timed(30.0, th)
+        c0[th] = {"rtfx": round(30.0 / dt, 4), "wall_s": round(dt, 3), "tokens": ntok,
+                  "stage_ms": {"mel": round(t[0], 1), "encode+prefill": round(t[1], 1), "decode": round(t[2], 1)}}
+    runs = {}   # the short sample, extrapolated per stage to the bench clip
+    for th in sorted({threads, allc}):
+        dt, t, ntok = timed(secs, th)
         est = (t[0] + t[1]) / 1e3 * (full_secs / secs) + t[2] / 1e3 * (full_tok / ntok)
         runs[th] = {"rtfx": round(secs / dt, 4), "wall_s": round(dt, 3),
                     "stage_ms": {"mel": round(t[0], 1), "encode+prefill": round(t[1], 1), "decode": round(t[2], 1)},
                     "est_configs1_rtfx": round(full_secs / est, 4)}
-    r4 = runs[threads]
+    r4 = c0[threads]
     return {
         "value": r4["rtfx"],
         "unit": "audio-sec/wall-sec (RTFx)",
         "cores": threads,
         "kind": "port",
-        "sample": f"one {secs:g} s synthetic clip, {ntok}-token greedy budget, full-size synthetic f16 model, "
-                  f"{threads} threads (ggml's default; mel single-thread fp64 DFT as the reference); "
-                  f"extrapolated to configs[1] ({full_secs:g} s, {full_tok} tokens): {r4['est_configs1_rtfx']} RTFx",
+        "sample": f"configs[0] measured at its own size: one 30 s synthetic clip, {r4['tokens']}-token greedy budget, "
+                  f"full-size synthetic f16 model, {threads} threads (ggml's default; mel single-thread fp64 DFT as the "
+                  f"reference); at all {allc} leased cores {c0[allc]['rtfx']} RTFx.  The {secs:g} s sample extrapolated "
+                  f"to the bench clip ({full_secs:g} s, {full_tok} tokens): {runs[threads]['est_configs1_rtfx']} RTFx",
+        "configs0_by_threads": c0,
         "runs_by_threads": runs,
         "all_cores": allc,
         "nproc": os.cpu_count(),
@@ -251,7 +266,9 @@ def utterance_main(args, m, rank, local, world, dist, model_path):
     utts = qd.utterance_set(args.utterances, args.utt_seed, args.utt_min, args.utt_max)
     lengths = [n for _, n in utts]
     batch = args.batch if args.batch > 1 else 64
-    shard = qd.shard_longest_first(lengths, world)[rank]
+    dynamic = args.queue == "dynamic"
+    # dynamic: any rank may take any utterance, so every rank stages them all
+    shard = list(range(len(utts))) if dynamic else qd.shard_longest_first(lengths, world)[rank]
     nmax = max(lengths)
     P = qasr.lib().qasr_prompt_len(qasr.encoder_frames(qasr.mel_frames(nmax)))
     ctx = qasr.Context(m, max_batch=batch, max_ctx=P + qd.budget(nmax, args.tok_rate) + 8)
@@ -263,8 +280,28 @@ def utterance_main(args, m, rank, local, world, dist, model_path):
     def transcribe(idx, max_tokens):
         return ctx.run_staged([pos[i] for i in idx], max_tokens, ignore_eos=True).tokens
 
+    stream_stats = []
+
+    def stream(next_clip):   # staged index = utterance index (all staged, in order)
+        out, st = ctx.run_stream_staged(next_clip, max(qd.budget(n, args.tok_rate) for n in lengths), ignore_eos=True)
+        bad = [i for i, t in out.items() if isinstance(t, Exception)]
+        assert not bad, (bad[:4], out[bad[0]] if bad else None)
+        stream_stats.append(st)
+        return out
+
+    passes = [0]
+
+    def one_pass(after):
+        passes[0] += 1
+        if dynamic:
+            return qd.run_queue(stream, utts, rank, world, args.tok_rate, dist, f"cuda:{local}" if dist else None,
+                                key=f"utt_queue_{passes[0]}", after=after)
+        return qd.run_shard(transcribe, utts, rank, world, batch, args.tok_rate, dist, f"cuda:{local}" if dist else None,
+                            after)
+
     after = None
     actx = None
+    aligned = set()
     if args.pipeline == "align":   # configs[4]: ForcedAligner on every transcript (src/main.cpp:416-500)
         am = qasr.Model(os.environ.get("QASR_ALIGNER_MODEL") or synthetic_model(rank, "aligner", 8 if args.q8 else 1), local)
         # prompt: audio pads + per word its BPE ids and two timestamps (ForcedAligner::tokenize_with_timestamps)
@@ -272,13 +309,15 @@ def utterance_main(args, m, rank, local, world, dist, model_path):
 
         def after(idx, toks):
             for i, t in zip(idx, toks):
-                actx.align_json(pcm[i], m.detokenize(t))
+                doc, _ = actx.align_json(pcm[i], m.detokenize(t))
+                assert isinstance(doc, dict), i
+                aligned.add(i)
     for _ in range(args.warmup):
-        qd.run_shard(transcribe, utts, rank, world, batch, args.tok_rate, dist, f"cuda:{local}" if dist else None, after)
+        one_pass(after)
     wall, res = 0.0, None
+    stream_stats.clear()
     for _ in range(args.steps):
-        res = qd.run_shard(transcribe, utts, rank, world, batch, args.tok_rate, dist, f"cuda:{local}" if dist else None,
-                           after)
+        res = one_pass(after)
         wall += res["wall_s"]
     if rank != 0:
         return
@@ -303,13 +342,28 @@ def utterance_main(args, m, rank, local, world, dist, model_path):
                 + (", ForcedAligner-0.6B-shaped aligner GGUF)" if actx else ")"),
         "config": {"workload": f"{'configs[4]' if actx else 'configs[3]'}: {len(utts)} utterances of "
                                f"U[{args.utt_min:g}, {args.utt_max:g}] s (seed {args.utt_seed}, {res['audio_s']:.0f} s of "
-                               f"audio) sharded longest-first over {world} GPU(s), batches of {batch} per GPU, "
-                               f"greedy budget ceil(3.5 tok/s x duration), EOS ignored",
-                   "utterances": len(utts), "batch_per_gpu": batch, "parallelism": f"dp{world} (utterance sharding)",
-                   "collectives": "barrier + max wall time + one all_gather of token ids (RCCL), none on the data path"},
+                               f"audio) over {world} GPU(s), "
+                               + (f"a shared longest-first queue feeding {batch} continuous-batching slots per GPU"
+                                  if dynamic else f"sharded longest-first, batches of {batch} per GPU")
+                               + ", greedy budget ceil(3.5 tok/s x duration), EOS ignored",
+                   "utterances": len(utts), "batch_per_gpu": batch, "queue": args.queue,
+                   "parallelism": f"dp{world} (utterance data parallelism)",
+                   "collectives": "barrier + max wall time + one all_gather of token ids (RCCL), none on the data path"
+                                  + ("; the queue is a TCPStore counter (one add per utterance)" if dynamic and world > 1
+                                     else "")},
         "decode_tokens_per_s": round(res["decode_tokens"] * args.steps / wall, 2),
-        "batches_per_rank0_pass": res["batches"],
     }
+    if actx is not None:
+        out["aligned_rank0"] = len(aligned)
+    if dynamic:
+        ss = stream_stats
+        out["rank0_stream"] = {"clips": sum(x.n_clips for x in ss), "refill_prefills": sum(x.n_prefills for x in ss),
+                               "decode_steps": sum(x.n_steps for x in ss),
+                               "slot_utilisation": round(sum(x.live_steps for x in ss) / max(1, sum(x.slot_steps for x in ss)), 4),
+                               "prefill_ms": round(sum(x.t_prefill_ms for x in ss), 1),
+                               "decode_ms": round(sum(x.t_decode_ms for x in ss), 1)}
+    else:
+        out["batches_per_rank0_pass"] = res["batches"]
     print(json.dumps(out), flush=True)
 
 

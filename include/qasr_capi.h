@@ -168,6 +168,41 @@ int qasr_set_system_prompt(qasr_ctx *c, const int32_t *ids, int n);
 int qasr_transcribe_batch(qasr_ctx *c, const float *const *pcm, const int *n, int B, int max_tokens,
                           int ignore_eos, int32_t *tokens, int *n_tokens, qasr_timings *t);
 
+/* ---- continuous batching ---------------------------------------------------- */
+/* Greedy transcription of a queue of clips through `slots` KV-cache slots
+ * (1..max_batch; 0 = max_batch) decoding as one batch: a slot whose clip ends (EOS unless ignore_eos, or its token
+ * budget) is refilled from the queue at the next chunk boundary (<= 8 decode
+ * steps; 1 with a token callback), so a batch never waits for its longest
+ * member.  Clip results equal qasr_run's for the same clip.
+ *   fetch(user, &pcm, &n_samples, &max_tokens): the next clip -> its id
+ *       (>= 0), 16 kHz mono samples (read before fetch is called again) and
+ *       its budget (preset to the call's max_tokens); < 0: the queue is empty
+ *       (fetch is not called again).  A shared counter behind fetch makes a
+ *       dynamic work queue across contexts, threads or processes.
+ *   sink(user, id, status, tokens, n_tokens): once per fetched clip, in
+ *       completion order: status 0 with the tokens (trailing EOS popped, as
+ *       qasr_run), or a QASR_ERR_* code for that clip alone (no audio frames,
+ *       context length exceeded, bad arguments) with qasr_last_error() set
+ *       during the call; the run goes on with the other clips.
+ * The token callback (qasr_set_token_callback) receives the clip id as seq.
+ * Returns non-zero only for failures of the run itself (device errors). */
+typedef int (*qasr_fetch_fn)(void *user, const float **pcm, int *n_samples, int *max_tokens);
+typedef void (*qasr_sink_fn)(void *user, int id, int status, const int32_t *tokens, int n_tokens);
+typedef struct {
+    int32_t n_clips, n_errors, n_prefills;  /* clips delivered, clips rejected, refill prefills */
+    int64_t n_steps;                        /* decode steps (each over all the slots) */
+    int64_t slot_steps, live_steps;         /* slot-steps run, of which decoding a live clip */
+    double t_prefill_ms, t_decode_ms, t_total_ms;  /* host wall time: refills, decode chunks, call */
+} qasr_stream_stats;
+int qasr_run_stream(qasr_ctx *c, int slots, qasr_fetch_fn fetch, qasr_sink_fn sink, void *user, int max_tokens, int ignore_eos,
+                    qasr_stream_stats *stats);
+/* The same over the staged pool (qasr_stage_audio; inputs already in HBM):
+ * fetch(user, &max_tokens) returns the next staged clip's index, which is
+ * also its id for sink, or < 0 when the queue is empty. */
+typedef int (*qasr_fetch_staged_fn)(void *user, int *max_tokens);
+int qasr_run_stream_staged(qasr_ctx *c, int slots, qasr_fetch_staged_fn fetch, qasr_sink_fn sink, void *user,
+                           int max_tokens, int ignore_eos, qasr_stream_stats *stats);
+
 /* ---- per-context options (no reference counterpart: MI355X launch tuning) -- */
 /* Batch-1 decode runs two fused launches per layer whose roles wait on each
  * other in-launch.  Options, defaulted from the environment

@@ -62,18 +62,32 @@ public:
     // MI355X additions: device selection, batched transcription, and the
     // --profile report (src/timing.h sections, device time, of the last call)
     void set_device(int device) { device_ = device; }
+    // several clips: continuous batching over max_batch() KV-cache slots (a
+    // finished clip's slot is refilled at once); results in input order, each
+    // clip's success / error_msg its own
     std::vector<transcribe_result> transcribe_batch(const std::vector<std::vector<float>> &clips,
                                                     const transcribe_params &params = transcribe_params());
+    // a work queue: fetch(id, pcm) -> false when empty (called whenever a slot
+    // frees; a counter shared by several Qwen3ASR objects, one per device,
+    // balances them dynamically); sink(id, result) as each clip finishes.
+    // n_ctx: the context length (0: a 30 s clip's prompt + max_tokens);
+    // slots: 0 = max_batch().  false: the run itself failed (get_error()).
+    bool transcribe_stream(const std::function<bool(int &id, std::vector<float> &pcm)> &fetch,
+                           const std::function<void(int id, transcribe_result result)> &sink,
+                           const transcribe_params &params = transcribe_params(), int n_ctx = 0, int slots = 0);
+    void set_max_batch(int slots) { max_batch_ = slots > 0 ? slots : 1; }
+    int max_batch() const { return max_batch_; }
     void set_profile(bool on) { profile_ = on; }
     const std::string &profile_report() const { return profile_report_; }
 
 private:
     transcribe_result transcribe_internal(const float *samples, int n_samples, const transcribe_params &params);
     bool ensure_ctx(int batch, int n_ctx);
+    std::vector<transcribe_result> transcribe_run(const std::vector<std::vector<float>> &clips, const transcribe_params &params);
 
     qasr_model *model_ = nullptr;
     qasr_ctx *ctx_ = nullptr;
-    int ctx_batch_ = 0, ctx_len_ = 0, device_ = 0;
+    int ctx_batch_ = 0, ctx_len_ = 0, device_ = 0, max_batch_ = 16;
     text_decoder_config config_;
     std::string error_msg_;
     progress_callback_t progress_callback_;

@@ -1427,8 +1427,8 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
     mark(1);
     f16 acc = 0;
     {
-        // keys 0 .. n - 2 from V^T (the loop may run into key n - 1 and past n:
-        // zero weights), then the new key
+        // keys 0 .. n - 2 from V^T in 64-key steps (the last may run into key
+        // n - 1 and past n: zero weights in fsc), then the new key
         const int nl = n - 1;
         u32x4 va[DX_Q / 8], vb[DX_Q / 8];
         floatx4 wa, wb;
@@ -1436,9 +1436,10 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         fx_w8(fsc[hh], 0, wa, wb);
         for (int j0 = 0; j0 < nl; j0 += 2 * DX_Q) {
             fx_loadQ(vb, vt, loff, j0 + DX_Q);
-            fx_step1_lds(va, j0, nl, fsc[hh], flags, acc, wa, wb);
+            fx_step1_lds(va, j0, fsc[hh], flags, acc, wa, wb);
+            if (j0 + DX_Q >= nl) break;
             fx_loadQ(va, vt, loff, j0 + 2 * DX_Q);
-            fx_step1_lds(vb, j0 + DX_Q, nl, fsc[hh], flags, acc, wa, wb);
+            fx_step1_lds(vb, j0 + DX_Q, fsc[hh], flags, acc, wa, wb);
         }
         acc = fx_key_slow(acc, vnew, fwl[hh]);
     }

@@ -7,6 +7,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -100,7 +101,7 @@ struct qasr_ctx {
     float *rope = nullptr;
     std::vector<DevBuf> owned;     // everything hipMalloc'ed by the context
     // grow-on-demand scratch
-    DevBuf pcm, mel, meltmp, melmax, melclips, melblocks;
+    DevBuf pcm, spcm, mel, meltmp, melmax, melclips, melblocks;   // (spcm: qasr_run_stream's host clips)
     DevBuf chunks, rs1, rs2, rs3, pepos, act1, act2, act3;
     DevBuf ex, exh, eqkv, eatt, eff, feats, segs;
     DevBuf px, pxh, pqkv, pq, patt, pact, prow, plast, pids, pxl;
@@ -842,7 +843,7 @@ extern "C" int qasr_build_prompt(const qasr_model *m, int n_audio, int32_t *ids,
 // mel for B clips whose PCM is already in c->pcm (offsets/lengths given);
 // result in c->mel as B blocks [128][T_b].
 static int run_mel(qasr_ctx *c, const std::vector<long> &off, const std::vector<int> &n, std::vector<long> &mel_off,
-                   std::vector<int> &T) {
+                   std::vector<int> &T, const float *d_pcm = nullptr) {
     qasr_model *m = c->m;
     const int B = (int)n.size();
     std::vector<MelClip> clips(B);
@@ -866,7 +867,7 @@ static int run_mel(qasr_ctx *c, const std::vector<long> &off, const std::vector<
         (rc = ensure(c, c->melmax, B * 8)))
         return rc;
     HIPCHK(hipMemsetAsync(c->melmax.p, 0, B * 8, c->st));
-    launch_mel(c->pcm.as<float>(), c->melclips.as<MelClip>(), B, blocks.empty() ? nullptr : c->melblocks.as<int2>(),
+    launch_mel(d_pcm ? d_pcm : c->pcm.as<float>(), c->melclips.as<MelClip>(), B, blocks.empty() ? nullptr : c->melblocks.as<int2>(),
                (int)blocks.size(), m->tw, m->hann, m->filters, c->meltmp.as<double>(), c->melmax.as<unsigned long long>(),
                c->mel.as<float>(), c->st);
     HIPCHK(hipGetLastError());
@@ -1015,11 +1016,14 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
 // final hidden rows in c->px.  Row tables live in c->prow:
 // [row_seq | row_pos | row_audio] (3*rows ints) + [seq_row0 | seq_len | seq_slot].
 static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const std::vector<int> &P, const float *d_feats,
-                          const std::vector<int> &audio_pos, const std::vector<int> &N) {
+                          const std::vector<int> &audio_pos, const std::vector<int> &N, const std::vector<int> *slots) {
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
     const int B = (int)P.size(), H = hp.hidden, QD = hp.n_head * 128, KD = hp.n_kv_head * 128, F = hp.dec_ffn;
     if (B > c->max_batch) return fail(QASR_ERR_ARG, "batch exceeds context max_batch");
+    if (slots)
+        for (int v : *slots)
+            if (v < 0 || v >= c->max_batch) return fail(QASR_ERR_ARG, "KV-cache slot out of range");
     int rows = 0, maxp = 0;
     for (int b = 0; b < B; b++) {
         if (P[b] <= 0) return fail(QASR_ERR_ARG, "empty prompt");
@@ -1032,7 +1036,7 @@ static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const st
     for (int b = 0; b < B; b++) {
         const bool splice = d_feats && N[b] > 0 && audio_pos[b] >= 0 && audio_pos[b] + N[b] <= P[b];
         for (int t = 0; t < P[b]; t++, r++) {
-            tab[r] = b;
+            tab[r] = slots ? (*slots)[b] : b;   // the KV-cache slot the row writes
             tab[rows + r] = t;
             tab[2 * rows + r] = (splice && t >= audio_pos[b] && t < audio_pos[b] + N[b]) ? fr + (t - audio_pos[b]) : -1;
         }
@@ -1043,7 +1047,7 @@ static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const st
     for (int b = 0; b < B; b++) {   // seq_row0 | seq_len | seq_slot
         tab[3 * rows + b] = acc;
         tab[3 * rows + B + b] = P[b];
-        tab[3 * rows + 2 * B + b] = b;
+        tab[3 * rows + 2 * B + b] = slots ? (*slots)[b] : b;
         acc += P[b];
     }
     int rc;
@@ -1110,10 +1114,13 @@ static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const st
 
 // prefill (src/text_decoder.cpp:588-684): layers, then the LAST row of each
 // sequence -> RMSNorm -> tied LM head + argmax (:564-572)
+// slots: the KV-cache slot of each sequence (nullptr: sequence b -> slot b);
+// the decode state (d_tok / d_pos / d_nkv) is written for entries 0..B-1
 static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::vector<int> &P, const float *d_feats,
-                       const std::vector<int> &audio_pos, const std::vector<int> &N, bool want_logits) {
+                       const std::vector<int> &audio_pos, const std::vector<int> &N, bool want_logits,
+                       const std::vector<int> *slots = nullptr) {
     int rc;
-    if ((rc = prefill_layers(c, ids, P, d_feats, audio_pos, N))) return rc;
+    if ((rc = prefill_layers(c, ids, P, d_feats, audio_pos, N, slots))) return rc;
     // granule tags repeat across runs at the same positions: back to zero (no valid tag)
     HIPCHK(hipMemsetAsync(c->d_gran, 0, (size_t)(c->m->hp.n_head + 2 * c->m->hp.n_kv_head) * 128 * 8, c->st));
     HIPCHK(hipMemsetAsync(c->d_sgran, 0, (size_t)c->m->hp.n_head * sgran_ld(c->max_ctx) * 8, c->st));
@@ -1912,6 +1919,212 @@ extern "C" int qasr_run_staged(qasr_ctx *c, const int *clips, int B, int max_tok
     return rc;
 }
 
+// ------------------------------------------------------ continuous batching
+// qasr_run_stream: `slots` KV-cache slots (<= max_batch) decode together;
+// a slot whose clip ends (EOS, or its token budget) is refilled at the next
+// chunk boundary -- mel + encoder + prefill of the next clips from `fetch`
+// into exactly the freed slots (prefill_layers' slot map), the other slots'
+// caches untouched -- so a batch never idles on its longest member (the
+// reference decodes one utterance at a time, src/qwen3_asr.cpp:270-296; the
+// tokens of a clip depend only on its own rows).  Every chunk of <= 8 steps
+// (1 with a token callback) replays the step graphs of qasr_run, then the
+// host reads the chunk's tokens, delivers finished clips to `sink` and
+// re-uploads the slots' (token, position) state.  A slot with no clip is
+// parked at position 0 (its writes stay inside its own cache slot).
+namespace {
+struct StreamSlot {
+    int id = -1, P = 0, budget = 0;
+    std::vector<int32_t> toks;
+};
+}  // namespace
+
+// next(clip) -> false when the queue is empty; a clip is host samples (pcm, n)
+// or a clip of the staged pool (staged >= 0)
+struct StreamClip {
+    int id = -1, budget = 0, n = 0, staged = -1;
+    const float *pcm = nullptr;
+};
+static int run_stream(qasr_ctx *c, int slots, const std::function<bool(StreamClip &)> &next, qasr_sink_fn sink, void *user,
+                      int max_tokens, int ignore_eos, qasr_stream_stats *stats) {
+    if (!c || !sink || max_tokens <= 0 || slots < 0 || slots > c->max_batch) return fail(QASR_ERR_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(c->m->device));
+    const int S = slots ? slots : c->max_batch;
+    std::unique_lock<std::mutex> dev_lk;
+    if (takes_fused(c, S)) dev_lk = std::unique_lock<std::mutex>(device_lock(c->m->device));
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->pin_used = 0;
+    const Hparams &hp = c->m->hp;
+    hipStream_t s = c->st;
+    const auto t_start = std::chrono::steady_clock::now();
+    auto ms_since = [](std::chrono::steady_clock::time_point t0) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    };
+    qasr_stream_stats st{};
+    std::vector<StreamSlot> sl(S);
+    bool open = true;
+    int rc;
+    // a finished clip: trailing EOS popped (src/qwen3_asr.cpp:298-300)
+    auto deliver = [&](StreamSlot &x) {
+        std::vector<int32_t> &t = x.toks;
+        if (!ignore_eos && !t.empty() && t.back() == hp.eos_id) t.pop_back();
+        sink(user, x.id, 0, t.data(), (int)t.size());
+        st.n_clips++;
+        x.id = -1;
+        x.toks.clear();
+    };
+    auto reject = [&](int id, int code, const char *msg) {   // per-clip error: the message is qasr_last_error() inside sink
+        fail(code, msg);
+        sink(user, id, code, nullptr, 0);
+        st.n_errors++;
+    };
+    // fill free slots from the queue until every slot holds a live clip or the queue is empty
+    auto refill = [&]() -> int {
+        for (;;) {
+            std::vector<int> freeS;
+            for (int i = 0; i < S; i++)
+                if (sl[i].id < 0) freeS.push_back(i);
+            if (freeS.empty() || !open) return 0;
+            const auto t0 = std::chrono::steady_clock::now();
+            std::vector<int> ids, ns, budgets, slots;
+            std::vector<float> pcm;   // host clips of this refill, packed (-> c->spcm)
+            std::vector<long> off;
+            bool staged = false;
+            while (ids.size() < freeS.size()) {
+                StreamClip k;
+                k.budget = max_tokens;
+                if (!next(k)) { open = false; break; }
+                const int id = k.id;
+                if (k.staged >= 0) {
+                    if (k.staged >= (int)c->staged_n.size()) { reject(id, QASR_ERR_ARG, "staged clip index out of range"); continue; }
+                    k.n = c->staged_n[k.staged];
+                }
+                const int P = qasr_prompt_len(encoder_frames(mel_frames(std::max(k.n, 0)))) + (int)c->sys_ids.size();
+                if (k.n < 0 || (k.staged < 0 && k.n > 0 && !k.pcm) || k.budget <= 0) { reject(id, QASR_ERR_ARG, "bad clip (length, samples or budget)"); continue; }
+                if (encoder_frames(mel_frames(k.n)) <= 0) { reject(id, QASR_ERR_ARG, "No audio_pad token found in input sequence"); continue; }
+                if (P + k.budget > c->max_ctx) { reject(id, QASR_ERR_ARG, "Context length exceeded (prompt + max_tokens > max_ctx)"); continue; }
+                staged = k.staged >= 0;   // (one kind per run: the caller's API)
+                ids.push_back(id);
+                ns.push_back(k.n);
+                budgets.push_back(k.budget);
+                if (staged) {
+                    off.push_back(c->staged_off[k.staged]);
+                } else {
+                    off.push_back((long)pcm.size());
+                    pcm.insert(pcm.end(), k.pcm, k.pcm + k.n);
+                }
+                slots.push_back(freeS[ids.size() - 1]);
+            }
+            if (ids.empty()) return 0;
+            const int R = (int)ids.size();
+            if (!staged) {
+                if ((rc = ensure(c, c->spcm, std::max<size_t>(pcm.size(), 1) * 4))) return rc;
+                HIPCHK(hipMemcpyAsync(c->spcm.p, pcm.data(), pcm.size() * 4, hipMemcpyHostToDevice, s));
+            }
+            std::vector<long> mo;
+            std::vector<int> T, Nb;
+            if ((rc = run_mel(c, off, ns, mo, T, staged ? c->pcm.as<float>() : c->spcm.as<float>())) ||
+                (rc = run_encoder(c, c->mel.as<float>(), mo, T, false, Nb)))
+                return rc;
+            std::vector<int32_t> pids;
+            std::vector<int> P(R), ap(R);
+            for (int r = 0; r < R; r++) {
+                std::vector<int32_t> pr = build_prompt(hp, Nb[r], c->sys_ids, &ap[r]);
+                if (ap[r] < 0 || (int)pr.size() + budgets[r] > c->max_ctx) return fail(QASR_ERR_STATE, "prompt length differs from its estimate");
+                P[r] = (int)pr.size();
+                pids.insert(pids.end(), pr.begin(), pr.end());
+            }
+            if ((rc = run_prefill(c, pids, P, c->feats.as<float>(), ap, Nb, false, &slots))) return rc;
+            std::vector<int32_t> first(R);
+            HIPCHK(hipMemcpyAsync(first.data(), c->d_tok, R * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));   // (pcm host vector in flight until here)
+            if ((rc = check_dev_err(c))) return rc;
+            st.n_prefills++;
+            st.t_prefill_ms += ms_since(t0);
+            for (int r = 0; r < R; r++) {
+                StreamSlot &x = sl[slots[r]];
+                x.id = ids[r];
+                x.P = P[r];
+                x.budget = budgets[r];
+                x.toks.assign(1, first[r]);
+                if (c->tok_cb) c->tok_cb(c->tok_cb_user, x.id, 1, first[r]);
+                if ((!ignore_eos && first[r] == hp.eos_id) || x.budget == 1) deliver(x);
+            }
+        }
+    };
+    std::vector<int> pos(S), nkv(S), tok(S);
+    std::vector<int32_t> hist;
+    decode_graph(c, S, false, 0);
+    for (;;) {
+        if ((rc = refill())) return rc;
+        int live = 0, chunk = c->tok_cb ? 1 : 8, maxpos = 0;
+        for (int i = 0; i < S; i++) {
+            const StreamSlot &x = sl[i];
+            if (x.id < 0) { pos[i] = 0; nkv[i] = 1; tok[i] = 0; continue; }   // parked
+            live++;
+            pos[i] = x.P + (int)x.toks.size() - 1;   // the last token is fed at this position
+            nkv[i] = pos[i] + 1;
+            tok[i] = x.toks.back();
+            chunk = std::min(chunk, x.budget - (int)x.toks.size());
+            maxpos = std::max(maxpos, pos[i]);
+        }
+        if (live == 0) break;
+        HIPCHK(hipMemcpyAsync(c->d_pos, pos.data(), S * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->d_nkv, nkv.data(), S * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->d_tok, tok.data(), S * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemsetAsync(c->d_step, 0, 4, s));
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int k = 0; k < chunk; k++) {
+            const int splits = split_bucket(c, maxpos + k);
+            if (c->eager) {
+                decode_step_kernels(c, S, false, kWholeStep, splits);
+            } else {
+                qasr_ctx::StepGraphs *gs = nullptr;
+                if ((rc = step_graphs(c, splits, &gs))) return rc;
+                HIPCHK(hipGraphLaunch(gs->full, s));
+            }
+        }
+        hist.resize((size_t)S * chunk);
+        // (a decode step advances d_step, then writes hist[step]: the chunk's tokens are columns 1..chunk)
+        HIPCHK(hipMemcpy2DAsync(hist.data(), chunk * 4, c->d_hist + 1, (size_t)c->hist_cap * 4, chunk * 4, S, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));   // (the pos / nkv / tok host vectors in flight until here)
+        if ((rc = check_dev_err(c))) return rc;
+        st.t_decode_ms += ms_since(t0);
+        st.n_steps += chunk;
+        st.slot_steps += (int64_t)S * chunk;
+        for (int i = 0; i < S; i++) {
+            StreamSlot &x = sl[i];
+            if (x.id < 0) continue;
+            for (int k = 0; k < chunk; k++) {
+                const int32_t t = hist[(size_t)i * chunk + k];
+                x.toks.push_back(t);
+                st.live_steps++;
+                if (c->tok_cb) c->tok_cb(c->tok_cb_user, x.id, (int)x.toks.size(), t);
+                if ((!ignore_eos && t == hp.eos_id) || (int)x.toks.size() >= x.budget) {
+                    deliver(x);
+                    break;
+                }
+            }
+        }
+    }
+    st.t_total_ms = ms_since(t_start);
+    if (stats) *stats = st;
+    return 0;
+}
+
+extern "C" int qasr_run_stream(qasr_ctx *c, int slots, qasr_fetch_fn fetch, qasr_sink_fn sink, void *user, int max_tokens,
+                               int ignore_eos, qasr_stream_stats *stats) {
+    if (!fetch) return fail(QASR_ERR_ARG, "bad arguments");
+    return run_stream(c, slots, [&](StreamClip &k) { return (k.id = fetch(user, &k.pcm, &k.n, &k.budget)) >= 0; }, sink, user,
+                      max_tokens, ignore_eos, stats);
+}
+
+extern "C" int qasr_run_stream_staged(qasr_ctx *c, int slots, qasr_fetch_staged_fn fetch, qasr_sink_fn sink, void *user,
+                                      int max_tokens, int ignore_eos, qasr_stream_stats *stats) {
+    if (!fetch) return fail(QASR_ERR_ARG, "bad arguments");
+    return run_stream(c, slots, [&](StreamClip &k) { return (k.id = k.staged = fetch(user, &k.budget)) >= 0; }, sink, user,
+                      max_tokens, ignore_eos, stats);
+}
+
 extern "C" int qasr_set_token_callback(qasr_ctx *c, void (*cb)(void *user, int seq, int n_generated, int32_t token), void *user) {
     if (!c) return fail(QASR_ERR_ARG, "null context");
     c->tok_cb = cb;
@@ -2012,7 +2225,7 @@ static int align_classes(qasr_ctx *c, const float *pcm, int n, const std::vector
     if (P > c->max_ctx) return fail(QASR_ERR_ARG, "Context length exceeded (aligner prompt > max_ctx)");
     std::vector<int> rows;
     for (int i = 0; i < P; i++) if (ids[i] == hp.timestamp_id) rows.push_back(i);
-    if ((rc = prefill_layers(c, ids, {P}, c->feats.as<float>(), {1}, {Nb[0]}))) return rc;
+    if ((rc = prefill_layers(c, ids, {P}, c->feats.as<float>(), {1}, {Nb[0]}, nullptr))) return rc;
     const int NT = (int)rows.size(), H = hp.hidden;
     std::vector<unsigned long long> keys(NT);
     if (NT > 0) {

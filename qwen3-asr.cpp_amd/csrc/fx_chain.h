@@ -159,21 +159,34 @@ __device__ __forceinline__ void fx_w8(const float *ws, int k, floatx4 &wa, float
     wa = *(const floatx4 *)p;
     wb = *(const floatx4 *)(p + 4);
 }
-// keys [j0, min(j0 + DX_Q, n)) in groups of 8 from registers v (8 keys per
-// u32x4; the last group may run past n: those keys carry zero weights);
-// wa / wb: the weights of keys j0 .. j0 + 7 on entry, of j0 + DX_Q .. on exit
-__device__ __forceinline__ void fx_step1_lds(const u32x4 *v, int j0, int n, const float *ws, unsigned long long flags, f16 &acc,
+// keys [j0, j0 + DX_Q) from registers v (8 keys per u32x4); every weight past
+// the keys to take is 0 in ws (a no-op: fma(v, 0, acc) = acc).  wa / wb: the
+// weights of keys j0 .. j0 + 7 on entry, of j0 + DX_Q .. on exit.  One
+// decision per 64 keys: both 32-key batches fast (the common case: one
+// straight 1 KiB block, no branch inside), else all 64 keys on the slow path
+// -- exact for every key (ms = 1 leaves the accumulator unchanged), placed out
+// of line.  Branching per 8-key group cost ~2x in the fused launch (a taken
+// branch and an instruction fetch every 16 instructions; device trace).
+__device__ __forceinline__ void fx_step1_lds(const u32x4 *v, int j0, const float *ws, unsigned long long flags, f16 &acc,
                                              floatx4 &wa, floatx4 &wb) {
+    if (__builtin_expect(((flags >> (j0 / DX_B)) & 3ull) != 0, 0)) {
 #pragma unroll
-    for (int g8 = 0; g8 < DX_Q / 8; g8++) {
-        const int k = j0 + 8 * g8;
-        if (k >= n) break;
-        floatx4 na, nb;
-        fx_w8(ws, k + 8, na, nb);   // (row padding / the next row: in bounds of the chunk's LDS image)
-        if ((flags >> (k / DX_B)) & 1ull) fx8_slow(acc, v[g8], wa, wb);
-        else fx8_fast(acc, v[g8], wa, wb);
-        wa = na;
-        wb = nb;
+        for (int g8 = 0; g8 < DX_Q / 8; g8++) {
+            floatx4 na, nb;
+            fx_w8(ws, j0 + 8 * g8 + 8, na, nb);   // (row padding / the next row: in bounds of the chunk's LDS image)
+            fx8_slow(acc, v[g8], wa, wb);
+            wa = na;
+            wb = nb;
+        }
+    } else {
+#pragma unroll
+        for (int g8 = 0; g8 < DX_Q / 8; g8++) {
+            floatx4 na, nb;
+            fx_w8(ws, j0 + 8 * g8 + 8, na, nb);
+            fx8_fast(acc, v[g8], wa, wb);
+            wa = na;
+            wb = nb;
+        }
     }
 }
 

@@ -11,6 +11,7 @@
 #include <cctype>
 #include <chrono>
 #include <sys/stat.h>
+#include <mutex>
 #include <thread>
 #include <cstdio>
 #include <cstdlib>
@@ -48,7 +49,7 @@ static void usage(const char *prog) {
     fprintf(stderr, "  --device <n>           HIP device index (default: 0)\n");
     fprintf(stderr, "  --file-list <path>     Text file with one audio path per line (added to the -f files)\n");
     fprintf(stderr, "  --devices <i,j,...>    Shard the audio files over these HIP devices (one replica each)\n");
-    fprintf(stderr, "  --batch <n>            Clips per GPU batch with --devices / several files (default: 16)\n");
+    fprintf(stderr, "  --batch <n>            KV-cache slots per GPU (continuous batching) with --devices / several files (default: 16)\n");
     fprintf(stderr, "  --synthetic <cfg>      Write a synthetic GGUF (tiny|full|aligner|aligner-tiny) to --model and exit\n");
     fprintf(stderr, "\nForced Alignment:\n");
     fprintf(stderr, "  --align                Enable forced alignment mode\n");
@@ -288,9 +289,10 @@ static int run_transcribe_and_align(const cli_params &p) {
 }
 
 // --devices: one host thread per GPU, each with its own model replica and
-// context (the reference's objects are single-threaded; so are ours), the
-// files assigned longest-first by size, each GPU's share transcribed in
-// batches of --batch clips; output in input order
+// context (the reference's objects are single-threaded; so are ours), pulling
+// files from one shared queue (longest first) into its continuous-batching
+// stream of --batch slots: a device that finishes early takes the next file,
+// so the tail stays balanced whatever the decode lengths; output in input order
 static int run_transcription_sharded(const cli_params &p) {
     const size_t N = p.audio_paths.size();
     const int G = (int)p.devices.size();
@@ -302,45 +304,45 @@ static int run_transcription_sharded(const cli_params &p) {
     std::vector<size_t> order(N);
     for (size_t i = 0; i < N; i++) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return size[a] > size[b]; });
-    std::vector<std::vector<size_t>> shard(G);
-    std::vector<long long> load(G, 0);
-    for (size_t i : order) {   // longest processing time first
-        const int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-        shard[g].push_back(i);
-        load[g] += size[i];
-    }
-    fprintf(stderr, "qwen3-asr-cli (sharded)\n  Model: %s\n  Files: %zu over %d GPU(s), batches of %d\n\n", p.model_path.c_str(), N, G,
-            p.batch);
+    fprintf(stderr, "qwen3-asr-cli (sharded)\n  Model: %s\n  Files: %zu over %d GPU(s), %d slots each, shared queue\n\n",
+            p.model_path.c_str(), N, G, p.batch);
     std::vector<qwen3_asr::transcribe_result> results(N);
     std::vector<std::string> errors(G);
+    std::atomic<size_t> next{0};
     std::atomic<long long> samples{0};
+    std::mutex res_mu;
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
     for (int g = 0; g < G; g++) {
         th.emplace_back([&, g] {
             qwen3_asr::Qwen3ASR asr;
             asr.set_device(p.devices[g]);
+            asr.set_max_batch(p.batch);
             if (!asr.load_model(p.model_path)) { errors[g] = asr.get_error(); return; }
             qwen3_asr::transcribe_params tp;
             tp.max_tokens = p.max_tokens;
             tp.language = p.language;
             tp.print_timing = false;
-            for (size_t k = 0; k < shard[g].size(); k += p.batch) {
-                const size_t e = std::min(shard[g].size(), k + (size_t)p.batch);
-                std::vector<std::vector<float>> clips;
-                for (size_t j = k; j < e; j++) {
-                    std::vector<float> s;
+            auto fetch = [&](int &id, std::vector<float> &pcm) {
+                for (;;) {
+                    const size_t k = next++;
+                    if (k >= N) return false;
+                    const size_t i = order[k];
                     int sr = 0;
-                    if (!qwen3_asr::load_audio_file(p.audio_paths[shard[g][j]], s, sr) || sr != 16000) {
-                        errors[g] = "bad audio " + p.audio_paths[shard[g][j]];
-                        return;
+                    if (qwen3_asr::load_audio_file(p.audio_paths[i], pcm, sr) && sr == 16000) {
+                        samples += (long long)pcm.size();
+                        id = (int)i;
+                        return true;
                     }
-                    samples += (long long)s.size();
-                    clips.push_back(std::move(s));
+                    std::lock_guard<std::mutex> lk(res_mu);   // this file fails alone
+                    results[i].error_msg = "Failed to load audio file: " + p.audio_paths[i];
                 }
-                auto rs = asr.transcribe_batch(clips, tp);
-                for (size_t j = k; j < e; j++) results[shard[g][j]] = std::move(rs[j - k]);
-            }
+            };
+            auto sink = [&](int id, qwen3_asr::transcribe_result r) {
+                std::lock_guard<std::mutex> lk(res_mu);
+                results[id] = std::move(r);
+            };
+            if (!asr.transcribe_stream(fetch, sink, tp)) errors[g] = asr.get_error();
         });
     }
     for (auto &t : th) t.join();
@@ -383,6 +385,7 @@ static int run_transcription(const cli_params &p) {
             if (!qwen3_asr::load_audio_file(a, s, sr) || sr != 16000) { fprintf(stderr, "Error: bad audio %s\n", a.c_str()); return 1; }
             clips.push_back(std::move(s));
         }
+        asr.set_max_batch(p.batch);
         results = asr.transcribe_batch(clips, tp);
     }
     std::string all;

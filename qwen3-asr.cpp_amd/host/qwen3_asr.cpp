@@ -100,8 +100,10 @@ transcribe_result Qwen3ASR::transcribe(const float *samples, int n_samples, cons
     return transcribe_internal(samples, n_samples, params);
 }
 
-std::vector<transcribe_result> Qwen3ASR::transcribe_batch(const std::vector<std::vector<float>> &clips,
-                                                          const transcribe_params &params) {
+// one clip through qasr_run: the stage timings and --profile sections of the
+// reference's transcribe_internal (src/qwen3_asr.cpp:81-160)
+std::vector<transcribe_result> Qwen3ASR::transcribe_run(const std::vector<std::vector<float>> &clips,
+                                                        const transcribe_params &params) {
     const int B = (int)clips.size();
     std::vector<transcribe_result> out(B);
     if (!model_) { for (auto &r : out) r.error_msg = "Model not loaded"; return out; }
@@ -163,9 +165,93 @@ std::vector<transcribe_result> Qwen3ASR::transcribe_batch(const std::vector<std:
     return out;
 }
 
+// several clips: the continuous-batching stream (qasr_run_stream), up to
+// max_batch() slots; each clip succeeds or fails on its own, with the
+// reference's per-call error strings
+std::vector<transcribe_result> Qwen3ASR::transcribe_batch(const std::vector<std::vector<float>> &clips,
+                                                          const transcribe_params &params) {
+    if (clips.size() <= 1) return transcribe_run(clips, params);
+    if (!model_) return std::vector<transcribe_result>(clips.size(), [] { transcribe_result r; r.error_msg = "Model not loaded"; return r; }());
+    std::vector<transcribe_result> out(clips.size());
+    int maxP = 0;
+    for (const auto &c : clips) maxP = std::max(maxP, qasr_prompt_len(qasr_encoder_frames(qasr_mel_frames((int)c.size()))));
+    const int n_sys = params.system_prompt.empty() ? 0 : std::max(qasr_tokenize(model_, params.system_prompt.c_str(), nullptr, 0), 0);
+    size_t next = 0;
+    const bool ok = transcribe_stream(
+        [&](int &id, std::vector<float> &pcm) {
+            if (next >= clips.size()) return false;
+            id = (int)next;
+            pcm = clips[next++];
+            return true;
+        },
+        [&](int id, transcribe_result r) { out[id] = std::move(r); }, params, maxP + n_sys + params.max_tokens,
+        std::min((int)clips.size(), max_batch_));
+    if (!ok)
+        for (auto &r : out)
+            if (!r.success && r.error_msg.empty()) r.error_msg = error_msg_;
+    return out;
+}
+
+namespace {
+struct StreamCtx {
+    const std::function<bool(int &, std::vector<float> &)> *fetch;
+    const std::function<void(int, transcribe_result)> *sink;
+    qasr_model *model;
+    std::vector<float> pcm;
+    int64_t t0;
+};
+int stream_fetch(void *u, const float **pcm, int *n, int *) {
+    StreamCtx *s = (StreamCtx *)u;
+    int id = -1;
+    if (!(*s->fetch)(id, s->pcm) || id < 0) return -1;
+    *pcm = s->pcm.data();
+    *n = (int)s->pcm.size();
+    return id;
+}
+void stream_sink(void *u, int id, int status, const int32_t *toks, int n) {
+    StreamCtx *s = (StreamCtx *)u;
+    transcribe_result r;
+    if (status != 0) {
+        r.error_msg = std::string("Decoding failed: ") + qasr_last_error();
+    } else {
+        r.tokens.assign(toks, toks + n);
+        const int len = qasr_detokenize(s->model, toks, n, nullptr, 0);
+        std::string text(std::max(len, 0) + 1, '\0');
+        qasr_detokenize(s->model, toks, n, &text[0], (int)text.size());
+        text.resize(std::max(len, 0));
+        r.text = text;
+        r.success = true;
+        r.t_total_ms = now_ms() - s->t0;   // (completion time within the stream)
+    }
+    (*s->sink)(id, std::move(r));
+}
+}  // namespace
+
+bool Qwen3ASR::transcribe_stream(const std::function<bool(int &id, std::vector<float> &pcm)> &fetch,
+                                 const std::function<void(int id, transcribe_result result)> &sink,
+                                 const transcribe_params &params, int n_ctx, int slots) {
+    if (!model_) { error_msg_ = "Model not loaded"; return false; }
+    std::vector<int32_t> sys;
+    if (!params.system_prompt.empty()) {
+        const int k = qasr_tokenize(model_, params.system_prompt.c_str(), nullptr, 0);
+        sys.resize(std::max(k, 0));
+        qasr_tokenize(model_, params.system_prompt.c_str(), sys.data(), k);
+    }
+    // context length: n_ctx, or the prompt of a 30 s clip (the reference's
+    // chunking unit) plus the budget -- longer clips fail alone ("Context length")
+    const int need = n_ctx > 0 ? n_ctx : qasr_prompt_len(qasr_encoder_frames(qasr_mel_frames(30 * 16000))) + (int)sys.size() + params.max_tokens;
+    const int S = slots > 0 ? std::min(slots, max_batch_) : max_batch_;
+    if (!ensure_ctx(S, need)) return false;
+    qasr_set_system_prompt(ctx_, sys.data(), (int)sys.size());
+    StreamCtx sc{&fetch, &sink, model_, {}, now_ms()};
+    const int rc = qasr_run_stream(ctx_, S, stream_fetch, stream_sink, &sc, params.max_tokens, 0, nullptr);
+    if (rc != 0) { error_msg_ = std::string("Decoding failed: ") + qasr_last_error(); return false; }
+    return true;
+}
+
 transcribe_result Qwen3ASR::transcribe_internal(const float *samples, int n_samples, const transcribe_params &params) {
     std::vector<std::vector<float>> one(1, std::vector<float>(samples, samples + n_samples));
-    transcribe_result r = transcribe_batch(one, params)[0];
+    transcribe_result r = transcribe_run(one, params)[0];
     if (r.success && params.print_timing) {
         fprintf(stderr, "\nTiming:\n");
         fprintf(stderr, "  Mel spectrogram: %lld ms\n", (long long)r.t_mel_ms);

@@ -24,7 +24,7 @@ EXPORTS = [
     "qasr_ctx_create", "qasr_ctx_free",
     "qasr_mel_frames", "qasr_encoder_frames", "qasr_prompt_len", "qasr_build_prompt",
     "qasr_mel", "qasr_encode", "qasr_encode_conv", "qasr_prefill", "qasr_decode_step",
-    "qasr_stage_audio", "qasr_run", "qasr_run_staged", "qasr_set_system_prompt", "qasr_transcribe_batch",
+    "qasr_stage_audio", "qasr_run", "qasr_run_staged", "qasr_run_stream", "qasr_run_stream_staged", "qasr_set_system_prompt", "qasr_transcribe_batch",
     "qasr_set_probe", "qasr_get_probe", "qasr_get_probe_device",
     "qasr_ctx_set_option", "qasr_ctx_get_option", "qasr_debug_read",
     "qasr_set_token_callback", "qasr_set_profile", "qasr_profile_report",
@@ -49,9 +49,21 @@ class Timings(C.Structure):
                 ("t_decode_ms", C.c_double), ("t_total_ms", C.c_double), ("n_decode_steps", C.c_int32)]
 
 
+class StreamStats(C.Structure):
+    _fields_ = [("n_clips", C.c_int32), ("n_errors", C.c_int32), ("n_prefills", C.c_int32), ("n_steps", C.c_int64),
+                ("slot_steps", C.c_int64), ("live_steps", C.c_int64), ("t_prefill_ms", C.c_double),
+                ("t_decode_ms", C.c_double), ("t_total_ms", C.c_double)]
+
+
 _lib = None
 # void (*)(void *user, int seq, int n_generated, int32_t token)
 TOKEN_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.c_int32)
+# int (*)(void *user, const float **pcm, int *n_samples, int *max_tokens)
+FETCH_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.POINTER(C.c_float)), C.POINTER(C.c_int), C.POINTER(C.c_int))
+# int (*)(void *user, int *max_tokens)
+FETCH_STAGED_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_int))
+# void (*)(void *user, int id, int status, const int32_t *tokens, int n_tokens)
+SINK_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int32), C.c_int)
 
 
 def lib() -> C.CDLL:
@@ -78,6 +90,8 @@ def lib() -> C.CDLL:
             "qasr_stage_audio": ([P, C.POINTER(F), IP, I], I),
             "qasr_run": ([P, I, I, I32P, IP, C.POINTER(Timings)], I),
             "qasr_run_staged": ([P, IP, I, I, I, I32P, IP, C.POINTER(Timings)], I),
+            "qasr_run_stream": ([P, I, FETCH_FN, SINK_FN, P, I, I, C.POINTER(StreamStats)], I),
+            "qasr_run_stream_staged": ([P, I, FETCH_STAGED_FN, SINK_FN, P, I, I, C.POINTER(StreamStats)], I),
             "qasr_set_system_prompt": ([P, I32P, I], I),
             "qasr_transcribe_batch": ([P, C.POINTER(F), IP, I, I, I, I32P, IP, C.POINTER(Timings)], I),
             "qasr_set_probe": ([P, I], I),
@@ -258,6 +272,15 @@ class RunResult:
     timings: Timings
 
 
+def _sink_into(out: dict):
+    def sink(_u, cid, status, toks, n):
+        if status:
+            out[cid] = QasrError(lib().qasr_last_error().decode(errors="replace"))
+        else:
+            out[cid] = [int(toks[i]) for i in range(n)]
+    return sink
+
+
 class Context:
     """qasr_ctx: stream, KV cache, scratch (TextDecoder::init_kv_cache analogue)."""
 
@@ -366,6 +389,51 @@ class Context:
         _check(lib().qasr_run_staged(self.h, _i(idx), B, max_tokens, int(ignore_eos), _i32(toks), _i(nt), C.byref(t)),
                "qasr_run_staged")
         return RunResult([toks[b, :nt[b]].tolist() for b in range(B)], t)
+
+    def run_stream(self, next_clip, max_tokens: int, ignore_eos: bool = False, slots: int = 0):
+        """Continuous batching (qasr_run_stream): next_clip() -> (id, pcm[, budget])
+        or None when the queue is empty; returns ({id: tokens | QasrError},
+        StreamStats).  Slots (0: max_batch) freed by a finished clip are
+        refilled at the next chunk boundary; a clip that fails alone maps to
+        its QasrError."""
+        out, keep = {}, []
+
+        def fetch(_u, pcm_pp, n_p, budget_p):
+            item = next_clip()
+            if item is None:
+                return -1
+            cid, pcm = int(item[0]), np.ascontiguousarray(item[1], np.float32)
+            keep[:] = [pcm]   # alive until the next fetch (the engine copies it first)
+            pcm_pp[0] = _f(pcm)
+            n_p[0] = len(pcm)
+            if len(item) > 2:
+                budget_p[0] = int(item[2])
+            return cid
+
+        f, k = FETCH_FN(fetch), SINK_FN(_sink_into(out))
+        st = StreamStats()
+        _check(lib().qasr_run_stream(self.h, int(slots), f, k, None, int(max_tokens), int(ignore_eos), C.byref(st)), "qasr_run_stream")
+        return out, st
+
+    def run_stream_staged(self, next_clip, max_tokens: int, ignore_eos: bool = False, slots: int = 0):
+        """run_stream over the staged pool (stage_audio): next_clip() -> staged
+        index (its id) or (index, budget), None when the queue is empty"""
+        out = {}
+
+        def fetch(_u, budget_p):
+            item = next_clip()
+            if item is None:
+                return -1
+            if isinstance(item, tuple):
+                budget_p[0] = int(item[1])
+                return int(item[0])
+            return int(item)
+
+        f, k = FETCH_STAGED_FN(fetch), SINK_FN(_sink_into(out))
+        st = StreamStats()
+        _check(lib().qasr_run_stream_staged(self.h, int(slots), f, k, None, int(max_tokens), int(ignore_eos), C.byref(st)),
+               "qasr_run_stream_staged")
+        return out, st
 
     def set_system_prompt(self, ids: Sequence[int]) -> None:
         a = np.ascontiguousarray(ids, np.int32)

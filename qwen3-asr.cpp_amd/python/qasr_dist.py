@@ -1,7 +1,7 @@
 """qasr_dist -- utterance-level data parallelism.
 
-One process per GPU; utterances are independent, so each rank transcribes its
-own shard with no collective on the data path (configs[3]: a 1000-utterance
+One process per GPU; utterances are independent, so each rank transcribes
+utterances with no collective on the data path (configs[3]: a 1000-utterance
 f16 batch sharded over the node's GPUs; configs[4]: the same with the
 ForcedAligner leg on every utterance).  The reference's only batch mode is a
 shell loop over files (docs/usage.md:240-252); this is its sharded
@@ -10,6 +10,10 @@ xGMI on the GPU box, gloo in CPU tests) is used only to
   - synchronise the timed region (barrier) and take the max wall time,
   - gather the per-utterance token-id arrays to rank 0 at the end
     (allgather of lengths + one padded int32 gather: KBs per utterance).
+Two drivers: run_queue (default) -- a dynamic work queue, one shared counter
+in the process group's TCPStore (store.add per utterance, longest first), each
+rank's continuous-batching stream pulling the next utterance whenever a slot
+frees; run_shard -- the static longest-first split in fixed batches.
 """
 from __future__ import annotations
 
@@ -127,3 +131,61 @@ def run_shard(transcribe: Callable[[List[int], int], List[List[int]]], utts: Seq
     merged = gather_tokens(local, dist, device)
     return {"tokens": merged, "wall_s": wall, "audio_s": sum(lengths) / 16000.0,
             "decode_tokens": sum(budget(n, tok_rate) for n in lengths), "local": local, "batches": len(plan)}
+
+
+def queue_order(lengths: Sequence[int]) -> List[int]:
+    """the shared queue's order: longest first (ties by index)"""
+    return sorted(range(len(lengths)), key=lambda i: (-int(lengths[i]), i))
+
+
+def make_next(order: Sequence[int], lengths: Sequence[int], tok_rate: float, store=None, key: str = "q"):
+    """next_clip() for a rank's stream: the k-th utterance of `order`, k from
+    store.add(key, 1) (shared by every rank: a dynamic queue) or a local
+    counter (one rank); (index, budget) or None when the queue is drained"""
+    local = [0]
+
+    def next_clip():
+        if store is not None:
+            k = int(store.add(key, 1)) - 1
+        else:
+            k = local[0]
+            local[0] += 1
+        if k >= len(order):
+            return None
+        i = order[k]
+        return i, budget(lengths[i], tok_rate)
+    return next_clip
+
+
+def default_store(dist):
+    """the TCPStore of the default process group (None: one process)"""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return None
+    from torch.distributed import distributed_c10d
+    return distributed_c10d._get_default_store()
+
+
+def run_queue(stream: Callable[[Callable], Dict[int, List[int]]], utts: Sequence[Tuple[int, int]], rank: int, world: int,
+              tok_rate: float, dist=None, device=None, key: str = "q",
+              after: Optional[Callable[[List[int], List[List[int]]], None]] = None) -> Dict:
+    """The dynamic-queue driver.  stream(next_clip) -> {index: tokens} runs
+    this rank's continuous-batching stream until next_clip() is None
+    (qasr.Context.run_stream_staged).  key: a fresh store key per pass.
+    Barrier -> timed stream (+ after(indices, tokens), e.g. the aligner) ->
+    barrier; wall = max over ranks; tokens gathered to rank 0."""
+    lengths = [n for _, n in utts]
+    store = default_store(dist)
+    next_clip = make_next(queue_order(lengths), lengths, tok_rate, store, key)
+    if dist is not None and dist.is_initialized():
+        dist.barrier()
+    t0 = time.perf_counter()
+    local = dict(stream(next_clip))
+    if after is not None and local:
+        idx = sorted(local)
+        after(idx, [local[i] for i in idx])
+    if dist is not None and dist.is_initialized():
+        dist.barrier()
+    wall = max_over_ranks(time.perf_counter() - t0, dist, device)
+    merged = gather_tokens(local, dist, device)
+    return {"tokens": merged, "wall_s": wall, "audio_s": sum(lengths) / 16000.0,
+            "decode_tokens": sum(budget(n, tok_rate) for n in lengths), "local": local, "batches": None}

@@ -117,3 +117,58 @@ def test_gloo_sharded_driver(world):
     for _, _, _, mine, calls in res:   # batches of <= 8, each decoded to its longest clip's budget
         assert all(len(idx) <= 8 and mt == max(math.ceil(3.5 * utts[i][1] / 16000) for i in idx) for idx, mt in calls)
         assert sorted(i for idx, _ in calls for i in idx) == mine
+
+
+def _queue_worker(rank, world, port, q):
+    import time as _t
+    import torch.distributed as dist
+    from qasr_dist import budget, run_queue
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    utts = [(1000 + i, (5 + 3 * i) * 16000) for i in range(11)]
+
+    def stream(next_clip):   # a stand-in for Context.run_stream_staged: rank 1 is 3x slower per clip
+        out = {}
+        while True:
+            item = next_clip()
+            if item is None:
+                return out
+            i, b = item
+            _t.sleep(0.01 * (1 + 2 * rank))
+            out[i] = [i] * b
+    res = run_queue(stream, utts, rank, world, 3.5, dist, key="qtest")
+    q.put((rank, sorted(res["local"]), res["tokens"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_dynamic_queue():
+    """run_queue: the shared TCPStore counter hands every utterance to exactly
+    one rank, the faster rank takes more, rank 0 gathers all of them"""
+    import torch.multiprocessing as mp
+    from qasr_dist import budget
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_queue_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, l0, m0), (_, l1, m1) = res
+    assert sorted(l0 + l1) == list(range(11)) and not set(l0) & set(l1)
+    assert len(l0) > len(l1)
+    assert m1 is None
+    assert m0 == {i: [i] * budget((5 + 3 * i) * 16000, 3.5) for i in range(11)}
+
+
+def test_queue_order_and_local_counter():
+    from qasr_dist import make_next, queue_order
+    lens = [16000 * s for s in (5, 30, 12, 30, 7)]
+    assert queue_order(lens) == [1, 3, 2, 4, 0]
+    nxt = make_next(queue_order(lens), lens, 3.5)
+    got = [nxt() for _ in range(6)]
+    assert [g[0] for g in got[:5]] == [1, 3, 2, 4, 0] and got[5] is None
+    assert got[0][1] == 105

@@ -119,16 +119,26 @@ def test_cli_sharded_file_list(tiny, tmp_path, tiny_gguf):
     assert r.returncode == 0 and "TIMING PROFILE REPORT" in r.stderr and "decode.token" in r.stderr
 
 
-def test_bench_utterance_driver(gpu):
-    """bench.py --utterances (configs[3] driver) at a small size: every
-    utterance transcribed to its budget, one JSON line, strong scaling"""
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--utterances", "24", "--utt-min", "2",
-                        "--utt-max", "6", "--batch", "8", "--steps", "1", "--warmup", "1"],
-                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+@pytest.mark.parametrize("queue,pipeline,n", [("dynamic", "asr", 24), ("static", "asr", 24), ("dynamic", "align", 48)])
+def test_bench_utterance_driver(gpu, queue, pipeline, n):
+    """bench.py --utterances (configs[3] driver; configs[4] with --pipeline
+    align) at a small size, full-size synthetic models: every utterance
+    transcribed to its budget (bench.py asserts it), with align every
+    transcript aligned; one JSON line, strong scaling.  dynamic: the shared
+    queue feeding the continuous-batching stream"""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--utterances", str(n), "--utt-min", "2",
+                        "--utt-max", "6", "--batch", "8", "--steps", "1", "--warmup", "1", "--queue", queue,
+                        "--pipeline", pipeline],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')][-1])
-    assert line["scaling"] == "strong" and line["n_gpus"] == 1 and line["config"]["utterances"] == 24
-    assert line["value"] > 0 and line["decode_tokens_per_s"] > 0
+    assert line["scaling"] == "strong" and line["n_gpus"] == 1 and line["config"]["utterances"] == n
+    assert line["value"] > 0 and line["decode_tokens_per_s"] > 0 and line["config"]["queue"] == queue
+    if pipeline == "align":
+        assert line["aligned_rank0"] == n
+    if queue == "dynamic":
+        st = line["rank0_stream"]
+        assert st["clips"] == n and 0 < st["slot_utilisation"] <= 1
 
 
 def test_probe_stride_samples_steps(gpu, tiny_gguf):

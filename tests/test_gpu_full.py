@@ -380,3 +380,46 @@ def test_full_configs2_q8_b64_30s(gpu, tmp_path_factory):
     lo1, ln1 = d.forward([tok0], len(ids)), dn.forward([tok0], len(ids))
     tol1 = max(1e-2 * float(np.abs(lo1).max()), 2.5 * float(np.abs(lo1 - ln1).max()))
     assert np.abs(lg1[0] - lo1).max() <= tol1, (float(np.abs(lg1[0] - lo1).max()), tol1)
+
+
+@pytest.mark.timeout(900)
+def test_full_configs3_f16_b64_30s(full):
+    """configs[3]'s per-GPU shape at full size: Qwen3-ASR-0.6B f16 (synthetic
+    weights), 64 x 30 s clips (P = 405, 105-token budget) -- the skinny
+    QKV / o / gate-up / down tilings at 64 rows, per-sequence decode attention
+    over the exact kernels and the batched LM head.  All 64 rows bit-identical
+    (identical clips), every budget met, row 0's prefill and 5 teacher-forced
+    decode steps against the default oracle within 1e-2 of the logit scale
+    (absolute |delta| printed)."""
+    m, _, om = full
+    B, n, budget = 64, 30 * SR, 105
+    pcm = qasr.synth_pcm(17500, n)
+    mel = op.log_mel(pcm)
+    feats = om.encode(mel)
+    ids, pos = m.build_prompt(feats.shape[0])
+    assert len(ids) == 405
+    d = op.OracleDecoder(om, len(ids) + 8)
+    lo = [d.forward(ids, 0, feats, pos)]
+    toks = [int(np.argmax(lo[0]))]
+    for k in range(1, 6):
+        lo.append(d.forward([toks[-1]], len(ids) + k - 1))
+        toks.append(int(np.argmax(lo[-1])))
+    c = qasr.Context(m, max_batch=B, max_ctx=len(ids) + budget + 8)
+    try:
+        assert c.get_option("fa_exact_decode") == 1
+        r = c.transcribe([pcm] * B, max_tokens=budget, ignore_eos=True)
+        assert all(len(t) == budget for t in r.tokens)
+        assert all(t == r.tokens[0] for t in r.tokens)
+        lg, am = c.prefill([ids] * B, [feats] * B, [pos] * B)
+        for b in range(1, B):
+            assert np.array_equal(lg[b], lg[0]), b
+        errs = [_err(lg[0], lo[0])]
+        for k in range(1, 6):
+            lg, am = c.decode_step([toks[k - 1]] * B, [len(ids) + k - 1] * B)
+            for b in range(1, B):
+                assert np.array_equal(lg[b], lg[0]), (k, b)
+            errs.append(_err(lg[0], lo[k]))
+    finally:
+        c.close()
+    print("configs[3] prefill + decode steps (abs, rel):", [(round(a_, 4), round(r_, 5)) for a_, r_ in errs])
+    assert max(r_ for _, r_ in errs) <= 1e-2, errs

@@ -1,0 +1,92 @@
+"""Continuous batching (qasr_run_stream): slots refilled from a queue.
+
+The reference transcribes one utterance at a time (src/qwen3_asr.cpp:270-296),
+so a clip's tokens must not depend on which clips share its batch or when its
+slot was refilled: every clip of a stream run equals a one-clip qasr_run of
+the same clip and budget.  Ragged per-clip budgets stand in for natural EOS
+(random-init weights rarely emit it) and make the refill schedule
+deterministic; slot-steps must drop against static batches run to their
+longest member.
+"""
+import numpy as np
+import pytest
+
+import qasr
+
+SR = 16000
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def tiny_model(gpu, tiny_gguf):
+    m = qasr.Model(tiny_gguf)
+    yield m
+    m.close()
+
+
+def _single(m, pcm, budget, ignore_eos):
+    c = qasr.Context(m, max_batch=1, max_ctx=640)
+    try:
+        return c.transcribe([pcm], max_tokens=budget, ignore_eos=ignore_eos).tokens[0]
+    finally:
+        c.close()
+
+
+def _queue(items):
+    it = iter(items)
+    return lambda: next(it, None)
+
+
+@pytest.mark.parametrize("slots", [3, 1])
+def test_stream_ragged_budgets_equal_single(tiny_model, slots):
+    lens = [SR, 2 * SR + 333, 4 * SR, SR // 2, 3 * SR, 5 * SR + 7, SR + 999]
+    budgets = [3, 9, 5, 16, 1, 7, 12]
+    clips = [qasr.synth_pcm(7100 + i, n) for i, n in enumerate(lens)]
+    c = qasr.Context(tiny_model, max_batch=slots, max_ctx=640)
+    try:
+        out, st = c.run_stream(_queue([(10 + i, p, b) for i, (p, b) in enumerate(zip(clips, budgets))]), max_tokens=32,
+                               ignore_eos=True)
+    finally:
+        c.close()
+    assert sorted(out) == [10 + i for i in range(len(clips))]
+    for i, (p, b) in enumerate(zip(clips, budgets)):
+        assert out[10 + i] == _single(tiny_model, p, b, True), i
+        assert len(out[10 + i]) == b
+    assert st.n_clips == len(clips) and st.n_errors == 0
+    # every live slot-step produced one token after the prefill's
+    assert st.live_steps == sum(budgets) - len(clips)
+    # static batches of `slots` clips in queue order, each run to its longest budget
+    static = sum(slots * (max(budgets[k:k + slots]) - 1) for k in range(0, len(budgets), slots))
+    assert st.slot_steps < static or slots == 1
+
+
+def test_stream_natural_eos_and_per_clip_errors(tiny_model):
+    good = [qasr.synth_pcm(7200 + i, n) for i, n in enumerate([SR, 3 * SR, 2 * SR])]
+    items = [(0, good[0], 8), (1, qasr.synth_pcm(7300, 100), 8), (2, good[1], 8), (3, qasr.synth_pcm(7301, SR), 10000),
+             (4, good[2], 6)]
+    c = qasr.Context(tiny_model, max_batch=2, max_ctx=640)
+    try:
+        out, st = c.run_stream(_queue(items), max_tokens=8, ignore_eos=False)
+    finally:
+        c.close()
+    assert isinstance(out[1], qasr.QasrError) and "audio_pad" in str(out[1])
+    assert isinstance(out[3], qasr.QasrError) and "Context length" in str(out[3])
+    for cid, pcm, b in (items[0], items[2], items[4]):
+        assert out[cid] == _single(tiny_model, pcm, b, False), cid
+        assert 151645 not in out[cid]
+    assert st.n_clips == 3 and st.n_errors == 2
+
+
+def test_stream_token_callback_gets_clip_ids(tiny_model):
+    clips = [qasr.synth_pcm(7400 + i, SR + 500 * i) for i in range(3)]
+    seen = {}
+    c = qasr.Context(tiny_model, max_batch=2, max_ctx=640)
+    try:
+        c.set_token_callback(lambda cid, n, tok: seen.setdefault(cid, []).append((n, tok)))
+        out, _ = c.run_stream(_queue([(40 + i, p, 4 + i) for i, p in enumerate(clips)]), max_tokens=16, ignore_eos=True)
+        c.set_token_callback(None)
+    finally:
+        c.close()
+    for cid, toks in out.items():
+        assert [n for n, _ in seen[cid]] == list(range(1, len(toks) + 1))
+        assert [t for _, t in seen[cid]] == toks

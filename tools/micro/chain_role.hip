@@ -1,12 +1,12 @@
 // Micro-benchmark: the fused launch's chain loop outside the fused kernel,
 // to separate the loop's own cost from its environment (32 chain waves, 4 per
 // workgroup, n = 1370 keys, V^T double-buffered from global memory).
-//   mode 0: fx_step1_lds as built (slow path inline, flags 0)
+//   mode 0: fx_step1_lds as built (flags at run time)
 //   mode 1: fast path only (no slow-path code in the loop)
 //   mode 2: fast path only, V^T not reloaded (first two buffers reused)
 //   mode 3: as 2, and the weights not reloaded from LDS (fx8_fast on fixed registers)
 //   mode 4: as 0 (V^T reloaded), weights not reloaded from LDS
-//   argv[2] = waves per workgroup (4 or 1)
+//   argv[2] = waves per workgroup (4 or 1); argv[3] = the batches' slow-path flags (default 0)
 // Prints cycles per key (s_memtime), mean over the chain waves.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -17,7 +17,8 @@
 using namespace qasr;
 
 template <int MODE>
-__global__ __launch_bounds__(256) void chain_k(const uint16_t *vt_all, const float *wsrc, int n, long long *cyc, uint16_t *out) {
+__global__ __launch_bounds__(256) void chain_k(const uint16_t *vt_all, const float *wsrc, int n, long long *cyc, uint16_t *out,
+                                               unsigned long long flags) {
     __shared__ __attribute__((aligned(16))) float ws[4][DX_KC / DX_B * FX_ST];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (int i = lane; i < DX_KC / DX_B * FX_ST; i += 64) ws[wid][i] = wsrc[i];
@@ -46,9 +47,9 @@ __global__ __launch_bounds__(256) void chain_k(const uint16_t *vt_all, const flo
         } else
         for (int j0 = 0; j0 < n; j0 += 2 * DX_Q) {
             if constexpr (MODE < 2) fx_loadQ(vb, vt, loff, j0 + DX_Q);
-            fx_step1_lds(va, j0, n, ws[wid], 0ull, acc, wa, wb);
+            fx_step1_lds(va, j0, ws[wid], flags, acc, wa, wb);
             if constexpr (MODE < 2) fx_loadQ(va, vt, loff, j0 + 2 * DX_Q);
-            fx_step1_lds(vb, j0 + DX_Q, n, ws[wid], 0ull, acc, wa, wb);
+            fx_step1_lds(vb, j0 + DX_Q, ws[wid], flags, acc, wa, wb);
         }
     }
     const long long t1 = clock64();
@@ -58,6 +59,7 @@ __global__ __launch_bounds__(256) void chain_k(const uint16_t *vt_all, const flo
 
 int main(int argc, char **argv) {
     const int mode = argc > 1 ? atoi(argv[1]) : 0, wpb = argc > 2 ? atoi(argv[2]) : 4;
+    const unsigned long long flags = argc > 3 ? strtoull(argv[3], nullptr, 0) : 0ull;   // runtime: the slow path's code is present
     const int n = 1370, nwaves = 32, blocks = nwaves / wpb;
     uint16_t *vt, *o;
     float *w;
@@ -72,11 +74,11 @@ int main(int argc, char **argv) {
     for (auto &x : hw) x = 0.5f;
     (void)hipMemcpy(w, hw, sizeof hw, hipMemcpyHostToDevice);
     for (int rep = 0; rep < 3; rep++) {
-        if (mode == 0) hipLaunchKernelGGL(chain_k<0>, dim3(blocks), dim3(64 * wpb), 0, 0, vt, w, n, c, o);
-        if (mode == 1) hipLaunchKernelGGL(chain_k<1>, dim3(blocks), dim3(64 * wpb), 0, 0, vt, w, n, c, o);
-        if (mode == 2) hipLaunchKernelGGL(chain_k<2>, dim3(blocks), dim3(64 * wpb), 0, 0, vt, w, n, c, o);
-        if (mode == 3) hipLaunchKernelGGL(chain_k<3>, dim3(blocks), dim3(64 * wpb), 0, 0, vt, w, n, c, o);
-        if (mode == 4) hipLaunchKernelGGL(chain_k<4>, dim3(blocks), dim3(64 * wpb), 0, 0, vt, w, n, c, o);
+        if (mode == 0) hipLaunchKernelGGL(chain_k<0>, dim3(blocks), dim3(64 * wpb), 0, 0, vt, w, n, c, o, flags);
+        if (mode == 1) hipLaunchKernelGGL(chain_k<1>, dim3(blocks), dim3(64 * wpb), 0, 0, vt, w, n, c, o, flags);
+        if (mode == 2) hipLaunchKernelGGL(chain_k<2>, dim3(blocks), dim3(64 * wpb), 0, 0, vt, w, n, c, o, flags);
+        if (mode == 3) hipLaunchKernelGGL(chain_k<3>, dim3(blocks), dim3(64 * wpb), 0, 0, vt, w, n, c, o, flags);
+        if (mode == 4) hipLaunchKernelGGL(chain_k<4>, dim3(blocks), dim3(64 * wpb), 0, 0, vt, w, n, c, o, flags);
         (void)hipDeviceSynchronize();
     }
     long long hc[32];

@@ -6,4 +6,4 @@ timeout -k 10 200 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpuru
 grep '^{' gpurun_out/r3f_b.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['stage_ms_per_step_rank0']['decode'], d['roofline']['avg_launch_us'], d['decode_attention'][-40:])"
 QASR_DEV_TRACE=gpurun_out/r3f_tr.bin QASR_DEV_TRACE_LAYER=14 timeout -k 10 200 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-probe > gpurun_out/r3f_tr.log 2>&1 || exit 1
 python3 tools/trace_report.py gpurun_out/r3f_tr.bin
-for w in 4 1; do timeout -k 5 30 ./tools/micro/chain_role 0 $w || exit 1; done
+for m in "0 4" "0 4 0x10" "2 4" "3 4" "4 4"; do timeout -k 5 30 ./tools/micro/chain_role $m || exit 1; done
