@@ -221,6 +221,7 @@ static const std::vector<FuseOption> &fuse_options() {
         {"skinny", "QASR_SKINNY", &FuseCfg::skinny},
         {"att_spl", "QASR_ATT_SPL", &FuseCfg::att_spl},
         {"kv_nt", "QASR_KV_NT", &FuseCfg::kv_nt},
+        {"lmh", "QASR_LMH", &FuseCfg::lmh},
     };
     return v;
 }
@@ -239,6 +240,8 @@ static int reset_counters(qasr_ctx *c) {
     HIPCHK(hipMemsetAsync(c->d_qcnt, 0, (size_t)hp.n_kv_head * 8 * 16 * 4, c->st));
     HIPCHK(hipMemsetAsync(c->d_attdone, 0, (size_t)8 * 16 * 4, c->st));
     HIPCHK(hipMemsetAsync(c->d_counter, 0, (size_t)c->max_batch * hp.n_kv_head * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->d_done, 0, 4, c->st));
+    HIPCHK(hipMemsetAsync(c->d_amax, 0, (size_t)c->max_batch * 8, c->st));
     return 0;
 }
 
@@ -1188,6 +1191,8 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
     hipStream_t s = c->st;
     float *x = c->d_x;
     const bool skinny = B <= 8;
+    // decode batches: the LM head as one launch (lmhead.hip's shape conditions)
+    const bool lmh_one = !skinny && B <= 64 && c->fuse.lmh && H == 1024 && hp.vocab % 16 == 0;
     const size_t layer_kv = (size_t)c->max_batch * hp.n_kv_head * c->max_ctx * 128;
     const int nl = step_layers(c);   // diagnostic layer cap
     // probed group (emitted alone): every launch in it folds its block times into one record
@@ -1338,6 +1343,14 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             lm.pos = c->d_pos;
             lm.stamp = stamp;
             launch_gemv(EPI_ARGMAX, lm, s);
+        } else if (lmh_one) {   // norm + GEMM + argmax + bookkeeping in one launch (lmhead.hip)
+            GemvArgs lm{};
+            lm.x = x; lm.ldx = H; lm.norm_w = m->out_norm; lm.eps = hp.rms_eps; lm.W = m->embd; lm.K = H; lm.N = hp.vocab; lm.M = B;
+            lm.out_f32 = want_logits ? c->d_logits : nullptr; lm.ldo = hp.vocab; lm.amax = c->d_amax;
+            lm.done = c->d_done; lm.tok_out = c->d_tok; lm.hist = c->d_hist; lm.hist_stride = c->hist_cap; lm.step = c->d_step;
+            lm.pos = c->d_pos; lm.nkv = c->d_nkv;
+            lm.stamp = stamp;
+            (void)launch_lmhead_batch(lm, s);
         } else {
             launch_fill_u64(c->d_amax, B, 0ull, s);
             launch_rmsnorm_f16(x, H, nullptr, B, H, m->out_norm, hp.rms_eps, c->d_xh, s);
@@ -1347,7 +1360,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             dec_gemm(c, EPI_ARGMAX, lm, s);
         }
     }
-    if (r.in(2 + 2 * nl) && !skinny) {   // bookkeeping (fused into the LM-head GEMV at batch <= 8)
+    if (r.in(2 + 2 * nl) && !skinny && !lmh_one) {   // bookkeeping (fused into the LM-head GEMV at batch <= 8)
         launch_step_advance(c->d_pos, c->d_nkv, c->d_step, B, s);
         launch_argmax_finish(c->d_amax, B, c->d_tok, c->d_hist, c->hist_cap, c->d_step, s);
         launch_fill_u64(c->d_amax, B, 0ull, s);   // re-arm (zero at rest)

@@ -118,8 +118,15 @@ struct GemvArgs {
     unsigned long long *trace;           // dev trace: per block [start, end, ...] (8 slots, 100 MHz clock) or null
     unsigned int *zero8;                 // gemv1: block 0 re-arms these 8 replicated counters (16-word stride)
     unsigned long long *stamp;           // kernel-duration probe record (dev_common.h stamp_start/end) or null
+    int *nkv;                            // launch_lmhead_batch: n_kv[b] += 1 with pos[b] (decode batches) or null
+    int n_valid;                         // launch_lmhead_batch: columns >= n_valid never win; 0 = N
 };
 void launch_gemv(int epi, const GemvArgs &g, hipStream_t s);
+// lmhead.hip: decode-batch LM head in one launch (9..64 rows, K = 1024, f16 W):
+// RMS norm of x with norm_w, GEMM against W [N][K], optional fp32 logits,
+// per-row first-index argmax, and the fused bookkeeping of EPI_ARGMAX above
+// (plus nkv); amax and done zero at rest.  false = shape not covered
+bool launch_lmhead_batch(const GemvArgs &g, hipStream_t s);
 // gemv.hip: one-row f16 fast path of launch_gemv (false = not covered)
 bool launch_gemv1(int epi, const GemvArgs &g, hipStream_t s);
 
@@ -157,6 +164,7 @@ struct FuseCfg {
     int kv_nt = 1;                      // decode attention: K/V cache rows loaded nontemporal (read once per step by one
                                         // CU; tools/experiments.sh kvnt: configs[1] neutral, 64 x 30 s decode 205.0 -> 202.1 ms)
     int slots_stream = 0;               // ... its co-resident workgroups on this device
+    int lmh = 1;                        // decode batches of f16 models (9..64 rows): the LM head in one launch (lmhead.hip)
     unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
 };
 // co-resident workgroup capacity of the fused kernels on the current device

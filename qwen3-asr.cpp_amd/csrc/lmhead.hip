@@ -1,0 +1,221 @@
+// lmhead.hip -- the decode-batch LM head in one launch (9 <= M <= 64 rows):
+// final RMS norm + tied-embedding GEMM (151936 x 1024 f16) + first-index
+// argmax + the greedy step's bookkeeping (src/text_decoder.cpp forward's last
+// ggml_rms_norm / ggml_mul / ggml_mul_mat over model.output, then
+// src/qwen3_asr.cpp:270-296's sample_greedy per sequence).
+//
+// The skinny GEMM (gemm_skinny.hip) took 140-150 us for these 311 MB: 2374
+// workgroups each streamed 128 KB of weights but re-read the whole 64 x 1024
+// activation (another 128 KB) through LDS-DMA, every 64-column tile folded its
+// keys into the same 64 global argmax words (152k atomics on 64 addresses), and
+// the norm, the key reset and the bookkeeping were five more launches.
+//
+// Here one persistent workgroup per CU normalises the rows once into LDS
+// (rms_row's arithmetic: the values launch_rmsnorm_f16 writes), then each wave
+// streams a contiguous run of 16-column units of the weight matrix through a
+// D-deep ring of fragment registers (nontemporal buffer loads, out-of-range
+// items read as zeros without a memory access), multiplies them against the
+// LDS rows on v_mfma_f32_16x16x32_f16 (K ascending in 32-wide steps, fp32
+// accumulation; even and odd chunks in two accumulators summed at the end, the
+// order of gemm_skinny_kernel<4, 4, 2>'s two K waves, so the logits are
+// bit-identical to the separate launches'), keeps a per-lane running best key per row across all its
+// units, and reduces those once at the end: one atomicMax per row per
+// workgroup, then the last workgroup decodes the tokens (tok, hist[step+1],
+// pos += 1, n_kv += 1, step += 1) and re-arms amax / done (zero at rest).
+#include "dev_common.h"
+#include "kernels.h"
+
+namespace qasr {
+
+namespace {
+
+constexpr int LMH_K = 1024;   // hidden width this kernel is built for (host checks)
+
+// LDS row layout: 128 chunks of 16 B per row, chunk ch stored at ch ^ (row & 15)
+// so the 16 rows of a fragment read hit 16 distinct 16-B bank groups
+__device__ __forceinline__ int lmh_off(int row, int k) {   // element offset of (row, k), k % 8 == 0 .. +7
+    const int ch = k >> 3;
+    return row * LMH_K + ((ch ^ (row & 15)) << 3) + (k & 7);
+}
+
+template <int MT, int WPG, int D>
+__global__ __launch_bounds__(64 * WPG) void lmhead_batch_kernel(GemvArgs g) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];   // [MT*16][LMH_K] fp16, swizzled
+    __shared__ unsigned long long bestk[WPG][MT * 16];
+    __shared__ int last_wg, st;
+    stamp_start(g.stamp);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int q = lane >> 4, c16 = lane & 15;
+    const int M = g.M;
+
+    // ---- this wave's units (16 weight rows each) and items (unit, 128-wide K chunk)
+    const int U = g.N >> 4, TW = gridDim.x * WPG, gw = blockIdx.x * WPG + wid;
+    const int u0 = (int)((long)gw * U / TW), u1 = (int)((long)(gw + 1) * U / TW);
+    const int n_items = (u1 - u0) * (LMH_K / 128);
+    const uint32_t wbytes = (uint32_t)((long)g.N * LMH_K * 2);
+    const __amdgpu_buffer_rsrc_t wsrd = __builtin_amdgcn_make_buffer_rsrc((void *)g.W, (short)0, (int)wbytes, 0x00020000);
+    u32x4 wb[D][4];
+    auto load = [&](int b, int j) {
+        const int u = u0 + (j >> 3), c = j & 7;
+        const uint32_t base = (uint32_t)(((long)(u * 16 + c16) * LMH_K + c * 128 + q * 8) * 2);
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+            wb[b][s] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wsrd, j < n_items ? base + 64 * s : wbytes, 0, 2));
+    };
+#pragma unroll
+    for (int b = 0; b < D; b++) load(b, b);
+
+    // ---- prologue: rows -> RMS norm (rms_row<1024> arithmetic) -> fp16 LDS
+    for (int m = wid; m < MT * 16; m += WPG) {
+        if (m < M) {
+            const float *xr = g.x + (long)m * g.ldx;
+            float4 v[4], wv[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                v[i] = *(const float4 *)(xr + 4 * lane + 256 * i);
+                wv[i] = *(const float4 *)(g.norm_w + 4 * lane + 256 * i);
+            }
+            double s = 0.0;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                s += ((double)fmul_rn(v[i].x, v[i].x) + (double)fmul_rn(v[i].y, v[i].y)) +
+                     ((double)fmul_rn(v[i].z, v[i].z) + (double)fmul_rn(v[i].w, v[i].w));
+            s = wave_sum_d(s);
+            const float mean = (float)(s / LMH_K);
+            const float scale = 1.0f / sqrtf(mean + g.eps);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t lo = f_to_u16(fmul_rn(fmul_rn(v[i].x, scale), wv[i].x)) |
+                                    ((uint32_t)f_to_u16(fmul_rn(fmul_rn(v[i].y, scale), wv[i].y)) << 16);
+                const uint32_t hi = f_to_u16(fmul_rn(fmul_rn(v[i].z, scale), wv[i].z)) |
+                                    ((uint32_t)f_to_u16(fmul_rn(fmul_rn(v[i].w, scale), wv[i].w)) << 16);
+                *(uint2 *)(xs + lmh_off(m, 4 * lane + 256 * i)) = make_uint2(lo, hi);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++) *(uint2 *)(xs + lmh_off(m, 4 * lane + 256 * i)) = make_uint2(0u, 0u);
+        }
+    }
+    __syncthreads();
+
+    // ---- stream: item j = (unit u0 + j / 8, K chunk j % 8), ring slot j % D
+    unsigned long long best[MT][4];
+#pragma unroll
+    for (int i = 0; i < MT; i++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) best[i][r] = 0ull;
+    floatx4 acc[2][MT];   // even / odd K chunks: the skinny kernel's two K waves (bit-identical logits)
+    const int nvalid = g.n_valid > 0 ? g.n_valid : g.N;
+    for (int j0 = 0; j0 < n_items; j0 += D) {
+#pragma unroll
+        for (int b = 0; b < D; b++) {
+            const int j = j0 + b;
+            if (j >= n_items) break;
+            const int c = j & 7;
+            if (c == 0) {
+#pragma unroll
+                for (int i = 0; i < MT; i++) acc[0][i] = acc[1][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+#pragma unroll
+                for (int i = 0; i < MT; i++) {
+                    const half8 a8 = *(const half8 *)(xs + lmh_off(i * 16 + c16, c * 128 + 32 * s + 8 * q));
+                    acc[c & 1][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a8, __builtin_bit_cast(half8, wb[b][s]), acc[c & 1][i], 0, 0, 0);
+                }
+            }
+            load(b, j + D);
+            if (c == 7) {   // unit done: C layout, lane (q, c16) = rows 16i + 4q + r, column 16u + c16
+                const int col = (u0 + (j >> 3)) * 16 + c16;
+#pragma unroll
+                for (int i = 0; i < MT; i++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int row = i * 16 + 4 * q + r;
+                        const float v = acc[0][i][r] + acc[1][i][r];
+                        if (g.out_f32 && row < M) g.out_f32[(long)row * g.ldo + col] = v;
+                        const unsigned long long key = col < nvalid ? argmax_key(v, col) : 0ull;
+                        best[i][r] = key > best[i][r] ? key : best[i][r];
+                    }
+            }
+        }
+    }
+
+    // ---- per-row best over the 16 columns lanes, the waves, then the workgroups
+#pragma unroll
+    for (int i = 0; i < MT; i++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            unsigned long long k = best[i][r];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                const unsigned long long t = __shfl_xor(k, o, 64);
+                k = t > k ? t : k;
+            }
+            if (c16 == 0) bestk[wid][i * 16 + 4 * q + r] = k;
+        }
+    __syncthreads();
+    if (tid < M) {
+        unsigned long long b = bestk[0][tid];
+#pragma unroll
+        for (int w = 1; w < WPG; w++) b = bestk[w][tid] > b ? bestk[w][tid] : b;
+        const unsigned long long old = atomicMax(g.amax + tid, b);
+        asm volatile("" ::"v"(old));   // returned value used: the max has been performed at L2
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) last_wg = __hip_atomic_fetch_add(g.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (last_wg) {
+        if (tid == 0) st = *g.step;
+        __syncthreads();
+        if (tid < M) {
+            const unsigned long long k = __hip_atomic_load(g.amax + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int id = argmax_key_idx(k);
+            g.tok_out[tid] = id;
+            if (g.hist) g.hist[(long)tid * g.hist_stride + st + 1] = id;
+            g.pos[tid] += 1;
+            if (g.nkv) g.nkv[tid] += 1;
+            __hip_atomic_store(g.amax + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (tid == 0) {
+            *g.step = st + 1;
+            __hip_atomic_store(g.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    stamp_end(g.stamp);
+}
+
+// 16 waves a CU with a 3-deep ring up to 16 rows; more rows need more than
+// 128 VGPRs (the running keys and both accumulator sets), so 8 waves with a 4-deep ring
+template <int MT, int WPG = (MT < 2 ? 16 : 8), int D = (MT < 2 ? 3 : 4)>
+void run_lmhead(const GemvArgs &g, hipStream_t s) {
+    static int ncu_dev[64];   // per device: CU count once the LDS attribute is set
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int &ncu = ncu_dev[dev & 63];
+    if (!ncu) {
+        int n = 0;
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipFuncSetAttribute((const void *)lmhead_batch_kernel<MT, WPG, D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  MT * 16 * LMH_K * 2);
+        ncu = n > 0 ? n : 256;
+    }
+    hipLaunchKernelGGL((lmhead_batch_kernel<MT, WPG, D>), dim3(ncu), dim3(64 * WPG), MT * 16 * LMH_K * 2, s, g);
+}
+
+}  // namespace
+
+bool launch_lmhead_batch(const GemvArgs &g, hipStream_t s) {
+    if (g.M < 1 || g.M > 64 || g.K != LMH_K || g.N % 16 != 0 || !g.x || !g.norm_w || !g.amax || !g.done || !g.tok_out ||
+        !g.step || !g.pos || g.Wd)
+        return false;
+    const int mt = (g.M + 15) / 16;
+    if (mt == 1) run_lmhead<1>(g, s);
+    else if (mt == 2) run_lmhead<2>(g, s);
+    else if (mt == 3) run_lmhead<3>(g, s);
+    else run_lmhead<4>(g, s);
+    return true;
+}
+
+}  // namespace qasr

@@ -13,7 +13,8 @@ include/ + libqasr.so, in the build container.  Here:
   encoder: the restated ggml numerics), at the drivers' own tolerances (mel
   1e-5, encoder 2e-2 max |delta|); test_decoder_last_pos.cpp and
   test_decoder_no_audio.cpp run the TextDecoder on the synthetic full-size
-  GGUF and their printed top token equals the C-ABI prefill's argmax.
+  GGUF: one row of logits, and last_pos's printed argmax equals the C-ABI
+  prefill's.
 Random-init weights: the drivers' known answers (12095, 198, 11528) are
 real-weight facts (tests/test_kat_real_weights.py) and are not asserted.
 """
@@ -104,23 +105,28 @@ def test_reference_encoder_driver(gpu, tiny_gguf, tiny_oracle, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,n_pad", [("test_decoder_last_pos", 3), ("test_decoder_no_audio", 390)])
-def test_reference_decoder_drivers(gpu, full_f16_gguf, tmp_path, name, n_pad):
-    """TextDecoder::load_model / init_kv_cache / forward (last-row logits) on
-    the synthetic full-size model: the driver's top token equals the C-ABI
-    prefill's argmax over the same prompt"""
+@pytest.mark.parametrize("name", ["test_decoder_last_pos", "test_decoder_no_audio"])
+def test_reference_decoder_drivers(gpu, full_f16_gguf, tmp_path, name):
+    """TextDecoder::load_model / init_kv_cache / forward on the synthetic
+    full-size model.  forward returns the last row's logits only, as the
+    reference's graph does (src/text_decoder.cpp:563-565 views row n_tokens-1
+    before the norm; :674-677 copies ne[1] = 1 row).  Both drivers still index
+    logits + (n_tokens - 1) * vocab_size -- past the end of that vector on the
+    reference too -- so their "last position" lines are undefined and are not
+    read here.  Asserted: the driver runs, prints one row of logits
+    (no_audio's "Logits size"), and last_pos's "Position 0 argmax" (row 0 =
+    the one row returned) equals the C-ABI prefill's argmax over the prompt."""
     exe = _need(name)
     os.makedirs(tmp_path / "models")
     os.symlink(full_f16_gguf, tmp_path / "models" / "qwen3-asr-0.6b-f16.gguf")
     r = _run([exe], str(tmp_path), timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    top = re.search(r"\[0\] token=(\d+) logit=([-0-9.]+)", r.stdout)
+    if name == "test_decoder_no_audio":
+        assert re.search(r"Logits size: 151936\b", r.stdout), r.stdout[-2000:]
+        return
+    top = re.search(r"Position 0 argmax: (\d+) \(logit=([-0-9.]+)\)", r.stdout)
     assert top, r.stdout[-2000:]
-    if name == "test_decoder_last_pos":
-        ids = [151669] + [151676] * 3 + [151670]
-    else:
-        ids = [151644, 8948, 198, 151645, 198, 151644, 872, 198, 151669] + [151676] * 390 + \
-              [151670, 151645, 198, 151644, 77091, 198]
+    ids = [151669] + [151676] * 3 + [151670]
     m = qasr.Model(full_f16_gguf)
     c = qasr.Context(m, max_batch=1, max_ctx=len(ids) + 8)
     try:
