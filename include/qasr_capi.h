@@ -231,7 +231,10 @@ int qasr_debug_read(qasr_ctx *c, const char *buffer, void *dst, int64_t bytes);
  * qasr_run / qasr_run_staged -- the prefill's token first (n_generated = 1) --
  * for every sequence still decoding, in sequence order.  Each step then
  * synchronises the stream (the token must reach the host), so a callback
- * costs throughput; NULL removes it. */
+ * costs throughput; NULL removes it.  The callback must not start another
+ * qasr_run / qasr_run_staged / qasr_run_stream* / qasr_decode_step on any
+ * context of the same GPU: a batch-1 run holds that device's fused-launch
+ * lock (not recursive) while it calls back. */
 int qasr_set_token_callback(qasr_ctx *c, void (*cb)(void *user, int seq, int n_generated, int32_t token), void *user);
 
 /* ---- measurement ---------------------------------------------------------- */

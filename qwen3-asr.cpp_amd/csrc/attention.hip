@@ -1353,8 +1353,8 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
     //     fwl, applied once after the loop with vnew -- the same sequence of
     //     operations as fa_exact.hip's chain, so both launches agree bit for bit
     __shared__ float fwl[2];
+    __shared__ __attribute__((aligned(8))) uint16_t kmask[2][DX_KC / 16];   // per head: new-maximum bit of every key
     float M, S;
-    unsigned long long flags;
     {
         float *row = fsc[hh] + lane * FX_ST;   // this lane's 32 keys
         float sv[DX_B];
@@ -1373,17 +1373,19 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         const float inc = wave_scan_max(lm);
         const float Mp0 = dpp_ninf<0x138, 0xF>(inc);   // exclusive prefix (lane 0: -inf; the chunk is the first)
         M = lane_f(inc, 63);
-        flags = __ballot(lm > Mp0);
         float Mq = wu ? fmaxf(Mp0, lh) : Mp0;
         float x[DX_B / 2];
+        uint32_t kb = 0;
 #pragma unroll
         for (int i = 0; i < DX_B / 2; i++) {
             const float sc = wu ? sv[DX_B / 2 + i] : sv[i];
             const bool gt = sc > Mq;
             const float e = expf(gt ? Mq - sc : sc - Mq);
             x[i] = gt ? -e : (sc != -INFINITY ? e : 0.0f);
+            kb |= (uint32_t)gt << i;
             Mq = fmaxf(Mq, sc);
         }
+        kmask[hh][2 * lane + wu] = (uint16_t)kb;   // keys 32 lane + 16 wu ..: the slow path's 8-key groups
         __syncthreads();   // both waves have read their scores
 #pragma unroll
         for (int i = 0; i < DX_B / 2; i += 4) *(floatx4 *)&row[16 * wu + i] = floatx4{x[i], x[i + 1], x[i + 2], x[i + 3]};
@@ -1436,10 +1438,10 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         fx_w8(fsc[hh], 0, wa, wb);
         for (int j0 = 0; j0 < nl; j0 += 2 * DX_Q) {
             fx_loadQ(vb, vt, loff, j0 + DX_Q);
-            fx_step1_lds(va, j0, fsc[hh], flags, acc, wa, wb);
+            fx_step1_lds_m(va, j0, fsc[hh], fx_mask64(kmask[hh], j0), acc, wa, wb);
             if (j0 + DX_Q >= nl) break;
             fx_loadQ(va, vt, loff, j0 + 2 * DX_Q);
-            fx_step1_lds(vb, j0 + DX_Q, fsc[hh], flags, acc, wa, wb);
+            fx_step1_lds_m(vb, j0 + DX_Q, fsc[hh], fx_mask64(kmask[hh], j0 + DX_Q), acc, wa, wb);
         }
         acc = fx_key_slow(acc, vnew, fwl[hh]);
     }

@@ -1725,7 +1725,10 @@ extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_pa
         nkv[b] = n_past[b] + 1;
     }
     std::unique_lock<std::mutex> dev_lk;
-    if (takes_fused(c, B)) dev_lk = std::unique_lock<std::mutex>(device_lock(c->m->device));
+    if (takes_fused(c, B)) {
+        dev_lk = std::unique_lock<std::mutex>(device_lock(c->m->device));
+        if (int rc = reset_counters(c)) return rc;   // zero at rest whatever the previous call's launch modes were
+    }
     HIPCHK(hipMemcpyAsync(c->d_tok, tok, B * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemcpyAsync(c->d_pos, pos.data(), B * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemcpyAsync(c->d_nkv, nkv.data(), B * 4, hipMemcpyHostToDevice, c->st));
@@ -1760,7 +1763,13 @@ extern "C" int qasr_run(qasr_ctx *c, int max_tokens, int ignore_eos, int32_t *to
     if (B > c->max_batch) return fail(QASR_ERR_ARG, "staged clips exceed the context's max_batch (qasr_run_staged runs subsets)");
     HIPCHK(hipSetDevice(c->m->device));
     std::unique_lock<std::mutex> dev_lk;
-    if (takes_fused(c, B)) dev_lk = std::unique_lock<std::mutex>(device_lock(c->m->device));
+    if (takes_fused(c, B)) {
+        dev_lk = std::unique_lock<std::mutex>(device_lock(c->m->device));
+        // the fused launches re-arm the next layer's counters as they go; within
+        // a run the launch mode only moves from fused to separate (longer
+        // contexts), so zero them once here, whatever the previous run left
+        if (int rc = reset_counters(c)) return rc;
+    }
     HIPCHK(hipStreamSynchronize(c->st));
     c->pin_used = 0;
     qasr_model *m = c->m;
@@ -1963,7 +1972,10 @@ static int run_stream(qasr_ctx *c, int slots, const std::function<bool(StreamCli
     HIPCHK(hipSetDevice(c->m->device));
     const int S = slots ? slots : c->max_batch;
     std::unique_lock<std::mutex> dev_lk;
-    if (takes_fused(c, S)) dev_lk = std::unique_lock<std::mutex>(device_lock(c->m->device));
+    if (takes_fused(c, S)) {
+        dev_lk = std::unique_lock<std::mutex>(device_lock(c->m->device));
+        if (int rc = reset_counters(c)) return rc;
+    }
     HIPCHK(hipStreamSynchronize(c->st));
     c->pin_used = 0;
     const Hparams &hp = c->m->hp;

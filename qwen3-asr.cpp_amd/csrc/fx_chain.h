@@ -190,6 +190,47 @@ __device__ __forceinline__ void fx_step1_lds(const u32x4 *v, int j0, const float
     }
 }
 
+// fx_step1_lds with the slow path taken per 8-key group: m64 (uniform, in
+// SGPRs) = the 64 keys' new-maximum bits, bit i for key j0 + i.  A buffer
+// without a maximum runs the straight fast block (one branch per 64 keys);
+// one with a maximum decides per 8-key group, so only the groups holding one
+// run the slow asm block (per-group branches in every buffer measured 16 us a
+// chain against 13: a branch pair per 16 instructions); keys past the chunk
+// carry zero weights, which the fast path leaves as exact no-ops
+// (fma(v, 0, acc) = acc).  A running maximum over
+// n random scores has ~ln n records, so per-64-key decisions sent ~6 of 22
+// buffers of a 1.37k-key chain down the slow path.
+__device__ __forceinline__ void fx_step1_lds_m(const u32x4 *v, int j0, const float *ws, unsigned long long m64, f16 &acc,
+                                               floatx4 &wa, floatx4 &wb) {
+    if (__builtin_expect(m64 != 0ull, 0)) {   // out of line: per-group decisions only in a buffer holding a maximum
+#pragma unroll
+        for (int g8 = 0; g8 < DX_Q / 8; g8++) {
+            floatx4 na, nb;
+            fx_w8(ws, j0 + 8 * g8 + 8, na, nb);
+            if (((m64 >> (8 * g8)) & 0xffull) != 0) fx8_slow(acc, v[g8], wa, wb);
+            else fx8_fast(acc, v[g8], wa, wb);
+            wa = na;
+            wb = nb;
+        }
+    } else {
+#pragma unroll
+        for (int g8 = 0; g8 < DX_Q / 8; g8++) {
+            floatx4 na, nb;
+            fx_w8(ws, j0 + 8 * g8 + 8, na, nb);
+            fx8_fast(acc, v[g8], wa, wb);
+            wa = na;
+            wb = nb;
+        }
+    }
+}
+// the 64 new-maximum bits of keys j0 .. j0 + 63 from km (u16 per 16 keys) as a
+// uniform value
+__device__ __forceinline__ unsigned long long fx_mask64(const uint16_t *km, int j0) {
+    const uint2 m = *(const uint2 *)(km + j0 / 16);
+    return ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)m.y) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)m.x);
+}
+
 // DX_Q keys of V from key block j0 / 8 (vt: the wave's key block 0, uniform;
 // loff = 8 lane: kernels.h vt_index, 1024 halves per block)
 __device__ __forceinline__ void fx_loadQ(u32x4 *v, const uint16_t *__restrict__ vt, int loff, int j0) {

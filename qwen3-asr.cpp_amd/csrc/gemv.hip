@@ -15,10 +15,9 @@
 // fp16 (after rms_norm * w, text_decoder.cpp:480-481/546-547), fp32 sums.
 #include "dev_common.h"
 #include "kernels.h"
+#include "ffn_roles.h"
 
 namespace qasr {
-
-__device__ __forceinline__ float silu1(float g) { return g / (1.0f + expf(-g)); }
 
 template <int EPI, int K, int RPW>
 __global__ __launch_bounds__(256) void gemv1_kernel(GemvArgs g) {
@@ -183,139 +182,12 @@ static bool gemv1_k(const GemvArgs &g, hipStream_t s) {
 // next layer's (its last use ended a whole step ago), so the fusion needs two
 // or more layers.  The residual x is read by the gate/up blocks and rewritten
 // (row by row) by the down blocks only after every gate/up block has arrived.
-__device__ __forceinline__ void ld_sc1_x4_6(const uint16_t *p, u32x4 *v) {
-    asm volatile(
-        "global_load_dwordx4 %0, %6, off sc1\n\t"
-        "global_load_dwordx4 %1, %6, off offset:1024 sc1\n\t"
-        "global_load_dwordx4 %2, %6, off offset:2048 sc1\n\t"
-        "global_load_dwordx4 %3, %6, off offset:3072 sc1\n\t"
-        "global_load_dwordx4 %4, %7, off sc1\n\t"
-        "global_load_dwordx4 %5, %7, off offset:1024 sc1\n\t"
-        "s_waitcnt vmcnt(0)"
-        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5])
-        : "v"(p), "v"(p + 2048)
-        : "memory");
-}
-
-struct FfnCtl {
-    unsigned int *cnt, *cnt_next;   // this layer's 32 arrival shards (16-word stride), the next layer's
-    unsigned int *err;              // sticky device error word
-    int wdelay, delay, poll_limit, fence;
-};
-
 template <int K, int F>
 __global__ __launch_bounds__(256) void ffn1_kernel(GemvArgs g, GemvArgs d, FfnCtl c) {
-    constexpr int NT = K / 512, NTD = F / 512, NGU = F / 4;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr int NGU = F / 4;
     stamp_start(g.stamp);
-    if (blockIdx.x >= NGU) {   // ---- down projection
-        const int j = blockIdx.x - NGU, row = j * 4 + wid;
-        if (d.trace && threadIdx.x == 0) d.trace[j * 8] = rt_now();
-        for (int i = 0; i < c.wdelay; i++) __builtin_amdgcn_s_sleep(8);   // let the gate/up stream go first
-        half8 wv[NTD];
-#pragma unroll
-        for (int t = 0; t < NTD; t++) wv[t] = __builtin_nontemporal_load((const half8 *)(d.W + (long)row * F + t * 512 + lane * 8));
-        // one polling lane per block, and only once the gate/up stream is
-        // nearly done: pollers beside a weight stream cost it bandwidth
-        // (MI355X_MICROARCH.md, polling-cost)
-        __shared__ int ready;
-        if (wid == 0) {   // lane s polls shard s; every shard holds NGU / 32 arrivals when done
-            for (int i = 0; i < c.delay; i++) __builtin_amdgcn_s_sleep(8);
-            int ok = 0;
-            for (int it = 0; it < c.poll_limit; it++) {
-                const unsigned v = lane < 32 ? __hip_atomic_load(c.cnt + lane * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
-                if (__all(v >= (unsigned)(NGU / 32))) { ok = 1; break; }
-                __builtin_amdgcn_s_sleep(8);
-            }
-            if (c.fence) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            if (lane == 0) {
-                ready = ok;
-                if (!ok) __hip_atomic_fetch_or(c.err, (unsigned)DEVERR_FFN_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        __syncthreads();
-        if (!ready) { stamp_end(g.stamp); return; }   // reported through the error word; x keeps its old row
-        u32x4 xv[NTD];
-        static_assert(NTD == 6, "ld_sc1_x4_6 covers F = 3072");
-        ld_sc1_x4_6(d.xh + lane * 8, xv);
-        const float res = d.res[row];
-        float acc = 0.f;
-#pragma unroll
-        for (int t = 0; t < NTD; t++) {
-            const half8 h = __builtin_bit_cast(half8, xv[t]);
-#pragma unroll
-            for (int e = 0; e < 8; e++) acc = fmaf((float)wv[t][e], (float)h[e], acc);
-        }
-        acc = wave_sum(acc);
-        if (lane == 0) d.out_f32[row] = fadd_rn(acc, res);
-        if (d.trace && threadIdx.x == 0) d.trace[j * 8 + 1] = rt_now();
-        stamp_end(g.stamp);
-        return;
-    }
-    // ---- gate/up (16-row interleave: output o = rows 32 (o / 16) + o % 16 and + 16)
-    if (g.trace && threadIdx.x == 0) g.trace[blockIdx.x * 8] = rt_now();
-    if (blockIdx.x == 0 && threadIdx.x < 32) {   // re-arm: the next layer's shards and the fused o-proj's counters
-        c.cnt_next[threadIdx.x * 16] = 0u;
-        if (d.zero8 && threadIdx.x < 8) d.zero8[threadIdx.x * 16] = 0u;
-    }
-    const int o = blockIdx.x * 4 + wid;
-    half8 wv[2][NT];
-#pragma unroll
-    for (int q = 0; q < 2; q++)
-#pragma unroll
-        for (int t = 0; t < NT; t++)
-            wv[q][t] = __builtin_nontemporal_load((const half8 *)(g.W + (32L * (o >> 4) + (o & 15) + 16 * q) * K + t * 512 + lane * 8));
-    float xf[NT][8];
-#pragma unroll
-    for (int t = 0; t < NT; t++) {
-        const float4 a = *(const float4 *)(g.x + t * 512 + lane * 8);
-        const float4 b = *(const float4 *)(g.x + t * 512 + lane * 8 + 4);
-        xf[t][0] = a.x; xf[t][1] = a.y; xf[t][2] = a.z; xf[t][3] = a.w;
-        xf[t][4] = b.x; xf[t][5] = b.y; xf[t][6] = b.z; xf[t][7] = b.w;
-    }
-    double ss = 0.0;   // ggml_rms_norm: double sum of fp32 squares
-#pragma unroll
-    for (int t = 0; t < NT; t++)
-#pragma unroll
-        for (int e = 0; e < 8; e++) ss += (double)(xf[t][e] * xf[t][e]);
-    ss = wave_sum_d(ss);
-    const float scale = 1.0f / sqrtf((float)(ss / K) + g.eps);
-#pragma unroll
-    for (int t = 0; t < NT; t++) {
-        const float4 a = *(const float4 *)(g.norm_w + t * 512 + lane * 8);
-        const float4 b = *(const float4 *)(g.norm_w + t * 512 + lane * 8 + 4);
-        const float w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-        for (int e = 0; e < 8; e++) xf[t][e] = (float)f2h(fmul_rn(fmul_rn(xf[t][e], scale), w[e]));
-    }
-    float acc[2];
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-        acc[q] = 0.f;
-#pragma unroll
-        for (int t = 0; t < NT; t++)
-#pragma unroll
-            for (int e = 0; e < 8; e++) acc[q] = fmaf((float)wv[q][t][e], xf[t][e], acc[q]);
-        acc[q] = wave_sum(acc[q]);
-    }
-    __shared__ uint16_t outs[4];
-    if (lane == 0) outs[wid] = f_to_u16(silu1(acc[0]) * acc[1]);
-    __syncthreads();
-    if (wid == 0) {
-        if (lane < 2)
-            __hip_atomic_store((uint32_t *)(g.out_f16 + blockIdx.x * 4) + lane, (uint32_t)outs[2 * lane] | ((uint32_t)outs[2 * lane + 1] << 16),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (c.fence) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (lane == 0) __hip_atomic_fetch_add(c.cnt + (blockIdx.x & 31) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (g.trace && threadIdx.x == 0) g.trace[blockIdx.x * 8 + 1] = rt_now();
+    if (blockIdx.x >= NGU) ffn_dn_role<F, 1>(d, c, blockIdx.x - NGU, NGU / 32);
+    else ffn_gu_role<K, 1>(g, d, c, blockIdx.x);
     stamp_end(g.stamp);
 }
 

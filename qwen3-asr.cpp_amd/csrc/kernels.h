@@ -170,6 +170,12 @@ struct FuseCfg {
 // co-resident workgroup capacity of the fused kernels on the current device
 // (occupancy query x CUs); 0 = unknown (never fuse)
 void fused_slots(FuseCfg &cfg);
+// hand-off state of the batch-1 FFN roles (ffn_roles.h)
+struct FfnCtl {
+    unsigned int *cnt, *cnt_next;   // this layer's 32 gate/up arrival shards (16-word stride), the next layer's
+    unsigned int *err;              // sticky device error word
+    int wdelay, delay, poll_limit, fence;
+};
 // gemv.hip: batch-1 f16 gate/up + down in one launch; cnt = this layer's
 // 32 x 16 words (zero on entry), cnt_next = the next layer's, re-armed here
 // (false = not covered; dry: the decision only)

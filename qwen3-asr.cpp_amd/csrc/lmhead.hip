@@ -65,35 +65,44 @@ __global__ __launch_bounds__(64 * WPG) void lmhead_batch_kernel(GemvArgs g) {
 #pragma unroll
     for (int b = 0; b < D; b++) load(b, b);
 
-    // ---- prologue: rows -> RMS norm (rms_row<1024> arithmetic) -> fp16 LDS
-    for (int m = wid; m < MT * 16; m += WPG) {
-        if (m < M) {
-            const float *xr = g.x + (long)m * g.ldx;
-            float4 v[4], wv[4];
+    // ---- prologue: rows -> RMS norm (rms_row<1024> arithmetic) -> fp16 LDS;
+    //      the wave's rows in batches of RB, every load of a batch in flight
+    //      together (one row at a time left the weight ring idle for ~10 us at 64 rows)
+    constexpr int R = MT * 16 / WPG, RB = R < 4 ? R : 4;
+    static_assert(R * WPG == MT * 16, "rows split evenly over the waves");
+    float4 wv[4];
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                v[i] = *(const float4 *)(xr + 4 * lane + 256 * i);
-                wv[i] = *(const float4 *)(g.norm_w + 4 * lane + 256 * i);
-            }
+    for (int i = 0; i < 4; i++) wv[i] = *(const float4 *)(g.norm_w + 4 * lane + 256 * i);
+#pragma unroll
+    for (int r0 = 0; r0 < R; r0 += RB) {
+        float4 v[RB][4];
+#pragma unroll
+        for (int r = 0; r < RB; r++) {
+            const int m = wid + WPG * (r0 + r);
+            const float *xr = g.x + (long)(m < M ? m : 0) * g.ldx;
+#pragma unroll
+            for (int i = 0; i < 4; i++) v[r][i] = *(const float4 *)(xr + 4 * lane + 256 * i);
+        }
+#pragma unroll
+        for (int r = 0; r < RB; r++) {
+            const int m = wid + WPG * (r0 + r);
             double s = 0.0;
 #pragma unroll
             for (int i = 0; i < 4; i++)
-                s += ((double)fmul_rn(v[i].x, v[i].x) + (double)fmul_rn(v[i].y, v[i].y)) +
-                     ((double)fmul_rn(v[i].z, v[i].z) + (double)fmul_rn(v[i].w, v[i].w));
+                s += ((double)fmul_rn(v[r][i].x, v[r][i].x) + (double)fmul_rn(v[r][i].y, v[r][i].y)) +
+                     ((double)fmul_rn(v[r][i].z, v[r][i].z) + (double)fmul_rn(v[r][i].w, v[r][i].w));
             s = wave_sum_d(s);
             const float mean = (float)(s / LMH_K);
             const float scale = 1.0f / sqrtf(mean + g.eps);
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const uint32_t lo = f_to_u16(fmul_rn(fmul_rn(v[i].x, scale), wv[i].x)) |
-                                    ((uint32_t)f_to_u16(fmul_rn(fmul_rn(v[i].y, scale), wv[i].y)) << 16);
-                const uint32_t hi = f_to_u16(fmul_rn(fmul_rn(v[i].z, scale), wv[i].z)) |
-                                    ((uint32_t)f_to_u16(fmul_rn(fmul_rn(v[i].w, scale), wv[i].w)) << 16);
+                uint32_t lo = f_to_u16(fmul_rn(fmul_rn(v[r][i].x, scale), wv[i].x)) |
+                              ((uint32_t)f_to_u16(fmul_rn(fmul_rn(v[r][i].y, scale), wv[i].y)) << 16);
+                uint32_t hi = f_to_u16(fmul_rn(fmul_rn(v[r][i].z, scale), wv[i].z)) |
+                              ((uint32_t)f_to_u16(fmul_rn(fmul_rn(v[r][i].w, scale), wv[i].w)) << 16);
+                if (m >= M) lo = hi = 0u;   // rows past M: zeros
                 *(uint2 *)(xs + lmh_off(m, 4 * lane + 256 * i)) = make_uint2(lo, hi);
             }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 4; i++) *(uint2 *)(xs + lmh_off(m, 4 * lane + 256 * i)) = make_uint2(0u, 0u);
         }
     }
     __syncthreads();
@@ -186,9 +195,10 @@ __global__ __launch_bounds__(64 * WPG) void lmhead_batch_kernel(GemvArgs g) {
     stamp_end(g.stamp);
 }
 
-// 16 waves a CU with a 3-deep ring up to 16 rows; more rows need more than
-// 128 VGPRs (the running keys and both accumulator sets), so 8 waves with a 4-deep ring
-template <int MT, int WPG = (MT < 2 ? 16 : 8), int D = (MT < 2 ? 3 : 4)>
+// 8 waves a CU with a 4-deep ring (tools/micro/lmh_bench.hip, MI355X: 16 rows
+// 60.8 us against 68.9 with 16 waves x 3; 64 rows: 6- and 8-deep rings and 4
+// waves x 8 or 12 slower)
+template <int MT, int WPG = 8, int D = 4>
 void run_lmhead(const GemvArgs &g, hipStream_t s) {
     static int ncu_dev[64];   // per device: CU count once the LDS attribute is set
     int dev = 0;

@@ -6,6 +6,8 @@
 //   mode 2: fast path only, V^T not reloaded (first two buffers reused)
 //   mode 3: as 2, and the weights not reloaded from LDS (fx8_fast on fixed registers)
 //   mode 4: as 0 (V^T reloaded), weights not reloaded from LDS
+//   mode 5: as 0 with the slow path per 8-key group (fx_step1_lds_m): argv[3]
+//           = the 64-bit new-maximum mask of every 64-key buffer
 //   argv[2] = waves per workgroup (4 or 1); argv[3] = the batches' slow-path flags (default 0)
 // Prints cycles per key (s_memtime), mean over the chain waves.
 #include <hip/hip_runtime.h>
@@ -44,6 +46,14 @@ __global__ __launch_bounds__(256) void chain_k(const uint16_t *vt_all, const flo
 #pragma unroll
                 for (int g8 = 0; g8 < DX_Q / 8; g8++) fx8_fast(acc, vb[g8], wa, wb);
             }
+        } else if constexpr (MODE == 5) {
+            for (int j0 = 0; j0 < n; j0 += 2 * DX_Q) {
+                fx_loadQ(vb, vt, loff, j0 + DX_Q);
+                fx_step1_lds_m(va, j0, ws[wid], (unsigned long long)__builtin_amdgcn_readfirstlane((int)flags) |
+                               ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(flags >> 32)) << 32), acc, wa, wb);
+                fx_loadQ(va, vt, loff, j0 + 2 * DX_Q);
+                fx_step1_lds_m(vb, j0 + DX_Q, ws[wid], 0ull, acc, wa, wb);
+            }
         } else
         for (int j0 = 0; j0 < n; j0 += 2 * DX_Q) {
             if constexpr (MODE < 2) fx_loadQ(vb, vt, loff, j0 + DX_Q);
@@ -79,6 +89,7 @@ int main(int argc, char **argv) {
         if (mode == 2) hipLaunchKernelGGL(chain_k<2>, dim3(blocks), dim3(64 * wpb), 0, 0, vt, w, n, c, o, flags);
         if (mode == 3) hipLaunchKernelGGL(chain_k<3>, dim3(blocks), dim3(64 * wpb), 0, 0, vt, w, n, c, o, flags);
         if (mode == 4) hipLaunchKernelGGL(chain_k<4>, dim3(blocks), dim3(64 * wpb), 0, 0, vt, w, n, c, o, flags);
+        if (mode == 5) hipLaunchKernelGGL(chain_k<5>, dim3(blocks), dim3(64 * wpb), 0, 0, vt, w, n, c, o, flags);
         (void)hipDeviceSynchronize();
     }
     long long hc[32];

@@ -75,6 +75,21 @@ static double time_graph(F step, const std::vector<uint16_t *> &ws, hipStream_t 
     return best * 1e3 / NREP;
 }
 
+template <int MT, int WPG, int D>
+static void variant(const Bufs &b, const std::vector<uint16_t *> &ws, int M, int N, hipStream_t s) {
+    (void)hipFuncSetAttribute((const void *)lmhead_batch_kernel<MT, WPG, D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              MT * 16 * 1024 * 2);
+    GemvArgs g{};
+    g.x = b.x; g.ldx = 1024; g.norm_w = b.normw; g.eps = 1e-6f; g.K = 1024; g.N = N; g.M = M;
+    g.amax = b.amax; g.done = b.done; g.tok_out = b.tok;
+    g.hist = b.hist; g.hist_stride = 64; g.step = b.step; g.pos = b.pos; g.nkv = b.nkv;
+    const double t = time_graph([&](const uint16_t *W) {
+        g.W = W;
+        hipLaunchKernelGGL((lmhead_batch_kernel<MT, WPG, D>), dim3(256), dim3(64 * WPG), MT * 16 * 1024 * 2, s, g);
+    }, ws, s);
+    printf("  M=%d MT%d WPG%2d D%d  %7.2f us  %.3f of 8 TB/s\n", M, MT, WPG, D, t, (double)N * 2048 / t * 1e-3 / 8000.0);
+}
+
 int main() {
     const int N = 151936;
     hipStream_t s; CK(hipStreamCreate(&s));
@@ -139,5 +154,15 @@ int main() {
                ok ? "OK" : "MISMATCH");
         bad += !ok;
     }
+    reset_state(b);
+    variant<4, 8, 4>(b, ws, 64, N, s);
+    variant<4, 8, 6>(b, ws, 64, N, s);
+    variant<4, 8, 8>(b, ws, 64, N, s);
+    variant<4, 4, 8>(b, ws, 64, N, s);
+    variant<4, 4, 12>(b, ws, 64, N, s);
+    variant<1, 16, 3>(b, ws, 16, N, s);
+    variant<1, 8, 4>(b, ws, 16, N, s);
+    variant<1, 8, 8>(b, ws, 16, N, s);
+    variant<2, 8, 8>(b, ws, 32, N, s);
     return bad ? 1 : 0;
 }
