@@ -365,14 +365,14 @@ void launch_prefill_attention_exact(const PrefillAttnArgs &a, hipStream_t s) {
 // unconditionally (vt_ctx carries read-ahead slack), so the wait counts stay
 // exact.  c0: the first key of the current weights chunk.
 __device__ __forceinline__ void fx_chain1(const uint16_t *__restrict__ vt, int loff, int c0, int n, const float *w,
-                                          unsigned long long flags, f16 &acc) {
+                                          unsigned long long flags, uint32_t kb, f16 &acc) {
     u32x4 va[DX_Q / 8], vb[DX_Q / 8];
     fx_loadQ(va, vt, loff, c0);
     for (int j0 = 0; j0 < n; j0 += 2 * DX_Q) {
         fx_loadQ(vb, vt, loff, c0 + j0 + DX_Q);
-        fx_step1(va, j0, n, w, flags, acc);
+        fx_step1_m(va, j0, n, w, flags, kb, acc);
         fx_loadQ(va, vt, loff, c0 + j0 + 2 * DX_Q);
-        fx_step1(vb, j0 + DX_Q, n, w, flags, acc);
+        fx_step1_m(vb, j0 + DX_Q, n, w, flags, kb, acc);
     }
 }
 
@@ -399,11 +399,12 @@ __device__ __forceinline__ void decode_attn_exact_body(const DecodeAttnArgs &a, 
         unsigned long long flags;
         const float Mold = M;
         const float *sc = sg + c0;
-        const float Sc = fx_weights_reg([&](int j) { return sc[j]; }, n, M, w, flags, wl);
+        uint32_t kb;
+        const float Sc = fx_weights_reg([&](int j) { return sc[j]; }, n, M, w, flags, wl, &kb);
         S = (Mold == -INFINITY ? 0.0f : S * expf(Mold - M)) + Sc;
         FX_CLK(tb);
         FX_ADD(0, tb - ta);
-        fx_chain1(vcol, 8 * lane, c0, n, w, flags, acc);
+        fx_chain1(vcol, 8 * lane, c0, n, w, flags, kb, acc);
         FX_CLK(tc);
         FX_ADD(1, tc - tb);
     }

@@ -99,6 +99,35 @@ __device__ __forceinline__ void fx_step1(const u32x4 *v, int j0, int n, const fl
         }
     }
 }
+// fx_step1 with the slow path decided per 8-key group inside a flagged batch:
+// kb = this lane's new-maximum bits (bit i: key 32 lane + i, fx_weights_reg),
+// read for batch L by v_readlane; groups without a maximum take the fast path
+// (keys past n carry zero weights: exact no-ops there)
+__device__ __forceinline__ void fx_step1_m(const u32x4 *v, int j0, int n, const float *w, unsigned long long flags, uint32_t kb,
+                                           f16 &acc) {
+#pragma unroll
+    for (int bq = 0; bq < DX_Q / DX_B; bq++) {
+        const int jb = j0 + bq * DX_B;
+        const int L = jb / DX_B;
+        if (jb >= n) break;
+        if (!((flags >> L) & 1ull)) {
+#pragma unroll
+            for (int i = 0; i < DX_B; i++) acc = fx_mad1(acc, fx_elem(v, bq * DX_B + i), fx_lane(w[i], L));
+        } else {
+            const uint32_t m32 = (uint32_t)__builtin_amdgcn_readlane((int)kb, L);
+#pragma unroll
+            for (int g = 0; g < DX_B / 8; g++) {
+                if ((m32 >> (8 * g)) & 0xffu) {
+#pragma unroll
+                    for (int i = 8 * g; i < 8 * g + 8; i++) acc = fx_key_slow(acc, fx_elem(v, bq * DX_B + i), fx_lane(w[i], L));
+                } else {
+#pragma unroll
+                    for (int i = 8 * g; i < 8 * g + 8; i++) acc = fx_mad1(acc, fx_elem(v, bq * DX_B + i), fx_lane(w[i], L));
+                }
+            }
+        }
+    }
+}
 // fx_step1 with the weights in LDS instead of registers (the fused launch's
 // chain role): ws = the head's signed weights, FX_ST floats per 32-key row
 // (row L = lane L's keys of fx_weights_reg).  Per 8 keys the weights arrive
@@ -245,7 +274,8 @@ __device__ __forceinline__ void fx_loadQ(u32x4 *v, const uint16_t *__restrict__ 
 // maximum (per lane a sequential S = S * ms + vs as ggml, the lanes combined
 // in fp32).  wlast: the weight of key n - 1 (uniform).
 template <class Src>
-__device__ __forceinline__ float fx_weights_reg(Src src, int n, float &M, float *w, unsigned long long &flags, float &wlast) {
+__device__ __forceinline__ float fx_weights_reg(Src src, int n, float &M, float *w, unsigned long long &flags, float &wlast,
+                                                uint32_t *kbits = nullptr) {
     const int lane = threadIdx.x & 63;
     float lm = -INFINITY;
 #pragma unroll
@@ -262,6 +292,7 @@ __device__ __forceinline__ float fx_weights_reg(Src src, int n, float &M, float 
     // a new maximum gives ms = expf(Mold - M) (0 before the first key), stored
     // negated (its vs = 1); any other key vs = expf(s - M)
     bool nm = false;
+    uint32_t kb = 0;
 #pragma unroll
     for (int i = 0; i < DX_B; i++) {
         const float s = w[i];
@@ -270,7 +301,9 @@ __device__ __forceinline__ float fx_weights_reg(Src src, int n, float &M, float 
         w[i] = gt ? -e : (s != -INFINITY ? e : 0.0f);
         Mp = fmaxf(Mp, s);
         nm = nm || gt;
+        kb |= (uint32_t)gt << i;
     }
+    if (kbits) *kbits = kb;
     // the lane's sequential S = S * ms + vs, (ms, vs) recovered from the signed
     // weight (a second pass: the first keeps only w[] live)
     float Sl = 0.0f, wl = 0.0f;
