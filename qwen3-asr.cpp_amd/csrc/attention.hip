@@ -667,9 +667,11 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     const float w0 = nw[lane], w1 = nw[lane + 64];
     if constexpr (FUSED)   // let the QKV blocks' weight stream get ahead in the memory queues
         for (int i = 0; i < a.fuse_delay; i++) __builtin_amdgcn_s_sleep(8);
-    // ---- every K/V row of the split (addresses depend on blockIdx only; decode
-    //      contexts use identity sequence slots).  Rows past the position are
-    //      masked below; the cache is zero-initialised so they are finite.
+    // ---- every K/V row of the split (addresses depend on blockIdx only).  Decode
+    //      rows are cache slots: row b of a decode step is slot b (qasr_run_stream
+    //      refills a finished slot in place, its prefill writing through seq_slot
+    //      = b), so b indexes the K/V and V^T caches alike.  Rows past the position
+    //      are masked below; the cache is zero-initialised so they are finite.
     const long cbase = ((long)b * a.n_kv_head + g) * a.max_ctx;
     uint16_t *kc = a.kc + cbase * 128, *vc = a.vc + cbase * 128;
     const int k0 = sp * SPL;

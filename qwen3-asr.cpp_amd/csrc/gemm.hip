@@ -36,20 +36,20 @@ __device__ __forceinline__ float silu_f(float g) { return g / (1.0f + expf(-g));
 
 // ------------------------------------------------------------ epilogue
 // acc[i][j] holds rows m0 + wr*BM/2 + 16i + 4(lane>>4) + r, column
-// n0 + wc*BN/2 + 16j + (lane&15) (v_mfma_*_16x16x* C layout)
-template <int BM, int BN, int EPI>
-__device__ __forceinline__ void gemm_epilogue(const GemmArgs &g, floatx4 (&acc)[BM / 32][BN / 32], int m0, int n0, int wr,
+// n0 + wc*BN/WNW + 16j + (lane&15) (v_mfma_*_16x16x* C layout; WNW waves along N)
+template <int BM, int BN, int EPI, int WNW = 2>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs &g, floatx4 (&acc)[BM / 32][BN / (16 * WNW)], int m0, int n0, int wr,
                                               int wc, int lane) {
-    constexpr int FM = BM / 32, FN = BN / 32;
+    constexpr int FM = BM / 32, FN = BN / (16 * WNW);
     const int M = g.M;
     const int rbase = m0 + wr * (BM / 2) + 4 * (lane >> 4);
-    const int cbase = n0 + wc * (BN / 2) + (lane & 15);
+    const int cbase = n0 + wc * (BN / WNW) + (lane & 15);
     if constexpr (EPI == EPI_SWIGLU_F16 || EPI == EPI_SWIGLU_F32) {
 #pragma unroll
         for (int i = 0; i < FM; i++)
 #pragma unroll
             for (int p = 0; p < FN / 2; p++) {
-                const int ocol = (n0 + wc * (BN / 2)) / 2 + p * 16 + (lane & 15);
+                const int ocol = (n0 + wc * (BN / WNW)) / 2 + p * 16 + (lane & 15);
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const int row = rbase + i * 16 + r;
@@ -261,15 +261,19 @@ __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int KS, int NB, int AMODE, int EPI>
-__global__ __launch_bounds__(256) void gemm_glds_kernel(GemmArgs g) {
-    constexpr int FM = BM / 32, FN = BN / 32;
+// WNW: waves along N (2: 4 waves in a 2 x 2 grid, each BM/2 x BN/2; 4: 8 waves
+// in 2 x 4, each BM/2 x BN/4 -- the 256-row tiles, whose 128 KiB of stages leave
+// one workgroup a CU)
+template <int BM, int BN, int KS, int NB, int AMODE, int EPI, int WNW = 2>
+__global__ __launch_bounds__(128 * WNW) void gemm_glds_kernel(GemmArgs g) {
+    constexpr int NWAVE = 2 * WNW, NTHR = 64 * NWAVE;
+    constexpr int FM = BM / 32, FN = BN / (16 * WNW);
     constexpr int ROWS = BM + BN;
     constexpr int SLAB = ROWS * 32;        // halves per 32-deep slab
     constexpr int RG = ROWS / 16;          // 1-KiB pieces per slab
     constexpr int NP = KS * RG;            // pieces per stage
-    constexpr int NW = (NP + 3) / 4;       // pieces per wave per stage (uniform: vmcnt counts)
-    constexpr int PAD = NW * 4 - NP;       // dummy pieces (zero line -> a scratch KiB) keep it uniform
+    constexpr int NW = (NP + NWAVE - 1) / NWAVE;   // pieces per wave per stage (uniform: vmcnt counts)
+    constexpr int PAD = NW * NWAVE - NP;   // dummy pieces (zero line -> a scratch KiB) keep it uniform
     static_assert(ROWS % 16 == 0, "16-row pieces");
     static_assert(NB >= 2 && NB <= 4 && (NB - 2) * NW < 64, "ring depth");
     constexpr int INFO = AMODE == AM_DENSE ? 0 : BM * 8;   // int4 row descriptors (conv modes)
@@ -278,12 +282,12 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmArgs g) {
     int4 *rowinfo = (int4 *)(smem + NB * KS * SLAB + SCR);
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wr = wid >> 1, wc = wid & 1;
+    const int wr = wid / WNW, wc = wid % WNW;
     const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
     const int M = g.M, K = g.K;
 
     if constexpr (AMODE != AM_DENSE) {
-        for (int r = tid; r < BM; r += 256) {
+        for (int r = tid; r < BM; r += NTHR) {
             const int row = m0 + r;
             int4 info = make_int4(-1, 0, 0, 0);
             if (row < M) {
@@ -319,7 +323,7 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmArgs g) {
         }
 #pragma unroll
         for (int p = 0; p < NW; p++) {
-            const int i = wid + 4 * p;
+            const int i = wid + NWAVE * p;
             if (PAD && i >= NP) {   // wave-uniform
                 __builtin_amdgcn_global_load_lds((glb_void_g *)g_zero_line, (lds_void_g *)(smem + NB * KS * SLAB), 16, 0, 0);
                 continue;
@@ -384,7 +388,7 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmArgs g) {
             }
 #pragma unroll
             for (int j = 0; j < FN; j++) {
-                const int r = BM + wc * (BN / 2) + j * 16 + (lane & 15);
+                const int r = BM + wc * (BN / WNW) + j * 16 + (lane & 15);
                 bf[j] = *(const half8 *)(sl + r * 32 + ((q ^ ((r >> 1) & 3)) << 3));
             }
 #pragma unroll
@@ -394,7 +398,7 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmArgs g) {
         }
         if (++buf == NB) buf = 0;
     }
-    gemm_epilogue<BM, BN, EPI>(g, acc, m0, n0, wr, wc, lane);
+    gemm_epilogue<BM, BN, EPI, WNW>(g, acc, m0, n0, wr, wc, lane);
 }
 
 template <int BM, int BN, int KS, int AMODE, int EPI>
@@ -403,10 +407,10 @@ static void run_gemm(const GemmArgs &g, hipStream_t s) {
     hipLaunchKernelGGL((gemm_kernel<BM, BN, KS, AMODE, EPI>), grid, dim3(256), 0, s, g);
 }
 
-template <int BM, int BN, int KS, int NB, int AMODE, int EPI>
+template <int BM, int BN, int KS, int NB, int AMODE, int EPI, int WNW = 2>
 static void run_glds(const GemmArgs &g, hipStream_t s) {
     dim3 grid(g.N / BN, (g.M + BM - 1) / BM);
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, KS, NB, AMODE, EPI>), grid, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, KS, NB, AMODE, EPI, WNW>), grid, dim3(128 * WNW), 0, s, g);
 }
 
 template <int AMODE, int EPI>
@@ -430,9 +434,19 @@ static void dispatch_tiles(const GemmArgs &g, hipStream_t s) {
         // (one 32-deep slab per stage up to K = 1024); ~1.2k rows (a 92 s
         // clip) -> 64x64 with 4 slabs per stage for the narrow, deep
         // projections (N <= 1024), 96x64 for the wide ones (N >= 3072)
+        // round 3 (tools/micro/glds_gemm_bench.hip, MI355X, us per launch): 256 x 256
+        // tiles on 8 waves with a 3-stage ring for the large shapes whose N takes
+        // them (64 x 30 s prefill dn 272 -> 222, qkv 388 -> 374); 128 x 128 on 8
+        // waves, 4-stage ring, for the wide projections of one clip (~1.2k rows:
+        // prefill gate/up 39.6 -> 29.4, qkv 27.3 -> 25.1, encoder fc1 22.6 -> 21.3,
+        // encoder qkv 19.8 -> 18.9; the narrow deep ones stay on 64 x 64 x 4)
         const bool big = g.M >= 2048 && g.N % 128 == 0;
-        if (big && !g.regs_staged) {   // LDS-DMA stages (tools/micro/glds_gemm_bench.hip: +5-10 %)
+        if (big && !g.regs_staged && g.N % 256 == 0) {
+            run_glds<256, 256, 1, 3, AMODE, EPI, 4>(g, s);
+        } else if (big && !g.regs_staged) {   // LDS-DMA stages (tools/micro/glds_gemm_bench.hip: +5-10 %)
             run_glds<128, 128, 1, 2, AMODE, EPI>(g, s);
+        } else if (!big && !g.regs_staged && g.N >= 2048 && g.N % 128 == 0 && g.K % 32 == 0) {
+            run_glds<128, 128, 1, 3, AMODE, EPI, 4>(g, s);
         } else if (big && g.K % 64 == 0) {
             if (g.K <= 1024) run_gemm<128, 128, 1, AMODE, EPI>(g, s);
             else run_gemm<128, 128, 2, AMODE, EPI>(g, s);

@@ -50,14 +50,14 @@ static void ref(GemmArgs g, hipStream_t s) {
     printf("  regs  %3dx%-3d KS%d      %8.1f us  %7.1f TFLOP/s\n", BM, BN, KS, us, 2.0 * g.M * g.N * g.K / us * 1e-6);
 }
 
-template <int BM, int BN, int KS, int NB>
+template <int BM, int BN, int KS, int NB, int WNW = 2>
 static void glds(GemmArgs g, hipStream_t s) {
-    if (g.N % BN || g.K % (32 * KS)) { printf("  glds  %3dx%-3d KS%d NB%d  n/a\n", BM, BN, KS, NB); return; }
+    if (g.N % BN || g.K % (32 * KS)) { printf("  glds  %3dx%-3d KS%d NB%d W%d  n/a\n", BM, BN, KS, NB, 2 * WNW); return; }
     dim3 grid(g.N / BN, (g.M + BM - 1) / BM);
     CK(hipMemset(g.out_f32, 0, (size_t)g.M * g.N * 4));
-    double us = timeit([&] { hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, KS, NB, AM_DENSE, EPI_F32>), grid, dim3(256), 0, s, g); }, s);
-    printf("  glds  %3dx%-3d KS%d NB%d  %8.1f us  %7.1f TFLOP/s  maxdiff %.3g\n", BM, BN, KS, NB, us, 2.0 * g.M * g.N * g.K / us * 1e-6,
-           maxdiff(g.out_f32, (size_t)g.M * g.N));
+    double us = timeit([&] { hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, KS, NB, AM_DENSE, EPI_F32, WNW>), grid, dim3(128 * WNW), 0, s, g); }, s);
+    printf("  glds  %3dx%-3d KS%d NB%d W%d  %8.1f us  %7.1f TFLOP/s  maxdiff %.3g\n", BM, BN, KS, NB, 2 * WNW, us,
+           2.0 * g.M * g.N * g.K / us * 1e-6, maxdiff(g.out_f32, (size_t)g.M * g.N));
 }
 
 int main(int argc, char **argv) {
@@ -76,19 +76,42 @@ int main(int argc, char **argv) {
         CK(hipMemcpy(A, h.data(), MA * 2, hipMemcpyHostToDevice));
         CK(hipMemcpy(W, h.data() + 7, MW * 2, hipMemcpyHostToDevice));
     }
+    const bool b1only = argc > 1 && argv[1][0] == '1';
+    if (b1only) {   // single-clip (configs[1]) shapes: the dispatch's register tiles against 8-wave LDS-DMA tiles
+        Sh b1[] = {{"enc qkv b1", 1196, 2688, 896}, {"enc fc1 b1", 1196, 3584, 896}, {"enc fc2 b1", 1196, 896, 3584},
+                   {"enc o b1", 1196, 896, 896},    {"pre qkv b1", 1211, 4096, 1024}, {"pre o b1", 1211, 1024, 2048},
+                   {"pre gu b1", 1211, 6144, 1024}, {"pre dn b1", 1211, 1024, 3072}};
+        for (const Sh &sh : b1) {
+            GemmArgs g{};
+            g.A = A; g.lda = sh.K; g.W = W; g.ldw = sh.K; g.M = sh.M; g.N = sh.N; g.K = sh.K; g.out_f32 = out; g.ldo = sh.N;
+            printf("%s  M=%d N=%d K=%d\n", sh.name, sh.M, sh.N, sh.K);
+            ref<64, 64, 2>(g, s);
+            if (sh.K % 128 == 0) ref<64, 64, 4>(g, s);
+            if (sh.N % 96 == 0 || true) ref<96, 64, 2>(g, s);
+            glds<128, 128, 1, 2>(g, s);
+            glds<128, 128, 1, 4, 4>(g, s);
+            glds<128, 128, 1, 3, 4>(g, s);
+            glds<64, 128, 1, 4, 4>(g, s);
+            glds<128, 64, 1, 4, 4>(g, s);
+            glds<64, 64, 1, 4, 2>(g, s);
+            glds<64, 256, 1, 4, 4>(g, s);
+        }
+        return 0;
+    }
     for (const Sh &sh : shapes) {
         GemmArgs g{};
         g.A = A; g.lda = sh.K; g.W = W; g.ldw = sh.K; g.M = sh.M; g.N = sh.N; g.K = sh.K; g.out_f32 = out; g.ldo = sh.N;
         printf("%s  M=%d N=%d K=%d\n", sh.name, sh.M, sh.N, sh.K);
         ref<128, 128, 1>(g, s);
         glds<128, 128, 1, 2>(g, s);
-        glds<128, 128, 1, 3>(g, s);
-        glds<128, 128, 1, 4>(g, s);
-        glds<128, 128, 2, 2>(g, s);
-        glds<128, 128, 2, 3>(g, s);
-        glds<128, 64, 2, 3>(g, s);
-        glds<64, 128, 2, 3>(g, s);
-        glds<96, 160, 1, 4>(g, s);
+        glds<256, 256, 1, 4, 4>(g, s);
+        glds<256, 256, 1, 3, 4>(g, s);
+        glds<256, 256, 2, 2, 4>(g, s);
+        glds<256, 128, 1, 4, 4>(g, s);
+        glds<256, 128, 2, 3, 4>(g, s);
+        glds<256, 128, 1, 4, 2>(g, s);
+        glds<128, 256, 1, 4, 4>(g, s);
+        glds<128, 128, 1, 4, 4>(g, s);
     }
     return 0;
 }

@@ -1,0 +1,8 @@
+# 8-wave LDS-DMA GEMM tiles in the dispatch: parity / bit-identity tests, configs[1] and 64 x 30 s lines
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 800 python -u -m pytest tests/test_gpu_full.py tests/test_gpu_parity.py tests/test_gpu_aligner.py tests/test_hf_anchor.py -x -q --timeout 580 --timeout-method thread -k "not fused and not two_threads and not wait_timeout" > gpurun_out/r3t_t.log 2>&1; rc=$?; tail -3 gpurun_out/r3t_t.log; [ $rc -ne 0 ] && { grep -E "FAIL|Error" gpurun_out/r3t_t.log | head; exit $rc; }
+timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/r3t_b1.log 2>&1 || exit 1
+grep '^{' gpurun_out/r3t_b1.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c1', d['value'], d['stage_ms_per_step_rank0'], d['encoder_roofline']['frac'])"
+timeout -k 10 300 python -u bench.py --batch 64 --seconds 30 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/r3t_b64.log 2>&1 || exit 1
+grep '^{' gpurun_out/r3t_b64.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('b64', d['value'], d['stage_ms_per_step_rank0'], d['encoder_roofline']['frac'])"
