@@ -20,6 +20,7 @@
 
 #include "dev_common.h"
 #include "fx_chain.h"
+#include "fx_decode.h"
 #include "kernels.h"
 
 namespace qasr {
@@ -1071,8 +1072,18 @@ __device__ __forceinline__ void kvc_step(const DecodeAttnArgs &a, const half8 *q
     }
 }
 
-// grid (n_kv_head, B): kv group g of sequence b, both of its query heads
+// grid (n_kv_head, B): kv group g of sequence b, both of its query heads.
+// FX = 1: ggml's fp16-accumulating attention in one launch -- the scores
+// pass below writes both heads' scaled scores into LDS (dynamic, [2][max_ctx])
+// instead of global memory, and after one barrier the four waves run
+// fx_decode.h's chain (wave w: head 2 g + w / 2, dimensions 64 (w & 1) ..),
+// exactly the arithmetic of decode_attn_seq_kernel<0> in scores mode followed
+// by decode_attn_exact_pair_kernel, so the outputs are bit-identical; the
+// kernel boundary, the scores' round trip through HBM and the second
+// launch's ramp go, and one CU's workgroups overlap their K and V^T streams.
+template <int FX>
 __global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float fxs[];
     __shared__ __attribute__((aligned(16))) uint16_t qs[2][128];
     __shared__ __attribute__((aligned(16))) uint16_t knew[128];
     __shared__ __attribute__((aligned(16))) uint16_t vnew[128];
@@ -1086,7 +1097,7 @@ __global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) 
     const long cbase = ((long)b * a.n_kv_head + g) * a.max_ctx;
     uint16_t *kc = a.kc + cbase * 128, *vc = a.vc + cbase * 128;
     const int pos = a.pos[b], nkv = pos + 1, kcap = min(pos, a.max_ctx - 1);
-    const bool want_v = !a.scores;
+    const bool want_v = !FX && !a.scores;
     KvChunk A, B;
     kvc_issue(kc, vc, 0, kcap, want_v, A, a.kv_nt);
     // ---- the token's q / k / v: rms norm * weight + NEOX RoPE (decode_attn_body), new K/V row to the caches
@@ -1124,7 +1135,7 @@ __global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) 
 #pragma unroll
     for (int s4 = 0; s4 < 4; s4++)
         qa[s4] = c16 < 2 ? *(const half8 *)&qs[c16][32 * s4 + 8 * q4] : half8{0, 0, 0, 0, 0, 0, 0, 0};
-    float *sdst = a.scores ? a.scores + ((long)b * a.n_head + 2 * g) * a.max_ctx : nullptr;
+    float *sdst = FX ? fxs : a.scores ? a.scores + ((long)b * a.n_head + 2 * g) * a.max_ctx : nullptr;
     SeqSt st;
     st.m0 = st.m1 = -INFINITY;
     st.l0 = st.l1 = 0.f;
@@ -1136,6 +1147,12 @@ __global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) 
         if (c0 + 64 >= nkv) break;
         if (c0 + 128 < nkv) kvc_issue(kc, vc, c0 + 128, kcap, want_v, A, a.kv_nt);
         kvc_step(a, qa, knew, vnew, c0 + 64, pos, B, st, sdst);
+    }
+    if constexpr (FX) {
+        __syncthreads();   // both heads' scores in LDS; the new V^T row stored (this workgroup's own writes)
+        decode_attn_exact_body(a, 2 * g + (wid >> 1), b, wid & 1, fxs + (wid >> 1) * a.max_ctx);
+        stamp_end(a.stamp);
+        return;
     }
     if (sdst) { stamp_end(a.stamp); return; }
     // ---- merge: lanes of equal dl hold partial O over their keys (sub = 0..3): sum over sub, then over waves
@@ -1186,7 +1203,7 @@ __global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) 
 int decode_stream_slots() {
     int nb = 0, dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(decode_attn_seq_kernel), 256, 0) !=
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(decode_attn_seq_kernel<0>), 256, 0) !=
             hipSuccess)
         return 0;
     return nb * cus;
@@ -1436,13 +1453,14 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         const int nl = n - 1;
         u32x4 va[DX_Q / 8], vb[DX_Q / 8];
         floatx4 wa, wb;
-        fx_loadQ(va, vt, loff, 0);
+        const int lastb = nl > 0 ? (nl - 1) >> 3 : 0;
+        fx_loadQ(va, vt, loff, 0, lastb);
         fx_w8(fsc[hh], 0, wa, wb);
         for (int j0 = 0; j0 < nl; j0 += 2 * DX_Q) {
-            fx_loadQ(vb, vt, loff, j0 + DX_Q);
+            fx_loadQ(vb, vt, loff, j0 + DX_Q, lastb);
             fx_step1_lds_m(va, j0, fsc[hh], fx_mask64(kmask[hh], j0), acc, wa, wb);
             if (j0 + DX_Q >= nl) break;
-            fx_loadQ(va, vt, loff, j0 + 2 * DX_Q);
+            fx_loadQ(va, vt, loff, j0 + 2 * DX_Q, lastb);
             fx_step1_lds_m(vb, j0 + DX_Q, fsc[hh], fx_mask64(kmask[hh], j0 + DX_Q), acc, wa, wb);
         }
         acc = fx_key_slow(acc, vnew, fwl[hh]);
@@ -1628,7 +1646,7 @@ void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {
         }
     } else if (a.stream_blocks > 0 && a.n_head == 2 * a.n_kv_head && a.n_kv_head * a.B >= a.stream_blocks / 2) {
         // batches that give every CU a sequence or more: one workgroup per (kv group, sequence)
-        hipLaunchKernelGGL(decode_attn_seq_kernel, dim3(a.n_kv_head, a.B), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(decode_attn_seq_kernel<0>, dim3(a.n_kv_head, a.B), dim3(256), 0, s, a);
     } else {   // batches: longer splits (fewer workgroups and partials per sequence)
         if (a.spl_batch == 128) {
             const int g2 = (a.grid_splits * DSPLIT + 127) / 128;
@@ -1638,6 +1656,18 @@ void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {
             hipLaunchKernelGGL(decode_attn_kernel<256>, dim3(g4, a.n_kv_head, a.B), dim3(256), 0, s, a);
         }
     }
+}
+
+// the one-launch exact attention of a decode batch where the per-sequence
+// kernel is taken (launch_decode_attention) and both heads' scores fit the
+// LDS budget; false = not covered (the caller runs scores + chain launches)
+bool launch_decode_attention_exact_seq(const DecodeAttnArgs &a, hipStream_t s) {
+    const size_t lds = (size_t)2 * a.max_ctx * sizeof(float);
+    if (!a.fx_seq || a.B <= 8 || a.stream_blocks <= 0 || a.n_head != 2 * a.n_kv_head || a.n_kv_head * a.B < a.stream_blocks / 2 ||
+        lds > 32768)
+        return false;
+    hipLaunchKernelGGL(decode_attn_seq_kernel<1>, dim3(a.n_kv_head, a.B), dim3(256), lds, s, a);
+    return true;
 }
 
 int fused_slots_ffn();   // gemv.hip

@@ -222,6 +222,7 @@ static const std::vector<FuseOption> &fuse_options() {
         {"att_spl", "QASR_ATT_SPL", &FuseCfg::att_spl},
         {"kv_nt", "QASR_KV_NT", &FuseCfg::kv_nt},
         {"lmh", "QASR_LMH", &FuseCfg::lmh},
+        {"fx_seq", "QASR_FX_SEQ", &FuseCfg::fx_seq},
     };
     return v;
 }
@@ -1294,8 +1295,11 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
                 if (skip & 2) {
                 } else if (exact) {   // ggml CPU FA numerics: scores by the splits, then the in-order chain
                     da.scores = c->d_scores;
-                    launch_decode_attention(da, s);
-                    launch_decode_attention_exact(da, s);
+                    da.fx_seq = c->fuse.fx_seq;
+                    if (!launch_decode_attention_exact_seq(da, s)) {
+                        launch_decode_attention(da, s);
+                        launch_decode_attention_exact(da, s);
+                    }
                 } else {
                     launch_decode_attention(da, s);
                 }

@@ -43,6 +43,7 @@
 // more waves per SIMD do not slow each other.
 #include "dev_common.h"
 #include "fx_chain.h"
+#include "fx_decode.h"
 #include "kernels.h"
 
 namespace qasr {
@@ -347,95 +348,11 @@ void launch_prefill_attention_exact(const PrefillAttnArgs &a, hipStream_t s) {
     else hipLaunchKernelGGL(prefill_attn_exact_kernel<false>, grid, dim3(64 * PX_W), 0, s, a);
 }
 
-// ------------------------------------------------------------------- decode
-// The chain for one row, one dimension per lane, V from the V^T cache (this
-// lane's dimension: 8 keys per 16-B load, a wave's loads 1 KiB contiguous).
-// No LDS: each wave derives the whole chunk's weights itself, lane L holding
-// keys 32 L .. 32 L + 31 in registers, and the chain takes key k's weight
-// with v_readlane (an SGPR operand of v_fma_mix_f32, in the slot the mix ->
-// convert dependency leaves empty).  Measured alternatives that lost (tools/
-// micro/fx_bench.hip): weights read from LDS just in time (~15 cycles a key
-// of exposed latency), V prefetched through a four-slot register ring (the
-// loop-carried wait counts came out vmcnt(0)) or an LDS-DMA ring (~60 cycles
-// of issue per 1 KiB piece).
-//
-// keys [0, n) of one (head, sequence): the V^T rows of the wave's 64
-// dimensions from vt (its key block 0, uniform), two register buffers in
-// turn, the next step's loads issued before the current step's arithmetic --
-// unconditionally (vt_ctx carries read-ahead slack), so the wait counts stay
-// exact.  c0: the first key of the current weights chunk.
-__device__ __forceinline__ void fx_chain1(const uint16_t *__restrict__ vt, int loff, int c0, int n, const float *w,
-                                          unsigned long long flags, uint32_t kb, f16 &acc) {
-    u32x4 va[DX_Q / 8], vb[DX_Q / 8];
-    fx_loadQ(va, vt, loff, c0);
-    for (int j0 = 0; j0 < n; j0 += 2 * DX_Q) {
-        fx_loadQ(vb, vt, loff, c0 + j0 + DX_Q);
-        fx_step1_m(va, j0, n, w, flags, kb, acc);
-        fx_loadQ(va, vt, loff, c0 + j0 + 2 * DX_Q);
-        fx_step1_m(vb, j0 + DX_Q, n, w, flags, kb, acc);
-    }
-}
-
-// query head h of sequence b, wave wid (0, 1) running dimensions 64 wid +
-// lane; the waves share nothing (each derives the weights itself)
-__device__ __forceinline__ void decode_attn_exact_body(const DecodeAttnArgs &a, const int h, const int b, const int wid) {
-    const int lane = threadIdx.x & 63;
-    const int g = h / (a.n_head / a.n_kv_head);
-    const int nkv = a.pos[b] + 1;
-    const float *sg = a.scores + ((long)b * a.n_head + h) * a.max_ctx;
-    const long vtc = vt_ctx(a.max_ctx);
-    const int wu = __builtin_amdgcn_readfirstlane(wid);   // uniform: a scalar load base
-    const uint16_t *vcol = a.vt + ((long)b * a.n_kv_head + g) * 128 * vtc + 64 * wu * 8;   // the wave's key block 0
-    float M = -INFINITY, S = 0.0f;
-    f16 acc = 0;
-#ifdef FX_STAMPS
-    unsigned long long tsum[4] = {0, 0, 0, 0};
-    FX_CLK(tk0);
-#endif
-    for (int c0 = 0; c0 < nkv; c0 += DX_KC) {
-        FX_CLK(ta);
-        const int n = min(DX_KC, nkv - c0);
-        float w[DX_B], wl;
-        unsigned long long flags;
-        const float Mold = M;
-        const float *sc = sg + c0;
-        uint32_t kb;
-        const float Sc = fx_weights_reg([&](int j) { return sc[j]; }, n, M, w, flags, wl, &kb);
-        S = (Mold == -INFINITY ? 0.0f : S * expf(Mold - M)) + Sc;
-        FX_CLK(tb);
-        FX_ADD(0, tb - ta);
-        fx_chain1(vcol, 8 * lane, c0, n, w, flags, kb, acc);
-        FX_CLK(tc);
-        FX_ADD(1, tc - tb);
-    }
-#ifdef FX_STAMPS
-    if (lane == 0) {
-        unsigned long long *st = fx_stamps[60000 + 2 * (blockIdx.x + gridDim.x * blockIdx.y) + wid];
-        st[0] = tk0;
-        st[1] = clock64();
-        st[2] = tsum[0];
-        st[3] = tsum[1];
-    }
-#endif
-    const float ov = (float)acc * (S == 0.0f ? 0.0f : 1.0f / S);   // ggml: VKQ32 = fp32(VKQ16) * (1 / S)
-    const long e = (long)b * a.n_head * 128 + h * 128 + 64 * wid + lane;
-    if (a.outq) {   // Q8_0 for the o-proj of a decode batch: a 32-block = 32 lanes
-        float am = fabsf(ov);
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
-        a.outq[e] = q8_quant(ov, am);
-        if ((lane & 31) == 0) a.outd[e >> 5] = q8_scale(am);
-    } else if (a.out32) {
-        a.out32[e] = ov;
-    } else {
-        a.out[e] = f_to_u16(ov);
-    }
-}
-
 // grid (n_head, B), block 128: one query head per workgroup
 __global__ __launch_bounds__(128) void decode_attn_exact_kernel(DecodeAttnArgs a) {
     stamp_start(a.stamp);
-    decode_attn_exact_body(a, blockIdx.x, blockIdx.y, threadIdx.x >> 6);
+    decode_attn_exact_body(a, blockIdx.x, blockIdx.y, threadIdx.x >> 6,
+                           a.scores + ((long)blockIdx.y * a.n_head + blockIdx.x) * a.max_ctx);
     stamp_end(a.stamp);
 }
 
@@ -448,7 +365,8 @@ __global__ __launch_bounds__(128) void decode_attn_exact_kernel(DecodeAttnArgs a
 __global__ __launch_bounds__(256) void decode_attn_exact_pair_kernel(DecodeAttnArgs a) {
     stamp_start(a.stamp);
     const int wid = threadIdx.x >> 6;
-    decode_attn_exact_body(a, 2 * blockIdx.x + (wid >> 1), blockIdx.y, wid & 1);
+    const int h = 2 * blockIdx.x + (wid >> 1);
+    decode_attn_exact_body(a, h, blockIdx.y, wid & 1, a.scores + ((long)blockIdx.y * a.n_head + h) * a.max_ctx);
     stamp_end(a.stamp);
 }
 

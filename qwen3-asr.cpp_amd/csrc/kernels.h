@@ -164,6 +164,8 @@ struct FuseCfg {
     int kv_nt = 1;                      // decode attention: K/V cache rows loaded nontemporal (read once per step by one
                                         // CU; tools/experiments.sh kvnt: configs[1] neutral, 64 x 30 s decode 205.0 -> 202.1 ms)
     int slots_stream = 0;               // ... its co-resident workgroups on this device
+    int fx_seq = 1;                     // decode batches: the exact attention's scores + chain in one launch
+                                        // (decode_attn_seq_kernel<1>) where the per-sequence kernel is taken
     int lmh = 1;                        // decode batches of f16 models (9..64 rows): the LM head in one launch (lmhead.hip)
     unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
 };
@@ -294,6 +296,7 @@ struct DecodeAttnArgs {
                                          // kv group and sequence, taken once the batch fills them; 0 = split kernels)
     int spl_batch;                       // decode batches on the split kernels: 128- or 256-key splits (FuseCfg::att_spl)
     int kv_nt;                           // K/V cache loads nontemporal (FuseCfg::kv_nt)
+    int fx_seq;                          // decode batches on the per-sequence kernel: exact attention in one launch (FuseCfg::fx_seq)
     // batch-1 fused launch with ggml's fp16-accumulating attention (fx = 1,
     // needs gran): the splits publish their scaled scores as {fp32, tag}
     // granules in sgran [n_head][max_ctx]; one chain workgroup per kv group
@@ -310,6 +313,9 @@ struct DecodeAttnArgs {
 // keys in order with the fp16 V accumulator; reads scores, pos, vc, n_head,
 // n_kv_head, max_ctx and writes one of out / out32 / outq+outd
 void launch_decode_attention_exact(const DecodeAttnArgs &a, hipStream_t s);
+// attention.hip: scores + that chain in one launch for decode batches on the
+// per-sequence kernel (a.fx_seq); false = not covered, run the two launches
+bool launch_decode_attention_exact_seq(const DecodeAttnArgs &a, hipStream_t s);
 
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
 // batch 1, f16: the QKV projection (q: GemvArgs of the rmsnorm+QKV GEMV, K = 1024)

@@ -423,3 +423,29 @@ def test_full_configs3_f16_b64_30s(full):
         c.close()
     print("configs[3] prefill + decode steps (abs, rel):", [(round(a_, 4), round(r_, 5)) for a_, r_ in errs])
     assert max(r_ for _, r_ in errs) <= 1e-2, errs
+
+
+def test_full_fx_seq_one_launch_bit_identical(full):
+    """Decode batches on the per-sequence kernel run ggml's fp16-accumulating
+    attention as one launch (option fx_seq: scores kept in LDS, then the
+    chain) instead of a scores launch and a chain launch: the same arithmetic,
+    so decode-step logits of a ragged 64-row batch (contexts 40..400 keys)
+    are bit-identical with the option off."""
+    m, _, _ = full
+    B = 64
+    rng = np.random.default_rng(23)
+    lens = [40 + (b * 360) // (B - 1) for b in range(B)]
+    rows = [[int(t) for t in rng.integers(0, 151643, n)] for n in lens]
+    toks = [[int(t) for t in rng.integers(0, 151643, B)] for _ in range(3)]
+    runs = {}
+    for fx in (1, 0):
+        c = qasr.Context(m, max_batch=B, max_ctx=420)
+        try:
+            c.set_option("fx_seq", fx)
+            c.prefill(rows, want_logits=False)
+            runs[fx] = [c.decode_step(t, [n + s for n in lens])[0].copy() for s, t in enumerate(toks)]
+        finally:
+            c.close()
+    for s in range(len(toks)):
+        assert np.isfinite(runs[1][s]).all()
+        assert np.array_equal(runs[1][s], runs[0][s]), s
