@@ -484,6 +484,8 @@ def main():
         "decode_tokens_per_s": round(N * args.batch * ntok * args.steps / dt, 2),
         "decode_attention": ("fp16 V accumulation per key (ggml CPU flash-attention numerics" +
                              ("; chain role of the fused QKV + attention + o-proj launch)" if ctx.get_option("fused_exact")
+                              else "; scores + chain in one launch per kv group and sequence)"
+                              if args.batch >= 32 and ctx.get_option("fx_seq") and ctx.get_option("att_stream")
                               else "; separate scores + chain kernels)")) if exact else
                             "fp32 V accumulation (split-K)",
         "stage_ms_per_step_rank0": {k: round(v / args.steps, 3) for k, v in tm.items()},
