@@ -1303,7 +1303,8 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
     const int d = 64 * wu + lane, loff = 8 * lane;
     const uint16_t *vt = a.vt + (long)g * 128 * vt_ctx(a.max_ctx) + 64 * wu * 8;   // batch 1: slot 0; the wave's key block 0
     // dev trace (QASR_DEV_TRACE): rows 4000 + g of the attention kernel's table:
-    // [start, v ready, scores gathered, weights done, chain done, published]
+    // [start, v ready, scores gathered, weights done, chain done, published,
+    //  weights: expf pass done, weights stored]
     // (v ready comes after the weights: the new v is polled last)
     auto mark = [&](int slot) {
         if (a.trace && tid == 0) a.trace[(4000L + g) * 8 + slot] = rt_now();
@@ -1406,6 +1407,7 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         }
         kmask[hh][2 * lane + wu] = (uint16_t)kb;   // keys 32 lane + 16 wu ..: the slow path's 8-key groups
         __syncthreads();   // both waves have read their scores
+        mark(6);
 #pragma unroll
         for (int i = 0; i < DX_B / 2; i += 4) *(floatx4 *)&row[16 * wu + i] = floatx4{x[i], x[i + 1], x[i + 2], x[i + 3]};
         const int kl = n - 1;
@@ -1414,6 +1416,7 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
             row[kl & 31] = 0.0f;
         }
         __syncthreads();
+        mark(7);
         // the lane's sequential S = S * ms + vs over its 32 weights (key n - 1
         // read as 0 is S * 1 + 0 = S: its own term, the lane's last, goes after)
         const float wl = fwl[hh];

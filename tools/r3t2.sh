@@ -1,0 +1,7 @@
+# configs[1] device trace of layer 14 with the chain workgroup's weight-phase marks
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+QASR_DEV_TRACE=gpurun_out/r3t2_tr.bin QASR_DEV_TRACE_LAYER=14 timeout -k 10 200 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-probe > gpurun_out/r3t2_tr.log 2>&1 || exit 1
+python3 tools/trace_report.py gpurun_out/r3t2_tr.bin
+QASR_DEV_TRACE=gpurun_out/r3t2_tr4.bin QASR_DEV_TRACE_LAYER=4 timeout -k 10 200 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-probe > gpurun_out/r3t2_tr4.log 2>&1 || exit 1
+python3 tools/trace_report.py gpurun_out/r3t2_tr4.bin

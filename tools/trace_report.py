@@ -23,9 +23,10 @@ def main(path):
         if k == 1 and len(ch):   # fused exact attention: split blocks (scores) + chain workgroups
             print(f"{NAMES[k]:12s} split blocks {len(x):4d} start {us(st.min()):7.2f}..{us(st.max()):7.2f}  "
                   f"scores published max {us(x[:, 3].max()):7.2f}")
-            lab = ["start", "v ready", "scores gathered", "weights", "chain", "published"]
+            lab = ["start", "v ready", "scores gathered", "weights", "chain", "published", "w expf", "w stored"]
+            nl = 8 if (ch[:, 6] > 0).all() else 6
             print(f"{'':12s} chain wgs {len(ch)}: " + "  ".join(f"{lab[i]} {us(np.median(ch[:, i])):6.2f}/{us(ch[:, i].max()):6.2f}"
-                                                             for i in range(6)))
+                                                             for i in range(nl)))
             e = ch[:, 5].max()
         elif k == 1:
             kv, rdy, cnt = x[:, 1], x[:, 2], x[:, 3]
