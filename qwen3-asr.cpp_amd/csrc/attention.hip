@@ -15,6 +15,7 @@
 // Decoder single token: split-K flash decoding (VALU; 2 q heads per kv head)
 // + a combine kernel.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 #include <stdexcept>
 
@@ -1393,18 +1394,26 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         const float inc = wave_scan_max(lm);
         const float Mp0 = dpp_ninf<0x138, 0xF>(inc);   // exclusive prefix (lane 0: -inf; the chunk is the first)
         M = lane_f(inc, 63);
-        float Mq = wu ? fmaxf(Mp0, lh) : Mp0;
         float x[DX_B / 2];
         uint32_t kb = 0;
+        // the wave's half of the lane's keys, indexed statically in each branch
+        // (a select on wu became a wu-offset index into sv, which put sv in
+        // scratch memory: a global-memory round trip before the chain)
+        auto half = [&](auto hc) {
+            constexpr int H = decltype(hc)::value;
+            float Mq = H ? fmaxf(Mp0, lh) : Mp0;
 #pragma unroll
-        for (int i = 0; i < DX_B / 2; i++) {
-            const float sc = wu ? sv[DX_B / 2 + i] : sv[i];
-            const bool gt = sc > Mq;
-            const float e = expf(gt ? Mq - sc : sc - Mq);
-            x[i] = gt ? -e : (sc != -INFINITY ? e : 0.0f);
-            kb |= (uint32_t)gt << i;
-            Mq = fmaxf(Mq, sc);
-        }
+            for (int i = 0; i < DX_B / 2; i++) {
+                const float sc = sv[H * (DX_B / 2) + i];
+                const bool gt = sc > Mq;
+                const float e = expf(gt ? Mq - sc : sc - Mq);
+                x[i] = gt ? -e : (sc != -INFINITY ? e : 0.0f);
+                kb |= (uint32_t)gt << i;
+                Mq = fmaxf(Mq, sc);
+            }
+        };
+        if (wu) half(std::integral_constant<int, 1>{});
+        else half(std::integral_constant<int, 0>{});
         kmask[hh][2 * lane + wu] = (uint16_t)kb;   // keys 32 lane + 16 wu ..: the slow path's 8-key groups
         __syncthreads();   // both waves have read their scores
         mark(6);
@@ -1449,6 +1458,8 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         vnew = f_to_u16(__uint_as_float((uint32_t)v));
     }
     mark(1);
+    // (trace) shader clock against the 100 MHz counter over the chain: row 4010 + g
+    const unsigned long long ck0 = a.trace ? clock64() : 0ull;
     f16 acc = 0;
     {
         // keys 0 .. n - 2 from V^T in 64-key steps (the last may run into key
@@ -1469,6 +1480,19 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         acc = fx_key_slow(acc, vnew, fwl[hh]);
     }
     mark(4);
+    if (a.trace && tid == 0) {
+        a.trace[(4010L + g) * 8 + 0] = ck0;
+        a.trace[(4010L + g) * 8 + 1] = clock64();
+        a.trace[(4010L + g) * 8 + 2] = (unsigned long long)n;
+        unsigned nk = 0, ng = 0;   // head 2g's new-maximum keys and slow 8-key groups
+        for (int i = 0; i < DX_KC / 16; i++) {
+            const unsigned m = kmask[0][i];
+            nk += __builtin_popcount(m);
+            ng += ((m & 0xffu) != 0) + ((m >> 8) != 0);
+        }
+        a.trace[(4010L + g) * 8 + 3] = nk;
+        a.trace[(4010L + g) * 8 + 4] = ng;
+    }
     // ggml: VKQ32 = fp32(VKQ16) * (1 / S); fp16 for the o-projection
     const float ov = (float)acc * (S == 0.0f ? 0.0f : 1.0f / S);
     const uint32_t h16 = f_to_u16(ov);

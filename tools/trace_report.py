@@ -9,9 +9,10 @@ NAMES = ["qkv_gemv", "attention", "oproj_gemv", "gateup_gemv", "down_gemv"]
 
 def main(path):
     t = np.fromfile(path, dtype=np.uint64).reshape(6, 4096, 8).astype(np.int64)
-    ch = t[1][4000:4016]
+    ch = t[1][4000:4008]
     ch = ch[ch[:, 0] > 0]
-    t[1][4000:4016] = 0
+    ck = t[1][4010:4018].copy()   # chain workgroups: shader clock at chain start / end, keys
+    t[1][4000:4020] = 0
     live = [t[k][t[k][:, 0] > 0] for k in range(5)]
     t0 = min(int(x[:, 0].min()) for x in live if len(x))
     us = lambda v: (v - t0) / 100.0
@@ -28,6 +29,13 @@ def main(path):
             print(f"{'':12s} chain wgs {len(ch)}: " + "  ".join(f"{lab[i]} {us(np.median(ch[:, i])):6.2f}/{us(ch[:, i].max()):6.2f}"
                                                              for i in range(nl)))
             e = ch[:, 5].max()
+            ok = ck[:, 1] > ck[:, 0]
+            if ok.any() and len(ch) == len(ck[ok]):
+                cyc = (ck[ok, 1] - ck[ok, 0]).astype(np.float64)
+                dt = (ch[:, 4] - ch[:, 1]).astype(np.float64) / 100.0   # us, 'v ready' -> 'chain'
+                print(f"{'':12s} chain: {np.median(cyc):.0f} shader cycles over {ck[ok, 2][0]} keys "
+                      f"({np.median(cyc) / ck[ok, 2][0]:.1f} a key), {np.median(dt):.2f} us -> {np.median(cyc / dt) / 1e3:.2f} GHz; "
+                      f"head 2g new-maximum keys {ck[ok, 3].tolist()}, slow 8-key groups {ck[ok, 4].tolist()}")
         elif k == 1:
             kv, rdy, cnt = x[:, 1], x[:, 2], x[:, 3]
             lastb = x[x[:, 4] > 0]
