@@ -38,7 +38,8 @@ MFMA_F16_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense fp16 MFMA (no spars
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node; without a launcher (WORLD_SIZE unset) N > 1 spawns one rank per GPU")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--seconds", type=float, default=92.0, help="clip length (configs[1]: 92 s)")
@@ -66,7 +67,81 @@ def parse():
     ap.add_argument("--utt-min", type=float, default=5.0)
     ap.add_argument("--utt-max", type=float, default=30.0)
     ap.add_argument("--utt-seed", type=int, default=0)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rendezvous check without a GPU: ranks join a gloo group, time a barrier and rank 0 "
+                         "prints the JSON line with value 0 (tests/test_dist.py)")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): spawn N child
+    processes of this same command, one per GPU, with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (what torch.distributed.run
+    would set), wait for all of them and return the first non-zero exit code.
+    This parent never touches the GPU (no HIP call, no torch import), so the
+    children are plain forks + execs of a GPU-free process.  Rank 0 prints the
+    JSON line; the others print nothing on stdout."""
+    import signal
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                c = p.poll()
+                if c is None:
+                    continue
+                procs.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    for q in procs:   # one rank failed: the others would wait in a collective forever
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+def dry_run(args, world: int, rank: int) -> None:
+    """The launcher's rendezvous without the GPU: gloo group, barrier-timed
+    region, max over ranks, rank 0's line."""
+    if os.environ.get("QASR_BENCH_FAIL_RANK") == str(rank):   # (the launcher test's failing rank)
+        sys.exit(3)
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "value": 0.0, "unit": "audio-sec/wall-sec", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3),
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f16",
+                          "data": "none (dry run)", "config": {"workload": "dry run", "parallelism": f"dp{world}"}}),
+              flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 def synthetic_model(rank: int, config: str = "full", wtype: int = 1) -> str:
@@ -369,9 +444,16 @@ def utterance_main(args, m, rank, local, world, dist, model_path):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        dry_run(args, world, rank)
+        return
     dist = None
     if world > 1:
         import torch

@@ -172,3 +172,33 @@ def test_queue_order_and_local_counter():
     got = [nxt() for _ in range(6)]
     assert [g[0] for g in got[:5]] == [1, 3, 2, 4, 0] and got[5] is None
     assert got[0][1] == 105
+
+
+def test_bench_launcher_spawns_ranks():
+    """`python bench.py --gpus 2` without torchrun spawns two ranks itself
+    (bench.launch_ranks) and prints exactly one JSON line, rank 0's, with
+    n_gpus = 2 (dry run: gloo rendezvous, no GPU)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "3"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["config"]["parallelism"] == "dp2"
+
+
+def test_bench_launcher_propagates_failure():
+    """a rank that exits non-zero makes the launcher exit non-zero: rank 1
+    dies before the rendezvous (QASR_BENCH_FAIL_RANK), rank 0 is terminated"""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=dict(env, QASR_BENCH_FAIL_RANK="1"))
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
