@@ -72,6 +72,9 @@ public:
     // balances them dynamically); sink(id, result) as each clip finishes.
     // n_ctx: the context length (0: a 30 s clip's prompt + max_tokens);
     // slots: 0 = max_batch().  false: the run itself failed (get_error()).
+    // Per clip only t_total_ms is set (its completion time within the stream:
+    // the stages of different clips overlap); the progress callback sees
+    // every clip's running count; --profile's report covers the whole stream.
     bool transcribe_stream(const std::function<bool(int &id, std::vector<float> &pcm)> &fetch,
                            const std::function<void(int id, transcribe_result result)> &sink,
                            const transcribe_params &params = transcribe_params(), int n_ctx = 0, int slots = 0);

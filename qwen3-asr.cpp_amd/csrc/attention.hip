@@ -21,6 +21,7 @@
 
 #include "dev_common.h"
 #include "fx_chain.h"
+#include "fx_pipe.h"
 #include "fx_decode.h"
 #include "kernels.h"
 
@@ -1514,6 +1515,100 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
     mark(5);
 }
 
+// The chain role with fx_pipe.h (a.fx_pipe): each wave takes its head's
+// score granules one 64-key buffer at a time (lane = key, sc1 loads issued a
+// buffer and a half ahead, polled only if a tag is not there yet) and derives
+// that buffer's weights itself, so the chain starts on the first 64 scores
+// instead of after a gather of all of them and a weight pass over the context
+// (~4 us a layer at 1.4k keys).  No LDS, no barrier before the
+// output.  The new key (n - 1) is scored with the others but applied after
+// the loop from its QKV granule, as fx1_chain_body does.
+struct FxpGran {   // fxp_chain's score source: key j's {fp32 score, tag} granule of one head
+    const unsigned long long *gb;
+    int n;
+    uint32_t tag;
+    int poll_limit;
+    unsigned int *err;
+    __device__ __forceinline__ unsigned long long issue(int j0) const {
+        const int j = j0 + (int)(threadIdx.x & 63);
+        return j < n ? __hip_atomic_load(gb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    }
+    __device__ __forceinline__ float take(unsigned long long v, int j0) const {
+        const int j = j0 + (int)(threadIdx.x & 63);
+        bool ok = j >= n || (uint32_t)(v >> 32) == tag;
+        if (!__all(ok)) {   // not published yet: poll this buffer's granules (bounded)
+            for (int it = 0; it < poll_limit; it++) {
+                __builtin_amdgcn_s_sleep(1);
+                if (!ok) {
+                    v = __hip_atomic_load(gb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = (uint32_t)(v >> 32) == tag;
+                }
+                if (__all(ok)) break;
+            }
+            if (!__all(ok) && (threadIdx.x & 63) == 0)
+                __hip_atomic_fetch_or(err, (unsigned)DEVERR_SCORE_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return j < n ? __uint_as_float((uint32_t)v) : -INFINITY;
+    }
+};
+__device__ __forceinline__ void fx1_chain_pipe(const DecodeAttnArgs &a, const int g) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int hh = wid >> 1, wu = __builtin_amdgcn_readfirstlane(wid & 1);
+    const int d = 64 * wu + lane, loff = 8 * lane;
+    const uint16_t *vt = a.vt + (long)g * 128 * vt_ctx(a.max_ctx) + 64 * wu * 8;   // batch 1: slot 0; the wave's key block 0
+    auto mark = [&](int slot) {   // dev trace: rows 4000 + g as fx1_chain_body ([start, v ready, -, -, chain done, published])
+        if (a.trace && tid == 0) a.trace[(4000L + g) * 8 + slot] = rt_now();
+    };
+    mark(0);
+    const int pos = a.pos[0], nkv = pos + 1, nl = nkv - 1;
+    const uint32_t tag = gran_tag(pos, a.layer);
+    const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
+    const unsigned long long *gp = a.gran + QD + KD + g * 128 + d;   // the new key's v (this lane's dimension)
+    unsigned long long vg = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const FxpGran src{a.sgran + (long)(2 * g + hh) * sgran_ld(a.max_ctx), nkv, tag, a.poll_limit, a.err};
+    mark(2);   // (no gather or weight pass: the chain starts here; slots 2, 3 = its start)
+    mark(3);
+    const unsigned long long ck0 = a.trace ? clock64() : 0ull;
+    f16 acc = 0;
+    float wlast;
+    const float S = fxp_chain(src, vt, loff, nl, nl > 0 ? (nl - 1) >> 3 : 0, acc, wlast);
+    mark(4);
+    {   // the new key: its QKV granule (long published by now), cast to fp16 as the cache write is
+        bool ok = (uint32_t)(vg >> 32) == tag;
+        for (int it = 0; it < a.poll_limit && !__all(ok); it++) {
+            __builtin_amdgcn_s_sleep(2);
+            vg = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = (uint32_t)(vg >> 32) == tag;
+        }
+        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_QKV_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    mark(1);
+    acc = fx_key_slow(acc, f_to_u16(__uint_as_float((uint32_t)vg)), wlast);
+    if (a.trace && tid == 0) {
+        a.trace[(4010L + g) * 8 + 0] = ck0;
+        a.trace[(4010L + g) * 8 + 1] = clock64();
+        a.trace[(4010L + g) * 8 + 2] = (unsigned long long)nkv;
+    }
+    const float ov = (float)acc * (S == 0.0f ? 0.0f : 1.0f / S);   // ggml: VKQ32 = fp32(VKQ16) * (1 / S)
+    const uint32_t h16 = f_to_u16(ov);
+    const uint32_t hn = __shfl_xor(h16, 1, 64);
+    uint16_t *out = a.out + (2 * g + hh) * 128 + d;
+    if (a.att_done) {   // as fx1_chain_body: write-through pairs, drained, one arrival per replica
+        if ((lane & 1) == 0) __hip_atomic_store((uint32_t *)out, h16 | (hn << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (a.fence && tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (a.fence) __syncthreads();
+        if (tid < 8) __hip_atomic_fetch_add(a.att_done + tid * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        *out = (uint16_t)h16;
+    }
+    mark(5);
+}
+
 template <int SPL>
 __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnArgs a, GemvArgs o) {
     constexpr int K = 1024, NT = 2, RPW = 2;
@@ -1526,7 +1621,10 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
         const int j = blockIdx.x - 512, nsp = a.grid_splits, nat = nsp * a.n_kv_head;   // grid_splits: this launch's splits
         const int nfx = a.fx ? a.n_kv_head : 0;
         if (j >= nat + nfx) oproj1_body(o, a, j - nat - nfx);
-        else if (j >= nat) fx1_chain_body(a, j - nat);
+        else if (j >= nat) {
+            if (a.fx_pipe) fx1_chain_pipe(a, j - nat);
+            else fx1_chain_body(a, j - nat);
+        }
         else decode_attn_body<SPL, true>(a, j / a.n_kv_head, j % a.n_kv_head, 0, nsp);
         stamp_end(a.stamp);
         return;
@@ -1636,7 +1734,7 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     // ones): fall back to separate launches for contexts that would not fit
     // (exact attention: n_kv_head chain workgroups too; they read the new v
     // from its granule, so the fused exact path needs the granule hand-off)
-    if (a.fx && (!a.gran || !a.sgran || ns * spl1 > DX_KC)) return 0;   // (one chain chunk)
+    if (a.fx && (!a.gran || !a.sgran || (!a.fx_pipe && ns * spl1 > DX_KC))) return 0;   // (fx_chain.h: one chain chunk)
     const int nfx = a.fx ? a.n_kv_head : 0;
     const int slots = spl1 == 128 ? cfg.slots_qkv128 : cfg.slots_qkv64;
     const bool fit_o = 512 + ns * a.n_kv_head + nfx + 256 <= slots;
@@ -1653,7 +1751,10 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     ad.err = cfg.err;
     ad.grid_splits = ns;   // the kernel's split count
     ad.fx_delay = cfg.fx_delay;
-    ad.fx_vpf = cfg.fx_vpf;
+    // fx_pipe: the chain starts on the first scores, so its V^T rows come from
+    // the splits' pull (bit 0): the chain workgroup's own LDS-DMA pull (bit 1)
+    // would sit in its vmcnt queue ahead of the chain's first loads
+    ad.fx_vpf = a.fx_pipe ? (cfg.fx_vpf | 1) & ~2 : cfg.fx_vpf;
     if (!with_o2) ad.att_done = nullptr;
     const GemvArgs qa = q;
     const GemvArgs oa = with_o2 ? *o : GemvArgs{};

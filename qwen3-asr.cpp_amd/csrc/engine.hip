@@ -223,6 +223,7 @@ static const std::vector<FuseOption> &fuse_options() {
         {"kv_nt", "QASR_KV_NT", &FuseCfg::kv_nt},
         {"lmh", "QASR_LMH", &FuseCfg::lmh},
         {"fx_seq", "QASR_FX_SEQ", &FuseCfg::fx_seq},
+        {"fx_pipe", "QASR_FX_PIPE", &FuseCfg::fx_pipe},
     };
     return v;
 }
@@ -1223,6 +1224,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         da.stream_blocks = !skinny && c->fuse.att_stream ? c->fuse.slots_stream : 0;
         da.spl_batch = c->fuse.att_spl;
         da.kv_nt = c->fuse.kv_nt;
+        da.fx_pipe = c->fuse.fx_pipe;
         da.stamp = stamp;
         GemvArgs o{};
         if (skinny) {

@@ -167,6 +167,7 @@ struct FuseCfg {
     int fx_seq = 1;                     // decode batches: the exact attention's scores + chain in one launch
                                         // (decode_attn_seq_kernel<1>) where the per-sequence kernel is taken
     int lmh = 1;                        // decode batches of f16 models (9..64 rows): the LM head in one launch (lmhead.hip)
+    int fx_pipe = 0;                    // exact decode chains: weights one 64-key buffer ahead, SGPR operands (fx_pipe.h)
     unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
 };
 // co-resident workgroup capacity of the fused kernels on the current device
@@ -307,6 +308,8 @@ struct DecodeAttnArgs {
     int fx_delay;                        // chain workgroups: first score poll after fx_delay x ~0.2 us
     int fx_vpf;                          // bit 0: the splits pull their keys' V^T rows into their XCD's L2 for the
                                          // chain; bit 1: the chain workgroups pull their own (LDS-DMA, while waiting)
+    int fx_pipe;                         // every exact decode chain derives its weights one 64-key buffer ahead
+                                         // (fx_pipe.h; FuseCfg::fx_pipe) instead of all of them first (fx_chain.h)
 };
 // the decode attention with ggml's CPU flash-attention numerics (fa_exact.hip),
 // after launch_decode_attention in scores mode: per (query head, sequence) the

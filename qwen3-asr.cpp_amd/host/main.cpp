@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "forced_aligner.h"
+#include "qasr_capi.h"
 #include "qwen3_asr.h"
 
 struct cli_params {
@@ -306,6 +307,12 @@ static int run_transcription_sharded(const cli_params &p) {
     std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return size[a] > size[b]; });
     fprintf(stderr, "qwen3-asr-cli (sharded)\n  Model: %s\n  Files: %zu over %d GPU(s), %d slots each, shared queue\n\n",
             p.model_path.c_str(), N, G, p.batch);
+    // the context: the longest file's prompt + the budget (16-bit PCM: at most
+    // size / 2 samples), so long files transcribe as in the reference, which
+    // sizes its context per clip (src/qwen3_asr.cpp:223)
+    const long long max_samples = N ? size[order[0]] / 2 : 0;
+    const int n_ctx = qasr_prompt_len(qasr_encoder_frames(qasr_mel_frames((int)std::min<long long>(max_samples, 1LL << 30)))) +
+                      p.max_tokens + 64;
     std::vector<qwen3_asr::transcribe_result> results(N);
     std::vector<std::string> errors(G);
     std::atomic<size_t> next{0};
@@ -342,7 +349,7 @@ static int run_transcription_sharded(const cli_params &p) {
                 std::lock_guard<std::mutex> lk(res_mu);
                 results[id] = std::move(r);
             };
-            if (!asr.transcribe_stream(fetch, sink, tp)) errors[g] = asr.get_error();
+            if (!asr.transcribe_stream(fetch, sink, tp, n_ctx)) errors[g] = asr.get_error();
         });
     }
     for (auto &t : th) t.join();

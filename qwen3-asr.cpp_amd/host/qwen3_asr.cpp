@@ -26,6 +26,14 @@ static void token_cb(void *user, int seq, int n_generated, int32_t) {
     if (t->print && n_generated % 10 == 0) fprintf(stderr, "Generated %d tokens...\n", n_generated);
 }
 
+// the stream's callback: every clip's tokens (seq = the clip's id), so a
+// progress callback sees each clip's running count in turn
+static void stream_token_cb(void *user, int seq, int n_generated, int32_t) {
+    const TokenCb *t = (const TokenCb *)user;
+    if (t->cb && *t->cb) (*t->cb)(n_generated, t->max_tokens);
+    if (t->print && n_generated % 10 == 0) fprintf(stderr, "Clip %d: generated %d tokens...\n", seq, n_generated);
+}
+
 static int64_t now_ms() {
     return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -243,9 +251,21 @@ bool Qwen3ASR::transcribe_stream(const std::function<bool(int &id, std::vector<f
     const int S = slots > 0 ? std::min(slots, max_batch_) : max_batch_;
     if (!ensure_ctx(S, need)) return false;
     qasr_set_system_prompt(ctx_, sys.data(), (int)sys.size());
+    qasr_set_profile(ctx_, profile_ ? 1 : 0);   // the report covers the whole stream
+    TokenCb tcb{&progress_callback_, params.max_tokens, params.print_progress};
+    const bool per_token = progress_callback_ || params.print_progress;
+    qasr_set_token_callback(ctx_, per_token ? stream_token_cb : nullptr, per_token ? &tcb : nullptr);
     StreamCtx sc{&fetch, &sink, model_, {}, now_ms()};
     const int rc = qasr_run_stream(ctx_, S, stream_fetch, stream_sink, &sc, params.max_tokens, 0, nullptr);
+    qasr_set_token_callback(ctx_, nullptr, nullptr);
     if (rc != 0) { error_msg_ = std::string("Decoding failed: ") + qasr_last_error(); return false; }
+    if (profile_) {
+        const int len = qasr_profile_report(ctx_, nullptr, 0);
+        std::string rep(std::max(len, 0) + 1, '\0');
+        qasr_profile_report(ctx_, &rep[0], (int)rep.size());
+        rep.resize(std::max(len, 0));
+        profile_report_ = rep;
+    }
     return true;
 }
 

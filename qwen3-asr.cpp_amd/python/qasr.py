@@ -272,13 +272,32 @@ class RunResult:
     timings: Timings
 
 
-def _sink_into(out: dict):
+def _sink_into(out: dict, failed: list):
     def sink(_u, cid, status, toks, n):
-        if status:
-            out[cid] = QasrError(lib().qasr_last_error().decode(errors="replace"))
-        else:
-            out[cid] = [int(toks[i]) for i in range(n)]
+        try:
+            if status:
+                out[cid] = QasrError(lib().qasr_last_error().decode(errors="replace"))
+            else:
+                out[cid] = [int(toks[i]) for i in range(n)]
+        except BaseException as e:   # (ctypes would swallow it)
+            failed.append(e)
     return sink
+
+
+def _guarded_fetch(fetch, failed: list):
+    """A ctypes callback cannot raise: an exception in next_clip() (e.g. a
+    TCPStore failure of the shared queue) is stored, the queue reported empty
+    (-1, so the engine drains its slots and returns), and the caller re-raises
+    it after the run instead of the engine taking 0 as a clip id."""
+    def f(*a):
+        if failed:
+            return -1
+        try:
+            return fetch(*a)
+        except BaseException as e:
+            failed.append(e)
+            return -1
+    return f
 
 
 class Context:
@@ -410,9 +429,13 @@ class Context:
                 budget_p[0] = int(item[2])
             return cid
 
-        f, k = FETCH_FN(fetch), SINK_FN(_sink_into(out))
+        failed = []
+        f, k = FETCH_FN(_guarded_fetch(fetch, failed)), SINK_FN(_sink_into(out, failed))
         st = StreamStats()
-        _check(lib().qasr_run_stream(self.h, int(slots), f, k, None, int(max_tokens), int(ignore_eos), C.byref(st)), "qasr_run_stream")
+        rc = lib().qasr_run_stream(self.h, int(slots), f, k, None, int(max_tokens), int(ignore_eos), C.byref(st))
+        if failed:
+            raise failed[0]
+        _check(rc, "qasr_run_stream")
         return out, st
 
     def run_stream_staged(self, next_clip, max_tokens: int, ignore_eos: bool = False, slots: int = 0):
@@ -429,10 +452,13 @@ class Context:
                 return int(item[0])
             return int(item)
 
-        f, k = FETCH_STAGED_FN(fetch), SINK_FN(_sink_into(out))
+        failed = []
+        f, k = FETCH_STAGED_FN(_guarded_fetch(fetch, failed)), SINK_FN(_sink_into(out, failed))
         st = StreamStats()
-        _check(lib().qasr_run_stream_staged(self.h, int(slots), f, k, None, int(max_tokens), int(ignore_eos), C.byref(st)),
-               "qasr_run_stream_staged")
+        rc = lib().qasr_run_stream_staged(self.h, int(slots), f, k, None, int(max_tokens), int(ignore_eos), C.byref(st))
+        if failed:
+            raise failed[0]
+        _check(rc, "qasr_run_stream_staged")
         return out, st
 
     def set_system_prompt(self, ids: Sequence[int]) -> None:

@@ -94,11 +94,13 @@ def test_staged_pool_subsets(tiny):
 
 def test_cli_sharded_file_list(tiny, tmp_path, tiny_gguf):
     """qwen3-asr-cli --devices / --file-list / --batch: outputs in input
-    order, identical to one file at a time; --profile prints the report"""
+    order, identical to one file at a time (a 40 s file included: the
+    sharded path sizes its context to the longest file); --profile prints
+    the report"""
     paths = []
-    for i in range(3):
+    for i, secs in enumerate((1.2, 2.2, 40.0, 3.2)):
         p = str(tmp_path / f"c{i}.wav")
-        qasr.write_wav(p, qasr.synth_pcm(33000 + i, int((1.2 + i) * SR)))
+        qasr.write_wav(p, qasr.synth_pcm(33000 + i, int(secs * SR)))
         paths.append(p)
     lst = tmp_path / "list.txt"
     lst.write_text("\n".join(paths) + "\n")

@@ -90,3 +90,30 @@ def test_stream_token_callback_gets_clip_ids(tiny_model):
     for cid, toks in out.items():
         assert [n for n, _ in seen[cid]] == list(range(1, len(toks) + 1))
         assert [t for _, t in seen[cid]] == toks
+
+
+def test_stream_fetch_exception_is_raised(tiny_model):
+    """a Python exception inside next_clip() (ctypes would swallow it and the
+    engine take 0 as a clip id) closes the queue and is re-raised after the
+    run; the clips fetched before it are still transcribed"""
+    clips = [qasr.synth_pcm(7400 + i, SR) for i in range(3)]
+    calls = []
+
+    def next_clip():
+        calls.append(1)
+        if len(calls) == 3:
+            raise RuntimeError("queue store failed")
+        return (len(calls), clips[len(calls) - 1], 4) if len(calls) < 3 else None
+
+    c = qasr.Context(tiny_model, max_batch=2, max_ctx=640)
+    try:
+        with pytest.raises(RuntimeError, match="queue store failed"):
+            c.run_stream(next_clip, max_tokens=4, ignore_eos=True)
+        c.stage_audio(clips)
+        with pytest.raises(ValueError, match="bad index"):
+            c.run_stream_staged(lambda: (_ for _ in ()).throw(ValueError("bad index")), max_tokens=4, ignore_eos=True)
+        # the context stays usable
+        out, st = c.run_stream(_queue([(5, clips[0], 4)]), max_tokens=4, ignore_eos=True)
+        assert out[5] == _single(tiny_model, clips[0], 4, True)
+    finally:
+        c.close()

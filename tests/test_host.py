@@ -109,3 +109,20 @@ def test_wav_roundtrip(tmp_path, built):
     qasr.write_wav(p, a)
     b, sr = qasr.load_wav(p)
     assert sr == 16000 and np.array_equal(a, b)
+
+
+def test_stream_fetch_guard_stores_exception():
+    """qasr._guarded_fetch: an exception in the Python fetch becomes -1 (queue
+    empty) and is kept for the caller; later calls return -1 without calling
+    fetch again"""
+    import qasr
+    failed, n = [], []
+
+    def fetch(*a):
+        n.append(1)
+        raise KeyError("x")
+    f = qasr._guarded_fetch(fetch, failed)
+    assert f(None, None) == -1 and f(None, None) == -1
+    assert len(n) == 1 and isinstance(failed[0], KeyError)
+    ok = qasr._guarded_fetch(lambda *a: 7, [])
+    assert ok(None) == 7

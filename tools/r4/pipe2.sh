@@ -1,0 +1,14 @@
+# fx_pipe round 2: micro with L2-warm V^T; bench pipe (splits pull V^T) vs default; layer trace of both
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+for a in "1370 2 1" "1370 2 0" "600 2 1"; do
+  timeout -k 5 60 tools/micro/chain_pipe $a >> gpurun_out/p2_micro.log 2>&1; rc=$?
+  [ $rc -gt 1 ] && { echo "micro rc=$rc"; cat gpurun_out/p2_micro.log; exit $rc; }
+done
+cat gpurun_out/p2_micro.log
+for fp in 1 0; do
+  QASR_FX_PIPE=$fp timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/p2_b$fp.log 2>&1 || { tail -5 gpurun_out/p2_b$fp.log; exit 1; }
+  grep '^{' gpurun_out/p2_b$fp.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('fx_pipe', $fp, d['value'], d['stage_ms_per_step_rank0'], [(x['kernel'][:30], x['avg_launch_us'], x['frac']) for x in [d['roofline']]+d['roofline_other']])"
+  QASR_FX_PIPE=$fp QASR_DEV_TRACE=gpurun_out/p2_tr$fp.bin QASR_DEV_TRACE_LAYER=14 timeout -k 10 200 python -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-probe > gpurun_out/p2_trb$fp.log 2>&1 || { tail -5 gpurun_out/p2_trb$fp.log; exit 1; }
+  python3 tools/trace_report.py gpurun_out/p2_tr$fp.bin > gpurun_out/p2_tr$fp.txt 2>&1; cat gpurun_out/p2_tr$fp.txt
+done
