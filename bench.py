@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--utt-min", type=float, default=5.0)
     ap.add_argument("--utt-max", type=float, default=30.0)
     ap.add_argument("--utt-seed", type=int, default=0)
+    ap.add_argument("--align-batch", type=int, default=32,
+                    help="--pipeline align: clips per ForcedAligner pass (qasr_align_json_batch)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous check without a GPU: ranks join a gloo group, time a barrier and rank 0 "
                          "prints the JSON line with value 0 (tests/test_dist.py)")
@@ -380,13 +382,15 @@ def utterance_main(args, m, rank, local, world, dist, model_path):
     if args.pipeline == "align":   # configs[4]: ForcedAligner on every transcript (src/main.cpp:416-500)
         am = qasr.Model(os.environ.get("QASR_ALIGNER_MODEL") or synthetic_model(rank, "aligner", 8 if args.q8 else 1), local)
         # prompt: audio pads + per word its BPE ids and two timestamps (ForcedAligner::tokenize_with_timestamps)
-        actx = qasr.Context(am, max_batch=1, max_ctx=P + 8 * qd.budget(nmax, args.tok_rate) + 64)
+        ab = args.align_batch
+        actx = qasr.Context(am, max_batch=ab, max_ctx=P + 8 * qd.budget(nmax, args.tok_rate) + 64)
 
-        def after(idx, toks):
-            for i, t in zip(idx, toks):
-                doc, _ = actx.align_json(pcm[i], m.detokenize(t))
-                assert isinstance(doc, dict), i
-                aligned.add(i)
+        def after(idx, toks):   # the rank's transcripts, ab clips per aligner pass (qasr_align_json_batch)
+            for k in range(0, len(idx), ab):
+                sub = idx[k:k + ab]
+                docs, _ = actx.align_json_batch([pcm[i] for i in sub], [m.detokenize(t) for t in toks[k:k + ab]])
+                assert len(docs) == len(sub) and all(isinstance(d, dict) for d in docs), sub
+                aligned.update(sub)
     for _ in range(args.warmup):
         one_pass(after)
     wall, res = 0.0, None
@@ -487,11 +491,13 @@ def main():
         r0 = ctx.run(ntok, ignore_eos=True)
         texts = [m.detokenize(t) for t in r0.tokens]
         need = max(qasr.align_prompt_len(n, len(am.align_tokenize(t)[0])) for t in texts)
-        actx = qasr.Context(am, max_batch=1, max_ctx=need + 8)
+        actx = qasr.Context(am, max_batch=min(args.batch, args.align_batch), max_ctx=need + 8)
 
-    def align_all():
-        for pcm, t in zip(clips, texts):
-            actx.align_json(pcm, t)
+    def align_all():   # the step's clips, align_batch per aligner pass
+        ab = min(args.batch, args.align_batch)
+        for k in range(0, len(clips), ab):
+            docs, _ = actx.align_json_batch(clips[k:k + ab], texts[k:k + ab])
+            assert len(docs) == len(clips[k:k + ab])
     if args.fa_exact_decode is not None:
         ctx.set_option("fa_exact_decode", args.fa_exact_decode)
     fx = ctx.get_option("fa_exact_decode")

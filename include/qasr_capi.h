@@ -129,6 +129,12 @@ int qasr_encode_conv(qasr_ctx *c, const float *mel, const int *T, int B, float *
  * logits_last (optional) [B][vocab]; argmax (optional) [B]. */
 int qasr_prefill(qasr_ctx *c, const int32_t *ids, const int *P, const float *feats,
                  const int *audio_pos, const int *N, int B, float *logits_last, int32_t *argmax);
+/* A chunk of P[b] tokens after n_past[b] cached ones (no audio splice), one
+ * causal prefill over the cache and the chunk; logits of each chunk's last
+ * row.  <- TextDecoder::forward(tokens, n_tokens > 1, n_past > 0)
+ *    src/text_decoder.h:125-126 / .cpp:392-581, 583-586 */
+int qasr_prefill_chunk(qasr_ctx *c, const int32_t *ids, const int *P, const int *n_past, int B,
+                       float *logits_last, int32_t *argmax);
 /* One decode step for B sequences at positions n_past[b] (token tok[b]). */
 int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_past, int B,
                      float *logits, int32_t *argmax);
@@ -290,6 +296,14 @@ int qasr_align_prompt_len(int n_samples, int n_text);
  * code on failure); writes at most cap-1 bytes + NUL. */
 int qasr_align_json(qasr_ctx *c, const float *pcm, int n_samples, const char *text, const char *language,
                     char *out, int cap, qasr_timings *t);
+/* B clips in one aligner pass (mel + windowed encoder of all clips, one
+ * prefill of the B prompts, one classify GEMM over every timestamp row): the
+ * B documents of qasr_align_json as one JSON array, in input order; each
+ * clip's classes equal its single-clip run.  B <= the context's max_batch.
+ * Returns the length (or minus the error code); writes at most cap-1 + NUL.
+ * <- the --transcribe-align pipeline over many files, src/main.cpp:416-500 */
+int qasr_align_json_batch(qasr_ctx *c, const float *const *pcm, const int *n_samples, const char *const *text, int B,
+                          const char *language, char *out, int cap, qasr_timings *t);
 
 /* ---- text (host) ---------------------------------------------------------- */
 /* UTF-8 text for ids (special <|..|> and [PAD..] tokens skipped); returns the

@@ -463,10 +463,12 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(PrefillAttnArgs a) {
     const int L = a.seq_len[sq];
     const int q0 = blockIdx.x * 32;
     if (q0 >= L) return;
+    const int P0 = a.seq_pos0 ? a.seq_pos0[sq] : 0;   // a chunk after P0 cached tokens: query t at position P0 + t
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int g = lane >> 4, ql = lane & 15;
     const int head = gk * 2 + (wid >> 1);
     const int q = q0 + (wid & 1) * 16 + ql;
+    const int qp = P0 + q, KL = P0 + L;   // the query's position; keys 0 .. KL - 1
     const int row0 = a.seq_row0[sq];
     const int QD = a.n_head * 128;
     const long cbase = ((long)a.seq_slot[sq] * a.n_kv_head + gk) * a.max_ctx;
@@ -480,13 +482,13 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(PrefillAttnArgs a) {
 #pragma unroll
     for (int d = 0; d < 8; d++) o[d] = floatx4{0.f, 0.f, 0.f, 0.f};
     float m_run = -INFINITY, l_run = 0.0f;
-    const int kend = min(L, q0 + 32);   // causal: keys <= last query of the block
+    const int kend = min(KL, P0 + q0 + 32);   // causal: keys <= last query of the block
     for (int k0 = 0; k0 < kend; k0 += 64) {
         __syncthreads();
         for (int i = tid; i < 64 * 16; i += 256) {
             const int key = i >> 4, ch = i & 15;
             u32x4 kv = u32x4{0u, 0u, 0u, 0u}, vv = kv;
-            if (k0 + key < L) {
+            if (k0 + key < KL) {
                 kv = *(const u32x4 *)(kc + (long)(k0 + key) * 128 + ch * 8);
                 vv = *(const u32x4 *)(vc + (long)(k0 + key) * 128 + ch * 8);
             }
@@ -514,7 +516,7 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(PrefillAttnArgs a) {
             for (int i = 0; i < 4; i++) {
                 const int key = k0 + t * 16 + 4 * g + i;
                 float v = st[t][i] * a.scale;
-                if (key > q || key >= L) v = -INFINITY;
+                if (key > qp || key >= KL) v = -INFINITY;
                 st[t][i] = v;
                 tmax = fmaxf(tmax, v);
             }

@@ -219,6 +219,21 @@ void launch_argmax_finish(const unsigned long long *amax, int B, int32_t *ids, i
     hipLaunchKernelGGL(argmax_finish_kernel, dim3(1), dim3(256), 0, s, amax, B, ids, hist, hist_stride, step);
 }
 
+// dst row r = src row idx[r] (fp32 rows of D floats, 16-B lanes)
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float *__restrict__ src, const int *__restrict__ idx, int rows, int D,
+                                                          float *__restrict__ dst) {
+    const int per = D / 4;
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long)rows * per) return;
+    const int r = (int)(i / per), c = (int)(i - (long)r * per);
+    *(float4 *)(dst + (long)r * D + 4 * c) = *(const float4 *)(src + (long)idx[r] * D + 4 * c);
+}
+void launch_gather_rows(const float *src, const int *idx, int rows, int D, float *dst, hipStream_t s) {
+    if (rows <= 0) return;
+    const long n = (long)rows * (D / 4);
+    hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, idx, rows, D, dst);
+}
+
 __global__ void fill_u64_kernel(unsigned long long *p, int n, unsigned long long v) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) p[i] = v;

@@ -107,6 +107,7 @@ struct qasr_ctx {
     DevBuf px, pxh, pqkv, pq, patt, pact, prow, plast, pids, pxl;
     DevBuf pq32, pk32;             // ForcedAligner prefill: fp32 Q / K rows
     DevBuf ats, atx, aam;          // aligner: timestamp-row indices, their normed rows, argmax keys
+    DevBuf exp_, gidx;             // aligner batches: conv_out over every padded chunk row, the valid rows' indices
     DevBuf q8a, q8d, x32;          // Q8_0 models: quantised activations (int8 + scales), fp32 layer inputs
     float *d_att32 = nullptr, *d_act32 = nullptr;   // Q8_0 decode: fp32 attention output / SwiGLU output
     int8_t *d_q8a = nullptr; float *d_q8d = nullptr, *d_x32 = nullptr;   // Q8_0 batched (B > 8) decode, graph-fixed
@@ -892,10 +893,14 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     Nb.assign(B, 0);
     // ASR: each chunk on its own length (src/audio_encoder.cpp:331-409).  Aligner:
     // every chunk zero-padded to 100 frames, the valid frames of the (short)
-    // last one kept (src/forced_aligner.cpp:601-735); one clip per call, so
-    // the valid conv_out rows are the leading rows.
+    // last one kept (src/forced_aligner.cpp:601-735).  One clip: the valid
+    // conv_out rows are the leading rows.  Several clips: a clip's short last
+    // chunk leaves padded rows before the next clip's, so conv_out runs over
+    // every padded row (PE position = row within its chunk, as for the valid
+    // ones) and the valid rows are gathered after it.
     const bool al = hp.aligner;
-    if (al && B != 1) return fail(QASR_ERR_ARG, "aligner encoder: one clip per call");
+    const bool al_gather = al && B > 1;
+    std::vector<int> pepos_pad, gidx;
     for (int b = 0; b < B; b++) {
         for (int s = 0; s < T[b]; s += 100) {
             ChunkDesc d;
@@ -909,6 +914,10 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
             d.row1 = r1; d.row2 = r2; d.row3 = r3; d.enc_row = er;
             s1.push_back(r1); s2.push_back(r2); s3.push_back(r3);
             const int valid = chunk_out_len(d.Lv);
+            if (al_gather) {
+                for (int w = 0; w < d.W3; w++) pepos_pad.push_back(w);
+                for (int w = 0; w < valid; w++) gidx.push_back(r3 / 16 + w);
+            }
             r1 += 64 * d.W1; r2 += 32 * d.W2; r3 += 16 * d.W3; er += valid;
             for (int w = 0; w < valid; w++) pepos.push_back(w);
             Nb[b] += valid;
@@ -918,8 +927,10 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     const int NC = (int)ch.size(), N = er;
     if (N == 0) return 0;
     int rc;
+    const int NP = r3 / 16;   // conv_out rows over every (padded) chunk row
+    if (al_gather && ((rc = upload(c, c->gidx, gidx)) || (rc = ensure(c, c->exp_, (size_t)NP * D * 4)))) return rc;
     if ((rc = upload(c, c->chunks, ch)) || (rc = upload(c, c->rs1, s1)) || (rc = upload(c, c->rs2, s2)) ||
-        (rc = upload(c, c->rs3, s3)) || (rc = upload(c, c->pepos, pepos)) ||
+        (rc = upload(c, c->rs3, s3)) || (rc = upload(c, c->pepos, al_gather ? pepos_pad : pepos)) ||
         (rc = ensure(c, c->act1, (size_t)r1 * C * 2)) || (rc = ensure(c, c->act2, (size_t)r2 * C * 2)) ||
         (rc = ensure(c, c->act3, (size_t)r3 * C * 2)) || (rc = ensure(c, c->ex, (size_t)N * D * 4)) ||
         (rc = ensure(c, c->exh, (size_t)N * std::max(D, FF) * 2)) || (rc = ensure(c, c->eqkv, (size_t)N * 3 * D * 4)) ||
@@ -943,17 +954,19 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     g.out_f16 = c->act3.as<uint16_t>();
     launch_gemm_c(c, AM_CONV3, EPI_GELU_F16, g, s);
     const bool q8 = m->q8;
-    if (q8 && (rc = ensure_q8(c, N, std::max(16 * C, std::max(D, FF)), D))) return rc;
+    const int MO = al_gather ? NP : N;
+    if (q8 && (rc = ensure_q8(c, MO, std::max(16 * C, std::max(D, FF)), D))) return rc;
     // conv_out (no bias) + per-chunk sinusoidal PE (src/audio_encoder.cpp:147-149, :400-404)
     GemmArgs o{};
-    o.M = N; o.N = D; o.K = 16 * C;
-    o.out_f32 = c->ex.as<float>(); o.ldo = D; o.pe = m->pe; o.pe_pos = c->pepos.as<int>();
+    o.M = MO; o.N = D; o.K = 16 * C;
+    o.out_f32 = al_gather ? c->exp_.as<float>() : c->ex.as<float>(); o.ldo = D; o.pe = m->pe; o.pe_pos = c->pepos.as<int>();
     if (q8) {
         gemm_q8(c, EPI_F32, o, nullptr, c->act3.as<uint16_t>(), 16 * C, C, m->conv_out_w, m->conv_out_d, s);
     } else {
         o.A = c->act3.as<uint16_t>(); o.lda = 16 * C; o.W = m->conv_out_w; o.ldw = 16 * C;
         launch_gemm_c(c, AM_DENSE, EPI_F32, o, s);
     }
+    if (al_gather) launch_gather_rows(c->exp_.as<float>(), c->gidx.as<int>(), N, D, c->ex.as<float>(), s);
     HIPCHK(hipGetLastError());
     if (c->profile_on) HIPCHK(hipEventRecord(c->ev[5], s));   // conv front-end | transformer
     if (conv_only) return 0;
@@ -1021,7 +1034,8 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
 // final hidden rows in c->px.  Row tables live in c->prow:
 // [row_seq | row_pos | row_audio] (3*rows ints) + [seq_row0 | seq_len | seq_slot].
 static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const std::vector<int> &P, const float *d_feats,
-                          const std::vector<int> &audio_pos, const std::vector<int> &N, const std::vector<int> *slots) {
+                          const std::vector<int> &audio_pos, const std::vector<int> &N, const std::vector<int> *slots,
+                          const std::vector<int> *pos0 = nullptr) {
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
     const int B = (int)P.size(), H = hp.hidden, QD = hp.n_head * 128, KD = hp.n_kv_head * 128, F = hp.dec_ffn;
@@ -1030,29 +1044,34 @@ static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const st
         for (int v : *slots)
             if (v < 0 || v >= c->max_batch) return fail(QASR_ERR_ARG, "KV-cache slot out of range");
     int rows = 0, maxp = 0;
+    auto p0 = [&](int b) { return pos0 ? (*pos0)[b] : 0; };   // a chunk after p0(b) cached tokens
     for (int b = 0; b < B; b++) {
         if (P[b] <= 0) return fail(QASR_ERR_ARG, "empty prompt");
-        if (P[b] > c->max_ctx) return fail(QASR_ERR_ARG, "Context length exceeded");
+        if (p0(b) < 0 || p0(b) + P[b] > c->max_ctx) return fail(QASR_ERR_ARG, "Context length exceeded");
         rows += P[b];
         maxp = std::max(maxp, P[b]);
     }
-    std::vector<int> tab(3 * rows + 3 * B), lastrow(B);
+    if (pos0 && (m->hp.aligner || !c->fuse.fa_exact_prefill))   // (the chunk form is built on the exact kernel)
+        for (int b = 0; b < B; b++)
+            if (p0(b)) return fail(QASR_ERR_ARG, "a chunk after cached tokens needs the exact prefill attention (ASR model)");
+    std::vector<int> tab(3 * rows + 4 * B), lastrow(B);
     int r = 0, fr = 0;
     for (int b = 0; b < B; b++) {
         const bool splice = d_feats && N[b] > 0 && audio_pos[b] >= 0 && audio_pos[b] + N[b] <= P[b];
         for (int t = 0; t < P[b]; t++, r++) {
             tab[r] = slots ? (*slots)[b] : b;   // the KV-cache slot the row writes
-            tab[rows + r] = t;
+            tab[rows + r] = p0(b) + t;
             tab[2 * rows + r] = (splice && t >= audio_pos[b] && t < audio_pos[b] + N[b]) ? fr + (t - audio_pos[b]) : -1;
         }
         fr += N[b];
         lastrow[b] = r - 1;
     }
     int acc = 0;
-    for (int b = 0; b < B; b++) {   // seq_row0 | seq_len | seq_slot
+    for (int b = 0; b < B; b++) {   // seq_row0 | seq_len | seq_slot | seq_pos0
         tab[3 * rows + b] = acc;
         tab[3 * rows + B + b] = P[b];
         tab[3 * rows + 2 * B + b] = slots ? (*slots)[b] : b;
+        tab[3 * rows + 3 * B + b] = p0(b);
         acc += P[b];
     }
     int rc;
@@ -1065,7 +1084,7 @@ static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const st
     if (al && ((rc = ensure(c, c->pq32, (size_t)rows * QD * 4)) || (rc = ensure(c, c->pk32, (size_t)rows * KD * 4)))) return rc;
     hipStream_t s = c->st;
     const int *d_seq = c->prow.as<int>(), *d_pos = d_seq + rows, *d_aud = d_seq + 2 * rows;
-    const int *d_srow0 = d_seq + 3 * rows, *d_slen = d_srow0 + B, *d_sslot = d_slen + B;
+    const int *d_srow0 = d_seq + 3 * rows, *d_slen = d_srow0 + B, *d_sslot = d_slen + B, *d_spos0 = d_sslot + B;
     float *x = c->px.as<float>();
     uint16_t *xh = c->pxh.as<uint16_t>();
     const bool q8 = m->q8;
@@ -1093,6 +1112,7 @@ static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const st
         pa.seq_slot = d_sslot; pa.n_seq = B; pa.max_len = maxp; pa.n_head = hp.n_head; pa.n_kv_head = hp.n_kv_head;
         pa.max_ctx = c->max_ctx; pa.scale = 1.0f / sqrtf(128.0f); pa.out = c->patt.as<uint16_t>(); pa.out32 = x32;
         if (al) { pa.q32 = qa.q32; pa.k32 = qa.k32; }
+        if (pos0) pa.seq_pos0 = d_spos0;
         if (c->fuse.fa_exact_prefill || al) launch_prefill_attention_exact(pa, s);   // ggml CPU FA numerics
         else launch_prefill_attention(pa, s);
         GemmArgs o{};
@@ -1123,9 +1143,9 @@ static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const st
 // the decode state (d_tok / d_pos / d_nkv) is written for entries 0..B-1
 static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::vector<int> &P, const float *d_feats,
                        const std::vector<int> &audio_pos, const std::vector<int> &N, bool want_logits,
-                       const std::vector<int> *slots = nullptr) {
+                       const std::vector<int> *slots = nullptr, const std::vector<int> *pos0 = nullptr) {
     int rc;
-    if ((rc = prefill_layers(c, ids, P, d_feats, audio_pos, N, slots))) return rc;
+    if ((rc = prefill_layers(c, ids, P, d_feats, audio_pos, N, slots, pos0))) return rc;
     // granule tags repeat across runs at the same positions: back to zero (no valid tag)
     HIPCHK(hipMemsetAsync(c->d_gran, 0, (size_t)(c->m->hp.n_head + 2 * c->m->hp.n_kv_head) * 128 * 8, c->st));
     HIPCHK(hipMemsetAsync(c->d_sgran, 0, (size_t)c->m->hp.n_head * sgran_ld(c->max_ctx) * 8, c->st));
@@ -1153,7 +1173,10 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
     launch_fill_u64(c->d_amax, B, 0ull, s);   // zero at rest for the decode graph
     // decode state: next position = P_b, n_kv = P_b + 1 (the fed token's own key included)
     std::vector<int> pos(B), nkv(B);
-    for (int b = 0; b < B; b++) { pos[b] = P[b]; nkv[b] = P[b] + 1; }
+    for (int b = 0; b < B; b++) {
+        pos[b] = (pos0 ? (*pos0)[b] : 0) + P[b];
+        nkv[b] = pos[b] + 1;
+    }
     HIPCHK(hipMemcpyAsync(c->d_pos, pos.data(), B * 4, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->d_nkv, nkv.data(), B * 4, hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));   // pos/nkv host vectors go out of scope
@@ -1717,6 +1740,31 @@ extern "C" int qasr_prefill(qasr_ctx *c, const int32_t *ids, const int *P, const
     return 0;
 }
 
+// TextDecoder::forward with n_tokens > 1 at n_past > 0 (src/text_decoder.cpp:
+// 392-581 builds one graph for the chunk): the chunk's rows through the
+// prefill layers at positions n_past[b] .. n_past[b] + P[b] - 1, causal
+// attention over the cached keys and the chunk's own; logits of each chunk's
+// last row.  n_past[b] = 0 is the plain prefill without audio.
+extern "C" int qasr_prefill_chunk(qasr_ctx *c, const int32_t *ids, const int *P, const int *n_past, int B, float *logits_last,
+                                  int32_t *argmax) {
+    if (!c || !ids || !P || !n_past || B <= 0) return fail(QASR_ERR_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(c->m->device));
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->pin_used = 0;
+    std::vector<int> Pv(P, P + B), Nv(B, 0), ap(B, -1), p0(n_past, n_past + B);
+    long nid = 0;
+    for (int b = 0; b < B; b++) nid += P[b];
+    for (long i = 0; i < nid; i++)
+        if (ids[i] < 0 || ids[i] >= c->m->hp.vocab) return fail(QASR_ERR_ARG, "token id out of range");
+    std::vector<int32_t> idv(ids, ids + nid);
+    int rc;
+    if ((rc = run_prefill(c, idv, Pv, nullptr, ap, Nv, logits_last != nullptr, nullptr, &p0))) return rc;
+    if (logits_last) HIPCHK(hipMemcpyAsync(logits_last, c->d_logits, (size_t)B * c->m->hp.vocab * 4, hipMemcpyDeviceToHost, c->st));
+    if (argmax) HIPCHK(hipMemcpyAsync(argmax, c->d_tok, B * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
 extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_past, int B, float *logits, int32_t *argmax) {
     if (!c || !tok || !n_past || B <= 0 || B > c->max_batch) return fail(QASR_ERR_ARG, "bad arguments");
     HIPCHK(hipSetDevice(c->m->device));
@@ -2232,31 +2280,55 @@ extern "C" int qasr_tokenize(const qasr_model *m, const char *text, int32_t *ids
 // <|audio_end|> text prompt (n from HF _get_feat_extract_output_lengths, the
 // encoder rows spliced from index 1) -> one causal prefill -> at every
 // timestamp-token row: RMSNorm -> classify head -> argmax (strict '>', :1280-1306).
-static int align_classes(qasr_ctx *c, const float *pcm, int n, const std::vector<int32_t> &text_ids,
-                         std::vector<int32_t> &classes, qasr_timings *t) {
+// B clips at once (configs[4]'s aligner leg over a rank's transcripts): the
+// mel and the windowed encoder of all clips in one pass, one prefill of the B
+// prompts (prefill_layers' sequences), one classify GEMM over every timestamp
+// row of every clip.  Rows are independent in each of them, so a clip's
+// classes are the same alone or in a batch (tests/test_gpu_aligner.py).
+static int align_classes(qasr_ctx *c, const float *const *pcm, const int *n, const std::vector<std::vector<int32_t>> &text_ids,
+                         std::vector<std::vector<int32_t>> &classes, qasr_timings *t) {
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
+    const int B = (int)text_ids.size();
     if (!hp.aligner || !m->cls_w) return fail(QASR_ERR_STATE, "not a ForcedAligner model");
+    if (B <= 0 || B > c->max_batch) return fail(QASR_ERR_ARG, "aligner batch exceeds the context's max_batch");
     HIPCHK(hipSetDevice(m->device));
     HIPCHK(hipStreamSynchronize(c->st));
     c->pin_used = 0;
     hipStream_t s = c->st;
     int rc;
-    if ((rc = ensure(c, c->pcm, (size_t)std::max(n, 1) * 4))) return rc;
-    HIPCHK(hipMemcpyAsync(c->pcm.p, pcm, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    std::vector<long> off(B);
+    std::vector<int> nv(n, n + B);
+    long tot = 0;
+    for (int b = 0; b < B; b++) {
+        if (n[b] <= 0) return fail(QASR_ERR_ARG, "bad arguments");
+        off[b] = tot;
+        tot += n[b];
+    }
+    if ((rc = ensure(c, c->pcm, (size_t)std::max<long>(tot, 1) * 4))) return rc;
+    for (int b = 0; b < B; b++)
+        HIPCHK(hipMemcpyAsync(c->pcm.as<float>() + off[b], pcm[b], (size_t)n[b] * 4, hipMemcpyHostToDevice, s));
     HIPCHK(hipEventRecord(c->ev[0], s));
     std::vector<long> mo;
     std::vector<int> T, Nb;
-    if ((rc = run_mel(c, {0L}, {n}, mo, T))) return rc;
+    if ((rc = run_mel(c, off, nv, mo, T))) return rc;
     HIPCHK(hipEventRecord(c->ev[1], s));
     if ((rc = run_encoder(c, c->mel.as<float>(), mo, T, false, Nb))) return rc;
     HIPCHK(hipEventRecord(c->ev[2], s));
-    const std::vector<int32_t> ids = build_align_tokens(hp, text_ids, feat_extract_output_lengths(T[0]));
-    const int P = (int)ids.size();
-    if (P > c->max_ctx) return fail(QASR_ERR_ARG, "Context length exceeded (aligner prompt > max_ctx)");
-    std::vector<int> rows;
-    for (int i = 0; i < P; i++) if (ids[i] == hp.timestamp_id) rows.push_back(i);
-    if ((rc = prefill_layers(c, ids, {P}, c->feats.as<float>(), {1}, {Nb[0]}, nullptr))) return rc;
+    std::vector<int32_t> ids;
+    std::vector<int> P(B), ap(B, 1), rows, nrows(B, 0);
+    for (int b = 0; b < B; b++) {
+        const std::vector<int32_t> ib = build_align_tokens(hp, text_ids[b], feat_extract_output_lengths(T[b]));
+        P[b] = (int)ib.size();
+        if (P[b] > c->max_ctx) return fail(QASR_ERR_ARG, "Context length exceeded (aligner prompt > max_ctx)");
+        for (int i = 0; i < P[b]; i++)
+            if (ib[i] == hp.timestamp_id) {
+                rows.push_back((int)ids.size() + i);   // the row in the prefill's concatenated rows
+                nrows[b]++;
+            }
+        ids.insert(ids.end(), ib.begin(), ib.end());
+    }
+    if ((rc = prefill_layers(c, ids, P, c->feats.as<float>(), ap, Nb, nullptr))) return rc;
     const int NT = (int)rows.size(), H = hp.hidden;
     std::vector<unsigned long long> keys(NT);
     if (NT > 0) {
@@ -2273,17 +2345,25 @@ static int align_classes(qasr_ctx *c, const float *pcm, int n, const std::vector
     }
     HIPCHK(hipEventRecord(c->ev[3], s));
     HIPCHK(hipEventSynchronize(c->ev[3]));
-    classes.resize(NT);
-    for (int i = 0; i < NT; i++) classes[i] = (int32_t)(0xffffffffu - (uint32_t)(keys[i] & 0xffffffffu));
+    classes.assign(B, {});
+    for (int b = 0, k = 0; b < B; b++)
+        for (int i = 0; i < nrows[b]; i++, k++) classes[b].push_back((int32_t)(0xffffffffu - (uint32_t)(keys[k] & 0xffffffffu)));
     if (t) {
-        float a = 0, b = 0, d = 0, tot = 0;
+        float a = 0, bb = 0, d = 0, tt = 0;
         HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
-        HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+        HIPCHK(hipEventElapsedTime(&bb, c->ev[1], c->ev[2]));
         HIPCHK(hipEventElapsedTime(&d, c->ev[2], c->ev[3]));
-        HIPCHK(hipEventElapsedTime(&tot, c->ev[0], c->ev[3]));
-        *t = qasr_timings{a, b, d, 0.0, tot, 0};
+        HIPCHK(hipEventElapsedTime(&tt, c->ev[0], c->ev[3]));
+        *t = qasr_timings{a, bb, d, 0.0, tt, 0};
     }
     return 0;
+}
+static int align_classes(qasr_ctx *c, const float *pcm, int n, const std::vector<int32_t> &text_ids, std::vector<int32_t> &classes,
+                         qasr_timings *t) {
+    std::vector<std::vector<int32_t>> cls;
+    const int rc = align_classes(c, &pcm, &n, {text_ids}, cls, t);
+    if (!rc) classes = cls[0];
+    return rc;
 }
 
 extern "C" int qasr_align(qasr_ctx *c, const float *pcm, int n, const int32_t *text_ids, int n_text, int32_t *classes,
@@ -2370,6 +2450,15 @@ static std::string json_escape(const std::string &s) {   // src/main.cpp:230-254
 // whole alignment -> the CLI's JSON document (src/main.cpp:257-276); returns
 // the JSON length (excluding NUL) or minus the error code; writes at most
 // cap-1 bytes + NUL
+static std::string align_doc(const qasr_model *m, const std::vector<std::string> &words, const std::vector<int32_t> &cls, int n);
+static int put_str(const std::string &js, char *out, int cap) {
+    if (out && cap > 0) {
+        const size_t k = std::min(js.size(), (size_t)cap - 1);
+        memcpy(out, js.data(), k);
+        out[k] = 0;
+    }
+    return (int)js.size();
+}
 extern "C" int qasr_align_json(qasr_ctx *c, const float *pcm, int n, const char *text, const char *language, char *out,
                                int cap, qasr_timings *t) {
     if (!c || !pcm || n <= 0 || !text) return -fail(QASR_ERR_ARG, "bad arguments");
@@ -2379,6 +2468,30 @@ extern "C" int qasr_align_json(qasr_ctx *c, const float *pcm, int n, const char 
     std::vector<int32_t> cls;
     int rc = align_classes(c, pcm, n, ids, cls, t);
     if (rc) return -rc;
+    return put_str(align_doc(m, words, cls, n), out, cap);
+}
+
+// B clips in one aligner pass (align_classes' batch form): the documents as
+// one JSON array, in input order; returns its length or minus the error code
+extern "C" int qasr_align_json_batch(qasr_ctx *c, const float *const *pcm, const int *n, const char *const *text, int B,
+                                     const char *language, char *out, int cap, qasr_timings *t) {
+    if (!c || !pcm || !n || !text || B <= 0) return -fail(QASR_ERR_ARG, "bad arguments");
+    const qasr_model *m = c->m;
+    std::vector<std::vector<std::string>> words(B);
+    std::vector<std::vector<int32_t>> ids(B), cls;
+    for (int b = 0; b < B; b++) {
+        if (!pcm[b] || n[b] <= 0 || !text[b]) return -fail(QASR_ERR_ARG, "bad arguments");
+        ids[b] = align_tokens(m, text[b], language ? language : "", words[b]);
+    }
+    int rc = align_classes(c, pcm, n, ids, cls, t);
+    if (rc) return -rc;
+    std::string js = "[";
+    for (int b = 0; b < B; b++) js += (b ? ",\n" : "") + align_doc(m, words[b], cls[b], n[b]);
+    return put_str(js + "]", out, cap);
+}
+
+// the CLI's document for one clip (src/main.cpp:257-276)
+static std::string align_doc(const qasr_model *m, const std::vector<std::string> &words, const std::vector<int32_t> &cls, int n) {
     const std::vector<int32_t> fixed = fix_timestamp_classes(cls);
     const float dur = (float)n / 16000.0f, seg = m->hp.ts_segment_ms / 1000.0f;
     std::vector<float> ts(fixed.size());
@@ -2394,12 +2507,7 @@ extern "C" int qasr_align_json(qasr_ctx *c, const float *pcm, int n, const char 
         js += "\n";
     }
     js += "  ]\n}";
-    if (out && cap > 0) {
-        const size_t k = std::min(js.size(), (size_t)cap - 1);
-        memcpy(out, js.data(), k);
-        out[k] = 0;
-    }
-    return (int)js.size();
+    return js;
 }
 
 // --------------------------------------------------------- host utilities

@@ -230,10 +230,13 @@ __global__ __launch_bounds__(64 * PX_W, PX_MINW) void prefill_attn_exact_kernel(
 #pragma unroll
     for (int s = 0; s < 4; s++)
         qf[s] = qv ? *(const half8 *)(a.q + (long)(row0 + q0 + ql) * QD + h * 128 + 32 * s + 8 * g) : half8{};
-    const int lim = qv ? q0 + ql : -1;   // causal: keys <= the query's position
-    const int kend = min(L, q0 + PX_ROWS);
-    const int r0 = PX_R * wid;                           // this wave's first row
-    const int wlast = min(L - 1, q0 + r0 + PX_R - 1);    // its last key (its longest row)
+    // a chunk after P0 cached tokens (TextDecoder::forward at n_past > 0): row t
+    // at position P0 + t, keys 0 .. P0 + L - 1 (the aligner's fp32 K rows: P0 = 0)
+    const int P0 = a.seq_pos0 ? a.seq_pos0[sq] : 0;
+    const int lim = qv ? P0 + q0 + ql : -1;   // causal: keys <= the query's position
+    const int kend = min(P0 + L, P0 + q0 + PX_ROWS);
+    const int r0 = PX_R * wid;                                     // this wave's first row
+    const int wlast = min(P0 + L - 1, P0 + q0 + r0 + PX_R - 1);    // its last key (its longest row)
     float M[PX_R], S[PX_R];
     half2v acc[PX_R];
 #pragma unroll

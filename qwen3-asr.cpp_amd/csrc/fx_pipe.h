@@ -34,7 +34,16 @@ namespace qasr {
 // is not a new maximum, w = -ms where it is (vs = 1 there); keys with -inf get
 // weight 0.  M: running maximum (in/out); Sl: this lane's share of S, rescaled
 // to the new maximum; returns the weight, m64 = the buffer's new-maximum bits.
+// A buffer without a new maximum (all but a few: a running maximum over n
+// scores has ~ln n records) takes one expf a lane and no scan; the full path
+// gives the same values there (Mp = Mn = M, expf(0) = 1).
 __device__ __forceinline__ float fxp_weights(float s, float &M, float &Sl, unsigned long long &m64) {
+    m64 = __ballot(s > M);
+    if (m64 == 0ull) {   // (uniform) s <= M on every lane
+        const float w = s != -INFINITY ? expf(s - M) : 0.0f;
+        Sl += w;
+        return w;
+    }
     const float inc = wave_scan_max(s);
     const float Mp = fmaxf(M, dpp_ninf<0x138, 0xF>(inc));   // exclusive prefix (lane 0: M)
     const float Mn = fmaxf(M, lane_f(inc, 63));
@@ -44,6 +53,16 @@ __device__ __forceinline__ float fxp_weights(float s, float &M, float &Sl, unsig
     Sl = (M == -INFINITY ? 0.0f : Sl * expf(M - Mn)) + (s == -INFINITY ? 0.0f : expf(s - Mn));
     M = Mn;
     return gt ? -e : (s != -INFINITY ? e : 0.0f);
+}
+
+// DX_Q keys of V^T from key block j0 / 8 through a buffer descriptor (vt:
+// the wave's key block 0; voff = 16 lane bytes): the block offset is an SGPR
+// (soffset), so the loads cost no VALU address arithmetic; blocks past lastb
+// re-read lastb (as fx_loadQ)
+__device__ __forceinline__ void fxp_loadQ(u32x4 *v, __amdgpu_buffer_rsrc_t rs, int voff, int j0, int lastb) {
+#pragma unroll
+    for (int i = 0; i < DX_Q / 8; i++)
+        v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, min(j0 / 8 + i, lastb) * 2048, 0));
 }
 
 // one 8-key group of the chain: v = 8 keys of this lane's dimension (fp16
@@ -192,7 +211,15 @@ __device__ __forceinline__ float fxp_chain(const Src &src, const uint16_t *__res
     };
     unsigned long long m0, m1;
     u32x4 va[DX_Q / 8], vb[DX_Q / 8];
-    fx_loadQ(va, vt, loff, 0, lastb);
+    // (vt and lastb are wave-uniform; readfirstlane says so, else every load
+    // becomes a waterfall loop over the lanes' descriptors)
+    const unsigned long long vtu = (unsigned long long)vt;
+    const uint16_t *vts = (const uint16_t *)(((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(vtu >> 32)) << 32) |
+                                             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)vtu));
+    lastb = __builtin_amdgcn_readfirstlane(lastb);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)vts, (short)0, (lastb + 1) * 2048, 0x00020000);
+    const int voff = 2 * loff;
+    fxp_loadQ(va, rs, voff, 0, lastb);
     auto q0 = src.issue(0);
     auto q1 = src.issue(DX_Q);
     auto q2 = src.issue(2 * DX_Q);
@@ -200,12 +227,12 @@ __device__ __forceinline__ float fxp_chain(const Src &src, const uint16_t *__res
     int w[8];
     fxp_first(wa, w);
     for (int j0 = 0; j0 < nl; j0 += 2 * DX_Q) {
-        fx_loadQ(vb, vt, loff, j0 + DX_Q, lastb);
+        fxp_loadQ(vb, rs, voff, j0 + DX_Q, lastb);
         wb = wts(src.take(q1, j0 + DX_Q), j0 + DX_Q, m1);
         q1 = src.issue(j0 + 3 * DX_Q);
         fxp_buffer(acc, va, w, wa, wb, m0);
         if (j0 + DX_Q >= nl) break;
-        fx_loadQ(va, vt, loff, j0 + 2 * DX_Q, lastb);
+        fxp_loadQ(va, rs, voff, j0 + 2 * DX_Q, lastb);
         wa = wts(src.take(q2, j0 + 2 * DX_Q), j0 + 2 * DX_Q, m0);
         q2 = src.issue(j0 + 4 * DX_Q);
         fxp_buffer(acc, vb, w, wb, wa, m1);

@@ -244,6 +244,9 @@ struct PrefillAttnArgs {
     const float *q32, *k32;              // non-null (exact kernel only): fp32 scores from these fp32 rows, key k of
                                          // sequence s at row seq_row0[s] + k (the aligner's K stays fp32,
                                          // src/forced_aligner.cpp:1041-1046)
+    const int *seq_pos0;                 // non-null: sequence s's rows sit at positions seq_pos0[s] + t (a chunk after
+                                         // seq_pos0[s] cached tokens, TextDecoder::forward at n_past > 0); keys
+                                         // 0 .. seq_pos0[s] + seq_len[s] - 1, causal by position (not with q32/k32)
 };
 void launch_prefill_attention(const PrefillAttnArgs &a, hipStream_t s);
 // the same attention with ggml's CPU flash-attention numerics (fa_exact.hip):
@@ -339,6 +342,8 @@ void launch_embed(const int32_t *ids, int rows, const uint16_t *embd, int hidden
 void launch_argmax_finish(const unsigned long long *amax, int B, int32_t *ids, int32_t *hist, int hist_stride,
                           const int *step, hipStream_t s);
 void launch_fill_u64(unsigned long long *p, int n, unsigned long long v, hipStream_t s);
+// dst row r = src row idx[r], fp32 rows of D floats (D % 4 == 0)
+void launch_gather_rows(const float *src, const int *idx, int rows, int D, float *dst, hipStream_t s);
 // decode-step bookkeeping on device: n_kv[b] += 1, row_pos[b] += 1, step += 1
 void launch_step_advance(int *row_pos, int *n_kv, int *step, int B, hipStream_t s);
 

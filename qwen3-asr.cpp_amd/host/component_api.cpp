@@ -375,13 +375,13 @@ bool TextDecoder::forward_with_audio(const int32_t *tokens, int32_t n_tokens, co
     } else if (splice) {
         error_msg_ = "audio embeddings are spliced by the prefill: forward_with_audio needs n_past = 0";
         return false;
+    } else if (n_tokens == 1) {
+        rc = qasr_decode_step(ctx_, tokens, &n_past, 1, output.data(), nullptr);
     } else {
-        // causal attention over the cache: the tokens one decode step each, in
-        // order (the logits of the last one kept)
-        for (int32_t i = 0; i < n_tokens && rc == 0; i++) {
-            const int np = n_past + i;
-            rc = qasr_decode_step(ctx_, tokens + i, &np, 1, i + 1 == n_tokens ? output.data() : nullptr, nullptr);
-        }
+        // one causal chunk prefill over the cache (src/text_decoder.cpp:392-581:
+        // one graph for the chunk), the logits of its last row
+        const int P = n_tokens;
+        rc = qasr_prefill_chunk(ctx_, tokens, &P, &n_past, 1, output.data(), nullptr);
     }
     if (rc != 0) {
         error_msg_ = std::string("Failed to compute graph: ") + qasr_last_error();

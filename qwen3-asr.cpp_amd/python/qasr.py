@@ -23,7 +23,7 @@ EXPORTS = [
     "qasr_model_load", "qasr_model_free", "qasr_model_hparams", "qasr_model_device_bytes",
     "qasr_ctx_create", "qasr_ctx_free",
     "qasr_mel_frames", "qasr_encoder_frames", "qasr_prompt_len", "qasr_build_prompt",
-    "qasr_mel", "qasr_encode", "qasr_encode_conv", "qasr_prefill", "qasr_decode_step",
+    "qasr_mel", "qasr_encode", "qasr_encode_conv", "qasr_prefill", "qasr_prefill_chunk", "qasr_decode_step",
     "qasr_stage_audio", "qasr_run", "qasr_run_staged", "qasr_run_stream", "qasr_run_stream_staged", "qasr_set_system_prompt", "qasr_transcribe_batch",
     "qasr_set_probe", "qasr_get_probe", "qasr_get_probe_device",
     "qasr_ctx_set_option", "qasr_ctx_get_option", "qasr_debug_read",
@@ -31,7 +31,7 @@ EXPORTS = [
     "qasr_detokenize", "qasr_tokenize",
     "qasr_load_wav", "qasr_write_wav", "qasr_synth_pcm", "qasr_write_synthetic_gguf",
     "qasr_align", "qasr_align_tokenize", "qasr_model_load_korean_dict", "qasr_fix_timestamps",
-    "qasr_align_prompt_len", "qasr_align_json", "qasr_align_words",
+    "qasr_align_prompt_len", "qasr_align_json", "qasr_align_json_batch", "qasr_align_words",
 ]
 
 
@@ -87,6 +87,7 @@ def lib() -> C.CDLL:
             "qasr_encode": ([P, F, IP, I, F], I), "qasr_encode_conv": ([P, F, IP, I, F], I),
             "qasr_prefill": ([P, I32P, IP, F, IP, IP, I, F, I32P], I),
             "qasr_decode_step": ([P, I32P, IP, I, F, I32P], I),
+            "qasr_prefill_chunk": ([P, I32P, IP, IP, I, F, I32P], I),
             "qasr_stage_audio": ([P, C.POINTER(F), IP, I], I),
             "qasr_run": ([P, I, I, I32P, IP, C.POINTER(Timings)], I),
             "qasr_run_staged": ([P, IP, I, I, I, I32P, IP, C.POINTER(Timings)], I),
@@ -112,6 +113,8 @@ def lib() -> C.CDLL:
             "qasr_align_prompt_len": ([I, I], I),
             "qasr_align_words": ([P, C.c_char_p, C.c_char_p, C.c_char_p, I], I),
             "qasr_align_json": ([P, F, I, C.c_char_p, C.c_char_p, C.c_char_p, I, C.POINTER(Timings)], I),
+            "qasr_align_json_batch": ([P, C.POINTER(F), IP, C.POINTER(C.c_char_p), I, C.c_char_p, C.c_char_p, I,
+                                       C.POINTER(Timings)], I),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -381,6 +384,20 @@ class Context:
                "qasr_decode_step")
         return logits, am
 
+    def prefill_chunk(self, ids_list, n_past, want_logits=True):
+        """qasr_prefill_chunk: sequence b's tokens ids_list[b] after n_past[b]
+        cached ones, one causal chunk (TextDecoder::forward, n_tokens > 1);
+        returns (logits of each chunk's last row, argmax)"""
+        P = np.array([len(x) for x in ids_list], np.int32)
+        ids = np.ascontiguousarray(np.concatenate([np.asarray(x, np.int32) for x in ids_list]), np.int32)
+        npast = np.ascontiguousarray(n_past, np.int32)
+        B = len(P)
+        logits = np.zeros((B, self.model.hp.vocab_size), np.float32) if want_logits else None
+        am = np.zeros(B, np.int32)
+        _check(lib().qasr_prefill_chunk(self.h, _i32(ids), _i(P), _i(npast), B, _f(logits) if want_logits else None, _i32(am)),
+               "qasr_prefill_chunk")
+        return logits, am
+
     # ---- whole path --------------------------------------------------------
     def stage_audio(self, clips: Sequence[np.ndarray]) -> None:
         self._staged = [np.ascontiguousarray(c, np.float32) for c in clips]
@@ -530,12 +547,35 @@ class Context:
         import json
         pcm = np.ascontiguousarray(pcm, np.float32)
         t = Timings()
-        n = lib().qasr_align_json(self.h, _f(pcm), len(pcm), text.encode(), language.encode(), None, 0, C.byref(t))
+        cap = 8192 + 40 * len(text.encode())   # (one call in practice: the escaped words + ~50 B a word)
+        buf = C.create_string_buffer(cap)
+        n = lib().qasr_align_json(self.h, _f(pcm), len(pcm), text.encode(), language.encode(), buf, cap, C.byref(t))
         if n < 0:
             raise QasrError(f"qasr_align_json: {lib().qasr_last_error().decode(errors='replace')}")
-        buf = C.create_string_buffer(n + 1)
-        lib().qasr_align_json(self.h, _f(pcm), len(pcm), text.encode(), language.encode(), buf, n + 1, C.byref(t))
+        if n >= cap:   # larger than the bound: run again into a buffer of the reported size
+            buf = C.create_string_buffer(n + 1)
+            lib().qasr_align_json(self.h, _f(pcm), len(pcm), text.encode(), language.encode(), buf, n + 1, C.byref(t))
         return json.loads(buf.raw[:n].decode("utf-8")), t
+
+    def align_json_batch(self, pcms, texts, language: str = ""):
+        """qasr_align_json_batch: B clips in one aligner pass -> (list of the
+        CLI documents, parsed, in input order; timings)"""
+        import json
+        arrs = [np.ascontiguousarray(p, np.float32) for p in pcms]
+        B = len(arrs)
+        ptrs = (C.POINTER(C.c_float) * B)(*[_f(a) for a in arrs])
+        n = np.array([len(a) for a in arrs], np.int32)
+        tx = (C.c_char_p * B)(*[t.encode() for t in texts])
+        t = Timings()
+        cap = 8192 * B + 40 * sum(len(x.encode()) for x in texts)
+        buf = C.create_string_buffer(cap)
+        k = lib().qasr_align_json_batch(self.h, ptrs, _i(n), tx, B, language.encode(), buf, cap, C.byref(t))
+        if k < 0:
+            raise QasrError(f"qasr_align_json_batch: {lib().qasr_last_error().decode(errors='replace')}")
+        if k >= cap:
+            buf = C.create_string_buffer(k + 1)
+            lib().qasr_align_json_batch(self.h, ptrs, _i(n), tx, B, language.encode(), buf, k + 1, C.byref(t))
+        return json.loads(buf.raw[:k].decode("utf-8")), t
 
     def transcribe(self, clips, max_tokens=1024, ignore_eos=False) -> RunResult:
         self.stage_audio(clips)

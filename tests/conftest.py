@@ -3,9 +3,11 @@
 `-m "not gpu"`: oracle vs golden vectors, host logic, C-ABI exports (no GPU).
 `-m gpu`: parity of the HIP path (through the C-ABI) against the oracle.
 """
+import json
 import os
 import subprocess
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -96,3 +98,39 @@ def gpu(built):
     if not gpu_available():
         pytest.fail("GPU tests need a HIP device: the HIP path has no CPU fallback")
     return True
+
+
+# ------------------------------------------------------------ parity record
+# Every GPU parity test records what it measured (absolute and relative max
+# |delta| against the oracle, margins, noise floors) through the `parity`
+# fixture; the session writes them to $QASR_PARITY_OUT (default
+# gpurun_out/parity.json), which tools/r4 copies to profiles/<round>/parity.json.
+_PARITY = {}
+
+
+def _plain(v):
+    if isinstance(v, (list, tuple)):
+        return [_plain(x) for x in v]
+    if isinstance(v, (np.floating, float)):
+        return float(f"{float(v):.6g}")
+    if isinstance(v, (np.integer, int)) and not isinstance(v, bool):
+        return int(v)
+    return v
+
+
+@pytest.fixture(scope="session")
+def parity():
+    def rec(name: str, **vals):
+        _PARITY.setdefault(name, {}).update({k: _plain(v) for k, v in vals.items()})
+    return rec
+
+
+def pytest_sessionfinish(session, exitstatus):
+    if not _PARITY:
+        return
+    out = os.environ.get("QASR_PARITY_OUT") or os.path.join(ROOT, "gpurun_out", "parity.json")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    env = {k: v for k, v in os.environ.items() if k.startswith("QASR_") and k != "QASR_PARITY_OUT"}
+    with open(out, "w") as f:
+        json.dump({"written": time.strftime("%Y-%m-%d %H:%M:%S"), "exitstatus": int(exitstatus), "env": env,
+                   "tests": dict(sorted(_PARITY.items()))}, f, indent=1)

@@ -131,7 +131,7 @@ def test_cli_align_and_transcribe_align(al, tiny_gguf, tmp_path):
 
 
 @pytest.mark.slow
-def test_full_aligner_encode_and_classes(gpu, tmp_path_factory):
+def test_full_aligner_encode_and_classes(gpu, tmp_path_factory, parity):
     """Qwen3-ForcedAligner-0.6B dimensions (24 x 1024 encoder, vocab 152064)."""
     p = str(tmp_path_factory.mktemp("alf") / "aligner-full.gguf")
     qasr.write_synthetic_gguf(p, "aligner", 42, 1)
@@ -151,7 +151,36 @@ def test_full_aligner_encode_and_classes(gpu, tmp_path_factory):
         srt = np.sort(olg, axis=1)
         margin = srt[:, -1] - srt[:, -2]
         same = np.array(cls) == np.array(ocls)
+        parity("full_aligner_1p6s", enc_abs_max=mx, enc_abs_mean=mean, rows=len(cls), classes_equal=int(same.sum()),
+               min_margin_rel=float((margin / scale).min()), mismatch_margins_rel=(margin / scale)[~same].tolist())
         assert same[margin > 5e-3 * scale].all(), (cls, ocls, margin / scale)
     finally:
         c.close()
         m.close()
+
+
+def test_align_json_batch_equals_single(al):
+    """qasr_align_json_batch (configs[4]'s aligner leg over many transcripts):
+    clips of different lengths and texts in one aligner pass give the same
+    documents as one clip at a time, and the classes match the oracle's"""
+    p, m, _, om = al
+    clips = [qasr.synth_pcm(8500 + i, int(s * SR)) for i, s in enumerate((2.0, 6.4, 0.9, 10.0))]
+    texts = ["ab cd ef", "ab cd ef gh ij kl mn op", "xy", 'zz "q" ab']
+    cb = qasr.Context(m, max_batch=4, max_ctx=2048)
+    try:
+        docs, t = cb.align_json_batch(clips, texts)
+        assert t.t_total_ms > 0
+        for pcm, text, d in zip(clips, texts, docs):
+            one, _ = cb.align_json(pcm, text)
+            assert d == one
+        ids, _ = m.align_tokenize(texts[1])
+        cls, _ = cb.align(clips[1], ids)
+        ocls, olg, _ = om.align_classes(clips[1], ids)
+        srt = np.sort(olg, axis=1)
+        margin = srt[:, -1] - srt[:, -2]
+        same = np.array(cls) == np.array(ocls)
+        assert same[margin > 5e-3 * float(np.abs(olg).max())].all(), (cls, ocls)
+        with pytest.raises(qasr.QasrError):   # more clips than the context's slots
+            cb.align_json_batch(clips + clips[:1], texts + texts[:1])
+    finally:
+        cb.close()

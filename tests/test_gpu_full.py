@@ -56,7 +56,7 @@ def test_full_encode(full, secs):
     assert d.max() <= 2e-2 and d.mean() <= 1e-3, (d.max(), d.mean())
 
 
-def test_full_prefill_and_steps(full):
+def test_full_prefill_and_steps(full, parity):
     m, c, om = full
     mel = op.log_mel(qasr.synth_pcm(12000, 2 * SR))
     feats = om.encode(mel)
@@ -65,6 +65,7 @@ def test_full_prefill_and_steps(full):
     d = op.OracleDecoder(om, 256)
     lo = d.forward(ids, 0, feats, pos)
     ab, rel = _err(lg[0], lo)
+    errs = [(ab, rel)]
     assert rel <= 1e-2, (ab, rel)
     rng = np.random.default_rng(3)
     n_past = len(ids)
@@ -73,8 +74,11 @@ def test_full_prefill_and_steps(full):
         lg, am = c.decode_step([tok], [n_past])
         lo = d.forward([tok], n_past)
         ab, rel = _err(lg[0], lo)
+        errs.append((ab, rel))
         assert rel <= 1e-2, (ab, rel)
         n_past += 1
+    parity("full_2s_prefill_and_6_steps", abs_max=[e[0] for e in errs], rel_max=[e[1] for e in errs],
+           scale=float(np.abs(lo).max()), fused_exact=c.get_option("fused_exact"))
 
 
 def test_full_transcribe_tokens(full):
@@ -290,7 +294,7 @@ def test_full_two_threads_one_device(full):
 
 
 @pytest.mark.timeout(900)
-def test_full_configs1_92s(full):
+def test_full_configs1_92s(full, parity):
     """configs[1] at its full size (92 s clip, N = 1196 encoder frames,
     P = 1211 prompt tokens): mel, encoder, prefill logits and 15
     teacher-forced decode steps against the oracle, and the first 16 greedy
@@ -305,6 +309,7 @@ def test_full_configs1_92s(full):
     feats_g = c.encode([mel_o])[0]
     assert feats_o.shape == (1196, 1024)
     d = np.abs(feats_g - feats_o)
+    parity("configs1_92s_encoder", abs_max=float(d.max()), abs_mean=float(d.mean()), mel_abs_max=float(np.abs(mel_g - mel_o).max()))
     assert d.max() <= 2e-2 and d.mean() <= 1e-3, (d.max(), d.mean())
     ids, pos = om.prompt(1196), 9
     assert len(ids) == 1211
@@ -329,13 +334,16 @@ def test_full_configs1_92s(full):
         assert c.get_option("fused_exact") == 1
         errs.append(_err(lg[0], lo[k]))
     print("configs[1] decode steps (abs, rel):", [(round(a_, 4), round(r_, 5)) for a_, r_ in errs])
-    assert max(r_ for _, r_ in errs) <= 1e-2, errs
     r = c.transcribe([pcm], max_tokens=16, ignore_eos=True)
+    parity("configs1_92s_prefill_and_15_steps", prefill_abs=ab, prefill_rel=rel, steps_abs=[e[0] for e in errs],
+           steps_rel=[e[1] for e in errs], scale=float(np.abs(lo[1]).max()), greedy16_equal=r.tokens[0] == toks,
+           fx_pipe=c.get_option("fx_pipe"))
+    assert max(r_ for _, r_ in errs) <= 1e-2, errs
     assert r.tokens[0] == toks
 
 
 @pytest.mark.timeout(900)
-def test_full_configs2_q8_b64_30s(gpu, tmp_path_factory):
+def test_full_configs2_q8_b64_30s(gpu, tmp_path_factory, parity):
     """configs[2] at its full size: Qwen3-ASR-0.6B Q8_0 (synthetic weights),
     64 x 30 s clips (P = 405 prompt tokens each, 105-token budget).  All 64
     rows bit-identical (identical clips), every budget met, and row 0 against
@@ -376,14 +384,17 @@ def test_full_configs2_q8_b64_30s(gpu, tmp_path_factory):
     d, dn = op.OracleDecoder(om, len(ids) + 8), op.OracleDecoder(om, len(ids) + 8)
     lo, ln = d.forward(ids, 0, feats, pos), dn.forward(ids, 0, featsn, pos)
     tol = max(1e-2 * float(np.abs(lo).max()), 2.5 * float(np.abs(lo - ln).max()))
-    assert np.abs(lg[0] - lo).max() <= tol, (float(np.abs(lg[0] - lo).max()), tol)
     lo1, ln1 = d.forward([tok0], len(ids)), dn.forward([tok0], len(ids))
     tol1 = max(1e-2 * float(np.abs(lo1).max()), 2.5 * float(np.abs(lo1 - ln1).max()))
+    parity("configs2_q8_b64_30s_row0", prefill_abs=float(np.abs(lg[0] - lo).max()), prefill_tol=tol,
+           step1_abs=float(np.abs(lg1[0] - lo1).max()), step1_tol=tol1, scale=float(np.abs(lo).max()),
+           noise_prefill=float(np.abs(lo - ln).max()), noise_step1=float(np.abs(lo1 - ln1).max()))
+    assert np.abs(lg[0] - lo).max() <= tol, (float(np.abs(lg[0] - lo).max()), tol)
     assert np.abs(lg1[0] - lo1).max() <= tol1, (float(np.abs(lg1[0] - lo1).max()), tol1)
 
 
 @pytest.mark.timeout(900)
-def test_full_configs3_f16_b64_30s(full):
+def test_full_configs3_f16_b64_30s(full, parity):
     """configs[3]'s per-GPU shape at full size: Qwen3-ASR-0.6B f16 (synthetic
     weights), 64 x 30 s clips (P = 405, 105-token budget) -- the skinny
     QKV / o / gate-up / down tilings at 64 rows, per-sequence decode attention
@@ -422,6 +433,8 @@ def test_full_configs3_f16_b64_30s(full):
     finally:
         c.close()
     print("configs[3] prefill + decode steps (abs, rel):", [(round(a_, 4), round(r_, 5)) for a_, r_ in errs])
+    parity("configs3_f16_b64_30s_row0_prefill_and_5_steps", abs_max=[e[0] for e in errs], rel_max=[e[1] for e in errs],
+           scale=float(np.abs(lo[0]).max()))
     assert max(r_ for _, r_ in errs) <= 1e-2, errs
 
 

@@ -135,7 +135,7 @@ def test_prefill_logits_match_oracle(tiny, tiny_oracle):
 
 
 @pytest.mark.parametrize("exact", [1, 0])
-def test_decode_steps_teacher_forced(tiny, tiny_oracle, exact):
+def test_decode_steps_teacher_forced(tiny, tiny_oracle, exact, parity):
     """exact = 1 (the default): ggml's fp16 V accumulation (fx_chain.h),
     against the default oracle; exact = 0 (option fa_exact_decode = 0): the
     fp32-accumulating split-K decode attention, against the oracle's
@@ -165,6 +165,7 @@ def test_decode_steps_teacher_forced(tiny, tiny_oracle, exact):
             n_past += 1
     finally:
         c.set_option("fa_exact_decode", 1)   # the default
+    parity(f"tiny_decode_24_steps_exact{exact}", abs_max=worst_abs, rel_max=worst)
     assert worst <= 1e-2, (worst_abs, worst)
 
 
@@ -218,3 +219,36 @@ def test_transcribe_eos_and_errors(tiny):
         c.transcribe([qasr.synth_pcm(9001, 100)], max_tokens=4)   # < 160 samples: no audio frames
     with pytest.raises(qasr.QasrError, match="Context length"):
         c.transcribe([qasr.synth_pcm(9002, SR)], max_tokens=10000)
+
+
+def test_chunk_prefill_after_cached_tokens(tiny, tiny_oracle, parity):
+    """TextDecoder::forward with n_tokens > 1 at n_past > 0 (src/text_decoder.cpp:
+    392-581: one causal graph for the chunk) = qasr_prefill_chunk: the chunk's
+    last-row logits, and a decode step after it, against the oracle's chunk
+    forward; two chunks back to back, then a chunk at n_past = 0"""
+    m, c = tiny
+    feats = tiny_oracle.encode(op.log_mel(qasr.synth_pcm(6300, SR)))
+    ids, pos = m.build_prompt(feats.shape[0])
+    c.prefill([ids], [feats], [pos], want_logits=False)
+    d = op.OracleDecoder(tiny_oracle, 512)
+    d.forward(ids, 0, feats, pos)
+    rng = np.random.default_rng(13)
+    n_past, errs = len(ids), []
+    for n in (5, 17):
+        chunk = [int(t) for t in rng.integers(0, 151643, n)]
+        lg, am = c.prefill_chunk([chunk], [n_past])
+        lo = d.forward(chunk, n_past)
+        errs.append(float(np.abs(lg[0] - lo).max()) / float(np.abs(lo).max()))
+        assert errs[-1] <= 1e-2, errs
+        n_past += n
+    tok = int(rng.integers(0, 151643))
+    lg, _ = c.decode_step([tok], [n_past])
+    lo = d.forward([tok], n_past)
+    errs.append(float(np.abs(lg[0] - lo).max()) / float(np.abs(lo).max()))
+    parity("tiny_chunk_prefill_5_17_then_step", rel_max=errs)
+    assert errs[-1] <= 1e-2, errs
+    chunk = [int(t) for t in rng.integers(0, 151643, 9)]
+    lg, _ = c.prefill_chunk([chunk], [0])
+    d0 = op.OracleDecoder(tiny_oracle, 64)
+    lo = d0.forward(chunk, 0)
+    assert float(np.abs(lg[0] - lo).max()) <= 1e-2 * float(np.abs(lo).max())

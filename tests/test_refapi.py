@@ -58,17 +58,19 @@ def test_reference_drivers_compile_against_component_api():
 
 def test_reference_injection_driver(tmp_path):
     """src/audio_injection.h's helpers: the reference's test_injection.cpp, host only"""
-    exe = os.path.join(OUT, "test_injection")
-    if not os.path.isfile(exe):
-        pytest.skip("tools/refapi not built (build container: make -C tools/refapi)")
+    exe = _need("test_injection")
     r = _run([exe], str(tmp_path))
     assert r.returncode == 0 and "All tests passed" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
 def _need(name):
+    """the driver binary: __graft_entry__.build() compiles them in the build
+    container (where /root/reference exists) and they travel with the tree,
+    so a missing one is a failure, not a skip"""
     exe = os.path.join(OUT, name)
     if not os.path.isfile(exe):
-        pytest.skip("tools/refapi not built (build container: make -C tools/refapi)")
+        pytest.fail(f"tools/refapi/_out/{name} missing: run __graft_entry__.build() (make -C tools/refapi) in the "
+                    "build container before the GPU run")
     return exe
 
 

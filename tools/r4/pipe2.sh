@@ -12,3 +12,6 @@ for fp in 1 0; do
   QASR_FX_PIPE=$fp QASR_DEV_TRACE=gpurun_out/p2_tr$fp.bin QASR_DEV_TRACE_LAYER=14 timeout -k 10 200 python -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-probe > gpurun_out/p2_trb$fp.log 2>&1 || { tail -5 gpurun_out/p2_trb$fp.log; exit 1; }
   python3 tools/trace_report.py gpurun_out/p2_tr$fp.bin > gpurun_out/p2_tr$fp.txt 2>&1; cat gpurun_out/p2_tr$fp.txt
 done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_stream.py tests/test_gpu_api.py tests/test_refapi.py -x -v --timeout 300 --timeout-method thread > gpurun_out/p2_t.log 2>&1; rc=$?
+tail -3 gpurun_out/p2_t.log; [ $rc -ne 0 ] && { grep -E "FAIL|Error|assert" gpurun_out/p2_t.log | head -20; exit $rc; }
+exit 0
