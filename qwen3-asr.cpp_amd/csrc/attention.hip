@@ -645,6 +645,87 @@ __device__ __forceinline__ half8 kv_load(const uint16_t *p, int nt) {
     return nt ? __builtin_nontemporal_load((const half8 *)p) : *(const half8 *)p;
 }
 
+// Exact decode attention with the weights computed by the splits (a.fx = 2,
+// option fx_pipe = 2): split sp of head 2g + hh holds its keys' scaled scores
+// (scr, -inf past the context).  It publishes its maximum, takes the earlier
+// splits' maxima (the running maximum before its first key: a bounded poll;
+// every split of the launch is co-resident), derives its keys' weights --
+// fx_weights_reg's values, signed the same way (w = vs, or -ms at a new
+// maximum) -- and publishes them as {fp32, tag} granules in place of the
+// scores, so the chain workgroup starts on the first 64 keys' weights with no
+// gather or weight pass of its own.  S: fx_weights_reg's per-lane sequence
+// (a lane = 32 keys) for this split's 32-key groups, published as {S, running
+// maximum at the group's end}; the chain sums them as fx_weights_reg does, so
+// fused and separate launches stay bit-identical.
+#define SS_LD 192   // a.sstat per head: [0, 64) split maxima; [64 + 2q], [65 + 2q]: 32-key group q's (S, running max)
+template <int SPL>
+__device__ __forceinline__ void split_weights(const DecodeAttnArgs &a, const float *scr, int g, int hh, int sp, int k0, int k1,
+                                              int pos) {
+    __shared__ float wsh[2][SPL];
+    __shared__ float gmx[2][SPL / 32];
+    const int lane = threadIdx.x & 63;
+    const uint32_t tag = gran_tag(pos, a.layer);
+    const long head = 2 * g + hh;
+    unsigned long long *st = a.sstat + head * SS_LD;
+    auto gran = [&](float v) { return ((unsigned long long)tag << 32) | __float_as_uint(v); };
+    float sv[SPL / 64];
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < SPL / 64; i++) {
+        sv[i] = scr[64 * i + lane];
+        m = fmaxf(m, sv[i]);
+    }
+    m = wave_max(m);
+    if (lane == 0) __hip_atomic_store(st + sp, gran(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float M = -INFINITY;   // the running maximum before this split: the earlier splits' maxima
+    if (sp > 0) {
+        unsigned long long v = 0;
+        bool ok = lane >= sp;
+        for (int it = 0; it < a.poll_limit; it++) {
+            if (!ok) {
+                v = __hip_atomic_load(st + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = (uint32_t)(v >> 32) == tag;
+            }
+            if (__all(ok)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_SCORE_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        M = wave_max(lane < sp ? __uint_as_float((uint32_t)v) : -INFINITY);
+    }
+    const float M0 = M;
+    unsigned long long *wg = a.sgran + head * sgran_ld(a.max_ctx);
+#pragma unroll
+    for (int i = 0; i < SPL / 64; i++) {   // lane = key: the running maximum before it by a wave scan
+        const float s = sv[i];
+        const float inc = wave_scan_max(s);
+        const float Mx = fmaxf(M, dpp_ninf<0x138, 0xF>(inc));
+        const bool gt = s > Mx;
+        const float e = expf(gt ? Mx - s : s - Mx);
+        const float w = gt ? -e : (s != -INFINITY ? e : 0.0f);
+        M = fmaxf(M, lane_f(inc, 63));
+        wsh[hh][64 * i + lane] = w;
+        const int key = k0 + 64 * i + lane;
+        if (key < k1) __hip_atomic_store(wg + key, gran(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane < SPL / 32) {
+        float gm = -INFINITY;
+        for (int i = 0; i < 32; i++) gm = fmaxf(gm, scr[32 * lane + i]);
+        gmx[hh][lane] = gm;
+    }
+    if (lane < SPL / 32 && k0 + 32 * lane < k1) {   // (the chain takes 0 for groups past the context, as fx_weights_reg's lanes give)
+        float Mg = M0, Sl = 0.0f;
+        for (int j = 0; j < lane; j++) Mg = fmaxf(Mg, gmx[hh][j]);
+        for (int i = 0; i < 32; i++) {
+            const float x = wsh[hh][32 * lane + i];
+            Sl = __builtin_signbit(x) ? fadd_rn(fmul_rn(Sl, -x), 1.0f) : fadd_rn(fmul_rn(Sl, 1.0f), x);
+            Mg = fmaxf(Mg, scr[32 * lane + i]);
+        }
+        const int q = k0 / 32 + lane;
+        __hip_atomic_store(st + 64 + 2 * q, gran(Sl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(st + 65 + 2 * q, gran(Mg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 template <int SPL, bool FUSED>
 __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const int sp, const int g, const int b, const int nsp) {
     __shared__ __attribute__((aligned(16))) uint16_t qs[2][128];
@@ -827,6 +908,14 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     __syncthreads();
     mark(6);
     if constexpr (FUSED) {
+        if (a.fx == 2) {   // exact attention, the weights here (fx1_chain_w reads them)
+            if (wid < 2) split_weights<SPL>(a, sc[wid], g, wid, sp, k0, k1, pos);
+            if (a.fx_vpf & 1)
+#pragma unroll
+                for (int i = 0; i < KPW; i++) asm volatile("" ::"v"(vv[i]));
+            mark(3);
+            return;
+        }
         if (a.fx) {   // exact attention: the scaled scores to the kv group's chain workgroup, one {fp32, tag} granule each
             const uint32_t tag = gran_tag(pos, a.layer);
             if (tid < 2 * SPL) {
@@ -1611,6 +1700,120 @@ __device__ __forceinline__ void fx1_chain_pipe(const DecodeAttnArgs &a, const in
     mark(5);
 }
 
+// The chain role with the weights from the splits (a.fx = 2, split_weights):
+// per 64-key buffer one {weight, tag} granule a lane, the chain as
+// fx1_chain_pipe's; S from the splits' 32-key group sums, combined as
+// fx_weights_reg combines its lanes' (one chunk: the launch is taken only
+// while n_kv <= DX_KC), so fused and separate launches agree bit for bit.
+struct FxpWGran {   // fxp_chain_w's weight source: key j's {fp32 weight, tag} granule of one head
+    const unsigned long long *gb;
+    int n;
+    uint32_t tag;
+    int poll_limit;
+    unsigned int *err;
+    __device__ __forceinline__ unsigned long long issue(int j0) const {
+        const int j = j0 + (int)(threadIdx.x & 63);
+        return j < n ? __hip_atomic_load(gb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    }
+    __device__ __forceinline__ float take(unsigned long long v, int j0) const {
+        const int j = j0 + (int)(threadIdx.x & 63);
+        bool ok = j >= n || (uint32_t)(v >> 32) == tag;
+        if (!__all(ok)) {
+            for (int it = 0; it < poll_limit; it++) {
+                __builtin_amdgcn_s_sleep(1);
+                if (!ok) {
+                    v = __hip_atomic_load(gb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = (uint32_t)(v >> 32) == tag;
+                }
+                if (__all(ok)) break;
+            }
+            if (!__all(ok) && (threadIdx.x & 63) == 0)
+                __hip_atomic_fetch_or(err, (unsigned)DEVERR_SCORE_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return j < n ? __uint_as_float((uint32_t)v) : 0.0f;
+    }
+};
+__device__ __forceinline__ void fx1_chain_w(const DecodeAttnArgs &a, const int g) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int hh = wid >> 1, wu = __builtin_amdgcn_readfirstlane(wid & 1);
+    const int d = 64 * wu + lane, loff = 8 * lane;
+    const uint16_t *vt = a.vt + (long)g * 128 * vt_ctx(a.max_ctx) + 64 * wu * 8;   // batch 1: slot 0; the wave's key block 0
+    auto mark = [&](int slot) {   // dev trace: rows 4000 + g ([start, v ready, first weights, -, chain done, published])
+        if (a.trace && tid == 0) a.trace[(4000L + g) * 8 + slot] = rt_now();
+    };
+    mark(0);
+    const int pos = a.pos[0], nkv = pos + 1, nl = nkv - 1;
+    const uint32_t tag = gran_tag(pos, a.layer);
+    const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
+    const long head = 2 * g + hh;
+    const unsigned long long *gp = a.gran + QD + KD + g * 128 + d;   // the new key's v (this lane's dimension)
+    unsigned long long vg = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const FxpWGran src{a.sgran + head * sgran_ld(a.max_ctx), nkv, tag, a.poll_limit, a.err};
+    mark(2);
+    mark(3);
+    const unsigned long long ck0 = a.trace ? clock64() : 0ull;
+    f16 acc = 0;
+    float wlast;
+    fxp_chain_w(src, vt, loff, nl, nl > 0 ? (nl - 1) >> 3 : 0, acc, wlast);
+    mark(4);
+    {   // the new key: its QKV granule (long published by now), cast to fp16 as the cache write is
+        bool ok = (uint32_t)(vg >> 32) == tag;
+        for (int it = 0; it < a.poll_limit && !__all(ok); it++) {
+            __builtin_amdgcn_s_sleep(2);
+            vg = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = (uint32_t)(vg >> 32) == tag;
+        }
+        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_QKV_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    mark(1);
+    acc = fx_key_slow(acc, f_to_u16(__uint_as_float((uint32_t)vg)), wlast);
+    // S: lane q = 32-key group q: {S_q, running max at its end} from the splits (long published)
+    float S;
+    {
+        const unsigned long long *st = a.sstat + head * SS_LD + 64;
+        const bool has = 32 * lane < nkv;
+        unsigned long long s2 = 0, m2 = 0;
+        bool ok = !has;
+        for (int it = 0; it < a.poll_limit; it++) {
+            if (!ok) {
+                s2 = __hip_atomic_load(st + 2 * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                m2 = __hip_atomic_load(st + 2 * lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = (uint32_t)(s2 >> 32) == tag && (uint32_t)(m2 >> 32) == tag;
+            }
+            if (__all(ok)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_SCORE_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float Sl = has ? __uint_as_float((uint32_t)s2) : 0.0f;
+        const float Ml = has ? __uint_as_float((uint32_t)m2) : -INFINITY;
+        const float Mn = wave_max(Ml);
+        S = wave_sum(!has || Ml == -INFINITY ? 0.0f : Sl * expf(Ml - Mn));
+    }
+    if (a.trace && tid == 0) {
+        a.trace[(4010L + g) * 8 + 0] = ck0;
+        a.trace[(4010L + g) * 8 + 1] = clock64();
+        a.trace[(4010L + g) * 8 + 2] = (unsigned long long)nkv;
+    }
+    const float ov = (float)acc * (S == 0.0f ? 0.0f : 1.0f / S);   // ggml: VKQ32 = fp32(VKQ16) * (1 / S)
+    const uint32_t h16 = f_to_u16(ov);
+    const uint32_t hn = __shfl_xor(h16, 1, 64);
+    uint16_t *out = a.out + (2 * g + hh) * 128 + d;
+    if (a.att_done) {   // as fx1_chain_body: write-through pairs, drained, one arrival per replica
+        if ((lane & 1) == 0) __hip_atomic_store((uint32_t *)out, h16 | (hn << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (a.fence && tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (a.fence) __syncthreads();
+        if (tid < 8) __hip_atomic_fetch_add(a.att_done + tid * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        *out = (uint16_t)h16;
+    }
+    mark(5);
+}
+
 template <int SPL>
 __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnArgs a, GemvArgs o) {
     constexpr int K = 1024, NT = 2, RPW = 2;
@@ -1624,7 +1827,8 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
         const int nfx = a.fx ? a.n_kv_head : 0;
         if (j >= nat + nfx) oproj1_body(o, a, j - nat - nfx);
         else if (j >= nat) {
-            if (a.fx_pipe) fx1_chain_pipe(a, j - nat);
+            if (a.fx == 2) fx1_chain_w(a, j - nat);
+            else if (a.fx_pipe == 1) fx1_chain_pipe(a, j - nat);
             else fx1_chain_body(a, j - nat);
         }
         else decode_attn_body<SPL, true>(a, j / a.n_kv_head, j % a.n_kv_head, 0, nsp);
@@ -1736,7 +1940,8 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     // ones): fall back to separate launches for contexts that would not fit
     // (exact attention: n_kv_head chain workgroups too; they read the new v
     // from its granule, so the fused exact path needs the granule hand-off)
-    if (a.fx && (!a.gran || !a.sgran || (!a.fx_pipe && ns * spl1 > DX_KC))) return 0;   // (fx_chain.h: one chain chunk)
+    // (fx_chain.h and the split weights' S: one chain chunk)
+    if (a.fx && (!a.gran || !a.sgran || (a.fx_pipe != 1 && ns * spl1 > DX_KC) || (a.fx == 2 && !a.sstat))) return 0;
     const int nfx = a.fx ? a.n_kv_head : 0;
     const int slots = spl1 == 128 ? cfg.slots_qkv128 : cfg.slots_qkv64;
     const bool fit_o = 512 + ns * a.n_kv_head + nfx + 256 <= slots;
@@ -1756,7 +1961,7 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     // fx_pipe: the chain starts on the first scores, so its V^T rows come from
     // the splits' pull (bit 0): the chain workgroup's own LDS-DMA pull (bit 1)
     // would sit in its vmcnt queue ahead of the chain's first loads
-    ad.fx_vpf = a.fx_pipe ? (cfg.fx_vpf | 1) & ~2 : cfg.fx_vpf;
+    ad.fx_vpf = a.fx_pipe ? (cfg.fx_vpf | 1) & ~2 : cfg.fx_vpf;   // (fx_pipe 1 and 2)
     if (!with_o2) ad.att_done = nullptr;
     const GemvArgs qa = q;
     const GemvArgs oa = with_o2 ? *o : GemvArgs{};

@@ -120,6 +120,7 @@ struct qasr_ctx {
     unsigned int *d_counter = nullptr, *d_done = nullptr;
     unsigned int *d_qcnt = nullptr;   // fused batch-1 QKV + attention: QKV-block arrivals per kv group
     unsigned long long *d_gran = nullptr;   // ... or its outputs as tagged granules (zeroed by every prefill)
+    unsigned long long *d_sstat = nullptr;  // ... and fx_pipe = 2's split maxima / 32-key group sums [n_head][SS_LD] (zeroed likewise)
     unsigned long long *d_sgran = nullptr;  // ... exact attention: the splits' scores as granules [n_head][max_ctx] (zeroed likewise)
     bool qkv_in_gran = false;               // the captured step's last layer hands its QKV over in granules
     unsigned int *d_attdone = nullptr;   // fused batch-1 o-proj: combiner arrivals (8 replicas)
@@ -225,6 +226,7 @@ static const std::vector<FuseOption> &fuse_options() {
         {"lmh", "QASR_LMH", &FuseCfg::lmh},
         {"fx_seq", "QASR_FX_SEQ", &FuseCfg::fx_seq},
         {"fx_pipe", "QASR_FX_PIPE", &FuseCfg::fx_pipe},
+        {"skinny_inf", "QASR_SKINNY_INF", &FuseCfg::skinny_inf},
     };
     return v;
 }
@@ -359,6 +361,7 @@ static void gemm_q8(qasr_ctx *c, int epi, GemmArgs g, const float *a32, const ui
     g.Aq = qa; g.lda = g.K; g.Ad = qd; g.ldad = g.K / 32;
     g.Wq = (const int8_t *)W; g.ldw = g.K; g.Wd = Wd;
     g.no_skinny = !c->fuse.skinny;
+    g.skinny_inflight = c->fuse.skinny_inf;
     if (decode && launch_gemm_skinny_q8(epi, g, s)) return;
     launch_gemm_q8(epi, g, s);
 }
@@ -370,6 +373,7 @@ static void gemm_q8_pre(qasr_ctx *c, int epi, GemmArgs g, const uint16_t *W, con
     g.Aq = qa ? qa : c->d_q8a; g.lda = g.K; g.Ad = qa ? qd : c->d_q8d; g.ldad = g.K / 32;
     g.Wq = (const int8_t *)W; g.ldw = g.K; g.Wd = Wd;
     g.no_skinny = !c->fuse.skinny;
+    g.skinny_inflight = c->fuse.skinny_inf;
     if (launch_gemm_skinny_q8(epi, g, s)) return;
     launch_gemm_q8(epi, g, s);
 }
@@ -726,6 +730,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_attdone, (size_t)8 * 16 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_gran, (size_t)(QD + 2 * KD) * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_sgran, (size_t)hp.n_head * sgran_ld(max_ctx) * 8)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_sstat, (size_t)hp.n_head * 192 * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_ffncnt, (size_t)hp.dec_layers * 512 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_err, 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_pstamp, (size_t)max_ctx * kStampRec * 8)) ||
@@ -740,6 +745,7 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     HIPCHK(hipMemset(c->d_attdone, 0, (size_t)8 * 16 * 4));
     HIPCHK(hipMemset(c->d_gran, 0, (size_t)(QD + 2 * KD) * 8));
     HIPCHK(hipMemset(c->d_sgran, 0, (size_t)hp.n_head * sgran_ld(max_ctx) * 8));
+    HIPCHK(hipMemset(c->d_sstat, 0, (size_t)hp.n_head * 192 * 8));
     HIPCHK(hipMemset(c->d_ffncnt, 0, (size_t)hp.dec_layers * 512 * 4));
     HIPCHK(hipMemset(c->d_done, 0, 4));
     HIPCHK(hipMemset(c->d_err, 0, 4));
@@ -1149,6 +1155,7 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
     // granule tags repeat across runs at the same positions: back to zero (no valid tag)
     HIPCHK(hipMemsetAsync(c->d_gran, 0, (size_t)(c->m->hp.n_head + 2 * c->m->hp.n_kv_head) * 128 * 8, c->st));
     HIPCHK(hipMemsetAsync(c->d_sgran, 0, (size_t)c->m->hp.n_head * sgran_ld(c->max_ctx) * 8, c->st));
+    HIPCHK(hipMemsetAsync(c->d_sstat, 0, (size_t)c->m->hp.n_head * 192 * 8, c->st));
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
     const int B = (int)P.size(), H = hp.hidden;
@@ -1188,6 +1195,7 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
 // the shape, the tiled GEMM otherwise
 static void dec_gemm(qasr_ctx *c, int epi, GemmArgs g, hipStream_t s) {
     g.no_skinny = !c->fuse.skinny;
+    g.skinny_inflight = c->fuse.skinny_inf;
     if (launch_gemm_skinny(epi, g, s)) return;
     launch_gemm(AM_DENSE, epi, g, s);
 }
@@ -1282,7 +1290,8 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         const bool fusable = skinny && B == 1 && !q8 && !skip;
         if (fusable) da.att_done = c->d_attdone;
         if (fusable && exact && c->fuse.gran) {   // ggml's attention numerics as the fused launch's chain role
-            da.fx = 1;
+            da.fx = c->fuse.fx_pipe == 2 ? 2 : 1;   // 2: the splits derive the weights (attention.hip split_weights)
+            da.sstat = c->d_sstat;
             da.sgran = c->d_sgran;
             da.gran = c->d_gran;   // (the fused decision needs the granule hand-off)
             da.layer = l;
@@ -1771,6 +1780,7 @@ extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_pa
     // a caller may repeat a position (same tag): no granule of an earlier call may match
     HIPCHK(hipMemsetAsync(c->d_gran, 0, (size_t)(c->m->hp.n_head + 2 * c->m->hp.n_kv_head) * 128 * 8, c->st));
     HIPCHK(hipMemsetAsync(c->d_sgran, 0, (size_t)c->m->hp.n_head * sgran_ld(c->max_ctx) * 8, c->st));
+    HIPCHK(hipMemsetAsync(c->d_sstat, 0, (size_t)c->m->hp.n_head * 192 * 8, c->st));
     std::vector<int> pos(B), nkv(B);
     for (int b = 0; b < B; b++) {
         if (n_past[b] < 0 || n_past[b] + 1 > c->max_ctx) return fail(QASR_ERR_ARG, "Context length exceeded");

@@ -54,7 +54,7 @@ __device__ __forceinline__ void decode_attn_exact_body(const DecodeAttnArgs &a, 
     const uint16_t *vcol = a.vt + ((long)b * a.n_kv_head + g) * 128 * vtc + 64 * wu * 8;   // the wave's key block 0
     float M = -INFINITY, S = 0.0f;
     f16 acc = 0;
-    if (a.fx_pipe) {   // the weights one 64-key buffer ahead of the chain (fx_pipe.h), every key in the loop
+    if (a.fx_pipe == 1) {   // the weights one 64-key buffer ahead of the chain (fx_pipe.h), every key in the loop
         float wl;
         S = fxp_chain(FxpScores{sg, nkv}, vcol, 8 * lane, nkv, (nkv - 1) >> 3, acc, wl);
     } else

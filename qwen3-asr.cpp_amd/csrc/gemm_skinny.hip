@@ -25,6 +25,8 @@
 namespace qasr {
 
 __device__ __forceinline__ float silu_s(float g) { return g / (1.0f + expf(-g)); }
+// an s_waitcnt vmcnt immediate: 63 at most (a smaller count only waits longer)
+constexpr int vmc(int x) { return x > 63 ? 63 : x; }
 
 // Residual prefetch: epilogue element e -> (tile, row in tile, column in
 // tile); the residual values a thread adds are requested at kernel entry, so
@@ -112,13 +114,20 @@ __device__ __attribute__((aligned(64))) uint32_t g_zero_line_s[16];
 // VAR: diagnostic knob for tools/skinny_bench.hip (1 = no activation loads,
 // 2 = no weight loads, 4 = activations through LDS by LDS-DMA); the engine
 // launches VAR = 0
-template <int MT, int NT, int KW, int EPI, int VAR = 0>
+// CPW > 0 (with VAR 4): every one of the wave's CPW K chunks (nch == KW * CPW)
+// requested at entry -- LDS-DMA pieces and weight fragments, each chunk in an
+// LDS region of its own -- then consumed in the same order: the same fragments
+// and accumulation order as the one-chunk-at-a-time loop (bit-identical), but
+// one memory latency per launch instead of one per chunk (the batch decode's
+// o / down / gate-up projections waited 2-3 HBM latencies a launch)
+template <int MT, int NT, int KW, int EPI, int VAR = 0, int CPW = 0>
 __global__ __launch_bounds__(64 * KW) void gemm_skinny_kernel(GemmArgs g) {
     constexpr int NTILE = MT * NT;
     constexpr bool ALDS = (VAR & 4) != 0;
     // VAR 4: one K chunk (MT*16 rows x 128 halves, 16-B chunks XOR-swizzled by
-    // row) per wave, in the same LDS as the partial-tile reduction after the loop
-    constexpr int RED_B = KW * NTILE * 64 * 16, ALDS_B = ALDS ? KW * MT * 16 * 128 * 2 : 0;
+    // row) per wave (CPW of them with CPW > 0), in the same LDS as the
+    // partial-tile reduction after the loop
+    constexpr int RED_B = KW * NTILE * 64 * 16, ALDS_B = ALDS ? KW * MT * 16 * 128 * 2 * (CPW > 0 ? CPW : 1) : 0;
     __shared__ __attribute__((aligned(16))) unsigned char lds_raw[RED_B > ALDS_B ? RED_B : ALDS_B];
     floatx4 (*red)[NTILE][64] = reinterpret_cast<floatx4 (*)[NTILE][64]>(lds_raw);
     uint16_t *alds = reinterpret_cast<uint16_t *>(lds_raw);
@@ -173,7 +182,47 @@ __global__ __launch_bounds__(64 * KW) void gemm_skinny_kernel(GemmArgs g) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, ab[buf][i][s]),
                                                                        __builtin_bit_cast(half8, wb[buf][j][s]), acc[i][j], 0, 0, 0);
     };
-    if constexpr (ALDS) {
+    if constexpr (ALDS && CPW > 0) {
+        uint16_t *my = alds + wid * (CPW * MT * 16 * 128);
+        u32x4 wq[CPW][NT][4];
+#pragma unroll
+        for (int k = 0; k < CPW; k++) {
+            const int c = wid + k * KW;
+#pragma unroll
+            for (int p = 0; p < MT * 4; p++) {   // 1 KiB = 4 rows of 256 B per piece
+                const int r = p * 4 + (lane >> 4), ch = (lane & 15) ^ (r & 15);
+                const int m = m0 + r;
+                const uint16_t *src = m < M ? g.A + (long)m * g.lda + c * 128 + ch * 8 : (const uint16_t *)g_zero_line_s;
+                __builtin_amdgcn_global_load_lds((glb_void_s *)src, (lds_void_s *)(my + k * (MT * 16 * 128) + p * 512), 16, 0, 0);
+            }
+#pragma unroll
+            for (int t = 0; t < NT; t++)
+#pragma unroll
+                for (int s4 = 0; s4 < 4; s4++) wq[k][t][s4] = __builtin_nontemporal_load(wrow[t] + c * 16 + 4 * s4);
+            asm volatile("" ::: "memory");   // chunk k's requests stay together, in chunk order (the waits below count them)
+        }
+#pragma unroll
+        for (int k = 0; k < CPW; k++) {
+            // chunk k's pieces and fragments landed: (MT + NT) * 4 loads per chunk, issued in chunk order
+            // (vmcnt holds 63 at most: a smaller count only waits longer)
+            if (k == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vmc((CPW - 1) * (MT + NT) * 4)) : "memory");
+            else if (k == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vmc((CPW > 1 ? CPW - 2 : 0) * (MT + NT) * 4)) : "memory");
+            else if (k == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vmc((CPW > 2 ? CPW - 3 : 0) * (MT + NT) * 4)) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vmc((CPW > 3 ? CPW - 4 : 0) * (MT + NT) * 4)) : "memory");
+            const uint16_t *mk = my + k * (MT * 16 * 128);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; s4++)
+#pragma unroll
+                for (int i = 0; i < MT; i++) {
+                    const int r = i * 16 + c16, ch = (4 * s4 + q) ^ (r & 15);
+                    const half8 a8 = *(const half8 *)(mk + r * 128 + ch * 8);
+#pragma unroll
+                    for (int j = 0; j < NT; j++)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a8, __builtin_bit_cast(half8, wq[k][j][s4]), acc[i][j], 0, 0, 0);
+                }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else if constexpr (ALDS) {
         uint16_t *my = alds + wid * (MT * 16 * 128);
         for (int c = wid; c < nch; c += KW) {
 #pragma unroll
@@ -230,11 +279,11 @@ __global__ __launch_bounds__(64 * KW) void gemm_skinny_kernel(GemmArgs g) {
 // zero accumulator gives the exact integer dot, then acc += (d_w * d_x) *
 // sumi in fp32 -- the numerics of gemm_q8_kernel (gemm.hip).  Operands are
 // 8-byte fragment loads (one instruction = 32 contiguous bytes of 16 rows).
-template <int MT, int NT, int KW, int EPI, int VAR = 0>
+template <int MT, int NT, int KW, int EPI, int VAR = 0, int CPW = 0>
 __global__ __launch_bounds__(64 * KW) void gemm_skinny_q8_kernel(GemmArgs g) {
     constexpr int NTILE = MT * NT;
     constexpr bool ALDS = (VAR & 4) != 0;   // int8 activations through LDS-DMA, as gemm_skinny_kernel
-    constexpr int RED_B = KW * NTILE * 64 * 16, ALDS_B = ALDS ? KW * MT * 16 * 128 : 0;
+    constexpr int RED_B = KW * NTILE * 64 * 16, ALDS_B = ALDS ? KW * MT * 16 * 128 * (CPW > 0 ? CPW : 1) : 0;
     __shared__ __attribute__((aligned(16))) unsigned char lds_raw[RED_B > ALDS_B ? RED_B : ALDS_B];
     floatx4 (*red)[NTILE][64] = reinterpret_cast<floatx4 (*)[NTILE][64]>(lds_raw);
     __shared__ unsigned long long rmax[64];
@@ -317,7 +366,62 @@ __global__ __launch_bounds__(64 * KW) void gemm_skinny_q8_kernel(GemmArgs g) {
                 }
         }
     };
-    if constexpr (ALDS) {
+    if constexpr (ALDS && CPW > 0) {   // every chunk of the wave in flight at once (gemm_skinny_kernel's CPW)
+        uint8_t *my = (uint8_t *)lds_raw + wid * (CPW * MT * 16 * 128);
+        long wq[CPW][NT][4];
+        uint2 wdq[CPW][NT];
+        float4 adq[CPW][MT][4];
+#pragma unroll
+        for (int k = 0; k < CPW; k++) {
+            const int c = wid + k * KW;
+#pragma unroll
+            for (int t = 0; t < NT; t++) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) wq[k][t][u] = __builtin_nontemporal_load((const long *)(wrow[t] + c * 128 + u * 32));
+                wdq[k][t] = *(const uint2 *)(wdrow[t] + c * 4);
+            }
+#pragma unroll
+            for (int t = 0; t < MT; t++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) adq[k][t][r] = *(const float4 *)(adrow[t][r] + c * 4);
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int p = 0; p < MT * 2; p++) {   // 1 KiB = 8 rows of 128 B per piece
+                const int r = p * 8 + (lane >> 3), ch = (lane & 7) ^ (r & 7);
+                const int m = m0 + r;
+                const int8_t *src = m < M ? g.Aq + (long)m * g.lda + c * 128 + ch * 16 : (const int8_t *)g_zero_line_s;
+                __builtin_amdgcn_global_load_lds((glb_void_s *)src, (lds_void_s *)(my + k * (MT * 16 * 128) + p * 1024), 16, 0, 0);
+            }
+            asm volatile("" ::: "memory");   // chunk k's requests together, in chunk order (the waits below count them)
+        }
+        constexpr int PER = MT * 2 + NT * 5 + MT * 4;   // VMEM requests per chunk
+#pragma unroll
+        for (int k = 0; k < CPW; k++) {
+            if (k == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vmc((CPW - 1) * PER)) : "memory");
+            else if (k == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vmc((CPW > 1 ? CPW - 2 : 0) * PER)) : "memory");
+            else if (k == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vmc((CPW > 2 ? CPW - 3 : 0) * PER)) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vmc((CPW > 3 ? CPW - 4 : 0) * PER)) : "memory");
+            const uint8_t *mk = my + k * (MT * 16 * 128);
+#pragma unroll
+            for (int t = 0; t < NT; t++) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) wb[0][t][u] = wq[k][t][u];
+                wd[0][t] = wdq[k][t];
+            }
+#pragma unroll
+            for (int t = 0; t < MT; t++) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) ad[0][t][r] = adq[k][t][r];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int r = t * 16 + c16, b = 32 * u + 8 * q;
+                    ab[0][t][u] = *(const long *)(mk + r * 128 + ((((b >> 4) ^ (r & 7)) << 4) | (b & 15)));
+                }
+            }
+            mma(0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else if constexpr (ALDS) {
         uint8_t *my = (uint8_t *)lds_raw + wid * (MT * 16 * 128);
         for (int c = wid; c < nch; c += KW) {
 #pragma unroll
@@ -381,14 +485,25 @@ __global__ __launch_bounds__(64 * KW) void gemm_skinny_q8_kernel(GemmArgs g) {
 template <int MT, int NT, int KW, int EPI>
 static void run_skinny(const GemmArgs &g, hipStream_t s) {
     dim3 grid(g.N / (16 * NT), (g.M + 16 * MT - 1) / (16 * MT));
+    const int cpw = (g.K >> 7) % KW == 0 && g.skinny_inflight ? (g.K >> 7) / KW : 0;   // whole chunks a wave: all in flight
+    // (a CPW form is instantiated only where its chunk images fit the LDS: <= 128 KiB)
+    constexpr int CH = KW * MT * 16 * 128 * 2;
     if (g.regs_staged) hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, EPI, 0>), grid, dim3(64 * KW), 0, s, g);
+    else if (cpw == 1) hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, EPI, 4, 1>), grid, dim3(64 * KW), 0, s, g);
+    else if (cpw == 2 && 2 * CH <= 131072) hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, EPI, 4, 2 * CH <= 131072 ? 2 : 1>), grid, dim3(64 * KW), 0, s, g);
+    else if (cpw == 3 && 3 * CH <= 131072) hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, EPI, 4, 3 * CH <= 131072 ? 3 : 1>), grid, dim3(64 * KW), 0, s, g);
     else hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, EPI, 4>), grid, dim3(64 * KW), 0, s, g);
 }
 
 template <int MT, int NT, int KW, int EPI>
 static void run_skinny_q8(const GemmArgs &g, hipStream_t s) {
     dim3 grid(g.N / (16 * NT), (g.M + 16 * MT - 1) / (16 * MT));
+    const int cpw = (g.K >> 7) % KW == 0 && g.skinny_inflight ? (g.K >> 7) / KW : 0;
+    constexpr int CH = KW * MT * 16 * 128;
     if (g.regs_staged) hipLaunchKernelGGL((gemm_skinny_q8_kernel<MT, NT, KW, EPI, 0>), grid, dim3(64 * KW), 0, s, g);
+    else if (cpw == 1) hipLaunchKernelGGL((gemm_skinny_q8_kernel<MT, NT, KW, EPI, 4, 1>), grid, dim3(64 * KW), 0, s, g);
+    else if (cpw == 2 && 2 * CH <= 131072) hipLaunchKernelGGL((gemm_skinny_q8_kernel<MT, NT, KW, EPI, 4, 2 * CH <= 131072 ? 2 : 1>), grid, dim3(64 * KW), 0, s, g);
+    else if (cpw == 3 && 3 * CH <= 131072) hipLaunchKernelGGL((gemm_skinny_q8_kernel<MT, NT, KW, EPI, 4, 3 * CH <= 131072 ? 3 : 1>), grid, dim3(64 * KW), 0, s, g);
     else hipLaunchKernelGGL((gemm_skinny_q8_kernel<MT, NT, KW, EPI, 4>), grid, dim3(64 * KW), 0, s, g);
 }
 

@@ -74,6 +74,7 @@ struct GemmArgs {
     const int8_t *Wq; const uint16_t *Wd;
     int regs_staged;                      // 1: register-staged tiles instead of the LDS-DMA ones (A/B option)
     int no_skinny;                        // 1: launch_gemm_skinny / _q8 decline (per-context option skinny = 0)
+    int skinny_inflight;                  // skinny GEMMs: every K chunk of a wave requested at entry (FuseCfg::skinny_inf)
 };
 void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s);
 // decode-batch GEMM (gemm_skinny.hip): dense A, M <= 128, K % 128 == 0; returns
@@ -167,7 +168,10 @@ struct FuseCfg {
     int fx_seq = 1;                     // decode batches: the exact attention's scores + chain in one launch
                                         // (decode_attn_seq_kernel<1>) where the per-sequence kernel is taken
     int lmh = 1;                        // decode batches of f16 models (9..64 rows): the LM head in one launch (lmhead.hip)
-    int fx_pipe = 0;                    // exact decode chains: weights one 64-key buffer ahead, SGPR operands (fx_pipe.h)
+    int skinny_inf = 1;                 // decode-batch skinny GEMMs: all of a wave's K chunks in flight (gemm_skinny.hip CPW)
+    int fx_pipe = 0;                    // exact decode chains: 1 = weights one 64-key buffer ahead, SGPR operands (fx_pipe.h);
+                                        // 2 = batch 1 fused: the splits compute the weights (split_weights), the chain
+                                        // role reads them (fx1_chain_w); other paths as 0
     unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
 };
 // co-resident workgroup capacity of the fused kernels on the current device
@@ -311,6 +315,7 @@ struct DecodeAttnArgs {
     int fx_delay;                        // chain workgroups: first score poll after fx_delay x ~0.2 us
     int fx_vpf;                          // bit 0: the splits pull their keys' V^T rows into their XCD's L2 for the
                                          // chain; bit 1: the chain workgroups pull their own (LDS-DMA, while waiting)
+    unsigned long long *sstat;           // fx = 2: the splits' maxima and 32-key group S sums, [n_head][192] granules
     int fx_pipe;                         // every exact decode chain derives its weights one 64-key buffer ahead
                                          // (fx_pipe.h; FuseCfg::fx_pipe) instead of all of them first (fx_chain.h)
 };

@@ -462,3 +462,26 @@ def test_full_fx_seq_one_launch_bit_identical(full):
     for s in range(len(toks)):
         assert np.isfinite(runs[1][s]).all()
         assert np.array_equal(runs[1][s], runs[0][s]), s
+
+
+def test_full_skinny_inflight_bit_identical(full):
+    """decode batches (9..64 rows): the skinny GEMMs with every K chunk of a
+    wave in flight at once (option skinny_inf = 1, the default) multiply the
+    same fragments in the same order as the one-chunk-at-a-time loop
+    (skinny_inf = 0): logits bit-identical at 16 and 64 rows"""
+    m, _, om = full
+    feats = om.encode(op.log_mel(qasr.synth_pcm(18100, 2 * SR)))
+    ids, pos = m.build_prompt(feats.shape[0])
+    for B in (16, 64):
+        c = qasr.Context(m, max_batch=B, max_ctx=len(ids) + 16)
+        try:
+            toks = [int(t) for t in np.random.default_rng(B).integers(0, 151643, B)]
+            out = {}
+            for inf in (1, 0):
+                c.set_option("skinny_inf", inf)
+                c.prefill([ids] * B, [feats] * B, [pos] * B, want_logits=False)
+                lg, _ = c.decode_step(toks, [len(ids)] * B)
+                out[inf] = lg
+            assert np.array_equal(out[0], out[1]), (B, float(np.abs(out[0] - out[1]).max()))
+        finally:
+            c.close()

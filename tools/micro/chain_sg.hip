@@ -9,15 +9,16 @@
 //   6: single-rounding chain, VGPR weights (v_fma_mixlo_f16: one op a key)
 //   7: as 2, readlanes batched at the group's start
 //   8/9: LDS broadcast 1 / 2 groups ahead without the memory clobber
+//   13/14: two dimensions a lane (packed accumulator, v_cvt_pk_f16_f32), LDS / SGPR weights
 //   10/12: weights by s_load_dwordx8 (glc / K$) one group ahead; 11: x16 glc, 16-key double buffer
 // One wave per SIMD (8 workgroups of 4 waves), clock64 around 1024 groups.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
 
-typedef _Float16 f16;
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef float floatx4 __attribute__((ext_vector_type(4)));
+#include "../../qwen3-asr.cpp_amd/csrc/fx_pipe.h"
+using qasr::fxp_buffer;
+
 
 #define G 1024
 
@@ -136,7 +137,7 @@ __global__ __launch_bounds__(256) void k(const u32x4 *vin, const float *win, lon
                 wc = na;
                 wd = nb;
             }
-        } else if constexpr (MODE >= 10) {
+        } else if constexpr (MODE >= 10 && MODE <= 12) {
             // SMEM: the weights from global memory by s_load into SGPRs; MODE 10: one
             // group (x8) ahead, glc; 11: 16 keys (x16) double-buffered, glc; 12: as 10 without glc
             if constexpr (MODE == 10 || MODE == 12) {
@@ -174,6 +175,49 @@ __global__ __launch_bounds__(256) void k(const u32x4 *vin, const float *win, lon
                 cur = nx;
                 g++;
             }
+        } else if constexpr (MODE == 13 || MODE == 14) {
+            // two dimensions a lane (d, d + 64) in one packed accumulator: per key
+            // two mixes (lo / hi halves of acc as the fp16 addend) and one v_cvt_pk_f16_f32;
+            // 13: VGPR weights by LDS broadcast one group ahead; 14: fixed SGPR weights
+#define MIX2(VA, VB, W, SEL)                                                                     \
+    "v_fma_mix_f32 %[t], " VA ", " W ", %[a] op_sel:[" SEL ",0,0] op_sel_hi:[1,0,1]\n\t"        \
+    "v_fma_mix_f32 %[u], " VB ", " W ", %[a] op_sel:[" SEL ",0,1] op_sel_hi:[1,0,1]\n\t"        \
+    "v_cvt_pk_f16_f32 %[a], %[t], %[u]\n\t"
+            float u;
+            uint32_t a2 = __builtin_bit_cast(uint16_t, acc) * 0x10001u;
+            if constexpr (MODE == 13) {
+                const int o = ((g + 1) & 7) * 8;
+                const floatx4 na = *(const floatx4 *)&ws[wid][o], nb = *(const floatx4 *)&ws[wid][o + 4];
+                asm volatile(MIX2("%[v0]", "%[y0]", "%[w0]", "0") MIX2("%[v0]", "%[y0]", "%[w1]", "1")
+                             MIX2("%[v1]", "%[y1]", "%[w2]", "0") MIX2("%[v1]", "%[y1]", "%[w3]", "1")
+                             MIX2("%[v2]", "%[y2]", "%[w4]", "0") MIX2("%[v2]", "%[y2]", "%[w5]", "1")
+                             MIX2("%[v3]", "%[y3]", "%[w6]", "0") MIX2("%[v3]", "%[y3]", "%[w7]", "1")
+                             : [t] "=&v"(t), [u] "=&v"(u), [a] "+v"(a2)
+                             : [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [y0] "v"(v[1]), [y1] "v"(v[2]),
+                               [y2] "v"(v[3]), [y3] "v"(v[0]), [w0] "v"(wa[0]), [w1] "v"(wa[1]), [w2] "v"(wa[2]), [w3] "v"(wa[3]),
+                               [w4] "v"(wb[0]), [w5] "v"(wb[1]), [w6] "v"(wb[2]), [w7] "v"(wb[3]));
+                wa = na;
+                wb = nb;
+            } else {
+                asm volatile(MIX2("%[v0]", "%[y0]", "%[w0]", "0") MIX2("%[v0]", "%[y0]", "%[w1]", "1")
+                             MIX2("%[v1]", "%[y1]", "%[w2]", "0") MIX2("%[v1]", "%[y1]", "%[w3]", "1")
+                             MIX2("%[v2]", "%[y2]", "%[w4]", "0") MIX2("%[v2]", "%[y2]", "%[w5]", "1")
+                             MIX2("%[v3]", "%[y3]", "%[w6]", "0") MIX2("%[v3]", "%[y3]", "%[w7]", "1")
+                             : [t] "=&v"(t), [u] "=&v"(u), [a] "+v"(a2)
+                             : [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [y0] "v"(v[1]), [y1] "v"(v[2]),
+                               [y2] "v"(v[3]), [y3] "v"(v[0]), [w0] "s"(s0), [w1] "s"(s1), [w2] "s"(s2), [w3] "s"(s3),
+                               [w4] "s"(s4), [w5] "s"(s5), [w6] "s"(s6), [w7] "s"(s7));
+            }
+            acc = __builtin_bit_cast(f16, (uint16_t)(a2 ^ (a2 >> 16)));
+        } else if constexpr (MODE == 15 || MODE == 16) {
+            // fx_pipe.h's fxp_buffer (8 group blocks, lane-indexed readlanes) on
+            // register V; 15: fast buffer (m64 = 0), 16: the checked form (one record)
+            u32x4 vb8[8] = {v, v, v, v, v, v, v, v};
+            int ww[8] = {s0, s1, s2, s3, s4, s5, s6, s7};
+            fxp_buffer(acc, vb8, ww, wl, wl, MODE == 15 ? 0ull : (unsigned long long)__builtin_amdgcn_readfirstlane(g & 1) << 33);
+            s0 = ww[0]; s1 = ww[1]; s2 = ww[2]; s3 = ww[3]; s4 = ww[4]; s5 = ww[5]; s6 = ww[6]; s7 = ww[7];
+            g += 7;
+            (void)t;
         } else if constexpr (MODE == 6) {
 #define MIXLO(VI, W, SEL) "v_fma_mixlo_f16 %[a], " VI ", " W ", %[a] op_sel:[" SEL ",0,0] op_sel_hi:[1,0,1]\n\t"
             asm volatile(MIXLO("%[v0]", "%[w0]", "0") MIXLO("%[v0]", "%[w1]", "1") MIXLO("%[v1]", "%[w2]", "0")
@@ -210,8 +254,9 @@ int main() {
     const char *names[] = {"VGPR weights", "SGPR weights (fixed)", "SGPR by readlane in block", "readlane + S add",
                            "LDS broadcast one group ahead", "LDS + S add", "single rounding (mixlo), VGPR", "readlanes batched first",
                            "LDS 1 ahead, no clobber", "LDS 2 ahead, no clobber", "SMEM x8 glc, wait each group", "SMEM x16 glc, 16-key double buffer",
-                           "SMEM x8 no glc (K$ hits)"};
-    for (int mode = 0; mode < 13; mode++) {
+                           "SMEM x8 no glc (K$ hits)", "2 dims a lane, LDS weights", "2 dims a lane, SGPR weights",
+                           "fxp_buffer fast (8 blocks)", "fxp_buffer checked (1 record/2 buffers)"};
+    for (int mode = 0; mode < 17; mode++) {
         double best = 1e30;
         for (int rep = 0; rep < 4; rep++) {
             switch (mode) {
@@ -228,6 +273,10 @@ int main() {
             case 10: hipLaunchKernelGGL(k<10>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
             case 11: hipLaunchKernelGGL(k<11>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
             case 12: hipLaunchKernelGGL(k<12>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
+            case 13: hipLaunchKernelGGL(k<13>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
+            case 14: hipLaunchKernelGGL(k<14>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
+            case 15: hipLaunchKernelGGL(k<15>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
+            case 16: hipLaunchKernelGGL(k<16>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
             }
             (void)hipDeviceSynchronize();
             long long hc[32];
