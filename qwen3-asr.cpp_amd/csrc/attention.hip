@@ -1331,7 +1331,8 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
     if (threadIdx.x == 0) {
         int ok = 0;
         for (int it = 0; it < a.poll_limit; it++) {
-            if (__hip_atomic_load(a.att_done + (j & 7) * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)a.n_kv_head) {
+            if (__hip_atomic_load(a.att_done + (j & 7) * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                (unsigned)(a.fx == 2 ? 4 * a.n_kv_head : a.n_kv_head)) {   // (fx = 2: one arrival per single-wave chain block)
                 ok = 1;
                 break;
             }
@@ -1733,13 +1734,21 @@ struct FxpWGran {   // fxp_chain_w's weight source: key j's {fp32 weight, tag} g
         return j < n ? __uint_as_float((uint32_t)v) : 0.0f;
     }
 };
-__device__ __forceinline__ void fx1_chain_w(const DecodeAttnArgs &a, const int g) {
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int hh = wid >> 1, wu = __builtin_amdgcn_readfirstlane(wid & 1);
+// One wave a block (c = the chain block, 4 per kv group): the V^T rows of a
+// chain are the wave's own stream, and a CU's L2 -> CU path carried four
+// chains' V^T at once in the four-wave blocks -- ~0.5 KiB a key step, which
+// held the in-place chain at ~20 cycles a key against 15 with the V^T loads
+// cache-hot (device trace).  Blocks c and c + 8 share kv group c % 8 and so
+// the XCD the group's splits pulled its V^T rows into.
+__device__ __forceinline__ void fx1_chain_w(const DecodeAttnArgs &a, const int c) {
+    if (threadIdx.x >= 64) return;   // (no barrier below: the block's other waves are not needed)
+    const int g = c % a.n_kv_head, k = c / a.n_kv_head;
+    const int tid = threadIdx.x, lane = tid;
+    const int hh = k >> 1, wu = k & 1;
     const int d = 64 * wu + lane, loff = 8 * lane;
     const uint16_t *vt = a.vt + (long)g * 128 * vt_ctx(a.max_ctx) + 64 * wu * 8;   // batch 1: slot 0; the wave's key block 0
-    auto mark = [&](int slot) {   // dev trace: rows 4000 + g ([start, v ready, first weights, -, chain done, published])
-        if (a.trace && tid == 0) a.trace[(4000L + g) * 8 + slot] = rt_now();
+    auto mark = [&](int slot) {   // dev trace: rows 4000 + c ([start, v ready, first weights, -, chain done, published])
+        if (a.trace && tid == 0) a.trace[(4000L + c) * 8 + slot] = rt_now();
     };
     mark(0);
     const int pos = a.pos[0], nkv = pos + 1, nl = nkv - 1;
@@ -1790,23 +1799,21 @@ __device__ __forceinline__ void fx1_chain_w(const DecodeAttnArgs &a, const int g
         S = wave_sum(!has || Ml == -INFINITY ? 0.0f : Sl * expf(Ml - Mn));
     }
     if (a.trace && tid == 0) {
-        a.trace[(4010L + g) * 8 + 0] = ck0;
-        a.trace[(4010L + g) * 8 + 1] = clock64();
-        a.trace[(4010L + g) * 8 + 2] = (unsigned long long)nkv;
+        a.trace[(4040L + c) * 8 + 0] = ck0;
+        a.trace[(4040L + c) * 8 + 1] = clock64();
+        a.trace[(4040L + c) * 8 + 2] = (unsigned long long)nkv;
     }
     const float ov = (float)acc * (S == 0.0f ? 0.0f : 1.0f / S);   // ggml: VKQ32 = fp32(VKQ16) * (1 / S)
     const uint32_t h16 = f_to_u16(ov);
     const uint32_t hn = __shfl_xor(h16, 1, 64);
     uint16_t *out = a.out + (2 * g + hh) * 128 + d;
-    if (a.att_done) {   // as fx1_chain_body: write-through pairs, drained, one arrival per replica
+    if (a.att_done) {   // write-through pairs, drained (one wave: no barrier), one arrival per replica
         if ((lane & 1) == 0) __hip_atomic_store((uint32_t *)out, h16 | (hn << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
         if (a.fence && tid == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        if (a.fence) __syncthreads();
         if (tid < 8) __hip_atomic_fetch_add(a.att_done + tid * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
         *out = (uint16_t)h16;
@@ -1824,7 +1831,7 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
         // share one L2 -- speed only), the chain workgroups (exact attention),
         // the o-projection
         const int j = blockIdx.x - 512, nsp = a.grid_splits, nat = nsp * a.n_kv_head;   // grid_splits: this launch's splits
-        const int nfx = a.fx ? a.n_kv_head : 0;
+        const int nfx = a.fx == 2 ? 4 * a.n_kv_head : a.fx ? a.n_kv_head : 0;
         if (j >= nat + nfx) oproj1_body(o, a, j - nat - nfx);
         else if (j >= nat) {
             if (a.fx == 2) fx1_chain_w(a, j - nat);
@@ -1942,7 +1949,7 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     // from its granule, so the fused exact path needs the granule hand-off)
     // (fx_chain.h and the split weights' S: one chain chunk)
     if (a.fx && (!a.gran || !a.sgran || (a.fx_pipe != 1 && ns * spl1 > DX_KC) || (a.fx == 2 && !a.sstat))) return 0;
-    const int nfx = a.fx ? a.n_kv_head : 0;
+    const int nfx = a.fx == 2 ? 4 * a.n_kv_head : a.fx ? a.n_kv_head : 0;   // (fx = 2: single-wave chain blocks, fx1_chain_w)
     const int slots = spl1 == 128 ? cfg.slots_qkv128 : cfg.slots_qkv64;
     const bool fit_o = 512 + ns * a.n_kv_head + nfx + 256 <= slots;
     if (512 + ns * a.n_kv_head + nfx > slots) return 0;

@@ -15,11 +15,20 @@ pytestmark = pytest.mark.gpu
 SR = 16000
 
 
+# Absolute bars beside the relative ones, set from the recorded measurements
+# (profiles/r4/parity.json) with ~2x margin: the reference's own decoder bar is
+# absolute 1e-2 (tests/test_decoder.cpp:157) at a real model's logit scale;
+# the synthetic weights give a logit scale of ~18, where the measured max
+# |delta| is 0.017-0.027 (about 1.2e-3 of the scale).
+ABS_LOGITS = 5e-2
+REL_LOGITS = 3e-3
+
+
 def _err(g, o):
     """(absolute max |delta|, that / max |oracle|): the reference's own decoder
     bar is absolute 1e-2 (tests/test_decoder.cpp:157); with random-init weights
-    the logit scale is ~20x a real model's spread, so the tests here hold the
-    relative form and report both."""
+    the logit scale is ~20x a real model's spread.  The tests hold both the
+    relative 1e-2 of before and the measured-plus-margin bars above."""
     d = float(np.abs(np.asarray(g, np.float64) - np.asarray(o, np.float64)).max())
     return d, d / float(np.abs(o).max())
 
@@ -66,7 +75,7 @@ def test_full_prefill_and_steps(full, parity):
     lo = d.forward(ids, 0, feats, pos)
     ab, rel = _err(lg[0], lo)
     errs = [(ab, rel)]
-    assert rel <= 1e-2, (ab, rel)
+    assert rel <= REL_LOGITS and ab <= ABS_LOGITS, (ab, rel)
     rng = np.random.default_rng(3)
     n_past = len(ids)
     for _ in range(6):   # batch 1, f16: the fused launch with ggml's fp16-accumulating attention (the default)
@@ -75,7 +84,7 @@ def test_full_prefill_and_steps(full, parity):
         lo = d.forward([tok], n_past)
         ab, rel = _err(lg[0], lo)
         errs.append((ab, rel))
-        assert rel <= 1e-2, (ab, rel)
+        assert rel <= REL_LOGITS and ab <= ABS_LOGITS, (ab, rel)
         n_past += 1
     parity("full_2s_prefill_and_6_steps", abs_max=[e[0] for e in errs], rel_max=[e[1] for e in errs],
            scale=float(np.abs(lo).max()), fused_exact=c.get_option("fused_exact"))
@@ -310,7 +319,8 @@ def test_full_configs1_92s(full, parity):
     assert feats_o.shape == (1196, 1024)
     d = np.abs(feats_g - feats_o)
     parity("configs1_92s_encoder", abs_max=float(d.max()), abs_mean=float(d.mean()), mel_abs_max=float(np.abs(mel_g - mel_o).max()))
-    assert d.max() <= 2e-2 and d.mean() <= 1e-3, (d.max(), d.mean())
+    # the reference's bar (max 2e-2, mean 1e-3, tests/run_all_tests.sh:166) and the measured 1.7e-3 / 2.8e-4 with margin
+    assert d.max() <= 5e-3 and d.mean() <= 5e-4, (d.max(), d.mean())
     ids, pos = om.prompt(1196), 9
     assert len(ids) == 1211
     dec = op.OracleDecoder(om, 1300)
@@ -338,7 +348,8 @@ def test_full_configs1_92s(full, parity):
     parity("configs1_92s_prefill_and_15_steps", prefill_abs=ab, prefill_rel=rel, steps_abs=[e[0] for e in errs],
            steps_rel=[e[1] for e in errs], scale=float(np.abs(lo[1]).max()), greedy16_equal=r.tokens[0] == toks,
            fx_pipe=c.get_option("fx_pipe"))
-    assert max(r_ for _, r_ in errs) <= 1e-2, errs
+    assert rel <= REL_LOGITS and ab <= ABS_LOGITS, (ab, rel)
+    assert max(r_ for _, r_ in errs) <= REL_LOGITS and max(a_ for a_, _ in errs) <= ABS_LOGITS, errs
     assert r.tokens[0] == toks
 
 

@@ -166,7 +166,8 @@ def test_decode_steps_teacher_forced(tiny, tiny_oracle, exact, parity):
     finally:
         c.set_option("fa_exact_decode", 1)   # the default
     parity(f"tiny_decode_24_steps_exact{exact}", abs_max=worst_abs, rel_max=worst)
-    assert worst <= 1e-2, (worst_abs, worst)
+    # measured 0.012 / 0.017 absolute (6.6e-4 / 9.8e-4 of the scale): bars with ~2x margin
+    assert worst <= 3e-3 and worst_abs <= 4e-2, (worst_abs, worst)
 
 
 def _margin_aware_equal(gpu_toks, ora_toks, om, pcm, max_tokens, flags=0):

@@ -1,7 +1,7 @@
 # fx_pipe = 2 with the V^T ring: micro, bench + trace, parity (fused == separate, configs[1])
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 5 60 tools/micro/chain_pipe 1370 2 1 > gpurun_out/p6_micro.log 2>&1; rc=$?; cat gpurun_out/p6_micro.log; [ $rc -gt 1 ] && exit $rc
+
 QASR_FX_PIPE=2 timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/p6_b.log 2>&1 || { tail -5 gpurun_out/p6_b.log; exit 1; }
 grep '^{' gpurun_out/p6_b.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('fx2', d['value'], d['stage_ms_per_step_rank0'], [(x['kernel'][:30], x['avg_launch_us'], x['frac']) for x in [d['roofline']]+d['roofline_other']])"
 QASR_FX_PIPE=2 QASR_DEV_TRACE=gpurun_out/p6_tr.bin QASR_DEV_TRACE_LAYER=14 timeout -k 10 200 python -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-probe > gpurun_out/p6_trb.log 2>&1 || { tail -5 gpurun_out/p6_trb.log; exit 1; }

@@ -9,10 +9,11 @@ NAMES = ["qkv_gemv", "attention", "oproj_gemv", "gateup_gemv", "down_gemv"]
 
 def main(path):
     t = np.fromfile(path, dtype=np.uint64).reshape(6, 4096, 8).astype(np.int64)
-    ch = t[1][4000:4008]
+    wide = (t[1][4008:4040, 0] > 0).any()   # fx_pipe = 2: 32 single-wave chain blocks, clocks at rows 4040 +
+    ch = t[1][4000:4040] if wide else t[1][4000:4008]
     ch = ch[ch[:, 0] > 0]
-    ck = t[1][4010:4018].copy()   # chain workgroups: shader clock at chain start / end, keys
-    t[1][4000:4020] = 0
+    ck = (t[1][4040:4072] if wide else t[1][4010:4018]).copy()   # chain workgroups: shader clock at chain start / end, keys
+    t[1][4000:4080] = 0
     live = [t[k][t[k][:, 0] > 0] for k in range(5)]
     t0 = min(int(x[:, 0].min()) for x in live if len(x))
     us = lambda v: (v - t0) / 100.0
