@@ -219,6 +219,16 @@ def cpu_baseline(model_path: str, secs: float, tok_rate: float, threads: int, fu
     }
 
 
+ATTN_LABEL = {
+    0: "fp32 V accumulation (split-K)",
+    1: "fp16 V accumulation per key (ggml CPU flash-attention numerics; chain role of the fused QKV + attention + "
+       "o-proj launch)",
+    2: "fp16 V accumulation per key (ggml CPU flash-attention numerics; scores + chain in one launch per kv group and "
+       "sequence, decode_attn_seq_kernel)",
+    3: "fp16 V accumulation per key (ggml CPU flash-attention numerics; separate scores + chain kernels)",
+}
+
+
 def pmc_traffic(kernel_prefix: str):
     """HBM bytes per launch of the roofline kernel from the newest committed
     rocprofv3 PMC summary (profiles/<round>/summary.json, tools/profile_round.sh:
@@ -232,6 +242,46 @@ def pmc_traffic(kernel_prefix: str):
         for k in d.get("kernels", []):
             if k["name"].startswith(kernel_prefix) and "hbm_read_bytes" in k:
                 return k["hbm_read_bytes"] + k.get("hbm_write_bytes", 0), os.path.relpath(f, ROOT)
+    return None, None
+
+
+def pmc_group_traffic(kind: int, batch: int, q8: bool):
+    """HBM bytes of one probed batch launch group (kind 2: QKV projection +
+    attention; kind 3: o-proj + FFN) from the newest committed batch PMC
+    summary (profiles/<round>/batch/{f16,q8}/summary.json, tools/profile_batch.sh)
+    whose bench line ran this batch size.  Per layer-step: the attention
+    kernel's calls count the layer-steps; the QKV skinny GEMM is the plain-epilogue
+    instance launched once per layer-step, the SwiGLU instance and the o/down
+    instance go to the FFN group.  The rmsnorm launches are left out: their
+    profile line mixes the prefill's 64 x P-row launches with the decode's
+    64-row ones (0.4 MB a launch, under 0.5 % of either group)."""
+    import glob
+    import re
+    sub = "q8" if q8 else "f16"
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "batch", sub, "summary.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+            bl = json.load(open(os.path.join(os.path.dirname(f), "bench.json")))
+        except (OSError, ValueError):
+            continue
+        if bl.get("config", {}).get("clips_per_gpu") != batch:
+            continue
+        ks = [k for k in d.get("kernels", []) if "hbm_read_bytes" in k]
+        att = [k for k in ks if k["name"].startswith("void qasr::decode_attn")]
+        if not att:
+            continue
+        ls = max(k["calls"] for k in att)
+        tot = {2: 0.0, 3: 0.0}
+        for k in ks:
+            per = (k["hbm_read_bytes"] + k.get("hbm_write_bytes", 0)) * k["calls"] / ls
+            n = k["name"]
+            if n.startswith("void qasr::decode_attn"):
+                tot[2] += per
+            elif n.startswith("void qasr::gemm_skinny"):
+                m = re.match(r"void qasr::gemm_skinny\w*<([^>]*)>", n)
+                epi = int(m.group(1).split(",")[3]) if m else 0
+                tot[2 if epi == 0 and k["calls"] == ls else 3] += per
+        return round(tot[kind]), os.path.relpath(f, ROOT)
     return None, None
 
 
@@ -256,7 +306,7 @@ def profiled_mfma():
 
 
 def roofline_entry(kind: int, batch: int, total_ms: float, n: int, bytes_per_launch: float, dev_ms: float, dev_n: int,
-                   layer: int, exact: bool = False) -> dict:
+                   layer: int, exact: bool = False, q8: bool = False) -> dict:
     """HBM roofline of one probed launch group: algorithmic bytes per launch
     (engine.hip probe_bytes: weights + the layer's K/V rows at each step's
     n_kv, averaged over the probed steps) / its mean duration.  Both clocks of
@@ -284,7 +334,12 @@ def roofline_entry(kind: int, batch: int, total_ms: float, n: int, bytes_per_lau
     else:
         kname = "LM head (tied 151936x1024 f16 GEMV + fused argmax)"
         prefix = f"void qasr::gemv_kernel<3, 4, {next(r for r in (1, 2, 4, 8) if r >= batch)}," if batch <= 8 else None
-    traffic, src = pmc_traffic(prefix) if prefix else (None, None)
+    if prefix:
+        traffic, src = pmc_traffic(prefix)
+    elif kind in (2, 3):
+        traffic, src = pmc_group_traffic(kind, batch, q8)
+    else:
+        traffic, src = None, None
     return {"kernel": kname + (f", decoder layer {layer}" if kind != 1 else ""), "bound": "hbm",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic, "traffic_source": src, "bytes_per_launch": round(bytes_per_launch),
@@ -570,19 +625,16 @@ def main():
         "config": {"workload": workload(args, ntok, bool(actx)), "clips_per_gpu": args.batch,
                    "clip_seconds": args.seconds, "decode_tokens": ntok, "parallelism": f"dp{N} (utterance sharding)"},
         "decode_tokens_per_s": round(N * args.batch * ntok * args.steps / dt, 2),
-        "decode_attention": ("fp16 V accumulation per key (ggml CPU flash-attention numerics" +
-                             ("; chain role of the fused QKV + attention + o-proj launch)" if ctx.get_option("fused_exact")
-                              else "; scores + chain in one launch per kv group and sequence)"
-                              if args.batch >= 32 and ctx.get_option("fx_seq") and ctx.get_option("att_stream")
-                              else "; separate scores + chain kernels)")) if exact else
-                            "fp32 V accumulation (split-K)",
+        # from the launches the last step actually made (read-only option attn_path)
+        "decode_attention": ATTN_LABEL.get(ctx.get_option("attn_path"), "unknown"),
         "stage_ms_per_step_rank0": {k: round(v / args.steps, 3) for k, v in tm.items()},
     }
     if probe and probe[1]:
         # `roofline` = the decode launch with the larger time (both run once per
         # layer per step); the other one and the LM head go to roofline_other
-        ents = {2: roofline_entry(2, args.batch, *probe, args.probe_layer, exact)}
-        ents.update({k: roofline_entry(k, args.batch, *v, args.probe_layer, exact) for k, v in extra.items() if v[1]})
+        ents = {2: roofline_entry(2, args.batch, *probe, args.probe_layer, exact, args.q8)}
+        ents.update({k: roofline_entry(k, args.batch, *v, args.probe_layer, exact, args.q8) for k, v in extra.items()
+                     if v[1]})
         top = max((k for k in ents if k != 1), key=lambda k: ents[k]["avg_launch_us"])
         out["roofline"] = ents.pop(top)
         out["roofline_other"] = list(ents.values())

@@ -23,6 +23,7 @@
 #include "fx_chain.h"
 #include "fx_pipe.h"
 #include "fx_decode.h"
+#include "ffn_roles.h"
 #include "kernels.h"
 
 namespace qasr {
@@ -1358,7 +1359,20 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
         for (int e = 0; e < 8; e++) acc = fmaf((float)wv[t][e], (float)h[e], acc);
     }
     acc = wave_sum(acc);
-    if (lane == 0) o.out_f32[row] = fadd_rn(acc, res);
+    if (!a.ocnt) {
+        if (lane == 0) o.out_f32[row] = fadd_rn(acc, res);
+        return;
+    }
+    // the joined FFN reads x in this launch: write-through, drained, one arrival per block into shard j % 32
+    if (lane == 0) __hip_atomic_store((uint32_t *)(o.out_f32 + row), __float_as_uint(fadd_rn(acc, res)), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (a.fence && threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(a.ocnt + (j & 31) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Chain role of the fused exact attention (DecodeAttnArgs.fx): one workgroup
@@ -1821,18 +1835,27 @@ __device__ __forceinline__ void fx1_chain_w(const DecodeAttnArgs &a, const int c
     mark(5);
 }
 
+// the joined FFN's gate/up blocks (ffn_gu_role<1024, LFFN_OPW>): 3072 / (4 LFFN_OPW)
+constexpr int LFFN_OPW = 2, LFFN_NGU = 3072 / (4 * LFFN_OPW);
+
 template <int SPL>
-__global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnArgs a, GemvArgs o) {
+__global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnArgs a, GemvArgs o, GemvArgs g, GemvArgs d,
+                                                        FfnCtl fc) {
     constexpr int K = 1024, NT = 2, RPW = 2;
     stamp_start(a.stamp);
     if (blockIdx.x >= 512) {
         // splits (kv group j % n_kv_head: blocks b and b + 8 share an XCD under
         // round-robin placement, so a group's splits and its chain workgroup
         // share one L2 -- speed only), the chain workgroups (exact attention),
-        // the o-projection
+        // the o-projection, the joined FFN (gate/up, then down: each waits only
+        // on lower-numbered blocks, so in-order dispatch needs no co-residency
+        // for them)
         const int j = blockIdx.x - 512, nsp = a.grid_splits, nat = nsp * a.n_kv_head;   // grid_splits: this launch's splits
         const int nfx = a.fx == 2 ? 4 * a.n_kv_head : a.fx ? a.n_kv_head : 0;
-        if (j >= nat + nfx) oproj1_body(o, a, j - nat - nfx);
+        const int jf = j - nat - nfx - 256;   // joined FFN block (o-proj: 256 blocks of 4 rows)
+        if (a.ocnt && jf >= LFFN_NGU) ffn_dn_role<3072, 1>(d, fc, jf - LFFN_NGU, LFFN_NGU / 32);
+        else if (a.ocnt && jf >= 0) ffn_gu_role<1024, LFFN_OPW>(g, d, fc, jf);
+        else if (j >= nat + nfx) oproj1_body(o, a, j - nat - nfx);
         else if (j >= nat) {
             if (a.fx == 2) fx1_chain_w(a, j - nat);
             else if (a.fx_pipe == 1) fx1_chain_pipe(a, j - nat);
@@ -1934,7 +1957,8 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
 // partials to combine, still >= 64 workgroups per 8 kv heads)
 static int split1(int spl1, int grid_splits) { return spl1 == 64 || spl1 == 128 ? spl1 : grid_splits >= 16 ? 128 : 64; }
 
-int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s, bool dry) {
+int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s, bool dry,
+                          const GemvArgs *gu, const GemvArgs *dn, const FfnCtl *fc) {
     if (!cfg.qkv || !cfg.err || a.B != 1 || !a.qcnt || q.M != 1 || q.K != 1024 || q.Wd || !q.norm_w || q.xh || q.bias || q.res ||
         a.out32 || a.outq || q.N != a.n_head * 128 + 2 * a.n_kv_head * 128 || a.n_head != 2 * a.n_kv_head || a.n_kv_head * 64 != 512)
         return 0;
@@ -1954,8 +1978,15 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     const bool fit_o = 512 + ns * a.n_kv_head + nfx + 256 <= slots;
     if (512 + ns * a.n_kv_head + nfx > slots) return 0;
     const bool with_o2 = with_o && fit_o;
-    if (dry) return with_o2 ? 2 : 1;
-    const dim3 grid(512 + ns * a.n_kv_head + nfx + (with_o2 ? o->N / 4 : 0));
+    // the FFN joins behind the o-projection when it is launch_ffn1's shape, its
+    // counters are given, and the o-proj writes the x row the gate/up reads
+    const bool with_f = with_o2 && cfg.lffn && gu && dn && fc && fc->ocnt && fc->att_done && gu->M == 1 && dn->M == 1 &&
+                        !gu->Wd && !dn->Wd && gu->K == 1024 && gu->N == 3072 && gu->x == o->out_f32 && gu->norm_w &&
+                        !gu->xh && !gu->embd_ids && gu->out_f16 && dn->K == 3072 && dn->N == 1024 && dn->xh == gu->out_f16 &&
+                        dn->res == o->out_f32 && dn->out_f32 == o->out_f32 && !dn->bias && !dn->norm_w && !dn->zero8 &&
+                        fc->att_done == a.att_done;
+    if (dry) return with_f ? 3 : with_o2 ? 2 : 1;
+    const dim3 grid(512 + ns * a.n_kv_head + nfx + (with_o2 ? o->N / 4 : 0) + (with_f ? LFFN_NGU + 1024 / 4 : 0));
     // K/V delay ~2 us: measured optimum on MI355X (round-1 delay sweep: 0 -> 236.3, 10 -> 232.0, 18 -> 240.3 ms decode)
     DecodeAttnArgs ad = a;
     ad.fuse_delay = cfg.qkv_delay;
@@ -1970,11 +2001,24 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     // would sit in its vmcnt queue ahead of the chain's first loads
     ad.fx_vpf = a.fx_pipe ? (cfg.fx_vpf | 1) & ~2 : cfg.fx_vpf;   // (fx_pipe 1 and 2)
     if (!with_o2) ad.att_done = nullptr;
+    ad.ocnt = with_f ? fc->ocnt : nullptr;
     const GemvArgs qa = q;
     const GemvArgs oa = with_o2 ? *o : GemvArgs{};
-    if (spl1 == 128) hipLaunchKernelGGL(qkv_attn1_kernel<128>, grid, dim3(256), 0, s, qa, ad, oa);
-    else hipLaunchKernelGGL(qkv_attn1_kernel<DSPLIT>, grid, dim3(256), 0, s, qa, ad, oa);
-    return with_o2 ? 2 : 1;
+    const GemvArgs ga = with_f ? *gu : GemvArgs{}, da = with_f ? *dn : GemvArgs{};
+    FfnCtl fa{};
+    if (with_f) {
+        fa = *fc;
+        fa.att_need = a.fx == 2 ? 4 * a.n_kv_head : a.n_kv_head;   // as the o-proj's wait
+        fa.gdelay = cfg.lffn_gdelay;
+        fa.wdelay = cfg.lffn_wdelay;
+        fa.delay = 0;
+        fa.poll_limit = cfg.poll_limit;
+        fa.fence = cfg.fence;
+        fa.err = cfg.err;
+    }
+    if (spl1 == 128) hipLaunchKernelGGL(qkv_attn1_kernel<128>, grid, dim3(256), 0, s, qa, ad, oa, ga, da, fa);
+    else hipLaunchKernelGGL(qkv_attn1_kernel<DSPLIT>, grid, dim3(256), 0, s, qa, ad, oa, ga, da, fa);
+    return with_f ? 3 : with_o2 ? 2 : 1;
 }
 
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {

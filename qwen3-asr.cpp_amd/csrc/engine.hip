@@ -123,8 +123,8 @@ struct qasr_ctx {
     unsigned long long *d_sstat = nullptr;  // ... and fx_pipe = 2's split maxima / 32-key group sums [n_head][SS_LD] (zeroed likewise)
     unsigned long long *d_sgran = nullptr;  // ... exact attention: the splits' scores as granules [n_head][max_ctx] (zeroed likewise)
     bool qkv_in_gran = false;               // the captured step's last layer hands its QKV over in granules
-    unsigned int *d_attdone = nullptr;   // fused batch-1 o-proj: combiner arrivals (8 replicas)
-    unsigned int *d_ffncnt = nullptr;    // fused batch-1 FFN: gate/up arrivals, [layer][32 shards][16]
+    unsigned int *d_attdone = nullptr;   // fused batch-1 o-proj: combiner arrivals, [layer][8 replicas][16]
+    unsigned int *d_ffncnt = nullptr;    // fused batch-1 FFN: [layer][gate/up arrivals, o-proj arrivals][32 shards][16]
     uint16_t *d_q = nullptr, *d_att = nullptr, *d_act = nullptr, *d_xh = nullptr;
     unsigned long long *d_amax = nullptr;
     int max_splits = 0, hist_cap = 0;
@@ -160,9 +160,13 @@ struct qasr_ctx {
     int probe_stride = 1;          // probe decode steps k with k % probe_stride == 0 (the others replay the whole-step
                                    // graph: the probed step's split graphs and eager group cost ~3 % of a step)
     bool probe_o_fused = false;    // the probed layer's o-projection runs inside the QKV launch
+    bool probe_lffn = false;       // ... and its FFN too (FuseCfg::lffn)
     int last_fmode = 0, last_fx = 0;   // the last emitted decode step, layer 0: fused launch mode (0 separate, 1 QKV +
                                        // attention, 2 + o-proj) and whether its attention was the chain role (options
                                        // "fused_mode" / "fused_exact", read-only)
+    int last_attn = 0;             // the same step's decode attention launches (option "attn_path", read-only): 0 split-K
+                                   // fp32, 1 chain role of the fused launch, 2 scores + chain in one launch per sequence
+                                   // (decode_attn_seq_kernel), 3 separate scores and chain kernels
     double probe_ms = 0.0, probe_bytes = 0.0, probe_dev_ms = 0.0;
     long probe_dev_n = 0;
     unsigned long long *d_pstamp = nullptr;   // per decode step: [32 min-starts | 32 max-ends] of the probed launches
@@ -226,6 +230,9 @@ static const std::vector<FuseOption> &fuse_options() {
         {"lmh", "QASR_LMH", &FuseCfg::lmh},
         {"fx_seq", "QASR_FX_SEQ", &FuseCfg::fx_seq},
         {"fx_pipe", "QASR_FX_PIPE", &FuseCfg::fx_pipe},
+        {"lffn", "QASR_LFFN", &FuseCfg::lffn},
+        {"lffn_gdelay", "QASR_LFFN_GDELAY", &FuseCfg::lffn_gdelay},
+        {"lffn_wdelay", "QASR_LFFN_WDELAY", &FuseCfg::lffn_wdelay},
         {"skinny_inf", "QASR_SKINNY_INF", &FuseCfg::skinny_inf},
     };
     return v;
@@ -241,9 +248,9 @@ static void launch_gemm_c(qasr_ctx *c, int amode, int epi, GemmArgs g, hipStream
 // context stream: after an option change and after a wait that gave up
 static int reset_counters(qasr_ctx *c) {
     const Hparams &hp = c->m->hp;
-    HIPCHK(hipMemsetAsync(c->d_ffncnt, 0, (size_t)hp.dec_layers * 512 * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->d_ffncnt, 0, (size_t)hp.dec_layers * 1024 * 4, c->st));
     HIPCHK(hipMemsetAsync(c->d_qcnt, 0, (size_t)hp.n_kv_head * 8 * 16 * 4, c->st));
-    HIPCHK(hipMemsetAsync(c->d_attdone, 0, (size_t)8 * 16 * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->d_attdone, 0, (size_t)hp.dec_layers * 128 * 4, c->st));
     HIPCHK(hipMemsetAsync(c->d_counter, 0, (size_t)c->max_batch * hp.n_kv_head * 4, c->st));
     HIPCHK(hipMemsetAsync(c->d_done, 0, 4, c->st));
     HIPCHK(hipMemsetAsync(c->d_amax, 0, (size_t)c->max_batch * 8, c->st));
@@ -727,11 +734,11 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_counter, (size_t)B * hp.n_kv_head * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_scores, (size_t)B * hp.n_head * max_ctx * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_qcnt, (size_t)hp.n_kv_head * 8 * 16 * 4)) ||
-        (rc = dev_alloc(c.get(), (void **)&c->d_attdone, (size_t)8 * 16 * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_attdone, (size_t)hp.dec_layers * 128 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_gran, (size_t)(QD + 2 * KD) * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_sgran, (size_t)hp.n_head * sgran_ld(max_ctx) * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_sstat, (size_t)hp.n_head * 192 * 8)) ||
-        (rc = dev_alloc(c.get(), (void **)&c->d_ffncnt, (size_t)hp.dec_layers * 512 * 4)) ||
+        (rc = dev_alloc(c.get(), (void **)&c->d_ffncnt, (size_t)hp.dec_layers * 1024 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_err, 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_pstamp, (size_t)max_ctx * kStampRec * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_logits, (size_t)B * hp.vocab * 4)) ||
@@ -742,11 +749,11 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     HIPCHK(hipMemcpy(c->d_slot, slots.data(), B * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(c->d_counter, 0, (size_t)B * hp.n_kv_head * 4));
     HIPCHK(hipMemset(c->d_qcnt, 0, (size_t)hp.n_kv_head * 8 * 16 * 4));
-    HIPCHK(hipMemset(c->d_attdone, 0, (size_t)8 * 16 * 4));
+    HIPCHK(hipMemset(c->d_attdone, 0, (size_t)hp.dec_layers * 128 * 4));
     HIPCHK(hipMemset(c->d_gran, 0, (size_t)(QD + 2 * KD) * 8));
     HIPCHK(hipMemset(c->d_sgran, 0, (size_t)hp.n_head * sgran_ld(max_ctx) * 8));
     HIPCHK(hipMemset(c->d_sstat, 0, (size_t)hp.n_head * 192 * 8));
-    HIPCHK(hipMemset(c->d_ffncnt, 0, (size_t)hp.dec_layers * 512 * 4));
+    HIPCHK(hipMemset(c->d_ffncnt, 0, (size_t)hp.dec_layers * 1024 * 4));
     HIPCHK(hipMemset(c->d_done, 0, 4));
     HIPCHK(hipMemset(c->d_err, 0, 4));
     c->fuse.err = c->d_err;
@@ -803,6 +810,7 @@ extern "C" int qasr_ctx_get_option(const qasr_ctx *c, const char *name, int *val
     if (n == "slots_ffn") { *value = c->fuse.slots_ffn; return 0; }
     if (n == "fused_mode") { *value = c->last_fmode; return 0; }
     if (n == "fused_exact") { *value = c->last_fx; return 0; }
+    if (n == "attn_path") { *value = c->last_attn; return 0; }
     if (n == "slots_qkv") { *value = std::min(c->fuse.slots_qkv64, c->fuse.slots_qkv128); return 0; }
     for (const auto &o : fuse_options())
         if (n == o.name) { *value = c->fuse.*(o.field); return 0; }
@@ -1288,7 +1296,8 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         }
         const bool exact = exact_decode(c);
         const bool fusable = skinny && B == 1 && !q8 && !skip;
-        if (fusable) da.att_done = c->d_attdone;
+        unsigned int *att_done = c->d_attdone + (size_t)l * 128;   // this layer's replicas
+        if (fusable) da.att_done = att_done;
         if (fusable && exact && c->fuse.gran) {   // ggml's attention numerics as the fused launch's chain role
             da.fx = c->fuse.fx_pipe == 2 ? 2 : 1;   // 2: the splits derive the weights (attention.hip split_weights)
             da.sstat = c->d_sstat;
@@ -1296,21 +1305,30 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             da.gran = c->d_gran;   // (the fused decision needs the granule hand-off)
             da.layer = l;
         }
-        unsigned int *fcnt = c->d_ffncnt + (size_t)l * 512, *fcnt_next = c->d_ffncnt + (size_t)((l + 1) % nl) * 512;
-        // 0 = separate launches, 1 = QKV + attention in one launch, 2 = + o-projection
-        const int fmode = fusable ? launch_qkv_attention1(q1, da, &o, c->fuse, s, true) : 0;
-        const bool o_fused = fmode == 2;
-        if (l == std::min(c->probe_layer, nl - 1)) c->probe_o_fused = o_fused;
+        unsigned int *fcnt = c->d_ffncnt + (size_t)l * 1024, *fcnt_next = c->d_ffncnt + (size_t)((l + 1) % nl) * 1024;
+        // the FFN joined to the attention launch: o-proj shards after the gate/up ones, the next layer's re-armed
+        FfnCtl fc{};
+        fc.cnt = fcnt; fc.cnt_next = fcnt_next; fc.ocnt = fcnt + 512; fc.ocnt_next = fcnt_next + 512;
+        fc.att_done = att_done; fc.att_done_next = c->d_attdone + (size_t)((l + 1) % nl) * 128;
+        const bool join_ok = nl >= 2 && !(skip & 24) && c->fuse.ffn;
+        // 0 = separate launches, 1 = QKV + attention in one launch, 2 = + o-projection, 3 = + FFN
+        const int fmode = fusable ? launch_qkv_attention1(q1, da, &o, c->fuse, s, true, join_ok ? &gu : nullptr, &dn, &fc) : 0;
+        const bool o_fused = fmode >= 2, f_joined = fmode == 3;
+        if (l == std::min(c->probe_layer, nl - 1)) {
+            c->probe_o_fused = o_fused;
+            c->probe_lffn = f_joined;
+        }
         if (l == 0) {
             c->last_fmode = fmode;
             c->last_fx = fmode && da.fx;
+            c->last_attn = fmode ? (da.fx ? 1 : 0) : -1;   // -1: set below by the separate path
         }
         if (ga) {
             if (l == nl - 1) c->qkv_in_gran = false;
             if (fmode) {
                 if (c->fuse.gran) { da.gran = c->d_gran; da.layer = l; }
                 if (l == nl - 1) c->qkv_in_gran = c->fuse.gran != 0;
-                (void)launch_qkv_attention1(q1, da, &o, c->fuse, s, false);
+                (void)launch_qkv_attention1(q1, da, &o, c->fuse, s, false, join_ok ? &gu : nullptr, &dn, &fc);
             } else {
                 if (skinny) {
                     if (!(skip & 1)) launch_gemv(EPI_F32, q1, s);
@@ -1330,23 +1348,26 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
                 } else if (exact) {   // ggml CPU FA numerics: scores by the splits, then the in-order chain
                     da.scores = c->d_scores;
                     da.fx_seq = c->fuse.fx_seq;
-                    if (!launch_decode_attention_exact_seq(da, s)) {
+                    const bool one = launch_decode_attention_exact_seq(da, s);
+                    if (!one) {
                         launch_decode_attention(da, s);
                         launch_decode_attention_exact(da, s);
                     }
+                    if (l == 0) c->last_attn = one ? 2 : 3;
                 } else {
                     launch_decode_attention(da, s);
+                    if (l == 0) c->last_attn = 0;
                 }
             }
         }
-        if (!gb) continue;
+        if (!gb || f_joined) continue;
         if (skinny) {
             if (!o_fused && !(skip & 4)) launch_gemv(EPI_F32, o, s);
-            if (o_fused) dn.zero8 = c->d_attdone;   // re-arm the fused o-proj's arrival counters
+            if (o_fused) dn.zero8 = att_done;   // re-arm the fused o-proj's arrival counters
             if (skip & 24 || nl < 2 || !launch_ffn1(gu, dn, fcnt, fcnt_next, c->fuse, s)) {
                 if (!(skip & 8)) launch_gemv(q8 ? EPI_SWIGLU_F32 : EPI_SWIGLU_F16, gu, s);
                 if (!(skip & 16)) launch_gemv(EPI_F32, dn, s);
-                else if (o_fused) (void)hipMemsetAsync(c->d_attdone, 0, 8 * 16 * 4, s);   // the skipped down-proj re-arms these
+                else if (o_fused) (void)hipMemsetAsync(att_done, 0, 8 * 16 * 4, s);   // the skipped down-proj re-arms these
             }
         } else if (q8) {
             GemmArgs ob{};
@@ -1430,8 +1451,10 @@ static double probe_bytes(const qasr_ctx *c, int B, int k) {
         double kv = 0;
         for (int b = 0; b < B; b++) kv += (double)(c->run_P[b] + k + 1) * KD * 2 * 2;
         const bool o_in = c->probe_o_fused;
-        return (QD + 2 * KD) * H * wb + B * H * 4 + (o_in ? H * QD * wb + B * H * 8 : 0.0) + kv + B * (QD + 2 * KD) * 4;
+        const double ffn = c->probe_lffn ? 3 * F * H * wb + H * 4 * 3 : 0.0;   // the joined FFN (batch 1)
+        return (QD + 2 * KD) * H * wb + B * H * 4 + (o_in ? H * QD * wb + B * H * 8 : 0.0) + kv + B * (QD + 2 * KD) * 4 + ffn;
     }
+    if (c->probe_lffn) return 0.0;   // the group is empty: its FFN ran in the attention launch
     return 3 * F * H * wb + (c->probe_o_fused ? 0.0 : H * QD * wb) + B * H * 4 * 3;
 }
 

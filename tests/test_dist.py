@@ -202,3 +202,30 @@ def test_bench_launcher_propagates_failure():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
                        capture_output=True, text=True, timeout=300, env=dict(env, QASR_BENCH_FAIL_RANK="1"))
     assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+
+
+def test_bench_batch_group_traffic(tmp_path, monkeypatch):
+    """bench.pmc_group_traffic: the batch launch groups' HBM bytes per
+    layer-step from a batch PMC summary -- attention + the once-per-layer
+    plain-epilogue skinny GEMM (QKV) to group 2, the SwiGLU and o/down
+    instances to group 3, rmsnorm left out, other batch sizes ignored."""
+    import json
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    d = tmp_path / "profiles" / "r9" / "batch" / "f16"
+    d.mkdir(parents=True)
+    k = lambda n, c, r, w: {"name": n, "calls": c, "avg_us": 1.0, "total_ms": 1.0, "hbm_read_bytes": r, "hbm_write_bytes": w}
+    (d / "summary.json").write_text(json.dumps({"kernels": [
+        k("void qasr::decode_attn_seq_kernel<1>(qasr::DecodeAttnArgs)", 10, 100, 1),
+        k("void qasr::gemm_skinny_kernel<4, 1, 8, 0, 4, 2>(qasr::GemmArgs)", 10, 20, 2),
+        k("void qasr::gemm_skinny_kernel<2, 2, 4, 2, 4, 2>(qasr::GemmArgs)", 10, 30, 3),
+        k("void qasr::gemm_skinny_kernel<1, 1, 8, 0, 4, 2>(qasr::GemmArgs)", 20, 10, 1),
+        k("void qasr::rmsnorm_kernel<1024>(float const*)", 21, 1000, 1000)]}))
+    (d / "bench.json").write_text(json.dumps({"config": {"clips_per_gpu": 64}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.pmc_group_traffic(2, 64, False) == (123, "profiles/r9/batch/f16/summary.json")
+    assert bench.pmc_group_traffic(3, 64, False) == (33 + 22, "profiles/r9/batch/f16/summary.json")
+    assert bench.pmc_group_traffic(2, 32, False) == (None, None)
+    assert bench.pmc_group_traffic(2, 64, True) == (None, None)

@@ -154,7 +154,8 @@ def test_full_lds_dma_gemm_bit_identical(full):
     assert np.array_equal(single, out[0][0][3])
 
 
-FUSE_KNOBS = {"QASR_FUSE_FFN": dict(fuse_ffn=0), "QASR_FUSE_QKV": dict(fuse_qkv=0, fuse_o=0), "QASR_FUSE_O": dict(fuse_o=0)}
+FUSE_KNOBS = {"QASR_FUSE_FFN": dict(fuse_ffn=0), "QASR_FUSE_QKV": dict(fuse_qkv=0, fuse_o=0), "QASR_FUSE_O": dict(fuse_o=0),
+              "QASR_LFFN": dict(lffn=1)}   # (the joined FFN is an option: on against the default's off)
 
 
 def _step_state(c, ids, feats, pos, tok=1234):
@@ -217,7 +218,8 @@ def test_full_decode_from_position_zero(full):
             for k, tok in enumerate([151644, 8948, 198]):
                 lg, _ = c1.decode_step([tok], [k])
                 lgs.append(lg[0].copy())
-                assert c1.get_option("fused_exact") == fused and c1.get_option("fused_mode") == 2 * fused
+                # fused: QKV + attention + o-proj (+ the joined FFN, mode 3, when option lffn is on)
+                assert c1.get_option("fused_exact") == fused and c1.get_option("fused_mode") == (2 + c1.get_option("lffn")) * fused
             out[fused] = lgs
     finally:
         c1.close()
