@@ -69,6 +69,10 @@ def parse():
     ap.add_argument("--utt-seed", type=int, default=0)
     ap.add_argument("--align-batch", type=int, default=32,
                     help="--pipeline align: clips per ForcedAligner pass (qasr_align_json_batch)")
+    ap.add_argument("--dump-align", default="",
+                    help="--pipeline align with --utterances: rank 0 writes its shortest utterance's id, transcript and "
+                         "aligner document from the last timed pass to this JSON file (tests/test_gpu_api.py checks it "
+                         "against the oracle)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous check without a GPU: ranks join a gloo group, time a barrier and rank 0 "
                          "prints the JSON line with value 0 (tests/test_dist.py)")
@@ -434,8 +438,11 @@ def utterance_main(args, m, rank, local, world, dist, model_path):
     after = None
     actx = None
     aligned = set()
+    kept = {}   # --dump-align: rank 0's shortest utterance -> (transcript, document) of the latest pass
+    keep = min(shard, key=lambda i: utts[i][1]) if shard and args.dump_align and rank == 0 else None
     if args.pipeline == "align":   # configs[4]: ForcedAligner on every transcript (src/main.cpp:416-500)
-        am = qasr.Model(os.environ.get("QASR_ALIGNER_MODEL") or synthetic_model(rank, "aligner", 8 if args.q8 else 1), local)
+        am_path = os.environ.get("QASR_ALIGNER_MODEL") or synthetic_model(rank, "aligner", 8 if args.q8 else 1)
+        am = qasr.Model(am_path, local)
         # prompt: audio pads + per word its BPE ids and two timestamps (ForcedAligner::tokenize_with_timestamps)
         ab = args.align_batch
         actx = qasr.Context(am, max_batch=ab, max_ctx=P + 8 * qd.budget(nmax, args.tok_rate) + 64)
@@ -443,9 +450,12 @@ def utterance_main(args, m, rank, local, world, dist, model_path):
         def after(idx, toks):   # the rank's transcripts, ab clips per aligner pass (qasr_align_json_batch)
             for k in range(0, len(idx), ab):
                 sub = idx[k:k + ab]
-                docs, _ = actx.align_json_batch([pcm[i] for i in sub], [m.detokenize(t) for t in toks[k:k + ab]])
+                texts = [m.detokenize(t) for t in toks[k:k + ab]]
+                docs, _ = actx.align_json_batch([pcm[i] for i in sub], texts)
                 assert len(docs) == len(sub) and all(isinstance(d, dict) for d in docs), sub
                 aligned.update(sub)
+                if keep in sub:
+                    kept[keep] = (texts[sub.index(keep)], docs[sub.index(keep)])
     for _ in range(args.warmup):
         one_pass(after)
     wall, res = 0.0, None
@@ -489,6 +499,15 @@ def utterance_main(args, m, rank, local, world, dist, model_path):
     }
     if actx is not None:
         out["aligned_rank0"] = len(aligned)
+        if keep is not None:
+            assert keep in kept, "the kept utterance was not aligned on rank 0"
+            # (untimed) the same clip's raw timestamp classes, single-clip: the test checks the document against them
+            # and them against the oracle
+            cls, _ = actx.align(pcm[keep], am.align_tokenize(kept[keep][0])[0])
+            with open(args.dump_align, "w") as f:
+                json.dump({"utterance": keep, "seed": utts[keep][0], "n_samples": utts[keep][1], "text": kept[keep][0],
+                           "doc": kept[keep][1], "classes": [int(x) for x in cls], "aligner_model": am_path,
+                           "asr_model": model_path}, f)
     if dynamic:
         ss = stream_stats
         out["rank0_stream"] = {"clips": sum(x.n_clips for x in ss), "refill_prefills": sum(x.n_prefills for x in ss),

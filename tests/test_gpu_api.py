@@ -122,15 +122,20 @@ def test_cli_sharded_file_list(tiny, tmp_path, tiny_gguf):
 
 
 @pytest.mark.parametrize("queue,pipeline,n", [("dynamic", "asr", 24), ("static", "asr", 24), ("dynamic", "align", 48)])
-def test_bench_utterance_driver(gpu, queue, pipeline, n):
+def test_bench_utterance_driver(gpu, queue, pipeline, n, tmp_path):
     """bench.py --utterances (configs[3] driver; configs[4] with --pipeline
     align) at a small size, full-size synthetic models: every utterance
     transcribed to its budget (bench.py asserts it), with align every
     transcript aligned; one JSON line, strong scaling.  dynamic: the shared
-    queue feeding the continuous-batching stream"""
+    queue feeding the continuous-batching stream.  align: rank 0's shortest
+    utterance's document from the driver (--dump-align) against the oracle's
+    aligner on the same clip and transcript: the same words, and each
+    timestamp the oracle's class x 80 ms (LIS-repaired) wherever the oracle's
+    own top-1/top-2 margin is clear of its noise floor (tests/test_gpu_aligner.py)."""
+    dump = str(tmp_path / "align.json")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--utterances", str(n), "--utt-min", "2",
                         "--utt-max", "6", "--batch", "8", "--steps", "1", "--warmup", "1", "--queue", queue,
-                        "--pipeline", pipeline],
+                        "--pipeline", pipeline] + (["--dump-align", dump] if pipeline == "align" else []),
                        capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')][-1])
@@ -138,6 +143,7 @@ def test_bench_utterance_driver(gpu, queue, pipeline, n):
     assert line["value"] > 0 and line["decode_tokens_per_s"] > 0 and line["config"]["queue"] == queue
     if pipeline == "align":
         assert line["aligned_rank0"] == n
+        _check_dumped_alignment(json.load(open(dump)))
     if queue == "dynamic":
         st = line["rank0_stream"]
         assert st["clips"] == n and 0 < st["slot_utilisation"] <= 1
@@ -163,3 +169,26 @@ def test_probe_stride_samples_steps(gpu, tiny_gguf):
         m.close()
     assert got == ref
     assert n == 3 and ms > 0 and nbytes > 0   # decode steps 0, 4, 8 of the 12
+
+
+def _check_dumped_alignment(d):
+    """the driver's document = its classes LIS-repaired x 80 ms; those classes
+    = the oracle's wherever the oracle's own margin is clear"""
+    import oracle_py as op
+    pcm = qasr.synth_pcm(d["seed"], d["n_samples"])
+    am = qasr.Model(d["aligner_model"])
+    try:
+        ids, nw = am.align_tokenize(d["text"])
+    finally:
+        am.close()
+    words, cls = d["doc"]["words"], d["classes"]
+    assert [w["word"] for w in words] == d["text"].split() and len(words) == nw and len(cls) == 2 * nw
+    dur = np.float32(len(pcm) / SR)
+    ts = [float(min(np.float32(k) * np.float32(0.08), dur)) for k in qasr.fix_timestamps(cls)]
+    assert [v for w in words for v in (w["start"], w["end"])] == pytest.approx(ts, abs=5e-4)
+    op.set_threads(min(16, os.cpu_count() or 1))
+    ocls, olg, _ = op.OracleModel(d["aligner_model"]).align_classes(pcm, ids)
+    srt = np.sort(olg, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 5e-3 * float(np.abs(olg).max())
+    same = np.array(cls) == np.array(ocls)
+    assert same[clear].all(), (cls, list(ocls), clear)
