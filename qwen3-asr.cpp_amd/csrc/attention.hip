@@ -391,66 +391,87 @@ void launch_enc_attention(const float *qkv, const int *seg_start, const int *seg
 }
 
 // ===================================================== decoder q/k norm + RoPE
-// one wave per (row, head); head_dim 128 -> 2 values per lane.  q heads
-// first, then k heads; v heads are copied into the cache.
+// one wave per (row, HPW consecutive heads of one kind), head_dim 128 -> 2
+// values per lane per head.  q heads first, then k heads; v heads are copied
+// into the caches.  All HPW heads' loads are issued before any use: with one
+// head a wave (2 x 256 B in flight) the launch ran at the wave-slot bound of
+// bytes in flight (~2.3 TB/s at 64 x 405 rows); 4 heads a wave quadruple it.
+template <int HPW>
 __global__ __launch_bounds__(256) void qkv_post_kernel(QkvPostArgs a) {
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int nh = a.n_head, nkv = a.n_kv_head;
-    const int per_row = nh + 2 * nkv;
+    const int per_row = (nh + 2 * nkv) / HPW;
     if (wave >= a.rows * per_row) return;
-    const int row = wave / per_row, hh = wave - row * per_row;
+    const int row = wave / per_row, hh0 = (wave - row * per_row) * HPW;
     const int QD = nh * 128, KD = nkv * 128;
     const float *src = a.qkv + (long)row * (QD + 2 * KD);
     const int pos = a.row_pos[row], seq = a.row_seq[row];
-    if (hh >= nh + nkv) {   // V: ggml_cpy f32 -> f16 into the cache
-        const int g = hh - nh - nkv;
-        const float *v = src + QD + KD + g * 128;
-        uint16_t *dst = a.vc + (((long)seq * nkv + g) * a.max_ctx + pos) * 128;
-        const uint16_t v0 = f_to_u16(v[lane]), v1 = f_to_u16(v[lane + 64]);
-        dst[lane] = v0;
-        dst[lane + 64] = v1;
-        uint16_t *t = a.vt + ((long)seq * nkv + g) * 128 * vt_ctx(a.max_ctx);
-        t[vt_index(pos, lane)] = v0;
-        t[vt_index(pos, lane + 64)] = v1;
+    float x0[HPW], x1[HPW];
+#pragma unroll
+    for (int u = 0; u < HPW; u++) {   // the q / k / v column blocks are contiguous: head hh at src + 128 hh
+        x0[u] = src[(hh0 + u) * 128 + lane];
+        x1[u] = src[(hh0 + u) * 128 + lane + 64];
+    }
+    if (hh0 >= nh + nkv) {   // V: ggml_cpy f32 -> f16 into the cache
+#pragma unroll
+        for (int u = 0; u < HPW; u++) {
+            const int g = hh0 + u - nh - nkv;
+            uint16_t *dst = a.vc + (((long)seq * nkv + g) * a.max_ctx + pos) * 128;
+            const uint16_t v0 = f_to_u16(x0[u]), v1 = f_to_u16(x1[u]);
+            dst[lane] = v0;
+            dst[lane + 64] = v1;
+            uint16_t *t = a.vt + ((long)seq * nkv + g) * 128 * vt_ctx(a.max_ctx);
+            t[vt_index(pos, lane)] = v0;
+            t[vt_index(pos, lane + 64)] = v1;
+        }
         return;
     }
-    const bool isq = hh < nh;
-    const float *x = isq ? src + hh * 128 : src + QD + (hh - nh) * 128;
+    const bool isq = hh0 < nh;
     const float *w = isq ? a.q_norm : a.k_norm;
-    float x0 = x[lane], x1 = x[lane + 64];
-    // ggml_rms_norm (sum of squares in double) + ggml_mul
-    double ss = (double)(x0 * x0) + (double)(x1 * x1);
-    ss = wave_sum_d(ss);
-    const float mean = (float)(ss / 128.0);
-    const float scale = 1.0f / sqrtf(mean + a.eps);
-    x0 = fmul_rn(fmul_rn(x0, scale), w[lane]);
-    x1 = fmul_rn(fmul_rn(x1, scale), w[lane + 64]);
-    // NEOX rotation: pair (i, i+64), theta from the host table
+    const float w0 = w[lane], w1 = w[lane + 64];
     const float2 cs = *(const float2 *)(a.rope + ((long)pos * 64 + lane) * 2);
-    const float y0 = x0 * cs.x - x1 * cs.y;
-    const float y1 = x0 * cs.y + x1 * cs.x;
-    if (a.q32) {   // fp32 copies (ForcedAligner: ggml_flash_attn_ext on fp32 Q and K)
-        float *d32 = isq ? a.q32 + (long)row * QD + hh * 128 : a.k32 + (long)row * KD + (hh - nh) * 128;
-        d32[lane] = y0;
-        d32[lane + 64] = y1;
-    }
-    if (isq) {
-        uint16_t *dst = a.q_out + (long)row * QD + hh * 128;
-        dst[lane] = f_to_u16(y0);
-        dst[lane + 64] = f_to_u16(y1);
-    } else {
-        const int g = hh - nh;
-        uint16_t *dst = a.kc + (((long)seq * nkv + g) * a.max_ctx + pos) * 128;
-        dst[lane] = f_to_u16(y0);
-        dst[lane + 64] = f_to_u16(y1);
+#pragma unroll
+    for (int u = 0; u < HPW; u++) {
+        const int hh = hh0 + u;
+        // ggml_rms_norm (sum of squares in double) + ggml_mul
+        double ss = (double)(x0[u] * x0[u]) + (double)(x1[u] * x1[u]);
+        ss = wave_sum_d(ss);
+        const float mean = (float)(ss / 128.0);
+        const float scale = 1.0f / sqrtf(mean + a.eps);
+        const float n0 = fmul_rn(fmul_rn(x0[u], scale), w0);
+        const float n1 = fmul_rn(fmul_rn(x1[u], scale), w1);
+        // NEOX rotation: pair (i, i+64), theta from the host table
+        const float y0 = n0 * cs.x - n1 * cs.y;
+        const float y1 = n0 * cs.y + n1 * cs.x;
+        if (a.q32) {   // fp32 copies (ForcedAligner: ggml_flash_attn_ext on fp32 Q and K)
+            float *d32 = isq ? a.q32 + (long)row * QD + hh * 128 : a.k32 + (long)row * KD + (hh - nh) * 128;
+            d32[lane] = y0;
+            d32[lane + 64] = y1;
+        }
+        if (isq) {
+            uint16_t *dst = a.q_out + (long)row * QD + hh * 128;
+            dst[lane] = f_to_u16(y0);
+            dst[lane + 64] = f_to_u16(y1);
+        } else {
+            const int g = hh - nh;
+            uint16_t *dst = a.kc + (((long)seq * nkv + g) * a.max_ctx + pos) * 128;
+            dst[lane] = f_to_u16(y0);
+            dst[lane + 64] = f_to_u16(y1);
+        }
     }
 }
 
 void launch_qkv_post(const QkvPostArgs &a, hipStream_t s) {
-    const long waves = (long)a.rows * (a.n_head + 2 * a.n_kv_head);
-    if (waves <= 0) return;
-    hipLaunchKernelGGL(qkv_post_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, a);
+    const int heads = a.n_head + 2 * a.n_kv_head;
+    const long waves1 = (long)a.rows * heads;
+    if (waves1 <= 0) return;
+    if (a.n_head % 4 == 0 && a.n_kv_head % 4 == 0) {
+        const long waves = waves1 / 4;
+        hipLaunchKernelGGL(qkv_post_kernel<4>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(qkv_post_kernel<1>, dim3((unsigned)((waves1 + 3) / 4)), dim3(256), 0, s, a);
+    }
 }
 
 // ================================================= decoder prefill (fp16 MFMA)
@@ -1235,14 +1256,37 @@ __global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) 
     st.l0 = st.l1 = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; e++) { st.o0[e] = 0.f; st.o1[e] = 0.f; }
+    // FX with seq_vpf: the chain's V^T rows of each 64-key step pulled into L2
+    // beside that step's K loads (LDS-DMA pieces into this wave's 1 KiB of wo,
+    // contents unused: wo is the FX = 0 merge's), so the chain's loads hit L2
+    // instead of waiting an HBM latency per 64 keys.  Key blocks below the
+    // position's only: its block holds the V^T row wave 3 wrote above (no
+    // stale copy pulled before that store).
+    const uint16_t *vtb = a.vt + ((long)b * a.n_kv_head + g) * 128 * vt_ctx(a.max_ctx) + 8 * lane;
+    const int kb_end = pos >> 3;
+    auto vt_pull = [&](int c0) {
+        if (!FX || !a.seq_vpf) return;
+        typedef __attribute__((address_space(3))) void lds_void_v;
+        typedef __attribute__((address_space(1))) void glb_void_v;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {   // 16 pieces (8 key blocks x 2 dimension halves), 4 a wave
+            const int p = wid + 4 * i, kb = (c0 >> 3) + (p >> 1);
+            if (kb < kb_end)
+                __builtin_amdgcn_global_load_lds((glb_void_v *)(vtb + (long)kb * 1024 + (p & 1) * 512),
+                                                 (lds_void_v *)&wo[wid][0][0], 16, 0, 0);
+        }
+    };
     for (int c0 = 0; c0 < nkv; c0 += 128) {   // two chunks a trip, each prefetching the other set
         if (c0 + 64 < nkv) kvc_issue(kc, vc, c0 + 64, kcap, want_v, B, a.kv_nt);
+        vt_pull(c0);
         kvc_step(a, qa, knew, vnew, c0, pos, A, st, sdst);
         if (c0 + 64 >= nkv) break;
         if (c0 + 128 < nkv) kvc_issue(kc, vc, c0 + 128, kcap, want_v, A, a.kv_nt);
+        vt_pull(c0 + 64);
         kvc_step(a, qa, knew, vnew, c0 + 64, pos, B, st, sdst);
     }
     if constexpr (FX) {
+        if (a.seq_vpf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the pulls have landed (wo is never read here)
         __syncthreads();   // both heads' scores in LDS; the new V^T row stored (this workgroup's own writes)
         decode_attn_exact_body(a, 2 * g + (wid >> 1), b, wid & 1, fxs + (wid >> 1) * a.max_ctx);
         stamp_end(a.stamp);
@@ -1328,6 +1372,23 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
     half8 wv[NT];
 #pragma unroll
     for (int t = 0; t < NT; t++) wv[t] = __builtin_nontemporal_load((const half8 *)(o.W + (long)row * K + t * 512 + lane * 8));
+    // the weights the next launches stream (this layer's FFN, the next layer's
+    // QKV), pulled through the caches while HBM idles under the chain: LDS-DMA
+    // pieces of 1 KiB (nt) into pfbuf, contents unused (every wave's pieces
+    // land on the same 1 KiB: 4 blocks a CU keep within the LDS);
+    // wave w of the 1024 takes pieces w, w + 1024, ...
+    __shared__ __attribute__((aligned(16))) float pfbuf[256];
+    {
+        typedef __attribute__((address_space(3))) void lds_void_p;
+        typedef __attribute__((address_space(1))) void glb_void_p;
+        const int w = j * 4 + wid;
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const char *base = (const char *)a.pf_ptr[r];
+            for (int p = w; p < (int)a.pf_kib[r]; p += 1024)
+                __builtin_amdgcn_global_load_lds((glb_void_p *)(base + (long)p * 1024 + lane * 16), (lds_void_p *)pfbuf, 16, 0, 2);
+        }
+    }
     __shared__ int oready;
     if (threadIdx.x == 0) {
         int ok = 0;
@@ -1361,6 +1422,7 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
     acc = wave_sum(acc);
     if (!a.ocnt) {
         if (lane == 0) o.out_f32[row] = fadd_rn(acc, res);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the pulls into pfbuf, long landed)
         return;
     }
     // the joined FFN reads x in this launch: write-through, drained, one arrival per block into shard j % 32

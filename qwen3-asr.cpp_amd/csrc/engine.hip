@@ -231,6 +231,8 @@ static const std::vector<FuseOption> &fuse_options() {
         {"fx_seq", "QASR_FX_SEQ", &FuseCfg::fx_seq},
         {"fx_pipe", "QASR_FX_PIPE", &FuseCfg::fx_pipe},
         {"lffn", "QASR_LFFN", &FuseCfg::lffn},
+        {"seq_vpf", "QASR_SEQ_VPF", &FuseCfg::seq_vpf},
+        {"wpf", "QASR_WPF", &FuseCfg::wpf},
         {"lffn_gdelay", "QASR_LFFN_GDELAY", &FuseCfg::lffn_gdelay},
         {"lffn_wdelay", "QASR_LFFN_WDELAY", &FuseCfg::lffn_wdelay},
         {"skinny_inf", "QASR_SKINNY_INF", &FuseCfg::skinny_inf},
@@ -1264,6 +1266,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         da.spl_batch = c->fuse.att_spl;
         da.kv_nt = c->fuse.kv_nt;
         da.fx_pipe = c->fuse.fx_pipe;
+        da.seq_vpf = c->fuse.seq_vpf;
         da.stamp = stamp;
         GemvArgs o{};
         if (skinny) {
@@ -1298,6 +1301,11 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         const bool fusable = skinny && B == 1 && !q8 && !skip;
         unsigned int *att_done = c->d_attdone + (size_t)l * 128;   // this layer's replicas
         if (fusable) da.att_done = att_done;
+        if (fusable && c->fuse.wpf) {   // weights the next launches stream, pulled by the o-proj blocks under the chain
+            da.pf_ptr[0] = L.wgu; da.pf_kib[0] = (unsigned)((size_t)2 * F * H * 2 / 1024);
+            da.pf_ptr[1] = L.wd; da.pf_kib[1] = (unsigned)((size_t)H * F * 2 / 1024);
+            if (l + 1 < nl) { da.pf_ptr[2] = m->dec[l + 1].wqkv; da.pf_kib[2] = (unsigned)((size_t)(QD + 2 * KD) * H * 2 / 1024); }
+        }
         if (fusable && exact && c->fuse.gran) {   // ggml's attention numerics as the fused launch's chain role
             da.fx = c->fuse.fx_pipe == 2 ? 2 : 1;   // 2: the splits derive the weights (attention.hip split_weights)
             da.sstat = c->d_sstat;

@@ -170,6 +170,11 @@ struct FuseCfg {
                                         // (decode_attn_seq_kernel<1>) where the per-sequence kernel is taken
     int lmh = 1;                        // decode batches of f16 models (9..64 rows): the LM head in one launch (lmhead.hip)
     int skinny_inf = 1;                 // decode-batch skinny GEMMs: all of a wave's K chunks in flight (gemm_skinny.hip CPW)
+    int wpf = 0;                        // batch 1 fused: the o-proj blocks pull the FFN and next-layer QKV weights during the
+                                        // chain (DecodeAttnArgs.pf_ptr); off: configs[1] 241.4 vs 251.9 RTFx with it (the
+                                        // pulls delay the chain's score gather ~3 us, ffn1 no faster: 8.02 vs 7.95 us)
+    int seq_vpf = 0;                    // decode batches, one-launch exact attention: V^T pulled into L2 beside the K stream
+                                        // (off: 64 x 30 s, layer 14 attention group 30.2 -> 38.1 us with it)
     int lffn = 0;                       // batch 1 fused: the FFN (gate/up + down) joins the QKV + attention + o-proj
                                         // launch, its weights in registers while the chain runs (attention.hip); off:
                                         // bit-identical but the o-proj -> gate/up fan-in (256 arrivals, 640 polling
@@ -334,6 +339,10 @@ struct DecodeAttnArgs {
     int fx_pipe;                         // every exact decode chain derives its weights one 64-key buffer ahead
                                          // (fx_pipe.h; FuseCfg::fx_pipe) instead of all of them first (fx_chain.h)
     unsigned int *ocnt;                  // fused o-proj: rows written through and counted into 32 shards (the joined FFN)
+    const uint16_t *pf_ptr[3];           // batch-1 fused o-proj blocks: weight regions pulled into the caches while they
+    unsigned pf_kib[3];                  // wait for the chain (the FFN's, the next layer's QKV), KiB each (0 = none)
+    int seq_vpf;                         // decode_attn_seq_kernel<1>: each 64-key K step also pulls the chain's V^T rows
+                                         // of those keys into L2 (FuseCfg::seq_vpf)
 };
 // the decode attention with ggml's CPU flash-attention numerics (fa_exact.hip),
 // after launch_decode_attention in scores mode: per (query head, sequence) the
