@@ -448,7 +448,8 @@ def test_full_configs3_f16_b64_30s(full, parity):
     print("configs[3] prefill + decode steps (abs, rel):", [(round(a_, 4), round(r_, 5)) for a_, r_ in errs])
     parity("configs3_f16_b64_30s_row0_prefill_and_5_steps", abs_max=[e[0] for e in errs], rel_max=[e[1] for e in errs],
            scale=float(np.abs(lo[0]).max()))
-    assert max(r_ for _, r_ in errs) <= 1e-2, errs
+    # measured abs <= 0.0226, rel <= 1.1e-3 (profiles/r4/parity.json): the bars above with ~2x margin
+    assert max(r_ for _, r_ in errs) <= REL_LOGITS and max(a_ for a_, _ in errs) <= ABS_LOGITS, errs
 
 
 def test_full_fx_seq_one_launch_bit_identical(full):
