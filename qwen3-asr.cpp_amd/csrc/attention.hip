@@ -1364,19 +1364,26 @@ int decode_stream_slots() {
 // (att_done replica block % 8), then the fp16 attention output and the
 // residual row read with sc1 loads.  att_done is re-armed by the down-proj
 // launch that follows (GemvArgs.zero8).
+// ORPW rows a wave (OPROJ_ROWS = 4 ORPW a block, 1024 / OPROJ_ROWS blocks):
+// 1 -- 256 blocks (2 -- 128 blocks, fitting 3 workgroups a CU, went with the
+// FX_W2 chain experiment); each row's arithmetic is the same either way
+constexpr int ORPW = 1, OPROJ_ROWS = 4 * ORPW;
 __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnArgs a, int j) {
-    constexpr int K = 2048, NT = 4;
+    constexpr int K = 2048, NT = 4, NOB = 1024 / OPROJ_ROWS;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int row = j * 4 + wid;
+    const int row0 = j * OPROJ_ROWS + wid * ORPW;
     for (int i = 0; i < a.oproj_delay; i++) __builtin_amdgcn_s_sleep(8);
-    half8 wv[NT];
+    half8 wv[ORPW][NT];
 #pragma unroll
-    for (int t = 0; t < NT; t++) wv[t] = __builtin_nontemporal_load((const half8 *)(o.W + (long)row * K + t * 512 + lane * 8));
+    for (int r = 0; r < ORPW; r++)
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+            wv[r][t] = __builtin_nontemporal_load((const half8 *)(o.W + (long)(row0 + r) * K + t * 512 + lane * 8));
     // the weights the next launches stream (this layer's FFN, the next layer's
     // QKV), pulled through the caches while HBM idles under the chain: LDS-DMA
     // pieces of 1 KiB (nt) into pfbuf, contents unused (every wave's pieces
-    // land on the same 1 KiB: 4 blocks a CU keep within the LDS);
-    // wave w of the 1024 takes pieces w, w + 1024, ...
+    // land on the same 1 KiB: the blocks a CU holds keep within the LDS);
+    // wave w of the 4 NOB takes pieces w, w + 4 NOB, ...
     __shared__ __attribute__((aligned(16))) float pfbuf[256];
     {
         typedef __attribute__((address_space(3))) void lds_void_p;
@@ -1385,7 +1392,7 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
 #pragma unroll
         for (int r = 0; r < 3; r++) {
             const char *base = (const char *)a.pf_ptr[r];
-            for (int p = w; p < (int)a.pf_kib[r]; p += 1024)
+            for (int p = w; p < (int)a.pf_kib[r]; p += 4 * NOB)
                 __builtin_amdgcn_global_load_lds((glb_void_p *)(base + (long)p * 1024 + lane * 16), (lds_void_p *)pfbuf, 16, 0, 2);
         }
     }
@@ -1408,26 +1415,35 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
         oready = ok;
     }
     __syncthreads();
-    if (!oready) return;   // reported through the error word; x keeps its old row
+    if (!oready) return;   // reported through the error word; x keeps its old rows
     u32x4 xv[NT];
     ld_sc1_x4_4(o.xh + lane * 8, xv);
-    const float res = __uint_as_float(__hip_atomic_load((const uint32_t *)(o.res + row), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    float acc = 0.f;
+    float res[ORPW];
 #pragma unroll
-    for (int t = 0; t < NT; t++) {
-        const half8 h = __builtin_bit_cast(half8, xv[t]);
+    for (int r = 0; r < ORPW; r++)
+        res[r] = __uint_as_float(__hip_atomic_load((const uint32_t *)(o.res + row0 + r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 #pragma unroll
-        for (int e = 0; e < 8; e++) acc = fmaf((float)wv[t][e], (float)h[e], acc);
+    for (int r = 0; r < ORPW; r++) {
+        float acc = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            const half8 h = __builtin_bit_cast(half8, xv[t]);
+#pragma unroll
+            for (int e = 0; e < 8; e++) acc = fmaf((float)wv[r][t][e], (float)h[e], acc);
+        }
+        acc = wave_sum(acc);
+        if (!a.ocnt) {
+            if (lane == 0) o.out_f32[row0 + r] = fadd_rn(acc, res[r]);
+        } else if (lane == 0) {   // the joined FFN reads x in this launch: write-through
+            __hip_atomic_store((uint32_t *)(o.out_f32 + row0 + r), __float_as_uint(fadd_rn(acc, res[r])), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
-    acc = wave_sum(acc);
     if (!a.ocnt) {
-        if (lane == 0) o.out_f32[row] = fadd_rn(acc, res);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the pulls into pfbuf, long landed)
         return;
     }
-    // the joined FFN reads x in this launch: write-through, drained, one arrival per block into shard j % 32
-    if (lane == 0) __hip_atomic_store((uint32_t *)(o.out_f32 + row), __float_as_uint(fadd_rn(acc, res)), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
+    // ... drained, one arrival per block into shard j % 32
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (a.fence && threadIdx.x == 0) {
@@ -1639,6 +1655,20 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         const int lastb = nl > 0 ? (nl - 1) >> 3 : 0;
         fx_loadQ(va, vt, loff, 0, lastb);
         fx_w8(fsc[hh], 0, wa, wb);
+#ifndef FX_W2
+#define FX_W2 0   // weights two groups ahead: 134 VGPRs (3 blocks a CU, o-proj at 2 rows a wave), chain still 20.2
+#endif            // cycles a key in place, configs[1] 248 vs 252 RTFx -- the chain does not wait on the weight reads
+        if (FX_W2) {   // weights two 8-key groups ahead (fx_step1_lds_m2)
+            floatx4 wc, wd;
+            fx_w8(fsc[hh], 8, wc, wd);
+            for (int j0 = 0; j0 < nl; j0 += 2 * DX_Q) {
+                fx_loadQ(vb, vt, loff, j0 + DX_Q, lastb);
+                fx_step1_lds_m2(va, j0, fsc[hh], fx_mask64(kmask[hh], j0), acc, wa, wb, wc, wd);
+                if (j0 + DX_Q >= nl) break;
+                fx_loadQ(va, vt, loff, j0 + 2 * DX_Q, lastb);
+                fx_step1_lds_m2(vb, j0 + DX_Q, fsc[hh], fx_mask64(kmask[hh], j0 + DX_Q), acc, wa, wb, wc, wd);
+            }
+        } else
         for (int j0 = 0; j0 < nl; j0 += 2 * DX_Q) {
             fx_loadQ(vb, vt, loff, j0 + DX_Q, lastb);
             fx_step1_lds_m(va, j0, fsc[hh], fx_mask64(kmask[hh], j0), acc, wa, wb);
@@ -1914,7 +1944,7 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
         // for them)
         const int j = blockIdx.x - 512, nsp = a.grid_splits, nat = nsp * a.n_kv_head;   // grid_splits: this launch's splits
         const int nfx = a.fx == 2 ? 4 * a.n_kv_head : a.fx ? a.n_kv_head : 0;
-        const int jf = j - nat - nfx - 256;   // joined FFN block (o-proj: 256 blocks of 4 rows)
+        const int jf = j - nat - nfx - 1024 / OPROJ_ROWS;   // joined FFN block (after the o-proj blocks)
         if (a.ocnt && jf >= LFFN_NGU) ffn_dn_role<3072, 1>(d, fc, jf - LFFN_NGU, LFFN_NGU / 32);
         else if (a.ocnt && jf >= 0) ffn_gu_role<1024, LFFN_OPW>(g, d, fc, jf);
         else if (j >= nat + nfx) oproj1_body(o, a, j - nat - nfx);
@@ -2037,7 +2067,8 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     if (a.fx && (!a.gran || !a.sgran || (a.fx_pipe != 1 && ns * spl1 > DX_KC) || (a.fx == 2 && !a.sstat))) return 0;
     const int nfx = a.fx == 2 ? 4 * a.n_kv_head : a.fx ? a.n_kv_head : 0;   // (fx = 2: single-wave chain blocks, fx1_chain_w)
     const int slots = spl1 == 128 ? cfg.slots_qkv128 : cfg.slots_qkv64;
-    const bool fit_o = 512 + ns * a.n_kv_head + nfx + 256 <= slots;
+    const int o_blocks = 1024 / OPROJ_ROWS;
+    const bool fit_o = 512 + ns * a.n_kv_head + nfx + o_blocks <= slots;
     if (512 + ns * a.n_kv_head + nfx > slots) return 0;
     const bool with_o2 = with_o && fit_o;
     // the FFN joins behind the o-projection when it is launch_ffn1's shape, its
@@ -2048,7 +2079,7 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
                         dn->res == o->out_f32 && dn->out_f32 == o->out_f32 && !dn->bias && !dn->norm_w && !dn->zero8 &&
                         fc->att_done == a.att_done;
     if (dry) return with_f ? 3 : with_o2 ? 2 : 1;
-    const dim3 grid(512 + ns * a.n_kv_head + nfx + (with_o2 ? o->N / 4 : 0) + (with_f ? LFFN_NGU + 1024 / 4 : 0));
+    const dim3 grid(512 + ns * a.n_kv_head + nfx + (with_o2 ? o_blocks : 0) + (with_f ? LFFN_NGU + 1024 / 4 : 0));
     // K/V delay ~2 us: measured optimum on MI355X (round-1 delay sweep: 0 -> 236.3, 10 -> 232.0, 18 -> 240.3 ms decode)
     DecodeAttnArgs ad = a;
     ad.fuse_delay = cfg.qkv_delay;
@@ -2071,6 +2102,7 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     if (with_f) {
         fa = *fc;
         fa.att_need = a.fx == 2 ? 4 * a.n_kv_head : a.n_kv_head;   // as the o-proj's wait
+        fa.o_need = (unsigned)(o_blocks / 32);                     // o-proj arrivals per shard
         fa.gdelay = cfg.lffn_gdelay;
         fa.wdelay = cfg.lffn_wdelay;
         fa.delay = 0;

@@ -72,8 +72,8 @@ __device__ __forceinline__ void ld_sc1_f32x16(const float *p, u32x4 *v) {
 }
 
 // joined FFN (c.ocnt): one lane waits for the attention (its att_done replica,
-// as the o-proj blocks do), then the wave polls the o-proj shards (need 8 each)
-// when `oshards`; wave 0 of the block calls it, the verdict in *ready
+// as the o-proj blocks do), then the wave polls the o-proj shards (o_need each)
+// when `oshards` (o_need each); wave 0 of the block calls it, the verdict in *ready
 __device__ __forceinline__ void ffn_wait_att(const FfnCtl &c, int blk, bool oshards, int *ready) {
     const int lane = threadIdx.x & 63;
     int ok = 1;
@@ -89,7 +89,7 @@ __device__ __forceinline__ void ffn_wait_att(const FfnCtl &c, int blk, bool osha
     }
     ok = __shfl(ok, 0, 64);
     if (ok && oshards) {
-        ffn_wait_shards(c.ocnt, 8u, 0, c.poll_limit, c.fence, c.err, DEVERR_GU_WAIT, ready);
+        ffn_wait_shards(c.ocnt, c.o_need, 0, c.poll_limit, c.fence, c.err, DEVERR_GU_WAIT, ready);
         return;
     }
     if (lane == 0) {

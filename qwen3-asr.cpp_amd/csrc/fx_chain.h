@@ -252,6 +252,33 @@ __device__ __forceinline__ void fx_step1_lds_m(const u32x4 *v, int j0, const flo
         }
     }
 }
+// fx_step1_lds_m with the weights requested two groups ahead: (wa, wb) = keys
+// j0 .. j0 + 7, (wc, wd) = j0 + 8 .. j0 + 15 on entry, the same for j0 + DX_Q
+// on exit (one group of LDS latency was not enough to cover the reads:
+// tools/micro/chain_role.hip, 15.4 cycles a key from LDS vs 11.7 from fixed
+// registers).  Reads past the chunk's image land in padding or another
+// head's rows and are never consumed.
+__device__ __forceinline__ void fx_step1_lds_m2(const u32x4 *v, int j0, const float *ws, unsigned long long m64, f16 &acc,
+                                                floatx4 &wa, floatx4 &wb, floatx4 &wc, floatx4 &wd) {
+    if (__builtin_expect(m64 != 0ull, 0)) {
+#pragma unroll
+        for (int g8 = 0; g8 < DX_Q / 8; g8++) {
+            floatx4 na, nb;
+            fx_w8(ws, j0 + 8 * g8 + 16, na, nb);
+            if (((m64 >> (8 * g8)) & 0xffull) != 0) fx8_slow(acc, v[g8], wa, wb);
+            else fx8_fast(acc, v[g8], wa, wb);
+            wa = wc; wb = wd; wc = na; wd = nb;
+        }
+    } else {
+#pragma unroll
+        for (int g8 = 0; g8 < DX_Q / 8; g8++) {
+            floatx4 na, nb;
+            fx_w8(ws, j0 + 8 * g8 + 16, na, nb);
+            fx8_fast(acc, v[g8], wa, wb);
+            wa = wc; wb = wd; wc = na; wd = nb;
+        }
+    }
+}
 // the 64 new-maximum bits of keys j0 .. j0 + 63 from km (u16 per 16 keys) as a
 // uniform value
 __device__ __forceinline__ unsigned long long fx_mask64(const uint16_t *km, int j0) {

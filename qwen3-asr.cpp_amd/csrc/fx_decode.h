@@ -29,15 +29,25 @@ namespace qasr {
 // turn, the next step's loads issued before the current step's arithmetic --
 // unconditionally (blocks past the sequence re-read its last one, fx_loadQ),
 // so the wait counts stay exact.  c0: the first key of the current weights chunk.
+// FX_VNB register buffers in turn (static indices: the loop body is unrolled
+// over them), FX_VNB - 1 of them in flight ahead of the one in use.  Two (one
+// of lead): four measured slower at 64 x 30 s (the QKV + attention group
+// 30.2 -> 32.4 us, 164 VGPRs) -- the batch chain does not wait on V^T latency.
+#ifndef FX_VNB
+#define FX_VNB 2
+#endif
 __device__ __forceinline__ void fx_chain1(const uint16_t *__restrict__ vt, int loff, int c0, int n, int lastb, const float *w,
                                           unsigned long long flags, uint32_t kb, f16 &acc) {
-    u32x4 va[DX_Q / 8], vb[DX_Q / 8];
-    fx_loadQ(va, vt, loff, c0, lastb);
-    for (int j0 = 0; j0 < n; j0 += 2 * DX_Q) {
-        fx_loadQ(vb, vt, loff, c0 + j0 + DX_Q, lastb);
-        fx_step1_m(va, j0, n, w, flags, kb, acc);
-        fx_loadQ(va, vt, loff, c0 + j0 + 2 * DX_Q, lastb);
-        fx_step1_m(vb, j0 + DX_Q, n, w, flags, kb, acc);
+    constexpr int NB = FX_VNB;
+    u32x4 v[NB][DX_Q / 8];
+#pragma unroll
+    for (int i = 0; i < NB - 1; i++) fx_loadQ(v[i], vt, loff, c0 + i * DX_Q, lastb);
+    for (int j0 = 0; j0 < n; j0 += NB * DX_Q) {
+#pragma unroll
+        for (int s = 0; s < NB; s++) {
+            fx_loadQ(v[(s + NB - 1) % NB], vt, loff, c0 + j0 + (s + NB - 1) * DX_Q, lastb);
+            fx_step1_m(v[s], j0 + s * DX_Q, n, w, flags, kb, acc);
+        }
     }
 }
 

@@ -200,7 +200,7 @@ struct FfnCtl {
     // blocks request their weights after gdelay x ~0.2 us and re-arm the next layer's ocnt / att_done shards
     unsigned int *ocnt, *ocnt_next, *att_done_next;
     const unsigned int *att_done;
-    unsigned att_need;
+    unsigned att_need, o_need;       // attention arrivals per replica; o-proj arrivals per ocnt shard
     int gdelay;
 };
 // gemv.hip: batch-1 f16 gate/up + down in one launch; cnt = this layer's

@@ -260,6 +260,7 @@ def test_full_fused_wait_timeout_is_an_error(full):
     m, _, _ = full
     c1 = qasr.Context(m, max_batch=1, max_ctx=256)
     try:   # every fused launch in play (chain role included)
+        # (the QKV launch: 512 QKV blocks, the splits, 8 chain blocks, 256 o-proj blocks)
         assert c1.get_option("slots_ffn") >= 1024 + 256 and c1.get_option("slots_qkv") >= 512 + 8 * 4 + 8 + 256
         pcm = qasr.synth_pcm(14000, 2 * SR)
         ref = c1.transcribe([pcm], max_tokens=4, ignore_eos=True).tokens
