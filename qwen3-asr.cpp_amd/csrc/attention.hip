@@ -1276,6 +1276,30 @@ __global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) 
                                                  (lds_void_v *)&wo[wid][0][0], 16, 0, 0);
         }
     };
+#ifndef SEQ_KNB
+#define SEQ_KNB 2   // FX: K register sets, SEQ_KNB - 1 chunks in flight ahead of the one scored (4: neutral at
+#endif              // 64 x 30 s, 30.35 vs 30.2 us a layer for the QKV + attention group, 164 VGPRs)
+    if constexpr (FX && SEQ_KNB > 2) {
+        // the exact path keeps no softmax state in the loop, so the K stream can
+        // run SEQ_KNB - 1 chunks ahead (a CU holds two of these workgroups: the
+        // registers are there); with one chunk of lead each 64-key chunk waited
+        // an HBM latency
+        KvChunk R[SEQ_KNB];
+        R[0] = A;
+#pragma unroll
+        for (int i = 1; i < SEQ_KNB - 1; i++)
+            if (64 * i < nkv) kvc_issue(kc, vc, 64 * i, kcap, want_v, R[i], a.kv_nt);
+        for (int c0 = 0; c0 < nkv; c0 += 64 * SEQ_KNB) {
+#pragma unroll
+            for (int u = 0; u < SEQ_KNB; u++) {
+                const int cs = c0 + 64 * u;
+                if (cs >= nkv) break;
+                if (cs + 64 * (SEQ_KNB - 1) < nkv) kvc_issue(kc, vc, cs + 64 * (SEQ_KNB - 1), kcap, want_v, R[(u + SEQ_KNB - 1) % SEQ_KNB], a.kv_nt);
+                vt_pull(cs);
+                kvc_step(a, qa, knew, vnew, cs, pos, R[u], st, sdst);
+            }
+        }
+    } else
     for (int c0 = 0; c0 < nkv; c0 += 128) {   // two chunks a trip, each prefetching the other set
         if (c0 + 64 < nkv) kvc_issue(kc, vc, c0 + 64, kcap, want_v, B, a.kv_nt);
         vt_pull(c0);
