@@ -1391,7 +1391,10 @@ int decode_stream_slots() {
 // ORPW rows a wave (OPROJ_ROWS = 4 ORPW a block, 1024 / OPROJ_ROWS blocks):
 // 1 -- 256 blocks (2 -- 128 blocks, fitting 3 workgroups a CU, went with the
 // FX_W2 chain experiment); each row's arithmetic is the same either way
-constexpr int ORPW = 1, OPROJ_ROWS = 4 * ORPW;
+#ifndef ORPW_N
+#define ORPW_N 1
+#endif
+constexpr int ORPW = ORPW_N, OPROJ_ROWS = 4 * ORPW;
 __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnArgs a, int j) {
     constexpr int K = 2048, NT = 4, NOB = 1024 / OPROJ_ROWS;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1425,7 +1428,7 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
         int ok = 0;
         for (int it = 0; it < a.poll_limit; it++) {
             if (__hip_atomic_load(a.att_done + (j & 7) * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                (unsigned)(a.fx == 2 ? 4 * a.n_kv_head : a.n_kv_head)) {   // (fx = 2: one arrival per single-wave chain block)
+                (unsigned)(a.fx >= 2 ? 4 * a.n_kv_head : a.n_kv_head)) {   // (fx = 2, 3: one arrival per single-wave chain block)
                 ok = 1;
                 break;
             }
@@ -1506,8 +1509,13 @@ __device__ __forceinline__ void ld_sc1_x4_8(const void *base, const uint32_t *of
         : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]), "v"(off[7]), "s"(base)
         : "memory");
 }
+// the chain roles' LDS (fx1_chain_body: both heads; fx1_chain_1w: row 0), one
+// allocation whichever role a workgroup takes
+__shared__ __attribute__((aligned(16))) float fx_fsc[2][DX_KC / DX_B * FX_ST];
+__shared__ __attribute__((aligned(8))) uint16_t fx_kmask[2][DX_KC / 16];
+__shared__ float fx_fwl[2];
 __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const int g) {
-    __shared__ __attribute__((aligned(16))) float fsc[2][DX_KC / DX_B * FX_ST];
+    auto &fsc = fx_fsc;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int hh = wid >> 1, wu = __builtin_amdgcn_readfirstlane(wid & 1);
     const int d = 64 * wu + lane, loff = 8 * lane;
@@ -1582,8 +1590,8 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
     //     reads the cache row another workgroup is writing) and its weight in
     //     fwl, applied once after the loop with vnew -- the same sequence of
     //     operations as fa_exact.hip's chain, so both launches agree bit for bit
-    __shared__ float fwl[2];
-    __shared__ __attribute__((aligned(8))) uint16_t kmask[2][DX_KC / 16];   // per head: new-maximum bit of every key
+    auto &fwl = fx_fwl;
+    auto &kmask = fx_kmask;   // per head: new-maximum bit of every key
     float M, S;
     {
         float *row = fsc[hh] + lane * FX_ST;   // this lane's 32 keys
@@ -1677,6 +1685,25 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         u32x4 va[DX_Q / 8], vb[DX_Q / 8];
         floatx4 wa, wb;
         const int lastb = nl > 0 ? (nl - 1) >> 3 : 0;
+#ifndef FX_CNB
+#define FX_CNB 2   // V^T register buffers of the chain (FX_CNB - 1 of lead)
+#endif
+        if constexpr (FX_CNB > 2) {
+            (void)va; (void)vb;
+            u32x4 vr[FX_CNB][DX_Q / 8];
+#pragma unroll
+            for (int i = 0; i < FX_CNB - 1; i++) fx_loadQ(vr[i], vt, loff, i * DX_Q, lastb);
+            fx_w8(fsc[hh], 0, wa, wb);
+            for (int j0 = 0; j0 < nl; j0 += FX_CNB * DX_Q) {
+#pragma unroll
+                for (int u = 0; u < FX_CNB; u++) {
+                    const int js = j0 + u * DX_Q;
+                    if (js >= nl) break;
+                    fx_loadQ(vr[(u + FX_CNB - 1) % FX_CNB], vt, loff, js + (FX_CNB - 1) * DX_Q, lastb);
+                    fx_step1_lds_m(vr[u], js, fsc[hh], fx_mask64(kmask[hh], js), acc, wa, wb);
+                }
+            }
+        } else {
         fx_loadQ(va, vt, loff, 0, lastb);
         fx_w8(fsc[hh], 0, wa, wb);
 #ifndef FX_W2
@@ -1699,6 +1726,7 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
             if (j0 + DX_Q >= nl) break;
             fx_loadQ(va, vt, loff, j0 + 2 * DX_Q, lastb);
             fx_step1_lds_m(vb, j0 + DX_Q, fsc[hh], fx_mask64(kmask[hh], j0 + DX_Q), acc, wa, wb);
+        }
         }
         acc = fx_key_slow(acc, vnew, fwl[hh]);
     }
@@ -1731,6 +1759,195 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         }
         if (a.fence) __syncthreads();
         if (tid < 8) __hip_atomic_fetch_add(a.att_done + tid * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        *out = (uint16_t)h16;
+    }
+    mark(5);
+}
+
+// The chain role with one wave a workgroup (DecodeAttnArgs.fx == 3, option
+// fx_pipe = 3): fx1_chain_body's arithmetic (so the same bits) for one query
+// head and one dimension half, 4 n_kv_head workgroups (c: kv group c % n_kv_head,
+// head 2 g + (c / n_kv_head) / 2, half (c / n_kv_head) & 1; a group's four
+// land on the XCD of its splits).  The wave gathers its head's score granules,
+// derives all 32 weights of each lane (both halves fx1_chain_body splits over a
+// head's two waves) and runs the chain: one wave's V^T stream per CU instead of
+// four.  Trace rows 4000 + c, clocks 4040 + c.
+__device__ __forceinline__ void fx1_chain_1w(const DecodeAttnArgs &a, const int c) {
+    float *const fs1 = fx_fsc[0];
+    uint16_t *const km1 = fx_kmask[0];
+    float &fwl1 = fx_fwl[0];
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    const int g = c % a.n_kv_head, k = c / a.n_kv_head;
+    const int hh = k >> 1, wu = __builtin_amdgcn_readfirstlane(k & 1);
+    const int d = 64 * wu + lane, loff = 8 * lane;
+    const uint16_t *vt = a.vt + (long)g * 128 * vt_ctx(a.max_ctx) + 64 * wu * 8;
+    auto mark = [&](int slot) {
+        if (a.trace && lane == 0) a.trace[(4000L + c) * 8 + slot] = rt_now();
+    };
+    mark(0);
+    const int pos = a.pos[0], nkv = pos + 1;
+    const uint32_t tag = gran_tag(pos, a.layer);
+    const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
+    if (a.fx_vpf & 2) {   // V^T of this half -> L2 (the group's other head pulls the other key blocks; same XCD)
+        typedef __attribute__((address_space(3))) void lds_void_c;
+        typedef __attribute__((address_space(1))) void glb_void_c;
+        for (int kb = hh; kb * 8 < nkv; kb += 2)
+            __builtin_amdgcn_global_load_lds((glb_void_c *)(vt + (long)kb * 1024 + loff), (lds_void_c *)fs1, 16, 0, 0);
+    }
+    const int n = nkv, np = (n + 1) >> 1;
+    {   // (1) this head's score granules -> LDS: pair q = lane + 64 u, all 16 in flight (the asm drains them)
+        const int ld = sgran_ld(a.max_ctx);
+        const unsigned long long *gb = a.sgran + (long)(2 * g + hh) * ld;   // uniform
+        uint32_t go[DX_KC / 128];
+#pragma unroll
+        for (int u = 0; u < DX_KC / 128; u++) {
+            const int q = lane + 64 * u;
+            go[u] = q < np ? (uint32_t)(2 * q * 8) : 0u;
+        }
+        u32x4 gv[DX_KC / 128];
+        bool ok = false;
+        for (int it = 0; it < a.poll_limit; it++) {
+            ld_sc1_x4_8(gb, go, gv);
+            ld_sc1_x4_8(gb, go + 8, gv + 8);
+            ok = true;
+#pragma unroll
+            for (int u = 0; u < DX_KC / 128; u++) {
+                const int q = lane + 64 * u;
+                if (q < np) ok = ok && gv[u][1] == tag && (2 * q + 1 >= n || gv[u][3] == tag);
+            }
+            if (__all(ok)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_SCORE_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int u = 0; u < DX_KC / 128; u++) {
+            const int q = lane + 64 * u, j = 2 * q;
+            if (q < np) *(float2 *)&fs1[(j >> 5) * FX_ST + (j & 31)] = make_float2(__uint_as_float(gv[u][0]), __uint_as_float(gv[u][2]));
+        }
+    }
+    mark(2);
+    float M, S;
+    {   // (2) the weights: fx1_chain_body's two halves, both here
+        float *row = fs1 + lane * FX_ST;
+        float sv[DX_B];
+#pragma unroll
+        for (int i = 0; i < DX_B; i += 4) {
+            const floatx4 r = *(const floatx4 *)&row[i];
+#pragma unroll
+            for (int e = 0; e < 4; e++) sv[i + e] = lane * DX_B + i + e < n ? r[e] : -INFINITY;
+        }
+        float lm = -INFINITY, lh = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < DX_B / 2; i++) lh = fmaxf(lh, sv[i]);
+#pragma unroll
+        for (int i = DX_B / 2; i < DX_B; i++) lm = fmaxf(lm, sv[i]);
+        lm = fmaxf(lm, lh);
+        const float inc = wave_scan_max(lm);
+        const float Mp0 = dpp_ninf<0x138, 0xF>(inc);
+        M = lane_f(inc, 63);
+        float x[DX_B];
+        uint32_t kb0 = 0, kb1 = 0;
+        {
+            float Mq = Mp0;
+#pragma unroll
+            for (int i = 0; i < DX_B / 2; i++) {
+                const float sc = sv[i];
+                const bool gt = sc > Mq;
+                const float e = expf(gt ? Mq - sc : sc - Mq);
+                x[i] = gt ? -e : (sc != -INFINITY ? e : 0.0f);
+                kb0 |= (uint32_t)gt << i;
+                Mq = fmaxf(Mq, sc);
+            }
+        }
+        {
+            float Mq = fmaxf(Mp0, lh);
+#pragma unroll
+            for (int i = 0; i < DX_B / 2; i++) {
+                const float sc = sv[DX_B / 2 + i];
+                const bool gt = sc > Mq;
+                const float e = expf(gt ? Mq - sc : sc - Mq);
+                x[DX_B / 2 + i] = gt ? -e : (sc != -INFINITY ? e : 0.0f);
+                kb1 |= (uint32_t)gt << i;
+                Mq = fmaxf(Mq, sc);
+            }
+        }
+        km1[2 * lane] = (uint16_t)kb0;
+        km1[2 * lane + 1] = (uint16_t)kb1;
+        mark(6);
+#pragma unroll
+        for (int i = 0; i < DX_B; i += 4) *(floatx4 *)&row[i] = floatx4{x[i], x[i + 1], x[i + 2], x[i + 3]};
+        const int kl = n - 1, kr = kl & 31;
+        const bool own = lane == (kl >> 5);
+        if (own) {   // the new key: weight 0 in LDS (a no-op for the loop), its own weight in fwl1, applied last
+            fwl1 = row[kr];
+            row[kr] = 0.0f;
+        }
+        mark(7);
+        const float wl = fwl1;   // (this wave's own LDS write above: in order)
+        float Sl = 0.0f;   // the lane's sequential S over its 32 weights, key n - 1 as 0, then its own term
+#pragma unroll
+        for (int i = 0; i < DX_B; i++) {
+            const float r = own && i == kr ? 0.0f : x[i];
+            Sl = __builtin_signbit(r) ? fadd_rn(fmul_rn(Sl, -r), 1.0f) : fadd_rn(fmul_rn(Sl, 1.0f), r);
+        }
+        if (own) Sl = __builtin_signbit(wl) ? fadd_rn(fmul_rn(Sl, -wl), 1.0f) : fadd_rn(fmul_rn(Sl, 1.0f), wl);
+        const float Ml = fmaxf(Mp0, lm);
+        S = wave_sum(Ml == -INFINITY ? 0.0f : Sl * expf(Ml - M));
+    }
+    mark(3);
+    uint16_t vnew = 0;
+    {
+        const unsigned long long *gp = a.gran + QD + KD + g * 128 + d;
+        unsigned long long v = 0;
+        bool ok = false;
+        for (int it = 0; it < a.poll_limit; it++) {
+            v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = (uint32_t)(v >> 32) == tag;
+            if (__all(ok)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_QKV_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        vnew = f_to_u16(__uint_as_float((uint32_t)v));
+    }
+    mark(1);
+    const unsigned long long ck0 = a.trace ? clock64() : 0ull;
+    f16 acc = 0;
+    {
+        const int nl = n - 1;
+        u32x4 va[DX_Q / 8], vb[DX_Q / 8];
+        floatx4 wa, wb;
+        const int lastb = nl > 0 ? (nl - 1) >> 3 : 0;
+        fx_loadQ(va, vt, loff, 0, lastb);
+        fx_w8(fs1, 0, wa, wb);
+        for (int j0 = 0; j0 < nl; j0 += 2 * DX_Q) {
+            fx_loadQ(vb, vt, loff, j0 + DX_Q, lastb);
+            fx_step1_lds_m(va, j0, fs1, fx_mask64(km1, j0), acc, wa, wb);
+            if (j0 + DX_Q >= nl) break;
+            fx_loadQ(va, vt, loff, j0 + 2 * DX_Q, lastb);
+            fx_step1_lds_m(vb, j0 + DX_Q, fs1, fx_mask64(km1, j0 + DX_Q), acc, wa, wb);
+        }
+        acc = fx_key_slow(acc, vnew, fwl1);
+    }
+    mark(4);
+    if (a.trace && lane == 0) {
+        a.trace[(4040L + c) * 8 + 0] = ck0;
+        a.trace[(4040L + c) * 8 + 1] = clock64();
+        a.trace[(4040L + c) * 8 + 2] = (unsigned long long)n;
+    }
+    const float ov = (float)acc * (S == 0.0f ? 0.0f : 1.0f / S);
+    const uint32_t h16 = f_to_u16(ov);
+    const uint32_t hn = __shfl_xor(h16, 1, 64);
+    uint16_t *out = a.out + (2 * g + hh) * 128 + d;
+    if (a.att_done) {   // write-through pairs, drained, one arrival per replica from this workgroup
+        if ((lane & 1) == 0) __hip_atomic_store((uint32_t *)out, h16 | (hn << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (a.fence) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (lane < 8) __hip_atomic_fetch_add(a.att_done + lane * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
         *out = (uint16_t)h16;
     }
@@ -1967,13 +2184,14 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
         // on lower-numbered blocks, so in-order dispatch needs no co-residency
         // for them)
         const int j = blockIdx.x - 512, nsp = a.grid_splits, nat = nsp * a.n_kv_head;   // grid_splits: this launch's splits
-        const int nfx = a.fx == 2 ? 4 * a.n_kv_head : a.fx ? a.n_kv_head : 0;
+        const int nfx = a.fx >= 2 ? 4 * a.n_kv_head : a.fx ? a.n_kv_head : 0;
         const int jf = j - nat - nfx - 1024 / OPROJ_ROWS;   // joined FFN block (after the o-proj blocks)
         if (a.ocnt && jf >= LFFN_NGU) ffn_dn_role<3072, 1>(d, fc, jf - LFFN_NGU, LFFN_NGU / 32);
         else if (a.ocnt && jf >= 0) ffn_gu_role<1024, LFFN_OPW>(g, d, fc, jf);
         else if (j >= nat + nfx) oproj1_body(o, a, j - nat - nfx);
         else if (j >= nat) {
             if (a.fx == 2) fx1_chain_w(a, j - nat);
+            else if (a.fx == 3) fx1_chain_1w(a, j - nat);
             else if (a.fx_pipe == 1) fx1_chain_pipe(a, j - nat);
             else fx1_chain_body(a, j - nat);
         }
@@ -2089,7 +2307,7 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     // from its granule, so the fused exact path needs the granule hand-off)
     // (fx_chain.h and the split weights' S: one chain chunk)
     if (a.fx && (!a.gran || !a.sgran || (a.fx_pipe != 1 && ns * spl1 > DX_KC) || (a.fx == 2 && !a.sstat))) return 0;
-    const int nfx = a.fx == 2 ? 4 * a.n_kv_head : a.fx ? a.n_kv_head : 0;   // (fx = 2: single-wave chain blocks, fx1_chain_w)
+    const int nfx = a.fx >= 2 ? 4 * a.n_kv_head : a.fx ? a.n_kv_head : 0;   // (fx = 2, 3: single-wave chain blocks)
     const int slots = spl1 == 128 ? cfg.slots_qkv128 : cfg.slots_qkv64;
     const int o_blocks = 1024 / OPROJ_ROWS;
     const bool fit_o = 512 + ns * a.n_kv_head + nfx + o_blocks <= slots;
@@ -2116,7 +2334,7 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     // fx_pipe: the chain starts on the first scores, so its V^T rows come from
     // the splits' pull (bit 0): the chain workgroup's own LDS-DMA pull (bit 1)
     // would sit in its vmcnt queue ahead of the chain's first loads
-    ad.fx_vpf = a.fx_pipe ? (cfg.fx_vpf | 1) & ~2 : cfg.fx_vpf;   // (fx_pipe 1 and 2)
+    ad.fx_vpf = a.fx_pipe == 1 || a.fx_pipe == 2 ? (cfg.fx_vpf | 1) & ~2 : cfg.fx_vpf;   // (fx_pipe 1 and 2)
     if (!with_o2) ad.att_done = nullptr;
     ad.ocnt = with_f ? fc->ocnt : nullptr;
     const GemvArgs qa = q;
@@ -2125,7 +2343,7 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     FfnCtl fa{};
     if (with_f) {
         fa = *fc;
-        fa.att_need = a.fx == 2 ? 4 * a.n_kv_head : a.n_kv_head;   // as the o-proj's wait
+        fa.att_need = a.fx >= 2 ? 4 * a.n_kv_head : a.n_kv_head;   // as the o-proj's wait
         fa.o_need = (unsigned)(o_blocks / 32);                     // o-proj arrivals per shard
         fa.gdelay = cfg.lffn_gdelay;
         fa.wdelay = cfg.lffn_wdelay;
