@@ -2287,9 +2287,13 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
     stamp_end(a.stamp);
 }
 
-// batch <= 8 key split: cfg 64 / 128, else 128 from 1k keys (half the
+// batch <= 8 key split: cfg 64 / 128, else 64 up to 1.9k keys and 128 beyond (half the
 // partials to combine, still >= 64 workgroups per 8 kv heads)
-static int split1(int spl1, int grid_splits) { return spl1 == 64 || spl1 == 128 ? spl1 : grid_splits >= 16 ? 128 : 64; }
+// (64-key splits up to 1.9k keys: with the fp16-V chain the split work is off the
+// critical path and more, shorter splits publish their scores sooner -- configs[1]
+// 256.2 -> 260.6 RTFx at ffn_wdelay 18, tools/r4/sweep.sh; past 1.9k keys the grid
+// would outgrow the co-resident slots)
+static int split1(int spl1, int grid_splits) { return spl1 == 64 || spl1 == 128 ? spl1 : grid_splits >= 30 ? 128 : 64; }
 
 int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s, bool dry,
                           const GemvArgs *gu, const GemvArgs *dn, const FfnCtl *fc) {

@@ -145,9 +145,11 @@ enum DevErr : unsigned {
 };
 struct FuseCfg {
     int ffn = 1, qkv = 1, o = 1;        // fused launches on/off
-    int ffn_delay = 4, ffn_wdelay = 14; // down blocks: first poll / weight request, s_sleep(8) units (~0.2 us)
-    int qkv_delay = 10, o_delay = 26;   // attention K/V request / o-proj weight request delays (o_delay re-swept in
-                                        // round 2, tools/experiments.sh delays: 20 -> 26, configs[1] decode 218.4 -> 212.4 ms)
+    int ffn_delay = 4, ffn_wdelay = 16; // down blocks: first poll / weight request, s_sleep(8) units (~0.2 us)
+    int qkv_delay = 10, o_delay = 32;   // attention K/V request / o-proj weight request delays (o_delay re-swept in
+                                        // round 2, tools/experiments.sh delays: 20 -> 26, configs[1] decode 218.4 -> 212.4 ms;
+                                        // round 4 with the fp16-V chain, tools/r4/sweep.sh on one box: ffn_wdelay 14 -> 16-18,
+                                        // o_delay 26 -> 30-38, 64-key splits to 1.9k keys: 248 -> 263 RTFx)
     int spl1 = 0;                       // batch-1 attention split: 0 = auto (64, or 128 from 1k keys)
     int poll_limit = 1 << 20;           // bounded waits: polls (s_sleep(4..8) apart) before giving up
     int fence = 0;                      // 1 = agent release before each arrival, acquire after each wait
