@@ -155,7 +155,11 @@ def test_full_lds_dma_gemm_bit_identical(full):
 
 
 FUSE_KNOBS = {"QASR_FUSE_FFN": dict(fuse_ffn=0), "QASR_FUSE_QKV": dict(fuse_qkv=0, fuse_o=0), "QASR_FUSE_O": dict(fuse_o=0),
-              "QASR_LFFN": dict(lffn=1)}   # (the joined FFN is an option: on against the default's off)
+              "QASR_LFFN": dict(lffn=1),   # (the joined FFN is an option: on against the default's off)
+              # single-wave chain blocks on the default weights path (option): the same bits.  (fx_pipe 1 and 2
+              # sum the softmax denominator S in another order -- per lane / per 32-key group -- so their logits
+              # differ from the default's in the last bits; each equals its own separate-launch path.)
+              "QASR_FX_PIPE3": dict(fx_pipe=3)}
 
 
 def _step_state(c, ids, feats, pos, tok=1234):
