@@ -7,15 +7,11 @@ run() {  # run TAG ENV...
     grep '^{' gpurun_out/sw.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag', d['value'], d['stage_ms_per_step_rank0']['decode'])"
 }
 run base QASR_X=0
-run q6 QASR_FUSE_DELAY=6
-run q8 QASR_FUSE_DELAY=8
-run q12 QASR_FUSE_DELAY=12
-run vpf0 QASR_FX_VPF=0
-run vpf1 QASR_FX_VPF=1
-run vpf3 QASR_FX_VPF=3
-run d2 QASR_FFN_DELAY=2
-run d6 QASR_FFN_DELAY=6
-run o28 QASR_FUSE_ODELAY=28
-run o36 QASR_FUSE_ODELAY=36
-run base2 QASR_X=0
+run lf QASR_LFFN=1
+run lfg10 QASR_LFFN=1 QASR_LFFN_GDELAY=10
+run lfg20 QASR_LFFN=1 QASR_LFFN_GDELAY=20
+run lfg45 QASR_LFFN=1 QASR_LFFN_GDELAY=45
+run lfw25 QASR_LFFN=1 QASR_LFFN_WDELAY=25
+run lfw55 QASR_LFFN=1 QASR_LFFN_WDELAY=55
+run lfg20w25 QASR_LFFN=1 QASR_LFFN_GDELAY=20 QASR_LFFN_WDELAY=25
 exit 0
