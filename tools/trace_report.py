@@ -9,7 +9,7 @@ NAMES = ["qkv_gemv", "attention", "oproj_gemv", "gateup_gemv", "down_gemv"]
 
 def main(path):
     t = np.fromfile(path, dtype=np.uint64).reshape(6, 4096, 8).astype(np.int64)
-    wide = (t[1][4020:4040, 0] > 0).any()   # fx_pipe = 2: 32 single-wave chain blocks, clocks at rows 4040 +
+    wide = (t[1][4040:4072, 0] > 0).any()   # fx_pipe 2, 3, 4: chain blocks c = 0 .. 31 at rows 4000 + c, clocks at 4040 + c
     ch = t[1][4000:4040] if wide else t[1][4000:4008]
     ch = ch[ch[:, 0] > 0]
     ck = (t[1][4040:4072] if wide else t[1][4010:4018]).copy()   # chain workgroups: shader clock at chain start / end, keys
