@@ -1442,7 +1442,7 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
         int ok = 0;
         for (int it = 0; it < a.poll_limit; it++) {
             if (__hip_atomic_load(a.att_done + (j & 7) * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                (unsigned)(a.fx >= 2 ? 4 * a.n_kv_head : a.n_kv_head)) {   // (fx = 2, 3, 4: one arrival per chain wave)
+                (unsigned)(a.fx >= 2 ? 4 * a.n_kv_head : a.n_kv_head)) {   // (fx = 2, 3: one arrival per chain wave)
                 ok = 1;
                 break;
             }
@@ -1524,9 +1524,9 @@ __device__ __forceinline__ void ld_sc1_x4_8(const void *base, const uint32_t *of
         : "memory");
 }
 // chain workgroups of the fused launch: fx 1 one a kv group (4 chain waves),
-// 2 and 3 four (single-wave chain blocks), 4 two (2 chain + 2 loader waves)
+// 2 and 3 four (single-wave chain blocks)
 __host__ __device__ inline int fx_chain_wgs(int fx, int n_kv_head) {
-    return fx == 4 ? 2 * n_kv_head : fx >= 2 ? 4 * n_kv_head : fx ? n_kv_head : 0;
+    return fx >= 2 ? 4 * n_kv_head : fx ? n_kv_head : 0;
 }
 // the chain roles' LDS (fx1_chain_body: both heads; fx1_chain_1w: row 0): a
 // layout of the fused launch's shared role buffer
@@ -1536,7 +1536,7 @@ struct alignas(16) ChainLds {
     float fwl[2];
 };
 // Phases (1) and (2) of a chain workgroup holding both query heads of kv group
-// g (fx1_chain_body, fx1_chain_ring): the score granules of both heads -> LDS,
+// g (fx1_chain_body): the score granules of both heads -> LDS,
 // then wave wid the weights of head wid / 2, half wid % 2 (C.fsc, C.kmask,
 // C.fwl); returns that head's S.  n: keys (<= DX_KC); trow: its trace row.
 __device__ __forceinline__ float fx1_gather_weights(const DecodeAttnArgs &a, const int g, const int n, ChainLds &C, const int trow) {
@@ -1798,167 +1798,6 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         }
         if (a.fence) __syncthreads();
         if (tid < 8) __hip_atomic_fetch_add(a.att_done + tid * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        *out = (uint16_t)h16;
-    }
-    mark(5);
-}
-
-// The chain role with loader waves (DecodeAttnArgs.fx == 4, option fx_pipe =
-// 4): 2 n_kv_head workgroups, c -> kv group g = c % n_kv_head, dimension half
-// h = c / n_kv_head (a group's two halves share an XCD, as its splits).  All
-// four waves gather both heads' scores and derive their weights exactly as
-// fx1_chain_body (fx1_gather_weights: the same bits); then waves 0 and 1 run
-// the chains of heads 2g and 2g + 1 over dimensions 64 h + lane with V^T read
-// from a two-slot LDS ring of 64-key buffers, which waves 2 and 3 fill (wave
-// 2 + (i & 1) writes buffer i into slot i & 1; two buffers a wave in flight in
-// registers, so the global loads run four buffers ahead), one s_barrier a
-// buffer.  The chain waves issue no global loads: the in-place chain's 1 KiB
-// V^T load per 8 keys cost ~4.7 of its 20 cycles a key (the
-// V-from-LDS diagnostic).  Barrier t (t = 0 .. nb): buffer t is in its slot
-// (the loader's ds_writes drained first); a chain wave reads buffer t + 1
-// right after barrier t + 1 and uses it after barrier t + 2, and its reads of
-// a slot are complete before the barrier after which a loader overwrites it
-// (LDS returns in order: the weight reads the chain waits on are issued after
-// them).  Trace rows 4000 + c, clocks 4040 + c (wave 0).
-struct alignas(16) RingLds {
-    ChainLds c;
-    u32x4 ring[2][DX_Q / 8][64];   // [slot][8-key block][lane]: the half's 64 dims x 8 keys a block, 1 KiB
-    float sh[2];                   // S of head 1 (from wave 2)
-};
-__device__ __forceinline__ void fx1_chain_ring(const DecodeAttnArgs &a, const int c, RingLds &R) {
-    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g = c % a.n_kv_head, h = c / a.n_kv_head;
-    const int loff = 8 * lane;
-    const uint16_t *vt = a.vt + (long)g * 128 * vt_ctx(a.max_ctx) + 64 * h * 8;   // batch 1: slot 0; the half's key block 0
-    auto mark = [&](int slot) {
-        if (a.trace && tid == 0) a.trace[(4000L + c) * 8 + slot] = rt_now();
-    };
-    mark(0);
-    const int pos = a.pos[0], n = pos + 1;
-    if (a.fx_vpf & 2) {   // V^T of this half -> L2 (wave w: key blocks w mod 4), drained by the gather's first poll
-        typedef __attribute__((address_space(3))) void lds_void_c;
-        typedef __attribute__((address_space(1))) void glb_void_c;
-        lds_void_c *dst = (lds_void_c *)((float *)R.c.fsc + wid * 256);
-        for (int kb = wid; kb * 8 < n; kb += 4)
-            __builtin_amdgcn_global_load_lds((glb_void_c *)(vt + (long)kb * 1024 + loff), dst, 16, 0, 0);
-    }
-    const float Sw = fx1_gather_weights(a, g, n, R.c, 4000 + c);   // S of head wid / 2
-    mark(3);
-    const int nl = n - 1, nb = (nl + DX_Q - 1) / DX_Q;   // keys 0 .. n - 2 from the cache, in nb buffers
-    const int lastb = nl > 0 ? (nl - 1) >> 3 : 0;
-    if (wid >= 2) {   // loader L = wid - 2: buffers L, L + 2, ... (r0 / r1 in turn)
-        if (wid == 2 && lane == 0) R.sh[1] = Sw;   // (drained by the first barrier)
-        // L static and every write unconditional (buffer nb: a slot no chain
-        // wave takes again), so the wait before a write is on its own buffer's
-        // eight loads only (a conditional write left vmcnt(0) at the merges)
-        auto loader = [&](auto lc) {
-            constexpr int L = decltype(lc)::value;
-            u32x4 r0[DX_Q / 8], r1[DX_Q / 8];
-            fx_loadQ(r0, vt, loff, L * DX_Q, lastb);
-            fx_loadQ(r1, vt, loff, (L + 2) * DX_Q, lastb);
-            u32x4 *const slot = &R.ring[L][0][lane];
-            unsigned long long lw = 0;   // (trace) cycles from a write's start to its reloads issued
-            for (int t0 = 0;; t0 += 4) {
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int t = t0 + u;
-                    if (t > nb) {   // past the last barrier
-                        if (a.trace && lane == 0) a.trace[(4040L + c) * 8 + 5 + L] = lw;
-                        return;
-                    }
-                    if ((u & 1) == L) {
-                        const unsigned long long tw = a.trace ? clock64() : 0ull;
-                        u32x4 *rr = (u >> 1) ? r1 : r0;
-#pragma unroll
-                        for (int k = 0; k < DX_Q / 8; k++) slot[64 * k] = rr[k];
-                        fx_loadQ(rr, vt, loff, (t + 4) * DX_Q, lastb);   // (past the sequence: re-reads of its last block)
-                        if (a.trace) lw += clock64() - tw;
-                    }
-                    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                }
-            }
-        };
-        if (wid == 2) loader(std::integral_constant<int, 0>{});
-        else loader(std::integral_constant<int, 1>{});
-        return;
-    }
-    // chain wave: head 2g + wid, dimension 64 h + lane
-    const int hh = wid, d = 64 * h + lane;
-    const float *const ws = R.c.fsc[hh];
-    const uint16_t *const km = R.c.kmask[hh];
-    const uint32_t tag = gran_tag(pos, a.layer);
-    uint16_t vnew = 0;
-    {   // the new key's v: its QKV granule (fx1_chain_body)
-        const unsigned long long *gp = a.gran + a.n_head * 128 + a.n_kv_head * 128 + g * 128 + d;
-        unsigned long long v = 0;
-        bool ok = false;
-        for (int it = 0; it < a.poll_limit; it++) {
-            v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ok = (uint32_t)(v >> 32) == tag;
-            if (__all(ok)) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_QKV_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        vnew = f_to_u16(__uint_as_float((uint32_t)v));
-    }
-    mark(1);
-    const unsigned long long ck0 = a.trace ? clock64() : 0ull;
-    auto rd = [&](u32x4 *v, int sl) {
-#pragma unroll
-        for (int k = 0; k < DX_Q / 8; k++) v[k] = R.ring[sl][k][lane];
-    };
-    unsigned long long bw = 0;   // (trace) cycles this chain wave spent at its barriers
-    auto bar = [&]() {
-        if (a.trace) {
-            const unsigned long long tb = clock64();
-            asm volatile("s_barrier" ::: "memory");
-            bw += clock64() - tb;
-        } else {
-            asm volatile("s_barrier" ::: "memory");
-        }
-    };
-    f16 acc = 0;
-    bar();   // barrier 0: buffer 0 and sh
-    const float S = hh ? R.sh[1] : Sw;
-    {
-        u32x4 va[DX_Q / 8], vb[DX_Q / 8];
-        floatx4 wa, wb;
-        rd(va, 0);
-        fx_w8(ws, 0, wa, wb);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // buffer 0 read before barrier 1 (nothing ran in between)
-        for (int i = 0; i < nb; i += 2) {
-            bar();   // barrier i + 1
-            rd(vb, 1);
-            fx_step1_lds_m(va, i * DX_Q, ws, fx_mask64(km, i * DX_Q), acc, wa, wb);
-            if (i + 1 >= nb) break;
-            bar();   // barrier i + 2
-            rd(va, 0);
-            fx_step1_lds_m(vb, (i + 1) * DX_Q, ws, fx_mask64(km, (i + 1) * DX_Q), acc, wa, wb);
-        }
-        acc = fx_key_slow(acc, vnew, R.c.fwl[hh]);
-    }
-    mark(4);
-    if (a.trace && lane == 0) {   // wave 0: chain clocks; each chain wave its barrier cycles (cols 3, 4), loaders 5, 6
-        if (wid == 0) {
-            a.trace[(4040L + c) * 8 + 0] = ck0;
-            a.trace[(4040L + c) * 8 + 1] = clock64();
-            a.trace[(4040L + c) * 8 + 2] = (unsigned long long)n;
-        }
-        a.trace[(4040L + c) * 8 + 3 + wid] = bw;
-    }
-    const float ov = (float)acc * (S == 0.0f ? 0.0f : 1.0f / S);   // ggml: VKQ32 = fp32(VKQ16) * (1 / S)
-    const uint32_t h16 = f_to_u16(ov);
-    const uint32_t hn = __shfl_xor(h16, 1, 64);
-    uint16_t *out = a.out + (2 * g + hh) * 128 + d;
-    if (a.att_done) {   // write-through pairs, drained, one arrival per replica from each chain wave
-        if ((lane & 1) == 0) __hip_atomic_store((uint32_t *)out, h16 | (hn << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (a.fence) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (lane < 8) __hip_atomic_fetch_add(a.att_done + lane * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
         *out = (uint16_t)h16;
     }
@@ -2377,7 +2216,7 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
     constexpr int K = 1024, NT = 2, RPW = 2;
     // one LDS buffer for the roles that need one (a workgroup takes one role):
     // the split and chain layouts overlap instead of adding up
-    constexpr size_t RLB = sizeof(SplitLds<SPL>) > sizeof(RingLds) ? sizeof(SplitLds<SPL>) : sizeof(RingLds);   // (RingLds holds ChainLds)
+    constexpr size_t RLB = sizeof(SplitLds<SPL>) > sizeof(ChainLds) ? sizeof(SplitLds<SPL>) : sizeof(ChainLds);
     __shared__ __attribute__((aligned(16))) unsigned char role_lds[RLB];
     stamp_start(a.stamp);
     if (blockIdx.x >= 512) {
@@ -2396,7 +2235,6 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
         else if (j >= nat) {
             if (a.fx == 2) fx1_chain_w(a, j - nat);
             else if (a.fx == 3) fx1_chain_1w(a, j - nat, *reinterpret_cast<ChainLds *>(role_lds));
-            else if (a.fx == 4) fx1_chain_ring(a, j - nat, *reinterpret_cast<RingLds *>(role_lds));
             else if (a.fx_pipe == 1) fx1_chain_pipe(a, j - nat);
             else fx1_chain_body(a, j - nat, *reinterpret_cast<ChainLds *>(role_lds));
         }

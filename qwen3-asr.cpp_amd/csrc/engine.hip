@@ -1307,9 +1307,8 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             if (l + 1 < nl) { da.pf_ptr[2] = m->dec[l + 1].wqkv; da.pf_kib[2] = (unsigned)((size_t)(QD + 2 * KD) * H * 2 / 1024); }
         }
         if (fusable && exact && c->fuse.gran) {   // ggml's attention numerics as the fused launch's chain role
-            da.fx = c->fuse.fx_pipe >= 2 && c->fuse.fx_pipe <= 4 ? c->fuse.fx_pipe : 1;   // 2: the splits derive the weights
-                                                    // (attention.hip split_weights); 3: single-wave chain blocks;
-                                                    // 4: chain waves fed by loader waves through LDS
+            da.fx = c->fuse.fx_pipe == 2 ? 2 : c->fuse.fx_pipe == 3 ? 3 : 1;   // 2: the splits derive the weights
+                                                    // (attention.hip split_weights); 3: single-wave chain blocks
             da.sstat = c->d_sstat;
             da.sgran = c->d_sgran;
             da.gran = c->d_gran;   // (the fused decision needs the granule hand-off)

@@ -186,7 +186,7 @@ struct FuseCfg {
     int fx_pipe = 0;                    // exact decode chains: 1 = weights one 64-key buffer ahead, SGPR operands (fx_pipe.h);
                                         // 2 = batch 1 fused: the splits compute the weights (split_weights), the chain
                                         // role reads them (fx1_chain_w); 3 = single-wave chain blocks (fx1_chain_1w);
-                                        // 4 = chain waves fed V^T through LDS by loader waves (fx1_chain_ring); other paths as 0
+                                        // other paths as 0
     unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
 };
 // co-resident workgroup capacity of the fused kernels on the current device

@@ -1,4 +1,5 @@
 # the loader-ring chain (fx_pipe 4): bit-identity, layer-14 device trace, configs[1] A/B
+# (fx_pipe 4 = the loader-ring chain of commit 34c4760, removed after this measurement)
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_full.py -k "fused_launches_match_separate and (FX_PIPE4 or FX_PIPE3)" > gpurun_out/ring_t.log 2>&1 || { tail -30 gpurun_out/ring_t.log; exit 1; }
