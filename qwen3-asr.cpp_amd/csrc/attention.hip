@@ -1770,18 +1770,14 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         acc = fx_key_slow(acc, vnew, fwl[hh]);
     }
     mark(4);
+    if (a.trace && lane == 0) {   // every wave: its chain's end (100 MHz) and shader cycles, rows 4020 + g, 4030 + g
+        a.trace[(4020L + g) * 8 + wid] = rt_now();
+        a.trace[(4030L + g) * 8 + wid] = clock64() - ck0;
+    }
     if (a.trace && tid == 0) {
         a.trace[(4010L + g) * 8 + 0] = ck0;
         a.trace[(4010L + g) * 8 + 1] = clock64();
         a.trace[(4010L + g) * 8 + 2] = (unsigned long long)n;
-        unsigned nk = 0, ng = 0;   // head 2g's new-maximum keys and slow 8-key groups
-        for (int i = 0; i < DX_KC / 16; i++) {
-            const unsigned m = kmask[0][i];
-            nk += __builtin_popcount(m);
-            ng += ((m & 0xffu) != 0) + ((m >> 8) != 0);
-        }
-        a.trace[(4010L + g) * 8 + 3] = nk;
-        a.trace[(4010L + g) * 8 + 4] = ng;
     }
     // ggml: VKQ32 = fp32(VKQ16) * (1 / S); fp16 for the o-projection
     const float ov = (float)acc * (S == 0.0f ? 0.0f : 1.0f / S);
@@ -1802,6 +1798,16 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         *out = (uint16_t)h16;
     }
     mark(5);
+    if (a.trace && tid == 0) {   // (after the hand-off: one thread's 128 LDS reads took ~5 us before it)
+        unsigned nk = 0, ng = 0;   // head 2g's new-maximum keys and slow 8-key groups
+        for (int i = 0; i < DX_KC / 16; i++) {
+            const unsigned m = kmask[0][i];
+            nk += __builtin_popcount(m);
+            ng += ((m & 0xffu) != 0) + ((m >> 8) != 0);
+        }
+        a.trace[(4010L + g) * 8 + 3] = nk;
+        a.trace[(4010L + g) * 8 + 4] = ng;
+    }
 }
 
 // The chain role with one wave a workgroup (DecodeAttnArgs.fx == 3, option
