@@ -1413,6 +1413,26 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
     constexpr int K = 2048, NT = 4, NOB = 1024 / OPROJ_ROWS;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int row0 = j * OPROJ_ROWS + wid * ORPW;
+    __shared__ __attribute__((aligned(16))) float pfbuf[256];
+    typedef __attribute__((address_space(3))) void lds_void_p;
+    typedef __attribute__((address_space(1))) void glb_void_p;
+    if ((a.fx_vpf & 4) && a.fx) {
+        // (fx_vpf bit 2) the V^T rows of the kv group whose chain workgroup
+        // shares this block's XCD (blocks b and b + 8 do under round-robin
+        // placement; speed only) -> that L2, in place of the chain's own pull
+        // (whose loads its score poll waited behind): the XCD's NOB / 8 blocks
+        // split the group's 1 KiB pieces (dimension half, 8-key block), into
+        // pfbuf as the weight pulls below
+        const int nfx = a.fx >= 2 ? 4 * a.n_kv_head : a.n_kv_head;
+        const int gg = (nfx + j) & 7, nkv = a.pos[0] + 1;
+        if (gg < a.n_kv_head) {
+            const uint16_t *vtg = a.vt + (long)gg * 128 * vt_ctx(a.max_ctx);
+            const int np = 2 * ((nkv + 7) >> 3);
+            for (int p = (j >> 3) * 4 + wid; p < np; p += 4 * (NOB / 8))
+                __builtin_amdgcn_global_load_lds((glb_void_p *)(vtg + (p & 1) * 512 + (long)(p >> 1) * 1024 + lane * 8),
+                                                 (lds_void_p *)pfbuf, 16, 0, 0);
+        }
+    }
     for (int i = 0; i < a.oproj_delay; i++) __builtin_amdgcn_s_sleep(8);
     half8 wv[ORPW][NT];
 #pragma unroll
@@ -1425,10 +1445,7 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
     // pieces of 1 KiB (nt) into pfbuf, contents unused (every wave's pieces
     // land on the same 1 KiB: the blocks a CU holds keep within the LDS);
     // wave w of the 4 NOB takes pieces w, w + 4 NOB, ...
-    __shared__ __attribute__((aligned(16))) float pfbuf[256];
     {
-        typedef __attribute__((address_space(3))) void lds_void_p;
-        typedef __attribute__((address_space(1))) void glb_void_p;
         const int w = j * 4 + wid;
 #pragma unroll
         for (int r = 0; r < 3; r++) {
@@ -1561,7 +1578,10 @@ __device__ __forceinline__ float fx1_gather_weights(const DecodeAttnArgs &a, con
         }
         u32x4 gv[DX_KC / 256];
         bool ok = false;
-        for (int it = 0; it < a.poll_limit; it++) {
+        int it = 0;
+        unsigned long long tis = 0;   // (trace) the last poll's issue time
+        for (; it < a.poll_limit; it++) {
+            if (a.trace) tis = rt_now();
             ld_sc1_x4_8(gb, go, gv);
             ok = true;
 #pragma unroll
@@ -1571,6 +1591,10 @@ __device__ __forceinline__ float fx1_gather_weights(const DecodeAttnArgs &a, con
             }
             if (__syncthreads_and(ok)) break;
             __builtin_amdgcn_s_sleep(2);
+        }
+        if (a.trace && tid == 0) {   // rows 4010 + g: polls, the successful poll's issue time
+            a.trace[(4010L + g) * 8 + 5] = (unsigned long long)it + 1;
+            a.trace[(4010L + g) * 8 + 6] = tis;
         }
         if (!ok && tid == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_SCORE_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll

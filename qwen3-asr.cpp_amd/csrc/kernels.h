@@ -337,7 +337,8 @@ struct DecodeAttnArgs {
     unsigned long long *sgran;           // row stride sgran_ld(max_ctx) (16-B aligned granule pairs)
     int fx_delay;                        // chain workgroups: first score poll after fx_delay x ~0.2 us
     int fx_vpf;                          // bit 0: the splits pull their keys' V^T rows into their XCD's L2 for the
-                                         // chain; bit 1: the chain workgroups pull their own (LDS-DMA, while waiting)
+                                         // chain; bit 1: the chain workgroups pull their own (LDS-DMA, while waiting);
+                                         // bit 2: the o-proj blocks of the chain's XCD pull them (oproj1_body)
     unsigned long long *sstat;           // fx = 2: the splits' maxima and 32-key group S sums, [n_head][192] granules
     int fx_pipe;                         // every exact decode chain derives its weights one 64-key buffer ahead
                                          // (fx_pipe.h; FuseCfg::fx_pipe) instead of all of them first (fx_chain.h)

@@ -13,3 +13,6 @@ for g in range(8):
     cyc = t[4030 + g, :4] / n
     print(f"g {g}: chain end per wave " + " ".join(f"{e:6.2f}" for e in ends) + " us;  cycles a key " +
           " ".join(f"{c:5.1f}" for c in cyc) + f";  published {(t[4000 + g, 5] - st) / 100.0:6.2f}")
+    if t[4010 + g, 6]:
+        print(f"      gather: {t[4010 + g, 5]} polls, the last issued at {(t[4010 + g, 6] - st) / 100.0:6.2f} us, "
+              f"gathered at {(t[4000 + g, 2] - st) / 100.0:6.2f} us")
