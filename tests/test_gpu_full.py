@@ -159,7 +159,8 @@ FUSE_KNOBS = {"QASR_FUSE_FFN": dict(fuse_ffn=0), "QASR_FUSE_QKV": dict(fuse_qkv=
               # single-wave chain blocks on the default weights path (option): the same bits.  (fx_pipe 1 and 2
               # sum the softmax denominator S in another order -- per lane / per 32-key group -- so their logits
               # differ from the default's in the last bits; each equals its own separate-launch path.)
-              "QASR_FX_PIPE3": dict(fx_pipe=3)}
+              "QASR_FX_PIPE3": dict(fx_pipe=3),
+              "QASR_FX_VPF4": dict(fx_vpf=4)}   # the chain's V^T pulled by the o-proj blocks (option): a prefetch only
 
 
 def _step_state(c, ids, feats, pos, tok=1234):
