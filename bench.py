@@ -73,6 +73,13 @@ def parse():
                     help="--pipeline align with --utterances: rank 0 writes its shortest utterance's id, transcript and "
                          "aligner document from the last timed pass to this JSON file (tests/test_gpu_api.py checks it "
                          "against the oracle)")
+    ap.add_argument("--set-utterances", type=int, default=1000,
+                    help="the default run's utterance_set leg (configs[3], SURVEY.md §8(d)): N fixed-length utterances "
+                         "through the dynamic queue into each GPU's continuous-batching stream, strong scaling over the "
+                         "ranks (0: skip)")
+    ap.add_argument("--set-seconds", type=float, default=30.0)
+    ap.add_argument("--set-pool", type=int, default=128, help="distinct seeded clips staged per GPU (utterance i = clip i mod pool)")
+    ap.add_argument("--set-slots", type=int, default=64, help="continuous-batching slots per GPU")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous check without a GPU: ranks join a gloo group, time a barrier and rank 0 "
                          "prints the JSON line with value 0 (tests/test_dist.py)")
@@ -150,14 +157,29 @@ def dry_run(args, world: int, rank: int) -> None:
         dist.destroy_process_group()
 
 
-def synthetic_model(rank: int, config: str = "full", wtype: int = 1) -> str:
-    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"qasr_synth_{config}_{'q8_0' if wtype == 8 else 'f16'}.gguf")
+def synthetic_model(rank: int, config: str = "full", wtype: int = 1, seed: int = 42) -> str:
+    """The synthetic GGUF, written once per host by rank 0 and shared.  The
+    cache is keyed on everything the file depends on -- config, weight type,
+    seed and the writer's output version (qasr_synthetic_gguf_version) -- and
+    the marker records the file's size, so neither a file of an older writer
+    nor a torn write is ever reused."""
+    ver = int(qasr.lib().qasr_synthetic_gguf_version())
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"),
+                        f"qasr_synth_{config}_{'q8_0' if wtype == 8 else 'f16'}_s{seed}_w{ver}.gguf")
     lock = path + ".done"
-    if rank == 0 and not os.path.exists(lock):
-        qasr.write_synthetic_gguf(path + ".tmp", config, 42, wtype)
+
+    def valid():
+        try:
+            return os.path.exists(path) and int(open(lock).read().strip()) == os.path.getsize(path)
+        except (OSError, ValueError):
+            return False
+    if rank == 0 and not valid():
+        qasr.write_synthetic_gguf(path + ".tmp", config, seed, wtype)
         os.replace(path + ".tmp", path)
-        open(lock, "w").close()
-    while not os.path.exists(lock):
+        with open(lock + ".tmp", "w") as f:
+            f.write(str(os.path.getsize(path)))
+        os.replace(lock + ".tmp", lock)
+    while not valid():
         time.sleep(0.5)
     return path
 
@@ -520,6 +542,71 @@ def utterance_main(args, m, rank, local, world, dist, model_path):
     print(json.dumps(out), flush=True)
 
 
+def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
+    """configs[3] inside the default run (1000 x 30 s f16
+    utterances; north_star's "throughput on synthetic 30 s / 16 kHz audio at
+    1, 2, 4 and 8 GPUs"): every rank stages a pool of distinct seeded 30 s
+    clips in HBM (utterance i = pool clip i mod pool; the engine processes each
+    utterance in full -- nothing is cached across them), then one shared
+    longest-first queue in the process group's TCPStore feeds each rank's
+    continuous-batching stream (qasr_run_stream_staged, --set-slots slots):
+    strong scaling, the set is fixed whatever N is.  One warm-up pass over a
+    subset (graph capture), then one timed pass: barrier -> streams -> barrier,
+    wall = max over ranks; each rank's own stream time and utterance count are
+    gathered for the tail imbalance.  Budget ceil(3.5 tok/s x 30 s) = 105
+    tokens a clip, EOS ignored (every budget is asserted)."""
+    import concurrent.futures as cf
+
+    import qasr_dist as qd
+    n_utt, secs = args.set_utterances, args.set_seconds
+    ns = int(round(secs * 100)) * 160
+    utts = [(50000 + i, ns) for i in range(n_utt)]
+    bud = qd.budget(ns, args.tok_rate)
+    P = qasr.lib().qasr_prompt_len(qasr.encoder_frames(qasr.mel_frames(ns)))
+    ctx = qasr.Context(m, max_batch=args.set_slots, max_ctx=P + bud + 8)
+    pool = min(args.set_pool, n_utt)
+    with cf.ThreadPoolExecutor(16) as ex:   # (ctypes releases the GIL: the C synthesiser runs in parallel)
+        pcm = list(ex.map(lambda i: qasr.synth_pcm(utts[i][0], ns), range(pool)))
+    ctx.stage_audio(pcm)
+    stats = []
+
+    def stream(next_clip):
+        out, st = ctx.run_stream_staged(next_clip, bud, ignore_eos=True, slots=args.set_slots)
+        bad = [i for i, t in out.items() if isinstance(t, Exception)]
+        assert not bad, (bad[:4], out[bad[0]] if bad else None)
+        stats.append(st)
+        return out
+    dev = f"cuda:{local}" if dist else None
+    warm = utts[:min(n_utt, 2 * args.set_slots * world)]
+    qd.run_queue(stream, warm, rank, world, args.tok_rate, dist, dev, key="utt_set_warm")
+    stats.clear()
+    res = qd.run_queue(stream, utts, rank, world, args.tok_rate, dist, dev, key="utt_set_timed")
+    ctx.close()
+    if rank != 0:
+        return {}
+    toks = res["tokens"]
+    assert len(toks) == n_utt and all(len(t) == bud for t in toks.values()), "utterance set: a budget was not met"
+    walls = res["rank_wall_s"]
+    st = stats[0]
+    return {
+        "workload": f"configs[3]: {n_utt} x {secs:g} s utterances (16 kHz, a pool of {pool} distinct seeded clips per "
+                    f"GPU), one shared longest-first queue feeding {args.set_slots} continuous-batching slots per GPU, "
+                    f"greedy budget {bud} tokens (3.5 tok/s), EOS ignored",
+        "scaling": "strong", "n_gpus": world, "utterances": n_utt, "audio_s": res["audio_s"],
+        "value": round(res["audio_s"] / res["wall_s"], 3), "unit": "audio-sec/wall-sec",
+        "wall_s": round(res["wall_s"], 4),
+        "decode_tokens_per_s": round(res["decode_tokens"] / res["wall_s"], 2),
+        "per_rank_wall_s": [round(w, 4) for w in walls],
+        "per_rank_utterances": [int(u) for u in res["rank_utterances"]],
+        "tail_imbalance": round((max(walls) - min(walls)) / max(walls), 4) if max(walls) > 0 else 0.0,
+        "rank0_stream": {"clips": st.n_clips, "refill_prefills": st.n_prefills, "decode_steps": st.n_steps,
+                         "slot_utilisation": round(st.live_steps / max(1, st.slot_steps), 4),
+                         "prefill_ms": round(st.t_prefill_ms, 1), "decode_ms": round(st.t_decode_ms, 1)},
+        "collectives": "barrier + max wall time + all_gather of per-rank times and token ids (RCCL); the queue is a "
+                       "TCPStore counter (one add per utterance)",
+    }
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
@@ -527,8 +614,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus is not None and args.gpus != world:
-        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    # --gpus counts this node's GPUs: under a multi-node launcher that is LOCAL_WORLD_SIZE, not WORLD_SIZE
+    node = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if args.gpus is not None and args.gpus != node:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but this node runs {node} ranks (LOCAL_WORLD_SIZE / WORLD_SIZE)")
     if args.dry_run:
         dry_run(args, world, rank)
         return
@@ -617,6 +706,7 @@ def main():
             extra[kind] = (*ctx.get_probe(), *ctx.get_probe_device())
         ctx.set_probe(0)
     assert all(len(x) == ntok for x in res.tokens), "decode budget not met"
+    uset = utterance_set_leg(args, m, rank, local, world, dist) if args.set_utterances > 0 and not actx else None
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -670,6 +760,8 @@ def main():
         db = decode_bytes(m.hp, args.q8, args.batch, P, ntok)
         out["decode_hbm"] = {"achieved": round(db / dec_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(db / dec_s / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_step": db}
+    if uset:
+        out["utterance_set"] = uset
     if N == 1 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(model_path, args.cpu_sample_seconds, args.tok_rate, args.cpu_threads,
                                            args.seconds, ntok)

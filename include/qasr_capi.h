@@ -203,8 +203,9 @@ typedef struct {
 int qasr_run_stream(qasr_ctx *c, int slots, qasr_fetch_fn fetch, qasr_sink_fn sink, void *user, int max_tokens, int ignore_eos,
                     qasr_stream_stats *stats);
 /* The same over the staged pool (qasr_stage_audio; inputs already in HBM):
- * fetch(user, &max_tokens) returns the next staged clip's index, which is
- * also its id for sink, or < 0 when the queue is empty. */
+ * fetch(user, &max_tokens) returns the next clip's id (>= 0), or < 0 when the
+ * queue is empty; the clip is staged clip id % (pool size), so an utterance
+ * set larger than the pool reuses its clips, each under its own id. */
 typedef int (*qasr_fetch_staged_fn)(void *user, int *max_tokens);
 int qasr_run_stream_staged(qasr_ctx *c, int slots, qasr_fetch_staged_fn fetch, qasr_sink_fn sink, void *user,
                            int max_tokens, int ignore_eos, qasr_stream_stats *stats);
@@ -323,6 +324,9 @@ int qasr_synth_pcm(uint64_t seed, int n_samples, float *out);
  * config: "full" (Qwen3-ASR-0.6B dims) or "tiny" (test dims);
  * wtype: 1 = f16, 8 = q8_0 for linear weights. */
 int qasr_write_synthetic_gguf(const char *path, const char *config, uint64_t seed, int wtype);
+/* version of that writer's output: bumped whenever the file it writes for a
+ * given (config, seed, wtype) changes, so a cached synthetic model is keyed on it */
+int qasr_synthetic_gguf_version(void);
 
 #ifdef __cplusplus
 }

@@ -91,6 +91,62 @@ float qo_f16_to_f32(uint16_t h) {
 
 static inline float round_f16(float x) { return qo_f16_to_f32(qo_f32_to_f16(x)); }
 
+/* ggml_vec_mad_f16's per-element step on F16C (x86): fp16(fmaf(x, v, y)) --
+ * the fma rounded to fp32, then RNE to fp16 (two roundings) */
+uint16_t qo_f16_mad_round2(uint16_t x, float v, uint16_t y) {
+    return qo_f32_to_f16(fmaf(qo_f16_to_f32(x), v, qo_f16_to_f32(y)));
+}
+
+/* the same step rounded ONCE: RNE to fp16 of the exact x * v + y (QO_FA_V_ROUND1;
+ * what a fused mixed-precision fma with an fp16 result computes).  x * v is
+ * exact in double (11 + 24 significant bits); TwoSum gives the double sum's
+ * error; the sum is then rounded to odd at fp32 precision (24 >= 11 + 2 bits,
+ * so the final RNE to fp16 equals RNE of the exact value) */
+/* f (finite) lies exactly half-way between two adjacent fp16 values */
+static int f16_midpoint(float f) {
+    uint32_t x;
+    memcpy(&x, &f, 4);
+    const uint32_t ax = x & 0x7fffffffu;
+    if (ax >= 0x477ff000u) return 0;                        /* rounds to inf */
+    if (ax >= 0x38800000u) return (ax & 0x1fffu) == 0x1000u;  /* normal fp16 range */
+    if (ax < 0x33000000u) return 0;
+    if (ax == 0x33000000u) return 1;                        /* 2^-25 */
+    const uint32_t sh = 126u - (ax >> 23);
+    const uint32_t mant = (ax & 0x7fffffu) | 0x800000u;
+    return (mant & ((1u << sh) - 1u)) == (1u << (sh - 1));
+}
+
+uint16_t qo_f16_mad_round1(uint16_t x, float v, uint16_t y) {
+    const double p = (double)qo_f16_to_f32(x) * (double)v;
+    const double a = qo_f16_to_f32(y);
+    const double s = p + a;
+    if (!isfinite(s)) return qo_f32_to_f16((float)s);
+    float f = (float)s;
+    /* rounding is monotone and fp16 midpoints are fp32 values: RNE16(RN24(RN53(exact)))
+     * errs only where the intermediate lands exactly on a midpoint the exact value is not */
+    if (!f16_midpoint(f)) return qo_f32_to_f16(f);
+    const double bp = s - a;
+    const double e = (p - bp) + (a - (s - bp));   /* s + e == p + a exactly */
+    if (e != 0.0 || (double)f != s) {
+        /* exact value strictly between two adjacent floats lo < hi: take the odd one */
+        float lo, hi;
+        if ((double)f == s) {
+            lo = e > 0 ? f : nextafterf(f, -INFINITY);
+            hi = e > 0 ? nextafterf(f, INFINITY) : f;
+        } else if ((double)f < s) {
+            lo = f;
+            hi = nextafterf(f, INFINITY);
+        } else {
+            lo = nextafterf(f, -INFINITY);
+            hi = f;
+        }
+        uint32_t bl;
+        memcpy(&bl, &lo, 4);
+        f = (bl & 1u) ? lo : hi;
+    }
+    return qo_f32_to_f16(f);
+}
+
 /* ======================================================================
  * Mel front-end
  * ====================================================================== */
@@ -280,7 +336,12 @@ static void vec_mad_f16(uint16_t *y, const uint16_t *x, int n, float v) {
         _mm_storeu_si128((__m128i *)(y + i), _mm256_cvtps_ph(_mm256_fmadd_ps(b, vv, a), _MM_FROUND_TO_NEAREST_INT));
     }
 #endif
-    for (; i < n; i++) y[i] = qo_f32_to_f16(fmaf(qo_f16_to_f32(x[i]), v, qo_f16_to_f32(y[i])));
+    for (; i < n; i++) y[i] = qo_f16_mad_round2(x[i], v, y[i]);
+}
+
+/* QO_FA_V_ROUND1: vec_mad_f16 with one rounding per element */
+static void vec_mad_f16_round1(uint16_t *y, const uint16_t *x, int n, float v) {
+    for (int i = 0; i < n; i++) y[i] = qo_f16_mad_round1(x[i], v, y[i]);
 }
 
 /* ggml_vec_scale_f16: y = fp16(y * v) */
@@ -802,6 +863,7 @@ static float *dec_stack(qo_dec *dd, const int32_t *tokens, int n_tokens, const f
                         vs = expf(s - M);
                     }
                     if (dd->flags & QO_FA_V_F32) for (int d = 0; d < HD; d++) acc32[d] += qo_f16_to_f32(vr[d]) * vs;
+                    else if (dd->flags & QO_FA_V_ROUND1) vec_mad_f16_round1(acc16, vr, HD, vs);
                     else vec_mad_f16(acc16, vr, HD, vs);
                     S = S * ms + vs;
                 }

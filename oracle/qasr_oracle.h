@@ -94,6 +94,14 @@ typedef struct {
 /* numerics switches ("switches for (iii) and (viii)") */
 #define QO_GELU_EXACT   1   /* tanh-GELU in fp32 instead of ggml's fp16 LUT   */
 #define QO_FA_V_F32     2   /* fp32 V accumulation instead of ggml's fp16 one */
+#define QO_FA_V_ROUND1  4   /* fp16 V accumulation, each key's fma rounded once
+                               (fp16 of the exact v*vs + acc) instead of ggml's
+                               x86 fp32-fma-then-fp16; the scale by ms unchanged */
+
+/* the V-accumulator step: ggml (F16C) fp16(fmaf(x, v, y)), and the single-
+ * rounding variant of QO_FA_V_ROUND1 (fp16 RNE of the exact x * v + y) */
+uint16_t qo_f16_mad_round2(uint16_t x, float v, uint16_t y);
+uint16_t qo_f16_mad_round1(uint16_t x, float v, uint16_t y);
 
 /* ---------------- fp16 helpers (ggml_compute_fp32_to_fp16, RNE) -------- */
 uint16_t qo_f32_to_f16(float f);

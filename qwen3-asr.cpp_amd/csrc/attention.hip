@@ -21,9 +21,7 @@
 
 #include "dev_common.h"
 #include "fx_chain.h"
-#include "fx_pipe.h"
 #include "fx_decode.h"
-#include "ffn_roles.h"
 #include "kernels.h"
 
 namespace qasr {
@@ -667,87 +665,6 @@ __device__ __forceinline__ half8 kv_load(const uint16_t *p, int nt) {
     return nt ? __builtin_nontemporal_load((const half8 *)p) : *(const half8 *)p;
 }
 
-// Exact decode attention with the weights computed by the splits (a.fx = 2,
-// option fx_pipe = 2): split sp of head 2g + hh holds its keys' scaled scores
-// (scr, -inf past the context).  It publishes its maximum, takes the earlier
-// splits' maxima (the running maximum before its first key: a bounded poll;
-// every split of the launch is co-resident), derives its keys' weights --
-// fx_weights_reg's values, signed the same way (w = vs, or -ms at a new
-// maximum) -- and publishes them as {fp32, tag} granules in place of the
-// scores, so the chain workgroup starts on the first 64 keys' weights with no
-// gather or weight pass of its own.  S: fx_weights_reg's per-lane sequence
-// (a lane = 32 keys) for this split's 32-key groups, published as {S, running
-// maximum at the group's end}; the chain sums them as fx_weights_reg does, so
-// fused and separate launches stay bit-identical.
-#define SS_LD 192   // a.sstat per head: [0, 64) split maxima; [64 + 2q], [65 + 2q]: 32-key group q's (S, running max)
-template <int SPL>
-__device__ __forceinline__ void split_weights(const DecodeAttnArgs &a, const float *scr, int g, int hh, int sp, int k0, int k1,
-                                              int pos) {
-    __shared__ float wsh[2][SPL];
-    __shared__ float gmx[2][SPL / 32];
-    const int lane = threadIdx.x & 63;
-    const uint32_t tag = gran_tag(pos, a.layer);
-    const long head = 2 * g + hh;
-    unsigned long long *st = a.sstat + head * SS_LD;
-    auto gran = [&](float v) { return ((unsigned long long)tag << 32) | __float_as_uint(v); };
-    float sv[SPL / 64];
-    float m = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < SPL / 64; i++) {
-        sv[i] = scr[64 * i + lane];
-        m = fmaxf(m, sv[i]);
-    }
-    m = wave_max(m);
-    if (lane == 0) __hip_atomic_store(st + sp, gran(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    float M = -INFINITY;   // the running maximum before this split: the earlier splits' maxima
-    if (sp > 0) {
-        unsigned long long v = 0;
-        bool ok = lane >= sp;
-        for (int it = 0; it < a.poll_limit; it++) {
-            if (!ok) {
-                v = __hip_atomic_load(st + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = (uint32_t)(v >> 32) == tag;
-            }
-            if (__all(ok)) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_SCORE_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        M = wave_max(lane < sp ? __uint_as_float((uint32_t)v) : -INFINITY);
-    }
-    const float M0 = M;
-    unsigned long long *wg = a.sgran + head * sgran_ld(a.max_ctx);
-#pragma unroll
-    for (int i = 0; i < SPL / 64; i++) {   // lane = key: the running maximum before it by a wave scan
-        const float s = sv[i];
-        const float inc = wave_scan_max(s);
-        const float Mx = fmaxf(M, dpp_ninf<0x138, 0xF>(inc));
-        const bool gt = s > Mx;
-        const float e = expf(gt ? Mx - s : s - Mx);
-        const float w = gt ? -e : (s != -INFINITY ? e : 0.0f);
-        M = fmaxf(M, lane_f(inc, 63));
-        wsh[hh][64 * i + lane] = w;
-        const int key = k0 + 64 * i + lane;
-        if (key < k1) __hip_atomic_store(wg + key, gran(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (lane < SPL / 32) {
-        float gm = -INFINITY;
-        for (int i = 0; i < 32; i++) gm = fmaxf(gm, scr[32 * lane + i]);
-        gmx[hh][lane] = gm;
-    }
-    if (lane < SPL / 32 && k0 + 32 * lane < k1) {   // (the chain takes 0 for groups past the context, as fx_weights_reg's lanes give)
-        float Mg = M0, Sl = 0.0f;
-        for (int j = 0; j < lane; j++) Mg = fmaxf(Mg, gmx[hh][j]);
-        for (int i = 0; i < 32; i++) {
-            const float x = wsh[hh][32 * lane + i];
-            Sl = __builtin_signbit(x) ? fadd_rn(fmul_rn(Sl, -x), 1.0f) : fadd_rn(fmul_rn(Sl, 1.0f), x);
-            Mg = fmaxf(Mg, scr[32 * lane + i]);
-        }
-        const int q = k0 / 32 + lane;
-        __hip_atomic_store(st + 64 + 2 * q, gran(Sl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(st + 65 + 2 * q, gran(Mg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
 // a split workgroup's LDS (decode_attn_body): its own __shared__ object in the
 // split kernel, one layout of the fused launch's shared role buffer there
 template <int SPL>
@@ -943,14 +860,6 @@ __device__ __forceinline__ void decode_attn_body(const DecodeAttnArgs a, const i
     __syncthreads();
     mark(6);
     if constexpr (FUSED) {
-        if (a.fx == 2) {   // exact attention, the weights here (fx1_chain_w reads them)
-            if (wid < 2) split_weights<SPL>(a, sc[wid], g, wid, sp, k0, k1, pos);
-            if (a.fx_vpf & 1)
-#pragma unroll
-                for (int i = 0; i < KPW; i++) asm volatile("" ::"v"(vv[i]));
-            mark(3);
-            return;
-        }
         if (a.fx) {   // exact attention: the scaled scores to the kv group's chain workgroup, one {fp32, tag} granule each
             const uint32_t tag = gran_tag(pos, a.layer);
             if (tid < 2 * SPL) {
@@ -1270,61 +1179,14 @@ __global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) 
     st.l0 = st.l1 = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; e++) { st.o0[e] = 0.f; st.o1[e] = 0.f; }
-    // FX with seq_vpf: the chain's V^T rows of each 64-key step pulled into L2
-    // beside that step's K loads (LDS-DMA pieces into this wave's 1 KiB of wo,
-    // contents unused: wo is the FX = 0 merge's), so the chain's loads hit L2
-    // instead of waiting an HBM latency per 64 keys.  Key blocks below the
-    // position's only: its block holds the V^T row wave 3 wrote above (no
-    // stale copy pulled before that store).
-    const uint16_t *vtb = a.vt + ((long)b * a.n_kv_head + g) * 128 * vt_ctx(a.max_ctx) + 8 * lane;
-    const int kb_end = pos >> 3;
-    auto vt_pull = [&](int c0) {
-        if (!FX || !a.seq_vpf) return;
-        typedef __attribute__((address_space(3))) void lds_void_v;
-        typedef __attribute__((address_space(1))) void glb_void_v;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {   // 16 pieces (8 key blocks x 2 dimension halves), 4 a wave
-            const int p = wid + 4 * i, kb = (c0 >> 3) + (p >> 1);
-            if (kb < kb_end)
-                __builtin_amdgcn_global_load_lds((glb_void_v *)(vtb + (long)kb * 1024 + (p & 1) * 512),
-                                                 (lds_void_v *)&wo[wid][0][0], 16, 0, 0);
-        }
-    };
-#ifndef SEQ_KNB
-#define SEQ_KNB 2   // FX: K register sets, SEQ_KNB - 1 chunks in flight ahead of the one scored (4: neutral at
-#endif              // 64 x 30 s, 30.35 vs 30.2 us a layer for the QKV + attention group, 164 VGPRs)
-    if constexpr (FX && SEQ_KNB > 2) {
-        // the exact path keeps no softmax state in the loop, so the K stream can
-        // run SEQ_KNB - 1 chunks ahead (a CU holds two of these workgroups: the
-        // registers are there); with one chunk of lead each 64-key chunk waited
-        // an HBM latency
-        KvChunk R[SEQ_KNB];
-        R[0] = A;
-#pragma unroll
-        for (int i = 1; i < SEQ_KNB - 1; i++)
-            if (64 * i < nkv) kvc_issue(kc, vc, 64 * i, kcap, want_v, R[i], a.kv_nt);
-        for (int c0 = 0; c0 < nkv; c0 += 64 * SEQ_KNB) {
-#pragma unroll
-            for (int u = 0; u < SEQ_KNB; u++) {
-                const int cs = c0 + 64 * u;
-                if (cs >= nkv) break;
-                if (cs + 64 * (SEQ_KNB - 1) < nkv) kvc_issue(kc, vc, cs + 64 * (SEQ_KNB - 1), kcap, want_v, R[(u + SEQ_KNB - 1) % SEQ_KNB], a.kv_nt);
-                vt_pull(cs);
-                kvc_step(a, qa, knew, vnew, cs, pos, R[u], st, sdst);
-            }
-        }
-    } else
     for (int c0 = 0; c0 < nkv; c0 += 128) {   // two chunks a trip, each prefetching the other set
         if (c0 + 64 < nkv) kvc_issue(kc, vc, c0 + 64, kcap, want_v, B, a.kv_nt);
-        vt_pull(c0);
         kvc_step(a, qa, knew, vnew, c0, pos, A, st, sdst);
         if (c0 + 64 >= nkv) break;
         if (c0 + 128 < nkv) kvc_issue(kc, vc, c0 + 128, kcap, want_v, A, a.kv_nt);
-        vt_pull(c0 + 64);
         kvc_step(a, qa, knew, vnew, c0 + 64, pos, B, st, sdst);
     }
     if constexpr (FX) {
-        if (a.seq_vpf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the pulls have landed (wo is never read here)
         __syncthreads();   // both heads' scores in LDS; the new V^T row stored (this workgroup's own writes)
         decode_attn_exact_body(a, 2 * g + (wid >> 1), b, wid & 1, fxs + (wid >> 1) * a.max_ctx);
         stamp_end(a.stamp);
@@ -1402,37 +1264,12 @@ int decode_stream_slots() {
 // (att_done replica block % 8), then the fp16 attention output and the
 // residual row read with sc1 loads.  att_done is re-armed by the down-proj
 // launch that follows (GemvArgs.zero8).
-// ORPW rows a wave (OPROJ_ROWS = 4 ORPW a block, 1024 / OPROJ_ROWS blocks):
-// 1 -- 256 blocks (2 -- 128 blocks, fitting 3 workgroups a CU, went with the
-// FX_W2 chain experiment); each row's arithmetic is the same either way
-#ifndef ORPW_N
-#define ORPW_N 1
-#endif
-constexpr int ORPW = ORPW_N, OPROJ_ROWS = 4 * ORPW;
+// One row a wave: 256 blocks of 4 rows.
+constexpr int ORPW = 1, OPROJ_ROWS = 4 * ORPW;
 __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnArgs a, int j) {
-    constexpr int K = 2048, NT = 4, NOB = 1024 / OPROJ_ROWS;
+    constexpr int K = 2048, NT = 4;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int row0 = j * OPROJ_ROWS + wid * ORPW;
-    __shared__ __attribute__((aligned(16))) float pfbuf[256];
-    typedef __attribute__((address_space(3))) void lds_void_p;
-    typedef __attribute__((address_space(1))) void glb_void_p;
-    if ((a.fx_vpf & 4) && a.fx) {
-        // (fx_vpf bit 2) the V^T rows of the kv group whose chain workgroup
-        // shares this block's XCD (blocks b and b + 8 do under round-robin
-        // placement; speed only) -> that L2, in place of the chain's own pull
-        // (whose loads its score poll waited behind): the XCD's NOB / 8 blocks
-        // split the group's 1 KiB pieces (dimension half, 8-key block), into
-        // pfbuf as the weight pulls below
-        const int nfx = a.fx >= 2 ? 4 * a.n_kv_head : a.n_kv_head;
-        const int gg = (nfx + j) & 7, nkv = a.pos[0] + 1;
-        if (gg < a.n_kv_head) {
-            const uint16_t *vtg = a.vt + (long)gg * 128 * vt_ctx(a.max_ctx);
-            const int np = 2 * ((nkv + 7) >> 3);
-            for (int p = (j >> 3) * 4 + wid; p < np; p += 4 * (NOB / 8))
-                __builtin_amdgcn_global_load_lds((glb_void_p *)(vtg + (p & 1) * 512 + (long)(p >> 1) * 1024 + lane * 8),
-                                                 (lds_void_p *)pfbuf, 16, 0, 0);
-        }
-    }
     for (int i = 0; i < a.oproj_delay; i++) __builtin_amdgcn_s_sleep(8);
     half8 wv[ORPW][NT];
 #pragma unroll
@@ -1440,26 +1277,12 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
 #pragma unroll
         for (int t = 0; t < NT; t++)
             wv[r][t] = __builtin_nontemporal_load((const half8 *)(o.W + (long)(row0 + r) * K + t * 512 + lane * 8));
-    // the weights the next launches stream (this layer's FFN, the next layer's
-    // QKV), pulled through the caches while HBM idles under the chain: LDS-DMA
-    // pieces of 1 KiB (nt) into pfbuf, contents unused (every wave's pieces
-    // land on the same 1 KiB: the blocks a CU holds keep within the LDS);
-    // wave w of the 4 NOB takes pieces w, w + 4 NOB, ...
-    {
-        const int w = j * 4 + wid;
-#pragma unroll
-        for (int r = 0; r < 3; r++) {
-            const char *base = (const char *)a.pf_ptr[r];
-            for (int p = w; p < (int)a.pf_kib[r]; p += 4 * NOB)
-                __builtin_amdgcn_global_load_lds((glb_void_p *)(base + (long)p * 1024 + lane * 16), (lds_void_p *)pfbuf, 16, 0, 2);
-        }
-    }
     __shared__ int oready;
     if (threadIdx.x == 0) {
         int ok = 0;
         for (int it = 0; it < a.poll_limit; it++) {
             if (__hip_atomic_load(a.att_done + (j & 7) * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                (unsigned)(a.fx >= 2 ? 4 * a.n_kv_head : a.n_kv_head)) {   // (fx = 2, 3: one arrival per chain wave)
+                (unsigned)a.n_kv_head) {
                 ok = 1;
                 break;
             }
@@ -1490,25 +1313,8 @@ __device__ __forceinline__ void oproj1_body(const GemvArgs o, const DecodeAttnAr
             for (int e = 0; e < 8; e++) acc = fmaf((float)wv[r][t][e], (float)h[e], acc);
         }
         acc = wave_sum(acc);
-        if (!a.ocnt) {
-            if (lane == 0) o.out_f32[row0 + r] = fadd_rn(acc, res[r]);
-        } else if (lane == 0) {   // the joined FFN reads x in this launch: write-through
-            __hip_atomic_store((uint32_t *)(o.out_f32 + row0 + r), __float_as_uint(fadd_rn(acc, res[r])), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (lane == 0) o.out_f32[row0 + r] = fadd_rn(acc, res[r]);
     }
-    if (!a.ocnt) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the pulls into pfbuf, long landed)
-        return;
-    }
-    // ... drained, one arrival per block into shard j % 32
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (a.fence && threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(a.ocnt + (j & 31) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Chain role of the fused exact attention (DecodeAttnArgs.fx): one workgroup
@@ -1540,13 +1346,10 @@ __device__ __forceinline__ void ld_sc1_x4_8(const void *base, const uint32_t *of
         : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]), "v"(off[7]), "s"(base)
         : "memory");
 }
-// chain workgroups of the fused launch: fx 1 one a kv group (4 chain waves),
-// 2 and 3 four (single-wave chain blocks)
-__host__ __device__ inline int fx_chain_wgs(int fx, int n_kv_head) {
-    return fx >= 2 ? 4 * n_kv_head : fx ? n_kv_head : 0;
-}
-// the chain roles' LDS (fx1_chain_body: both heads; fx1_chain_1w: row 0): a
-// layout of the fused launch's shared role buffer
+// chain workgroups of the fused launch: one a kv group (4 chain waves)
+__host__ __device__ inline int fx_chain_wgs(int fx, int n_kv_head) { return fx ? n_kv_head : 0; }
+// the chain role's LDS (fx1_chain_body: both heads): a layout of the fused
+// launch's shared role buffer
 struct alignas(16) ChainLds {
     float fsc[2][DX_KC / DX_B * FX_ST];
     uint16_t kmask[2][DX_KC / 16];
@@ -1748,48 +1551,14 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
         u32x4 va[DX_Q / 8], vb[DX_Q / 8];
         floatx4 wa, wb;
         const int lastb = nl > 0 ? (nl - 1) >> 3 : 0;
-#ifndef FX_CNB
-#define FX_CNB 2   // V^T register buffers of the chain (FX_CNB - 1 of lead)
-#endif
-        if constexpr (FX_CNB > 2) {
-            (void)va; (void)vb;
-            u32x4 vr[FX_CNB][DX_Q / 8];
-#pragma unroll
-            for (int i = 0; i < FX_CNB - 1; i++) fx_loadQ(vr[i], vt, loff, i * DX_Q, lastb);
-            fx_w8(fsc[hh], 0, wa, wb);
-            for (int j0 = 0; j0 < nl; j0 += FX_CNB * DX_Q) {
-#pragma unroll
-                for (int u = 0; u < FX_CNB; u++) {
-                    const int js = j0 + u * DX_Q;
-                    if (js >= nl) break;
-                    fx_loadQ(vr[(u + FX_CNB - 1) % FX_CNB], vt, loff, js + (FX_CNB - 1) * DX_Q, lastb);
-                    fx_step1_lds_m(vr[u], js, fsc[hh], fx_mask64(kmask[hh], js), acc, wa, wb);
-                }
-            }
-        } else {
         fx_loadQ(va, vt, loff, 0, lastb);
         fx_w8(fsc[hh], 0, wa, wb);
-#ifndef FX_W2
-#define FX_W2 0   // weights two groups ahead: 134 VGPRs (3 blocks a CU, o-proj at 2 rows a wave), chain still 20.2
-#endif            // cycles a key in place, configs[1] 248 vs 252 RTFx -- the chain does not wait on the weight reads
-        if (FX_W2) {   // weights two 8-key groups ahead (fx_step1_lds_m2)
-            floatx4 wc, wd;
-            fx_w8(fsc[hh], 8, wc, wd);
-            for (int j0 = 0; j0 < nl; j0 += 2 * DX_Q) {
-                fx_loadQ(vb, vt, loff, j0 + DX_Q, lastb);
-                fx_step1_lds_m2(va, j0, fsc[hh], fx_mask64(kmask[hh], j0), acc, wa, wb, wc, wd);
-                if (j0 + DX_Q >= nl) break;
-                fx_loadQ(va, vt, loff, j0 + 2 * DX_Q, lastb);
-                fx_step1_lds_m2(vb, j0 + DX_Q, fsc[hh], fx_mask64(kmask[hh], j0 + DX_Q), acc, wa, wb, wc, wd);
-            }
-        } else
         for (int j0 = 0; j0 < nl; j0 += 2 * DX_Q) {
             fx_loadQ(vb, vt, loff, j0 + DX_Q, lastb);
             fx_step1_lds_m(va, j0, fsc[hh], fx_mask64(kmask[hh], j0), acc, wa, wb);
             if (j0 + DX_Q >= nl) break;
             fx_loadQ(va, vt, loff, j0 + 2 * DX_Q, lastb);
             fx_step1_lds_m(vb, j0 + DX_Q, fsc[hh], fx_mask64(kmask[hh], j0 + DX_Q), acc, wa, wb);
-        }
         }
         acc = fx_key_slow(acc, vnew, fwl[hh]);
     }
@@ -1834,415 +1603,8 @@ __device__ __forceinline__ void fx1_chain_body(const DecodeAttnArgs &a, const in
     }
 }
 
-// The chain role with one wave a workgroup (DecodeAttnArgs.fx == 3, option
-// fx_pipe = 3): fx1_chain_body's arithmetic (so the same bits) for one query
-// head and one dimension half, 4 n_kv_head workgroups (c: kv group c % n_kv_head,
-// head 2 g + (c / n_kv_head) / 2, half (c / n_kv_head) & 1; a group's four
-// land on the XCD of its splits).  The wave gathers its head's score granules,
-// derives all 32 weights of each lane (both halves fx1_chain_body splits over a
-// head's two waves) and runs the chain: one wave's V^T stream per CU instead of
-// four.  Trace rows 4000 + c, clocks 4040 + c.
-__device__ __forceinline__ void fx1_chain_1w(const DecodeAttnArgs &a, const int c, ChainLds &C) {
-    float *const fs1 = C.fsc[0];
-    uint16_t *const km1 = C.kmask[0];
-    float &fwl1 = C.fwl[0];
-    if (threadIdx.x >= 64) return;
-    const int lane = threadIdx.x;
-    const int g = c % a.n_kv_head, k = c / a.n_kv_head;
-    const int hh = k >> 1, wu = __builtin_amdgcn_readfirstlane(k & 1);
-    const int d = 64 * wu + lane, loff = 8 * lane;
-    const uint16_t *vt = a.vt + (long)g * 128 * vt_ctx(a.max_ctx) + 64 * wu * 8;
-    auto mark = [&](int slot) {
-        if (a.trace && lane == 0) a.trace[(4000L + c) * 8 + slot] = rt_now();
-    };
-    mark(0);
-    const int pos = a.pos[0], nkv = pos + 1;
-    const uint32_t tag = gran_tag(pos, a.layer);
-    const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
-    if (a.fx_vpf & 2) {   // V^T of this half -> L2 (the group's other head pulls the other key blocks; same XCD)
-        typedef __attribute__((address_space(3))) void lds_void_c;
-        typedef __attribute__((address_space(1))) void glb_void_c;
-        for (int kb = hh; kb * 8 < nkv; kb += 2)
-            __builtin_amdgcn_global_load_lds((glb_void_c *)(vt + (long)kb * 1024 + loff), (lds_void_c *)fs1, 16, 0, 0);
-    }
-    const int n = nkv, np = (n + 1) >> 1;
-    {   // (1) this head's score granules -> LDS: pair q = lane + 64 u, all 16 in flight (the asm drains them)
-        const int ld = sgran_ld(a.max_ctx);
-        const unsigned long long *gb = a.sgran + (long)(2 * g + hh) * ld;   // uniform
-        uint32_t go[DX_KC / 128];
-#pragma unroll
-        for (int u = 0; u < DX_KC / 128; u++) {
-            const int q = lane + 64 * u;
-            go[u] = q < np ? (uint32_t)(2 * q * 8) : 0u;
-        }
-        u32x4 gv[DX_KC / 128];
-        bool ok = false;
-        for (int it = 0; it < a.poll_limit; it++) {
-            ld_sc1_x4_8(gb, go, gv);
-            ld_sc1_x4_8(gb, go + 8, gv + 8);
-            ok = true;
-#pragma unroll
-            for (int u = 0; u < DX_KC / 128; u++) {
-                const int q = lane + 64 * u;
-                if (q < np) ok = ok && gv[u][1] == tag && (2 * q + 1 >= n || gv[u][3] == tag);
-            }
-            if (__all(ok)) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_SCORE_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int u = 0; u < DX_KC / 128; u++) {
-            const int q = lane + 64 * u, j = 2 * q;
-            if (q < np) *(float2 *)&fs1[(j >> 5) * FX_ST + (j & 31)] = make_float2(__uint_as_float(gv[u][0]), __uint_as_float(gv[u][2]));
-        }
-    }
-    mark(2);
-    float M, S;
-    {   // (2) the weights: fx1_chain_body's two halves, both here
-        float *row = fs1 + lane * FX_ST;
-        float sv[DX_B];
-#pragma unroll
-        for (int i = 0; i < DX_B; i += 4) {
-            const floatx4 r = *(const floatx4 *)&row[i];
-#pragma unroll
-            for (int e = 0; e < 4; e++) sv[i + e] = lane * DX_B + i + e < n ? r[e] : -INFINITY;
-        }
-        float lm = -INFINITY, lh = -INFINITY;
-#pragma unroll
-        for (int i = 0; i < DX_B / 2; i++) lh = fmaxf(lh, sv[i]);
-#pragma unroll
-        for (int i = DX_B / 2; i < DX_B; i++) lm = fmaxf(lm, sv[i]);
-        lm = fmaxf(lm, lh);
-        const float inc = wave_scan_max(lm);
-        const float Mp0 = dpp_ninf<0x138, 0xF>(inc);
-        M = lane_f(inc, 63);
-        float x[DX_B];
-        uint32_t kb0 = 0, kb1 = 0;
-        {
-            float Mq = Mp0;
-#pragma unroll
-            for (int i = 0; i < DX_B / 2; i++) {
-                const float sc = sv[i];
-                const bool gt = sc > Mq;
-                const float e = expf(gt ? Mq - sc : sc - Mq);
-                x[i] = gt ? -e : (sc != -INFINITY ? e : 0.0f);
-                kb0 |= (uint32_t)gt << i;
-                Mq = fmaxf(Mq, sc);
-            }
-        }
-        {
-            float Mq = fmaxf(Mp0, lh);
-#pragma unroll
-            for (int i = 0; i < DX_B / 2; i++) {
-                const float sc = sv[DX_B / 2 + i];
-                const bool gt = sc > Mq;
-                const float e = expf(gt ? Mq - sc : sc - Mq);
-                x[DX_B / 2 + i] = gt ? -e : (sc != -INFINITY ? e : 0.0f);
-                kb1 |= (uint32_t)gt << i;
-                Mq = fmaxf(Mq, sc);
-            }
-        }
-        km1[2 * lane] = (uint16_t)kb0;
-        km1[2 * lane + 1] = (uint16_t)kb1;
-        mark(6);
-#pragma unroll
-        for (int i = 0; i < DX_B; i += 4) *(floatx4 *)&row[i] = floatx4{x[i], x[i + 1], x[i + 2], x[i + 3]};
-        const int kl = n - 1, kr = kl & 31;
-        const bool own = lane == (kl >> 5);
-        if (own) {   // the new key: weight 0 in LDS (a no-op for the loop), its own weight in fwl1, applied last
-            fwl1 = row[kr];
-            row[kr] = 0.0f;
-        }
-        mark(7);
-        const float wl = fwl1;   // (this wave's own LDS write above: in order)
-        float Sl = 0.0f;   // the lane's sequential S over its 32 weights, key n - 1 as 0, then its own term
-#pragma unroll
-        for (int i = 0; i < DX_B; i++) {
-            const float r = own && i == kr ? 0.0f : x[i];
-            Sl = __builtin_signbit(r) ? fadd_rn(fmul_rn(Sl, -r), 1.0f) : fadd_rn(fmul_rn(Sl, 1.0f), r);
-        }
-        if (own) Sl = __builtin_signbit(wl) ? fadd_rn(fmul_rn(Sl, -wl), 1.0f) : fadd_rn(fmul_rn(Sl, 1.0f), wl);
-        const float Ml = fmaxf(Mp0, lm);
-        S = wave_sum(Ml == -INFINITY ? 0.0f : Sl * expf(Ml - M));
-    }
-    mark(3);
-    uint16_t vnew = 0;
-    {
-        const unsigned long long *gp = a.gran + QD + KD + g * 128 + d;
-        unsigned long long v = 0;
-        bool ok = false;
-        for (int it = 0; it < a.poll_limit; it++) {
-            v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ok = (uint32_t)(v >> 32) == tag;
-            if (__all(ok)) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_QKV_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        vnew = f_to_u16(__uint_as_float((uint32_t)v));
-    }
-    mark(1);
-    const unsigned long long ck0 = a.trace ? clock64() : 0ull;
-    f16 acc = 0;
-    {
-        const int nl = n - 1;
-        u32x4 va[DX_Q / 8], vb[DX_Q / 8];
-        floatx4 wa, wb;
-        const int lastb = nl > 0 ? (nl - 1) >> 3 : 0;
-        fx_loadQ(va, vt, loff, 0, lastb);
-        fx_w8(fs1, 0, wa, wb);
-        for (int j0 = 0; j0 < nl; j0 += 2 * DX_Q) {
-            fx_loadQ(vb, vt, loff, j0 + DX_Q, lastb);
-            fx_step1_lds_m(va, j0, fs1, fx_mask64(km1, j0), acc, wa, wb);
-            if (j0 + DX_Q >= nl) break;
-            fx_loadQ(va, vt, loff, j0 + 2 * DX_Q, lastb);
-            fx_step1_lds_m(vb, j0 + DX_Q, fs1, fx_mask64(km1, j0 + DX_Q), acc, wa, wb);
-        }
-        acc = fx_key_slow(acc, vnew, fwl1);
-    }
-    mark(4);
-    if (a.trace && lane == 0) {
-        a.trace[(4040L + c) * 8 + 0] = ck0;
-        a.trace[(4040L + c) * 8 + 1] = clock64();
-        a.trace[(4040L + c) * 8 + 2] = (unsigned long long)n;
-    }
-    const float ov = (float)acc * (S == 0.0f ? 0.0f : 1.0f / S);
-    const uint32_t h16 = f_to_u16(ov);
-    const uint32_t hn = __shfl_xor(h16, 1, 64);
-    uint16_t *out = a.out + (2 * g + hh) * 128 + d;
-    if (a.att_done) {   // write-through pairs, drained, one arrival per replica from this workgroup
-        if ((lane & 1) == 0) __hip_atomic_store((uint32_t *)out, h16 | (hn << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (a.fence) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (lane < 8) __hip_atomic_fetch_add(a.att_done + lane * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        *out = (uint16_t)h16;
-    }
-    mark(5);
-}
-
-// The chain role with fx_pipe.h (a.fx_pipe): each wave takes its head's
-// score granules one 64-key buffer at a time (lane = key, sc1 loads issued a
-// buffer and a half ahead, polled only if a tag is not there yet) and derives
-// that buffer's weights itself, so the chain starts on the first 64 scores
-// instead of after a gather of all of them and a weight pass over the context
-// (~4 us a layer at 1.4k keys).  No LDS, no barrier before the
-// output.  The new key (n - 1) is scored with the others but applied after
-// the loop from its QKV granule, as fx1_chain_body does.
-struct FxpGran {   // fxp_chain's score source: key j's {fp32 score, tag} granule of one head
-    const unsigned long long *gb;
-    int n;
-    uint32_t tag;
-    int poll_limit;
-    unsigned int *err;
-    __device__ __forceinline__ unsigned long long issue(int j0) const {
-        const int j = j0 + (int)(threadIdx.x & 63);
-        return j < n ? __hip_atomic_load(gb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-    }
-    __device__ __forceinline__ float take(unsigned long long v, int j0) const {
-        const int j = j0 + (int)(threadIdx.x & 63);
-        bool ok = j >= n || (uint32_t)(v >> 32) == tag;
-        if (!__all(ok)) {   // not published yet: poll this buffer's granules (bounded)
-            for (int it = 0; it < poll_limit; it++) {
-                __builtin_amdgcn_s_sleep(1);
-                if (!ok) {
-                    v = __hip_atomic_load(gb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = (uint32_t)(v >> 32) == tag;
-                }
-                if (__all(ok)) break;
-            }
-            if (!__all(ok) && (threadIdx.x & 63) == 0)
-                __hip_atomic_fetch_or(err, (unsigned)DEVERR_SCORE_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return j < n ? __uint_as_float((uint32_t)v) : -INFINITY;
-    }
-};
-__device__ __forceinline__ void fx1_chain_pipe(const DecodeAttnArgs &a, const int g) {
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int hh = wid >> 1, wu = __builtin_amdgcn_readfirstlane(wid & 1);
-    const int d = 64 * wu + lane, loff = 8 * lane;
-    const uint16_t *vt = a.vt + (long)g * 128 * vt_ctx(a.max_ctx) + 64 * wu * 8;   // batch 1: slot 0; the wave's key block 0
-    auto mark = [&](int slot) {   // dev trace: rows 4000 + g as fx1_chain_body ([start, v ready, -, -, chain done, published])
-        if (a.trace && tid == 0) a.trace[(4000L + g) * 8 + slot] = rt_now();
-    };
-    mark(0);
-    const int pos = a.pos[0], nkv = pos + 1, nl = nkv - 1;
-    const uint32_t tag = gran_tag(pos, a.layer);
-    const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
-    const unsigned long long *gp = a.gran + QD + KD + g * 128 + d;   // the new key's v (this lane's dimension)
-    unsigned long long vg = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const FxpGran src{a.sgran + (long)(2 * g + hh) * sgran_ld(a.max_ctx), nkv, tag, a.poll_limit, a.err};
-    mark(2);   // (no gather or weight pass: the chain starts here; slots 2, 3 = its start)
-    mark(3);
-    const unsigned long long ck0 = a.trace ? clock64() : 0ull;
-    f16 acc = 0;
-    float wlast;
-    const float S = fxp_chain(src, vt, loff, nl, nl > 0 ? (nl - 1) >> 3 : 0, acc, wlast);
-    mark(4);
-    {   // the new key: its QKV granule (long published by now), cast to fp16 as the cache write is
-        bool ok = (uint32_t)(vg >> 32) == tag;
-        for (int it = 0; it < a.poll_limit && !__all(ok); it++) {
-            __builtin_amdgcn_s_sleep(2);
-            vg = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ok = (uint32_t)(vg >> 32) == tag;
-        }
-        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_QKV_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    mark(1);
-    acc = fx_key_slow(acc, f_to_u16(__uint_as_float((uint32_t)vg)), wlast);
-    if (a.trace && tid == 0) {
-        a.trace[(4010L + g) * 8 + 0] = ck0;
-        a.trace[(4010L + g) * 8 + 1] = clock64();
-        a.trace[(4010L + g) * 8 + 2] = (unsigned long long)nkv;
-    }
-    const float ov = (float)acc * (S == 0.0f ? 0.0f : 1.0f / S);   // ggml: VKQ32 = fp32(VKQ16) * (1 / S)
-    const uint32_t h16 = f_to_u16(ov);
-    const uint32_t hn = __shfl_xor(h16, 1, 64);
-    uint16_t *out = a.out + (2 * g + hh) * 128 + d;
-    if (a.att_done) {   // as fx1_chain_body: write-through pairs, drained, one arrival per replica
-        if ((lane & 1) == 0) __hip_atomic_store((uint32_t *)out, h16 | (hn << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (a.fence && tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (a.fence) __syncthreads();
-        if (tid < 8) __hip_atomic_fetch_add(a.att_done + tid * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        *out = (uint16_t)h16;
-    }
-    mark(5);
-}
-
-// The chain role with the weights from the splits (a.fx = 2, split_weights):
-// per 64-key buffer one {weight, tag} granule a lane, the chain as
-// fx1_chain_pipe's; S from the splits' 32-key group sums, combined as
-// fx_weights_reg combines its lanes' (one chunk: the launch is taken only
-// while n_kv <= DX_KC), so fused and separate launches agree bit for bit.
-struct FxpWGran {   // fxp_chain_w's weight source: key j's {fp32 weight, tag} granule of one head
-    const unsigned long long *gb;
-    int n;
-    uint32_t tag;
-    int poll_limit;
-    unsigned int *err;
-    __device__ __forceinline__ unsigned long long issue(int j0) const {
-        const int j = j0 + (int)(threadIdx.x & 63);
-        return j < n ? __hip_atomic_load(gb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-    }
-    __device__ __forceinline__ float take(unsigned long long v, int j0) const {
-        const int j = j0 + (int)(threadIdx.x & 63);
-        bool ok = j >= n || (uint32_t)(v >> 32) == tag;
-        if (!__all(ok)) {
-            for (int it = 0; it < poll_limit; it++) {
-                __builtin_amdgcn_s_sleep(1);
-                if (!ok) {
-                    v = __hip_atomic_load(gb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = (uint32_t)(v >> 32) == tag;
-                }
-                if (__all(ok)) break;
-            }
-            if (!__all(ok) && (threadIdx.x & 63) == 0)
-                __hip_atomic_fetch_or(err, (unsigned)DEVERR_SCORE_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return j < n ? __uint_as_float((uint32_t)v) : 0.0f;
-    }
-};
-// One wave a block (c = the chain block, 4 per kv group): the V^T rows of a
-// chain are the wave's own stream, and a CU's L2 -> CU path carried four
-// chains' V^T at once in the four-wave blocks -- ~0.5 KiB a key step, which
-// held the in-place chain at ~20 cycles a key against 15 with the V^T loads
-// cache-hot (device trace).  Blocks c and c + 8 share kv group c % 8 and so
-// the XCD the group's splits pulled its V^T rows into.
-__device__ __forceinline__ void fx1_chain_w(const DecodeAttnArgs &a, const int c) {
-    if (threadIdx.x >= 64) return;   // (no barrier below: the block's other waves are not needed)
-    const int g = c % a.n_kv_head, k = c / a.n_kv_head;
-    const int tid = threadIdx.x, lane = tid;
-    const int hh = k >> 1, wu = k & 1;
-    const int d = 64 * wu + lane, loff = 8 * lane;
-    const uint16_t *vt = a.vt + (long)g * 128 * vt_ctx(a.max_ctx) + 64 * wu * 8;   // batch 1: slot 0; the wave's key block 0
-    auto mark = [&](int slot) {   // dev trace: rows 4000 + c ([start, v ready, first weights, -, chain done, published])
-        if (a.trace && tid == 0) a.trace[(4000L + c) * 8 + slot] = rt_now();
-    };
-    mark(0);
-    const int pos = a.pos[0], nkv = pos + 1, nl = nkv - 1;
-    const uint32_t tag = gran_tag(pos, a.layer);
-    const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
-    const long head = 2 * g + hh;
-    const unsigned long long *gp = a.gran + QD + KD + g * 128 + d;   // the new key's v (this lane's dimension)
-    unsigned long long vg = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const FxpWGran src{a.sgran + head * sgran_ld(a.max_ctx), nkv, tag, a.poll_limit, a.err};
-    mark(2);
-    mark(3);
-    const unsigned long long ck0 = a.trace ? clock64() : 0ull;
-    f16 acc = 0;
-    float wlast;
-    fxp_chain_w(src, vt, loff, nl, nl > 0 ? (nl - 1) >> 3 : 0, acc, wlast);
-    mark(4);
-    {   // the new key: its QKV granule (long published by now), cast to fp16 as the cache write is
-        bool ok = (uint32_t)(vg >> 32) == tag;
-        for (int it = 0; it < a.poll_limit && !__all(ok); it++) {
-            __builtin_amdgcn_s_sleep(2);
-            vg = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ok = (uint32_t)(vg >> 32) == tag;
-        }
-        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_QKV_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    mark(1);
-    acc = fx_key_slow(acc, f_to_u16(__uint_as_float((uint32_t)vg)), wlast);
-    // S: lane q = 32-key group q: {S_q, running max at its end} from the splits (long published)
-    float S;
-    {
-        const unsigned long long *st = a.sstat + head * SS_LD + 64;
-        const bool has = 32 * lane < nkv;
-        unsigned long long s2 = 0, m2 = 0;
-        bool ok = !has;
-        for (int it = 0; it < a.poll_limit; it++) {
-            if (!ok) {
-                s2 = __hip_atomic_load(st + 2 * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                m2 = __hip_atomic_load(st + 2 * lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = (uint32_t)(s2 >> 32) == tag && (uint32_t)(m2 >> 32) == tag;
-            }
-            if (__all(ok)) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (!__all(ok) && lane == 0) __hip_atomic_fetch_or(a.err, (unsigned)DEVERR_SCORE_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const float Sl = has ? __uint_as_float((uint32_t)s2) : 0.0f;
-        const float Ml = has ? __uint_as_float((uint32_t)m2) : -INFINITY;
-        const float Mn = wave_max(Ml);
-        S = wave_sum(!has || Ml == -INFINITY ? 0.0f : Sl * expf(Ml - Mn));
-    }
-    if (a.trace && tid == 0) {
-        a.trace[(4040L + c) * 8 + 0] = ck0;
-        a.trace[(4040L + c) * 8 + 1] = clock64();
-        a.trace[(4040L + c) * 8 + 2] = (unsigned long long)nkv;
-    }
-    const float ov = (float)acc * (S == 0.0f ? 0.0f : 1.0f / S);   // ggml: VKQ32 = fp32(VKQ16) * (1 / S)
-    const uint32_t h16 = f_to_u16(ov);
-    const uint32_t hn = __shfl_xor(h16, 1, 64);
-    uint16_t *out = a.out + (2 * g + hh) * 128 + d;
-    if (a.att_done) {   // write-through pairs, drained (one wave: no barrier), one arrival per replica
-        if ((lane & 1) == 0) __hip_atomic_store((uint32_t *)out, h16 | (hn << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (a.fence && tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (tid < 8) __hip_atomic_fetch_add(a.att_done + tid * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        *out = (uint16_t)h16;
-    }
-    mark(5);
-}
-
-// the joined FFN's gate/up blocks (ffn_gu_role<1024, LFFN_OPW>): 3072 / (4 LFFN_OPW)
-constexpr int LFFN_OPW = 2, LFFN_NGU = 3072 / (4 * LFFN_OPW);
-
 template <int SPL>
-__global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnArgs a, GemvArgs o, GemvArgs g, GemvArgs d,
-                                                        FfnCtl fc) {
+__global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnArgs a, GemvArgs o) {
     constexpr int K = 1024, NT = 2, RPW = 2;
     // one LDS buffer for the roles that need one (a workgroup takes one role):
     // the split and chain layouts overlap instead of adding up
@@ -2253,21 +1615,11 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
         // splits (kv group j % n_kv_head: blocks b and b + 8 share an XCD under
         // round-robin placement, so a group's splits and its chain workgroup
         // share one L2 -- speed only), the chain workgroups (exact attention),
-        // the o-projection, the joined FFN (gate/up, then down: each waits only
-        // on lower-numbered blocks, so in-order dispatch needs no co-residency
-        // for them)
+        // the o-projection
         const int j = blockIdx.x - 512, nsp = a.grid_splits, nat = nsp * a.n_kv_head;   // grid_splits: this launch's splits
         const int nfx = fx_chain_wgs(a.fx, a.n_kv_head);
-        const int jf = j - nat - nfx - 1024 / OPROJ_ROWS;   // joined FFN block (after the o-proj blocks)
-        if (a.ocnt && jf >= LFFN_NGU) ffn_dn_role<3072, 1>(d, fc, jf - LFFN_NGU, LFFN_NGU / 32);
-        else if (a.ocnt && jf >= 0) ffn_gu_role<1024, LFFN_OPW>(g, d, fc, jf);
-        else if (j >= nat + nfx) oproj1_body(o, a, j - nat - nfx);
-        else if (j >= nat) {
-            if (a.fx == 2) fx1_chain_w(a, j - nat);
-            else if (a.fx == 3) fx1_chain_1w(a, j - nat, *reinterpret_cast<ChainLds *>(role_lds));
-            else if (a.fx_pipe == 1) fx1_chain_pipe(a, j - nat);
-            else fx1_chain_body(a, j - nat, *reinterpret_cast<ChainLds *>(role_lds));
-        }
+        if (j >= nat + nfx) oproj1_body(o, a, j - nat - nfx);
+        else if (j >= nat) fx1_chain_body(a, j - nat, *reinterpret_cast<ChainLds *>(role_lds));
         else decode_attn_body<SPL, true>(a, j / a.n_kv_head, j % a.n_kv_head, 0, nsp, *reinterpret_cast<SplitLds<SPL> *>(role_lds));
         stamp_end(a.stamp);
         return;
@@ -2368,8 +1720,7 @@ __global__ __launch_bounds__(256) void qkv_attn1_kernel(GemvArgs q, DecodeAttnAr
 // would outgrow the co-resident slots)
 static int split1(int spl1, int grid_splits) { return spl1 == 64 || spl1 == 128 ? spl1 : grid_splits >= 30 ? 128 : 64; }
 
-int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s, bool dry,
-                          const GemvArgs *gu, const GemvArgs *dn, const FfnCtl *fc) {
+int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s, bool dry) {
     if (!cfg.qkv || !cfg.err || a.B != 1 || !a.qcnt || q.M != 1 || q.K != 1024 || q.Wd || !q.norm_w || q.xh || q.bias || q.res ||
         a.out32 || a.outq || q.N != a.n_head * 128 + 2 * a.n_kv_head * 128 || a.n_head != 2 * a.n_kv_head || a.n_kv_head * 64 != 512)
         return 0;
@@ -2382,23 +1733,16 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     // ones): fall back to separate launches for contexts that would not fit
     // (exact attention: n_kv_head chain workgroups too; they read the new v
     // from its granule, so the fused exact path needs the granule hand-off)
-    // (fx_chain.h and the split weights' S: one chain chunk)
-    if (a.fx && (!a.gran || !a.sgran || (a.fx_pipe != 1 && ns * spl1 > DX_KC) || (a.fx == 2 && !a.sstat))) return 0;
+    // (fx_chain.h: one chain chunk)
+    if (a.fx && (!a.gran || !a.sgran || ns * spl1 > DX_KC)) return 0;
     const int nfx = fx_chain_wgs(a.fx, a.n_kv_head);
     const int slots = spl1 == 128 ? cfg.slots_qkv128 : cfg.slots_qkv64;
     const int o_blocks = 1024 / OPROJ_ROWS;
     const bool fit_o = 512 + ns * a.n_kv_head + nfx + o_blocks <= slots;
     if (512 + ns * a.n_kv_head + nfx > slots) return 0;
     const bool with_o2 = with_o && fit_o;
-    // the FFN joins behind the o-projection when it is launch_ffn1's shape, its
-    // counters are given, and the o-proj writes the x row the gate/up reads
-    const bool with_f = with_o2 && cfg.lffn && gu && dn && fc && fc->ocnt && fc->att_done && gu->M == 1 && dn->M == 1 &&
-                        !gu->Wd && !dn->Wd && gu->K == 1024 && gu->N == 3072 && gu->x == o->out_f32 && gu->norm_w &&
-                        !gu->xh && !gu->embd_ids && gu->out_f16 && dn->K == 3072 && dn->N == 1024 && dn->xh == gu->out_f16 &&
-                        dn->res == o->out_f32 && dn->out_f32 == o->out_f32 && !dn->bias && !dn->norm_w && !dn->zero8 &&
-                        fc->att_done == a.att_done;
-    if (dry) return with_f ? 3 : with_o2 ? 2 : 1;
-    const dim3 grid(512 + ns * a.n_kv_head + nfx + (with_o2 ? o_blocks : 0) + (with_f ? LFFN_NGU + 1024 / 4 : 0));
+    if (dry) return with_o2 ? 2 : 1;
+    const dim3 grid(512 + ns * a.n_kv_head + nfx + (with_o2 ? o_blocks : 0));
     // K/V delay ~2 us: measured optimum on MI355X (round-1 delay sweep: 0 -> 236.3, 10 -> 232.0, 18 -> 240.3 ms decode)
     DecodeAttnArgs ad = a;
     ad.fuse_delay = cfg.qkv_delay;
@@ -2407,31 +1751,13 @@ int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const Gemv
     ad.fence = cfg.fence;
     ad.err = cfg.err;
     ad.grid_splits = ns;   // the kernel's split count
-    ad.fx_delay = cfg.fx_delay;
-    // fx_pipe: the chain starts on the first scores, so its V^T rows come from
-    // the splits' pull (bit 0): the chain workgroup's own LDS-DMA pull (bit 1)
-    // would sit in its vmcnt queue ahead of the chain's first loads
-    ad.fx_vpf = a.fx_pipe == 1 || a.fx_pipe == 2 ? (cfg.fx_vpf | 1) & ~2 : cfg.fx_vpf;   // (fx_pipe 1 and 2)
+    ad.fx_vpf = cfg.fx_vpf;
     if (!with_o2) ad.att_done = nullptr;
-    ad.ocnt = with_f ? fc->ocnt : nullptr;
     const GemvArgs qa = q;
     const GemvArgs oa = with_o2 ? *o : GemvArgs{};
-    const GemvArgs ga = with_f ? *gu : GemvArgs{}, da = with_f ? *dn : GemvArgs{};
-    FfnCtl fa{};
-    if (with_f) {
-        fa = *fc;
-        fa.att_need = a.fx >= 2 ? 4 * a.n_kv_head : a.n_kv_head;   // as the o-proj's wait
-        fa.o_need = (unsigned)(o_blocks / 32);                     // o-proj arrivals per shard
-        fa.gdelay = cfg.lffn_gdelay;
-        fa.wdelay = cfg.lffn_wdelay;
-        fa.delay = 0;
-        fa.poll_limit = cfg.poll_limit;
-        fa.fence = cfg.fence;
-        fa.err = cfg.err;
-    }
-    if (spl1 == 128) hipLaunchKernelGGL(qkv_attn1_kernel<128>, grid, dim3(256), 0, s, qa, ad, oa, ga, da, fa);
-    else hipLaunchKernelGGL(qkv_attn1_kernel<DSPLIT>, grid, dim3(256), 0, s, qa, ad, oa, ga, da, fa);
-    return with_f ? 3 : with_o2 ? 2 : 1;
+    if (spl1 == 128) hipLaunchKernelGGL(qkv_attn1_kernel<128>, grid, dim3(256), 0, s, qa, ad, oa);
+    else hipLaunchKernelGGL(qkv_attn1_kernel<DSPLIT>, grid, dim3(256), 0, s, qa, ad, oa);
+    return with_o2 ? 2 : 1;
 }
 
 void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s) {

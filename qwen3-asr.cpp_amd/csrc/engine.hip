@@ -120,7 +120,6 @@ struct qasr_ctx {
     unsigned int *d_counter = nullptr, *d_done = nullptr;
     unsigned int *d_qcnt = nullptr;   // fused batch-1 QKV + attention: QKV-block arrivals per kv group
     unsigned long long *d_gran = nullptr;   // ... or its outputs as tagged granules (zeroed by every prefill)
-    unsigned long long *d_sstat = nullptr;  // ... and fx_pipe = 2's split maxima / 32-key group sums [n_head][SS_LD] (zeroed likewise)
     unsigned long long *d_sgran = nullptr;  // ... exact attention: the splits' scores as granules [n_head][max_ctx] (zeroed likewise)
     bool qkv_in_gran = false;               // the captured step's last layer hands its QKV over in granules
     unsigned int *d_attdone = nullptr;   // fused batch-1 o-proj: combiner arrivals, [layer][8 replicas][16]
@@ -160,7 +159,6 @@ struct qasr_ctx {
     int probe_stride = 1;          // probe decode steps k with k % probe_stride == 0 (the others replay the whole-step
                                    // graph: the probed step's split graphs and eager group cost ~3 % of a step)
     bool probe_o_fused = false;    // the probed layer's o-projection runs inside the QKV launch
-    bool probe_lffn = false;       // ... and its FFN too (FuseCfg::lffn)
     int last_fmode = 0, last_fx = 0;   // the last emitted decode step, layer 0: fused launch mode (0 separate, 1 QKV +
                                        // attention, 2 + o-proj) and whether its attention was the chain role (options
                                        // "fused_mode" / "fused_exact", read-only)
@@ -221,7 +219,6 @@ static const std::vector<FuseOption> &fuse_options() {
         {"gemm_regs", "QASR_GEMM_REGS", &FuseCfg::gemm_regs},
         {"gran", "QASR_GRAN", &FuseCfg::gran},
         {"fa_exact_decode", "QASR_FA_EXACT_DECODE", &FuseCfg::fa_exact_decode},
-        {"fx_delay", "QASR_FX_DELAY", &FuseCfg::fx_delay},
         {"fx_vpf", "QASR_FX_VPF", &FuseCfg::fx_vpf},
         {"att_stream", "QASR_ATT_STREAM", &FuseCfg::att_stream},
         {"skinny", "QASR_SKINNY", &FuseCfg::skinny},
@@ -229,12 +226,6 @@ static const std::vector<FuseOption> &fuse_options() {
         {"kv_nt", "QASR_KV_NT", &FuseCfg::kv_nt},
         {"lmh", "QASR_LMH", &FuseCfg::lmh},
         {"fx_seq", "QASR_FX_SEQ", &FuseCfg::fx_seq},
-        {"fx_pipe", "QASR_FX_PIPE", &FuseCfg::fx_pipe},
-        {"lffn", "QASR_LFFN", &FuseCfg::lffn},
-        {"seq_vpf", "QASR_SEQ_VPF", &FuseCfg::seq_vpf},
-        {"wpf", "QASR_WPF", &FuseCfg::wpf},
-        {"lffn_gdelay", "QASR_LFFN_GDELAY", &FuseCfg::lffn_gdelay},
-        {"lffn_wdelay", "QASR_LFFN_WDELAY", &FuseCfg::lffn_wdelay},
         {"skinny_inf", "QASR_SKINNY_INF", &FuseCfg::skinny_inf},
     };
     return v;
@@ -739,7 +730,6 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         (rc = dev_alloc(c.get(), (void **)&c->d_attdone, (size_t)hp.dec_layers * 128 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_gran, (size_t)(QD + 2 * KD) * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_sgran, (size_t)hp.n_head * sgran_ld(max_ctx) * 8)) ||
-        (rc = dev_alloc(c.get(), (void **)&c->d_sstat, (size_t)hp.n_head * 192 * 8)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_ffncnt, (size_t)hp.dec_layers * 1024 * 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_done, 4)) || (rc = dev_alloc(c.get(), (void **)&c->d_err, 4)) ||
         (rc = dev_alloc(c.get(), (void **)&c->d_pstamp, (size_t)max_ctx * kStampRec * 8)) ||
@@ -754,7 +744,6 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
     HIPCHK(hipMemset(c->d_attdone, 0, (size_t)hp.dec_layers * 128 * 4));
     HIPCHK(hipMemset(c->d_gran, 0, (size_t)(QD + 2 * KD) * 8));
     HIPCHK(hipMemset(c->d_sgran, 0, (size_t)hp.n_head * sgran_ld(max_ctx) * 8));
-    HIPCHK(hipMemset(c->d_sstat, 0, (size_t)hp.n_head * 192 * 8));
     HIPCHK(hipMemset(c->d_ffncnt, 0, (size_t)hp.dec_layers * 1024 * 4));
     HIPCHK(hipMemset(c->d_done, 0, 4));
     HIPCHK(hipMemset(c->d_err, 0, 4));
@@ -1165,7 +1154,6 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
     // granule tags repeat across runs at the same positions: back to zero (no valid tag)
     HIPCHK(hipMemsetAsync(c->d_gran, 0, (size_t)(c->m->hp.n_head + 2 * c->m->hp.n_kv_head) * 128 * 8, c->st));
     HIPCHK(hipMemsetAsync(c->d_sgran, 0, (size_t)c->m->hp.n_head * sgran_ld(c->max_ctx) * 8, c->st));
-    HIPCHK(hipMemsetAsync(c->d_sstat, 0, (size_t)c->m->hp.n_head * 192 * 8, c->st));
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
     const int B = (int)P.size(), H = hp.hidden;
@@ -1227,7 +1215,8 @@ static int step_layers(const qasr_ctx *c) { return c->dbg_layers > 0 ? c->dbg_la
 
 // one decode step for B sequences: token d_tok at position d_pos;
 // splits: attention grid (64-key splits) covering the longest context of the step
-static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange r, int splits) {
+// returns 0, or an error (a launch that declined its shape: nothing runs silently short)
+static int decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange r, int splits) {
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
     const int H = hp.hidden, QD = hp.n_head * 128, KD = hp.n_kv_head * 128, F = hp.dec_ffn;
@@ -1265,8 +1254,6 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         da.stream_blocks = !skinny && c->fuse.att_stream ? c->fuse.slots_stream : 0;
         da.spl_batch = c->fuse.att_spl;
         da.kv_nt = c->fuse.kv_nt;
-        da.fx_pipe = c->fuse.fx_pipe;
-        da.seq_vpf = c->fuse.seq_vpf;
         da.stamp = stamp;
         GemvArgs o{};
         if (skinny) {
@@ -1301,32 +1288,19 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         const bool fusable = skinny && B == 1 && !q8 && !skip;
         unsigned int *att_done = c->d_attdone + (size_t)l * 128;   // this layer's replicas
         if (fusable) da.att_done = att_done;
-        if (fusable && c->fuse.wpf) {   // weights the next launches stream, pulled by the o-proj blocks under the chain
-            da.pf_ptr[0] = L.wgu; da.pf_kib[0] = (unsigned)((size_t)2 * F * H * 2 / 1024);
-            da.pf_ptr[1] = L.wd; da.pf_kib[1] = (unsigned)((size_t)H * F * 2 / 1024);
-            if (l + 1 < nl) { da.pf_ptr[2] = m->dec[l + 1].wqkv; da.pf_kib[2] = (unsigned)((size_t)(QD + 2 * KD) * H * 2 / 1024); }
-        }
         if (fusable && exact && c->fuse.gran) {   // ggml's attention numerics as the fused launch's chain role
-            da.fx = c->fuse.fx_pipe == 2 ? 2 : c->fuse.fx_pipe == 3 ? 3 : 1;   // 2: the splits derive the weights
-                                                    // (attention.hip split_weights); 3: single-wave chain blocks
-            da.sstat = c->d_sstat;
+            da.fx = 1;
             da.sgran = c->d_sgran;
             da.gran = c->d_gran;   // (the fused decision needs the granule hand-off)
             da.layer = l;
         }
         unsigned int *fcnt = c->d_ffncnt + (size_t)l * 1024, *fcnt_next = c->d_ffncnt + (size_t)((l + 1) % nl) * 1024;
-        // the FFN joined to the attention launch: o-proj shards after the gate/up ones, the next layer's re-armed
-        FfnCtl fc{};
-        fc.cnt = fcnt; fc.cnt_next = fcnt_next; fc.ocnt = fcnt + 512; fc.ocnt_next = fcnt_next + 512;
-        fc.att_done = att_done; fc.att_done_next = c->d_attdone + (size_t)((l + 1) % nl) * 128;
-        const bool join_ok = nl >= 2 && !(skip & 24) && c->fuse.ffn;
-        // 0 = separate launches, 1 = QKV + attention in one launch, 2 = + o-projection, 3 = + FFN
-        const int fmode = fusable ? launch_qkv_attention1(q1, da, &o, c->fuse, s, true, join_ok ? &gu : nullptr, &dn, &fc) : 0;
-        const bool o_fused = fmode >= 2, f_joined = fmode == 3;
-        if (l == std::min(c->probe_layer, nl - 1)) {
-            c->probe_o_fused = o_fused;
-            c->probe_lffn = f_joined;
-        }
+        // 0 = separate launches, 1 = QKV + attention in one launch, 2 = + o-projection.  ggml's numerics
+        // in the fused launch need the granule hand-off (the chain role reads the new v from its granule):
+        // without it the exact attention runs as separate launches, never as the fused fp32 split-K form
+        const int fmode = fusable && (!exact || c->fuse.gran) ? launch_qkv_attention1(q1, da, &o, c->fuse, s, true) : 0;
+        const bool o_fused = fmode >= 2;
+        if (l == std::min(c->probe_layer, nl - 1)) c->probe_o_fused = o_fused;
         if (l == 0) {
             c->last_fmode = fmode;
             c->last_fx = fmode && da.fx;
@@ -1337,7 +1311,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             if (fmode) {
                 if (c->fuse.gran) { da.gran = c->d_gran; da.layer = l; }
                 if (l == nl - 1) c->qkv_in_gran = c->fuse.gran != 0;
-                (void)launch_qkv_attention1(q1, da, &o, c->fuse, s, false, join_ok ? &gu : nullptr, &dn, &fc);
+                (void)launch_qkv_attention1(q1, da, &o, c->fuse, s, false);
             } else {
                 if (skinny) {
                     if (!(skip & 1)) launch_gemv(EPI_F32, q1, s);
@@ -1369,7 +1343,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
                 }
             }
         }
-        if (!gb || f_joined) continue;
+        if (!gb) continue;
         if (skinny) {
             if (!o_fused && !(skip & 4)) launch_gemv(EPI_F32, o, s);
             if (o_fused) dn.zero8 = att_done;   // re-arm the fused o-proj's arrival counters
@@ -1418,7 +1392,8 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
             lm.done = c->d_done; lm.tok_out = c->d_tok; lm.hist = c->d_hist; lm.hist_stride = c->hist_cap; lm.step = c->d_step;
             lm.pos = c->d_pos; lm.nkv = c->d_nkv;
             lm.stamp = stamp;
-            (void)launch_lmhead_batch(lm, s);
+            if (!launch_lmhead_batch(lm, s))   // (lmh_one mirrors its shape conditions: never expected)
+                return fail(QASR_ERR_STATE, "decode step: the batched LM head declined B = " + std::to_string(B));
         } else {
             launch_fill_u64(c->d_amax, B, 0ull, s);
             launch_rmsnorm_f16(x, H, nullptr, B, H, m->out_norm, hp.rms_eps, c->d_xh, s);
@@ -1433,6 +1408,7 @@ static void decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange 
         launch_argmax_finish(c->d_amax, B, c->d_tok, c->d_hist, c->hist_cap, c->d_step, s);
         launch_fill_u64(c->d_amax, B, 0ull, s);   // re-arm (zero at rest)
     }
+    return 0;
 }
 
 // Kernel probes (qasr_set_probe): HIP events on the context stream around one
@@ -1460,18 +1436,20 @@ static double probe_bytes(const qasr_ctx *c, int B, int k) {
         double kv = 0;
         for (int b = 0; b < B; b++) kv += (double)(c->run_P[b] + k + 1) * KD * 2 * 2;
         const bool o_in = c->probe_o_fused;
-        const double ffn = c->probe_lffn ? 3 * F * H * wb + H * 4 * 3 : 0.0;   // the joined FFN (batch 1)
-        return (QD + 2 * KD) * H * wb + B * H * 4 + (o_in ? H * QD * wb + B * H * 8 : 0.0) + kv + B * (QD + 2 * KD) * 4 + ffn;
+        return (QD + 2 * KD) * H * wb + B * H * 4 + (o_in ? H * QD * wb + B * H * 8 : 0.0) + kv + B * (QD + 2 * KD) * 4;
     }
-    if (c->probe_lffn) return 0.0;   // the group is empty: its FFN ran in the attention launch
     return 3 * F * H * wb + (c->probe_o_fused ? 0.0 : H * QD * wb) + B * H * 4 * 3;
 }
 
 static int capture(qasr_ctx *c, int B, bool want_logits, StepRange r, int splits, hipGraphExec_t *out) {
     hipGraph_t gr;
     HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
-    decode_step_kernels(c, B, want_logits, r, splits);
+    const int rc = decode_step_kernels(c, B, want_logits, r, splits);
     HIPCHK(hipStreamEndCapture(c->st, &gr));
+    if (rc) {
+        (void)hipGraphDestroy(gr);
+        return rc;
+    }
     HIPCHK(hipGraphInstantiate(out, gr, nullptr, nullptr, 0));
     HIPCHK(hipGraphDestroy(gr));
     return 0;
@@ -1518,8 +1496,8 @@ static int launch_step(qasr_ctx *c, int B, int k) {
     int rc;
     if (!c->eager && (rc = step_graphs(c, splits, &gs))) return rc;
     if (!c->probe || k % c->probe_stride != 0) {
-        if (c->eager) decode_step_kernels(c, B, c->graph_logits, kWholeStep, splits);
-        else HIPCHK(hipGraphLaunch(gs->full, c->st));
+        if (c->eager) return decode_step_kernels(c, B, c->graph_logits, kWholeStep, splits);
+        HIPCHK(hipGraphLaunch(gs->full, c->st));
         return 0;
     }
     while ((int)c->pev.size() < 2 * (k + 1)) {
@@ -1528,15 +1506,22 @@ static int launch_step(qasr_ctx *c, int B, int k) {
         c->pev.push_back(e);
     }
     const int g = c->graph_probe_group;
-    if (c->eager) decode_step_kernels(c, B, c->graph_logits, StepRange{0, g}, splits);
-    else HIPCHK(hipGraphLaunch(gs->pre, c->st));
+    if (c->eager) {
+        if ((rc = decode_step_kernels(c, B, c->graph_logits, StepRange{0, g}, splits))) return rc;
+    } else {
+        HIPCHK(hipGraphLaunch(gs->pre, c->st));
+    }
     HIPCHK(hipEventRecord(c->pev[2 * k], c->st));
     c->cur_stamp = k < c->max_ctx ? c->d_pstamp + (size_t)k * kStampRec : nullptr;
-    decode_step_kernels(c, B, c->graph_logits, StepRange{g, g + 1}, splits);
+    rc = decode_step_kernels(c, B, c->graph_logits, StepRange{g, g + 1}, splits);
     c->cur_stamp = nullptr;
+    if (rc) return rc;
     HIPCHK(hipEventRecord(c->pev[2 * k + 1], c->st));
-    if (c->eager) decode_step_kernels(c, B, c->graph_logits, StepRange{g + 1, 1 << 30}, splits);
-    else HIPCHK(hipGraphLaunch(gs->post, c->st));
+    if (c->eager) {
+        if ((rc = decode_step_kernels(c, B, c->graph_logits, StepRange{g + 1, 1 << 30}, splits))) return rc;
+    } else {
+        HIPCHK(hipGraphLaunch(gs->post, c->st));
+    }
     return 0;
 }
 
@@ -1812,7 +1797,6 @@ extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_pa
     // a caller may repeat a position (same tag): no granule of an earlier call may match
     HIPCHK(hipMemsetAsync(c->d_gran, 0, (size_t)(c->m->hp.n_head + 2 * c->m->hp.n_kv_head) * 128 * 8, c->st));
     HIPCHK(hipMemsetAsync(c->d_sgran, 0, (size_t)c->m->hp.n_head * sgran_ld(c->max_ctx) * 8, c->st));
-    HIPCHK(hipMemsetAsync(c->d_sstat, 0, (size_t)c->m->hp.n_head * 192 * 8, c->st));
     std::vector<int> pos(B), nkv(B);
     for (int b = 0; b < B; b++) {
         if (n_past[b] < 0 || n_past[b] + 1 > c->max_ctx) return fail(QASR_ERR_ARG, "Context length exceeded");
@@ -1829,7 +1813,8 @@ extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_pa
     HIPCHK(hipMemcpyAsync(c->d_pos, pos.data(), B * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemcpyAsync(c->d_nkv, nkv.data(), B * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemsetAsync(c->d_step, 0, 4, c->st));
-    decode_step_kernels(c, B, logits != nullptr, kWholeStep, split_bucket(c, *std::max_element(pos.begin(), pos.end())));
+    if (int rc = decode_step_kernels(c, B, logits != nullptr, kWholeStep, split_bucket(c, *std::max_element(pos.begin(), pos.end()))))
+        return rc;
     HIPCHK(hipGetLastError());
     if (logits) HIPCHK(hipMemcpyAsync(logits, c->d_logits, (size_t)B * c->m->hp.vocab * 4, hipMemcpyDeviceToHost, c->st));
     if (argmax) HIPCHK(hipMemcpyAsync(argmax, c->d_tok, B * 4, hipMemcpyDeviceToHost, c->st));
@@ -2174,7 +2159,7 @@ static int run_stream(qasr_ctx *c, int slots, const std::function<bool(StreamCli
     };
     std::vector<int> pos(S), nkv(S), tok(S);
     std::vector<int32_t> hist;
-    decode_graph(c, S, false, 0);
+    if ((rc = decode_graph(c, S, false, 0))) return rc;
     for (;;) {
         if ((rc = refill())) return rc;
         int live = 0, chunk = c->tok_cb ? 1 : 8, maxpos = 0;
@@ -2197,7 +2182,7 @@ static int run_stream(qasr_ctx *c, int slots, const std::function<bool(StreamCli
         for (int k = 0; k < chunk; k++) {
             const int splits = split_bucket(c, maxpos + k);
             if (c->eager) {
-                decode_step_kernels(c, S, false, kWholeStep, splits);
+                if ((rc = decode_step_kernels(c, S, false, kWholeStep, splits))) return rc;
             } else {
                 qasr_ctx::StepGraphs *gs = nullptr;
                 if ((rc = step_graphs(c, splits, &gs))) return rc;
@@ -2242,8 +2227,12 @@ extern "C" int qasr_run_stream(qasr_ctx *c, int slots, qasr_fetch_fn fetch, qasr
 extern "C" int qasr_run_stream_staged(qasr_ctx *c, int slots, qasr_fetch_staged_fn fetch, qasr_sink_fn sink, void *user,
                                       int max_tokens, int ignore_eos, qasr_stream_stats *stats) {
     if (!fetch) return fail(QASR_ERR_ARG, "bad arguments");
-    return run_stream(c, slots, [&](StreamClip &k) { return (k.id = k.staged = fetch(user, &k.budget)) >= 0; }, sink, user,
-                      max_tokens, ignore_eos, stats);
+    const int pool = (int)c->staged_n.size();
+    return run_stream(c, slots, [&](StreamClip &k) {
+        k.id = fetch(user, &k.budget);
+        k.staged = k.id >= 0 && pool > 0 ? k.id % pool : k.id;   // (ids past the pool reuse its clips)
+        return k.id >= 0;
+    }, sink, user, max_tokens, ignore_eos, stats);
 }
 
 extern "C" int qasr_set_token_callback(qasr_ctx *c, void (*cb)(void *user, int seq, int n_generated, int32_t token), void *user) {
@@ -2573,6 +2562,9 @@ extern "C" int qasr_synth_pcm(uint64_t seed, int n, float *out) {
     synth_pcm(seed, n, out);
     return 0;
 }
+
+// bump with every change to host_util.cpp write_synthetic_gguf's output
+extern "C" int qasr_synthetic_gguf_version(void) { return 5; }
 
 extern "C" int qasr_write_synthetic_gguf(const char *path, const char *config, uint64_t seed, int wtype) {
     std::string err;

@@ -1,6 +1,6 @@
 // ffn_roles.h -- the batch-1 FFN's two workgroup roles (text_decoder.cpp:
 // 545-560: rms_norm * w -> silu(gate) * up -> down + residual), shared by
-// gemv.hip's ffn1_kernel and its experiments: one wave per OPW outputs, the
+// gemv.hip's ffn1_kernel: one wave per OPW outputs, the
 // gemv1_kernel lane split and wave_sum order (bit-identical to gemv1_kernel).
 //
 // Gate/up role: OPW SwiGLU outputs per wave (16-row interleave: output o =
@@ -58,59 +58,16 @@ __device__ __forceinline__ void ffn_wait_shards(const unsigned int *cnt, unsigne
     }
 }
 
-// eight 16-B sc1 loads: 1024 fp32 of lane `p` (lane * 8 + t * 512, t = 0, 1)
-__device__ __forceinline__ void ld_sc1_f32x16(const float *p, u32x4 *v) {
-    asm volatile(
-        "global_load_dwordx4 %0, %4, off sc1\n\t"
-        "global_load_dwordx4 %1, %4, off offset:16 sc1\n\t"
-        "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\t"
-        "global_load_dwordx4 %3, %4, off offset:2064 sc1\n\t"
-        "s_waitcnt vmcnt(0)"
-        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
-        : "v"(p)
-        : "memory");
-}
-
-// joined FFN (c.ocnt): one lane waits for the attention (its att_done replica,
-// as the o-proj blocks do), then the wave polls the o-proj shards (o_need each)
-// when `oshards` (o_need each); wave 0 of the block calls it, the verdict in *ready
-__device__ __forceinline__ void ffn_wait_att(const FfnCtl &c, int blk, bool oshards, int *ready) {
-    const int lane = threadIdx.x & 63;
-    int ok = 1;
-    if (lane == 0) {
-        ok = 0;
-        for (int it = 0; it < c.poll_limit; it++) {
-            if (__hip_atomic_load(c.att_done + (blk & 7) * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= c.att_need) {
-                ok = 1;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(8);
-        }
-    }
-    ok = __shfl(ok, 0, 64);
-    if (ok && oshards) {
-        ffn_wait_shards(c.ocnt, c.o_need, 0, c.poll_limit, c.fence, c.err, DEVERR_GU_WAIT, ready);
-        return;
-    }
-    if (lane == 0) {
-        *ready = ok;
-        if (!ok) __hip_atomic_fetch_or(c.err, (unsigned)DEVERR_GU_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
 // gate/up role, block blk of the role (4 waves x OPW outputs)
 template <int K, int OPW>
 __device__ __forceinline__ void ffn_gu_role(const GemvArgs &g, const GemvArgs &d, const FfnCtl &c, int blk) {
     constexpr int NT = K / 512;
-        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (g.trace && threadIdx.x == 0) g.trace[blk * 8] = rt_now();
     if (blk == 0 && threadIdx.x < 32) {   // re-arm the next layer's shards (their last use ended a step ago)
         c.cnt_next[threadIdx.x * 16] = 0u;
         if (d.zero8 && threadIdx.x < 8) d.zero8[threadIdx.x * 16] = 0u;   // the fused o-proj's counters
-        if (c.ocnt_next) c.ocnt_next[threadIdx.x * 16] = 0u;              // joined: the next layer's o-proj shards
-        if (c.att_done_next && threadIdx.x < 8) c.att_done_next[threadIdx.x * 16] = 0u;   // ... and attention arrivals
     }
-    for (int i = 0; i < c.gdelay; i++) __builtin_amdgcn_s_sleep(8);   // joined: after the QKV and K/V streams
     half8 wv[OPW][2][NT];
 #pragma unroll
     for (int i = 0; i < OPW; i++) {
@@ -122,26 +79,12 @@ __device__ __forceinline__ void ffn_gu_role(const GemvArgs &g, const GemvArgs &d
                 wv[i][q][t] = __builtin_nontemporal_load((const half8 *)(g.W + (32L * (o >> 4) + (o & 15) + 16 * q) * K + t * 512 + lane * 8));
     }
     float xf[NT][8];
-    if (c.ocnt) {   // joined: x is this launch's o-projection output
-        static_assert(NT == 2, "ld_sc1_f32x16 covers K = 1024");
-        __shared__ int xready;
-        if (wid == 0) ffn_wait_att(c, blk, true, &xready);
-        __syncthreads();
-        if (!xready) return;   // reported through the error word
-        u32x4 xv[4];
-        ld_sc1_f32x16(g.x + lane * 8, xv);
 #pragma unroll
-        for (int t = 0; t < NT; t++)
-#pragma unroll
-            for (int e = 0; e < 8; e++) xf[t][e] = __uint_as_float(xv[2 * t + (e >> 2)][e & 3]);
-    } else {
-#pragma unroll
-        for (int t = 0; t < NT; t++) {
-            const float4 a = *(const float4 *)(g.x + t * 512 + lane * 8);
-            const float4 b = *(const float4 *)(g.x + t * 512 + lane * 8 + 4);
-            xf[t][0] = a.x; xf[t][1] = a.y; xf[t][2] = a.z; xf[t][3] = a.w;
-            xf[t][4] = b.x; xf[t][5] = b.y; xf[t][6] = b.z; xf[t][7] = b.w;
-        }
+    for (int t = 0; t < NT; t++) {
+        const float4 a = *(const float4 *)(g.x + t * 512 + lane * 8);
+        const float4 b = *(const float4 *)(g.x + t * 512 + lane * 8 + 4);
+        xf[t][0] = a.x; xf[t][1] = a.y; xf[t][2] = a.z; xf[t][3] = a.w;
+        xf[t][4] = b.x; xf[t][5] = b.y; xf[t][6] = b.z; xf[t][7] = b.w;
     }
     double ss = 0.0;   // ggml_rms_norm: double sum of fp32 squares
 #pragma unroll
@@ -206,12 +149,7 @@ __device__ __forceinline__ void ffn_dn_role(const GemvArgs &d, const FfnCtl &c, 
     // one polling lane per shard, and only once the gate/up stream is nearly
     // done: pollers beside a weight stream cost it bandwidth (MI355X_MICROARCH.md, polling-cost)
     __shared__ int ready;
-    if (wid == 0) {
-        int pre = 1;
-        if (c.ocnt) ffn_wait_att(c, j, false, &pre);   // joined: first the attention (one polling lane)
-        if (__shfl(pre, 0, 64)) ffn_wait_shards(c.cnt, need, c.delay, c.poll_limit, c.fence, c.err, DEVERR_FFN_WAIT, &ready);
-        else if (lane == 0) ready = 0;
-    }
+    if (wid == 0) ffn_wait_shards(c.cnt, need, c.delay, c.poll_limit, c.fence, c.err, DEVERR_FFN_WAIT, &ready);
     __syncthreads();
     if (!ready) return;   // reported through the error word; x keeps its old row
     u32x4 xv[NTD];
@@ -219,9 +157,7 @@ __device__ __forceinline__ void ffn_dn_role(const GemvArgs &d, const FfnCtl &c, 
 #pragma unroll
     for (int r = 0; r < RPW; r++) {
         const int row = (j * 4 + wid) * RPW + r;
-        const float res = c.ocnt ? __uint_as_float(__hip_atomic_load((const uint32_t *)(d.res + row), __ATOMIC_RELAXED,
-                                                                     __HIP_MEMORY_SCOPE_AGENT))
-                                 : d.res[row];
+        const float res = d.res[row];
         float acc = 0.f;
 #pragma unroll
         for (int t = 0; t < NTD; t++) {

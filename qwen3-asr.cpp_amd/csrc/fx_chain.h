@@ -74,32 +74,11 @@ __device__ __forceinline__ f16 fx_key_slow(f16 acc, uint16_t v, float w) {
 }
 
 // keys [j0, min(j0 + DX_Q, n)) of the chunk (relative to its first key) from
-// registers v, in 32-key batches.  w: the weights registers (key 32 L + i in lane L, element i;
-// zero past the chunk's keys); flags: bit L = lane L's batch takes the slow
-// path (a new maximum among its keys, keys past the chunk, or key `last`) --
-// the others take two VALU instructions a key.  Key `last` (relative to the
-// chunk; -1: none) takes vnew instead of its V^T element (the fused launch's
-// new key, whose cache row is being written by another workgroup).
-__device__ __forceinline__ void fx_step1(const u32x4 *v, int j0, int n, const float *w, unsigned long long flags, f16 &acc,
-                                         int last = -1, uint16_t vnew = 0) {
-#pragma unroll
-    for (int bq = 0; bq < DX_Q / DX_B; bq++) {
-        const int jb = j0 + bq * DX_B;
-        const int L = jb / DX_B;
-        if (jb >= n) break;
-        if (!((flags >> L) & 1ull)) {
-#pragma unroll
-            for (int i = 0; i < DX_B; i++) acc = fx_mad1(acc, fx_elem(v, bq * DX_B + i), fx_lane(w[i], L));
-        } else {
-#pragma unroll
-            for (int i = 0; i < DX_B; i++) {
-                const uint16_t e = fx_elem(v, bq * DX_B + i);
-                acc = fx_key_slow(acc, jb + i == last ? vnew : e, fx_lane(w[i], L));
-            }
-        }
-    }
-}
-// fx_step1 with the slow path decided per 8-key group inside a flagged batch:
+// registers v, in 32-key batches, one dimension a lane (the decode chains of
+// fx_decode.h).  w: the weights registers (key 32 L + i in lane L, element i;
+// zero past the chunk's keys); flags: bit L = lane L's batch holds a new
+// maximum or keys past the chunk -- the others take two VALU instructions a
+// key.  In a flagged batch the slow path is decided per 8-key group:
 // kb = this lane's new-maximum bits (bit i: key 32 lane + i, fx_weights_reg),
 // read for batch L by v_readlane; groups without a maximum take the fast path
 // (keys past n carry zero weights: exact no-ops there)
@@ -128,7 +107,7 @@ __device__ __forceinline__ void fx_step1_m(const u32x4 *v, int j0, int n, const 
         }
     }
 }
-// fx_step1 with the weights in LDS instead of registers (the fused launch's
+// fx_step1_m with the weights in LDS instead of registers (the fused launch's
 // chain role): ws = the head's signed weights, FX_ST floats per 32-key row
 // (row L = lane L's keys of fx_weights_reg).  Per 8 keys the weights arrive
 // as two uniform ds_read_b128 (VGPR operands of v_fma_mix_f32), requested one
@@ -146,6 +125,12 @@ __device__ __forceinline__ void fx_step1_m(const u32x4 *v, int j0, int n, const 
 // against 17.1 with an s_nop 0 -- the padding hipcc adds in front of an asm
 // statement that reads a just-written VGPR)
 #define FX_CVT "v_cvt_f16_f32 %1, %0\n\t"
+#ifdef FX_R1_DIAG   // (timing diagnostic, tools/r5: single-rounding v_fma_mixlo_f16 chain)
+#undef FX_MIX
+#undef FX_CVT
+#define FX_MIX(VI, W, SEL) "v_fma_mixlo_f16 %1, " VI ", " W ", %1 op_sel:[" SEL ",0,0] op_sel_hi:[1,0,1]\n\t"
+#define FX_CVT ""
+#endif
 __device__ __forceinline__ void fx8_fast(f16 &acc, const u32x4 v, const floatx4 wa, const floatx4 wb) {
     float t;
     asm volatile(FX_MIX("%2", "%6", "0") FX_CVT FX_MIX("%2", "%7", "1") FX_CVT FX_MIX("%3", "%8", "0") FX_CVT
@@ -249,33 +234,6 @@ __device__ __forceinline__ void fx_step1_lds_m(const u32x4 *v, int j0, const flo
             fx8_fast(acc, v[g8], wa, wb);
             wa = na;
             wb = nb;
-        }
-    }
-}
-// fx_step1_lds_m with the weights requested two groups ahead: (wa, wb) = keys
-// j0 .. j0 + 7, (wc, wd) = j0 + 8 .. j0 + 15 on entry, the same for j0 + DX_Q
-// on exit (one group of LDS latency was not enough to cover the reads:
-// tools/micro/chain_role.hip, 15.4 cycles a key from LDS vs 11.7 from fixed
-// registers).  Reads past the chunk's image land in padding or another
-// head's rows and are never consumed.
-__device__ __forceinline__ void fx_step1_lds_m2(const u32x4 *v, int j0, const float *ws, unsigned long long m64, f16 &acc,
-                                                floatx4 &wa, floatx4 &wb, floatx4 &wc, floatx4 &wd) {
-    if (__builtin_expect(m64 != 0ull, 0)) {
-#pragma unroll
-        for (int g8 = 0; g8 < DX_Q / 8; g8++) {
-            floatx4 na, nb;
-            fx_w8(ws, j0 + 8 * g8 + 16, na, nb);
-            if (((m64 >> (8 * g8)) & 0xffull) != 0) fx8_slow(acc, v[g8], wa, wb);
-            else fx8_fast(acc, v[g8], wa, wb);
-            wa = wc; wb = wd; wc = na; wd = nb;
-        }
-    } else {
-#pragma unroll
-        for (int g8 = 0; g8 < DX_Q / 8; g8++) {
-            floatx4 na, nb;
-            fx_w8(ws, j0 + 8 * g8 + 16, na, nb);
-            fx8_fast(acc, v[g8], wa, wb);
-            wa = wc; wb = wd; wc = na; wd = nb;
         }
     }
 }

@@ -6,7 +6,6 @@
 #pragma once
 #include "dev_common.h"
 #include "fx_chain.h"
-#include "fx_pipe.h"
 #include "kernels.h"
 
 namespace qasr {
@@ -29,16 +28,12 @@ namespace qasr {
 // turn, the next step's loads issued before the current step's arithmetic --
 // unconditionally (blocks past the sequence re-read its last one, fx_loadQ),
 // so the wait counts stay exact.  c0: the first key of the current weights chunk.
-// FX_VNB register buffers in turn (static indices: the loop body is unrolled
-// over them), FX_VNB - 1 of them in flight ahead of the one in use.  Two (one
-// of lead): four measured slower at 64 x 30 s (the QKV + attention group
-// 30.2 -> 32.4 us, 164 VGPRs) -- the batch chain does not wait on V^T latency.
-#ifndef FX_VNB
-#define FX_VNB 2
-#endif
+// Two register buffers (one of lead): four measured slower at 64 x 30 s (the
+// QKV + attention group 30.2 -> 32.4 us, 164 VGPRs) -- the batch chain does not
+// wait on V^T latency.
 __device__ __forceinline__ void fx_chain1(const uint16_t *__restrict__ vt, int loff, int c0, int n, int lastb, const float *w,
                                           unsigned long long flags, uint32_t kb, f16 &acc) {
-    constexpr int NB = FX_VNB;
+    constexpr int NB = 2;
     u32x4 v[NB][DX_Q / 8];
 #pragma unroll
     for (int i = 0; i < NB - 1; i++) fx_loadQ(v[i], vt, loff, c0 + i * DX_Q, lastb);
@@ -64,10 +59,6 @@ __device__ __forceinline__ void decode_attn_exact_body(const DecodeAttnArgs &a, 
     const uint16_t *vcol = a.vt + ((long)b * a.n_kv_head + g) * 128 * vtc + 64 * wu * 8;   // the wave's key block 0
     float M = -INFINITY, S = 0.0f;
     f16 acc = 0;
-    if (a.fx_pipe == 1) {   // the weights one 64-key buffer ahead of the chain (fx_pipe.h), every key in the loop
-        float wl;
-        S = fxp_chain(FxpScores{sg, nkv}, vcol, 8 * lane, nkv, (nkv - 1) >> 3, acc, wl);
-    } else
     for (int c0 = 0; c0 < nkv; c0 += DX_KC) {
         const int n = min(DX_KC, nkv - c0);
         float w[DX_B], wl;

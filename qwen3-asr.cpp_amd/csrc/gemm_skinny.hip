@@ -183,6 +183,7 @@ __global__ __launch_bounds__(64 * KW) void gemm_skinny_kernel(GemmArgs g) {
                                                                        __builtin_bit_cast(half8, wb[buf][j][s]), acc[i][j], 0, 0, 0);
     };
     if constexpr (ALDS && CPW > 0) {
+        static_assert(CPW <= 4, "the per-chunk vmcnt waits below are written out for at most 4 chunks");
         uint16_t *my = alds + wid * (CPW * MT * 16 * 128);
         u32x4 wq[CPW][NT][4];
 #pragma unroll
@@ -367,6 +368,7 @@ __global__ __launch_bounds__(64 * KW) void gemm_skinny_q8_kernel(GemmArgs g) {
         }
     };
     if constexpr (ALDS && CPW > 0) {   // every chunk of the wave in flight at once (gemm_skinny_kernel's CPW)
+        static_assert(CPW <= 4, "the per-chunk vmcnt waits below are written out for at most 4 chunks");
         uint8_t *my = (uint8_t *)lds_raw + wid * (CPW * MT * 16 * 128);
         long wq[CPW][NT][4];
         uint2 wdq[CPW][NT];

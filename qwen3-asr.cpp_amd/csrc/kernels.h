@@ -141,7 +141,6 @@ enum DevErr : unsigned {
     DEVERR_O_WAIT = 2u,      // fused o-projection gave up on the attention combiners
     DEVERR_FFN_WAIT = 4u,    // fused down-projection gave up on the gate/up blocks
     DEVERR_SCORE_WAIT = 8u,  // fused exact attention: the chain gave up on the splits' score granules
-    DEVERR_GU_WAIT = 16u,    // FFN joined to the attention launch: gate/up gave up on the o-projection
 };
 struct FuseCfg {
     int ffn = 1, qkv = 1, o = 1;        // fused launches on/off
@@ -159,8 +158,8 @@ struct FuseCfg {
     int fa_exact_prefill = 1;           // prefill attention with ggml's CPU FA numerics (fa_exact.hip)
     int fa_exact_decode = 1;            // decode attention likewise: 1 on (every model and batch; batch 1 f16 in the
                                         // fused launch's chain role), 0 off (fp32 V accumulation, split-K)
-    int fx_delay = 0, fx_vpf = 2;       // batch-1 fused exact attention: chain first-poll delay (unused), V^T pulled
-                                        // into L2 ahead of the chain (DecodeAttnArgs.fx_vpf bits)
+    int fx_vpf = 2;                     // batch-1 fused exact attention: V^T pulled into L2 ahead of the chain
+                                        // (DecodeAttnArgs.fx_vpf bits)
     int slots_ffn = 0, slots_qkv64 = 0, slots_qkv128 = 0;   // co-resident workgroups on this device
     int att_stream = 1;                 // decode batches: one workgroup per (kv group, sequence) (decode_attn_seq_kernel)
     int skinny = 1;                     // decode batches: the weight-streaming skinny GEMMs (0 = tiled GEMMs)
@@ -172,21 +171,6 @@ struct FuseCfg {
                                         // (decode_attn_seq_kernel<1>) where the per-sequence kernel is taken
     int lmh = 1;                        // decode batches of f16 models (9..64 rows): the LM head in one launch (lmhead.hip)
     int skinny_inf = 1;                 // decode-batch skinny GEMMs: all of a wave's K chunks in flight (gemm_skinny.hip CPW)
-    int wpf = 0;                        // batch 1 fused: the o-proj blocks pull the FFN and next-layer QKV weights during the
-                                        // chain (DecodeAttnArgs.pf_ptr); off: configs[1] 241.4 vs 251.9 RTFx with it (the
-                                        // pulls delay the chain's score gather ~3 us, ffn1 no faster: 8.02 vs 7.95 us)
-    int seq_vpf = 0;                    // decode batches, one-launch exact attention: V^T pulled into L2 beside the K stream
-                                        // (off: 64 x 30 s, layer 14 attention group 30.2 -> 38.1 us with it)
-    int lffn = 0;                       // batch 1 fused: the FFN (gate/up + down) joins the QKV + attention + o-proj
-                                        // launch, its weights in registers while the chain runs (attention.hip); off:
-                                        // bit-identical but the o-proj -> gate/up fan-in (256 arrivals, 640 polling
-                                        // waves) cost more than the kernel boundary + weight stream it replaced
-                                        // (configs[1] 238.2 vs 254.7 RTFx, layer launch 38.6 us vs 26.3 + 5.0 us)
-    int lffn_gdelay = 30, lffn_wdelay = 40;   // ... gate/up and down weight requests after that many ~0.2 us
-    int fx_pipe = 0;                    // exact decode chains: 1 = weights one 64-key buffer ahead, SGPR operands (fx_pipe.h);
-                                        // 2 = batch 1 fused: the splits compute the weights (split_weights), the chain
-                                        // role reads them (fx1_chain_w); 3 = single-wave chain blocks (fx1_chain_1w);
-                                        // other paths as 0
     unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
 };
 // co-resident workgroup capacity of the fused kernels on the current device
@@ -197,14 +181,6 @@ struct FfnCtl {
     unsigned int *cnt, *cnt_next;   // this layer's 32 gate/up arrival shards (16-word stride), the next layer's
     unsigned int *err;              // sticky device error word
     int wdelay, delay, poll_limit, fence;
-    // FFN joined to the batch-1 attention launch (FuseCfg::lffn; null/0 in ffn1_kernel): the o-projection blocks
-    // count into ocnt's 32 shards (8 each); both roles first wait for the attention (att_done replica blk % 8 at
-    // att_need, one polling lane, as the o-proj blocks), x and the residual are read with sc1 loads; the gate/up
-    // blocks request their weights after gdelay x ~0.2 us and re-arm the next layer's ocnt / att_done shards
-    unsigned int *ocnt, *ocnt_next, *att_done_next;
-    const unsigned int *att_done;
-    unsigned att_need, o_need;       // attention arrivals per replica; o-proj arrivals per ocnt shard
-    int gdelay;
 };
 // gemv.hip: batch-1 f16 gate/up + down in one launch; cnt = this layer's
 // 32 x 16 words (zero on entry), cnt_next = the next layer's, re-armed here
@@ -335,18 +311,8 @@ struct DecodeAttnArgs {
     // o-projection role (att_done)
     int fx;
     unsigned long long *sgran;           // row stride sgran_ld(max_ctx) (16-B aligned granule pairs)
-    int fx_delay;                        // chain workgroups: first score poll after fx_delay x ~0.2 us
     int fx_vpf;                          // bit 0: the splits pull their keys' V^T rows into their XCD's L2 for the
-                                         // chain; bit 1: the chain workgroups pull their own (LDS-DMA, while waiting);
-                                         // bit 2: the o-proj blocks of the chain's XCD pull them (oproj1_body)
-    unsigned long long *sstat;           // fx = 2: the splits' maxima and 32-key group S sums, [n_head][192] granules
-    int fx_pipe;                         // every exact decode chain derives its weights one 64-key buffer ahead
-                                         // (fx_pipe.h; FuseCfg::fx_pipe) instead of all of them first (fx_chain.h)
-    unsigned int *ocnt;                  // fused o-proj: rows written through and counted into 32 shards (the joined FFN)
-    const uint16_t *pf_ptr[3];           // batch-1 fused o-proj blocks: weight regions pulled into the caches while they
-    unsigned pf_kib[3];                  // wait for the chain (the FFN's, the next layer's QKV), KiB each (0 = none)
-    int seq_vpf;                         // decode_attn_seq_kernel<1>: each 64-key K step also pulls the chain's V^T rows
-                                         // of those keys into L2 (FuseCfg::seq_vpf)
+                                         // chain; bit 1: the chain workgroups pull their own (LDS-DMA, while waiting)
 };
 // the decode attention with ggml's CPU flash-attention numerics (fa_exact.hip),
 // after launch_decode_attention in scores mode: per (query head, sequence) the
@@ -363,11 +329,8 @@ void launch_decode_attention(const DecodeAttnArgs &a, hipStream_t s);
 // (and, when o is the plain batch-1 o-projection, that too); returns 0 = not
 // taken, 1 = QKV + attention, 2 = QKV + attention + o-projection
 // dry = true: only the decision (nothing launched)
-// gu / dn / fc (optional): the batch-1 FFN of launch_ffn1 joined to the launch
-// after the o-projection (FuseCfg::lffn; returns 3 when taken)
 int launch_qkv_attention1(const GemvArgs &q, const DecodeAttnArgs &a, const GemvArgs *o, const FuseCfg &cfg, hipStream_t s,
-                          bool dry = false, const GemvArgs *gu = nullptr, const GemvArgs *dn = nullptr,
-                          const FfnCtl *fc = nullptr);
+                          bool dry = false);
 int decode_split_len();
 int decode_max_splits();
 

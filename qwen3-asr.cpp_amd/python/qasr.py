@@ -29,7 +29,7 @@ EXPORTS = [
     "qasr_ctx_set_option", "qasr_ctx_get_option", "qasr_debug_read",
     "qasr_set_token_callback", "qasr_set_profile", "qasr_profile_report",
     "qasr_detokenize", "qasr_tokenize",
-    "qasr_load_wav", "qasr_write_wav", "qasr_synth_pcm", "qasr_write_synthetic_gguf",
+    "qasr_load_wav", "qasr_write_wav", "qasr_synth_pcm", "qasr_write_synthetic_gguf", "qasr_synthetic_gguf_version",
     "qasr_align", "qasr_align_tokenize", "qasr_model_load_korean_dict", "qasr_fix_timestamps",
     "qasr_align_prompt_len", "qasr_align_json", "qasr_align_json_batch", "qasr_align_words",
 ]
@@ -106,6 +106,7 @@ def lib() -> C.CDLL:
             "qasr_load_wav": ([C.c_char_p, F, I, IP], I), "qasr_write_wav": ([C.c_char_p, F, I, I], I),
             "qasr_synth_pcm": ([C.c_uint64, I, F], I),
             "qasr_write_synthetic_gguf": ([C.c_char_p, C.c_char_p, C.c_uint64, I], I),
+            "qasr_synthetic_gguf_version": ([], I),
             "qasr_align": ([P, F, I, I32P, I, I32P, I, IP, C.POINTER(Timings)], I),
             "qasr_align_tokenize": ([P, C.c_char_p, C.c_char_p, I32P, I, IP], I),
             "qasr_model_load_korean_dict": ([P, C.c_char_p], I),

@@ -48,6 +48,17 @@ def max_over_ranks(value: float, dist, device=None) -> float:
     return float(t.item())
 
 
+def gather_floats(value: float, dist, device=None) -> List[float]:
+    """every rank's value (rank order), on every rank"""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [float(value)]
+    import torch
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]
+
+
 def gather_tokens(local: dict, dist, device=None):
     """local: {utterance_index: [token ids]} on every rank.  Returns the merged
     dict on rank 0 (None elsewhere).  Two collectives: an all_gather of the
@@ -183,9 +194,12 @@ def run_queue(stream: Callable[[Callable], Dict[int, List[int]]], utts: Sequence
     if after is not None and local:
         idx = sorted(local)
         after(idx, [local[i] for i in idx])
+    own = time.perf_counter() - t0   # this rank's stream (+ after) done: its own wall time, before the barrier
     if dist is not None and dist.is_initialized():
         dist.barrier()
     wall = max_over_ranks(time.perf_counter() - t0, dist, device)
+    rank_walls = gather_floats(own, dist, device)
     merged = gather_tokens(local, dist, device)
     return {"tokens": merged, "wall_s": wall, "audio_s": sum(lengths) / 16000.0,
-            "decode_tokens": sum(budget(n, tok_rate) for n in lengths), "local": local, "batches": None}
+            "decode_tokens": sum(budget(n, tok_rate) for n in lengths), "local": local, "batches": None,
+            "rank_wall_s": rank_walls, "rank_utterances": gather_floats(len(local), dist, device)}

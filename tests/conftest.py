@@ -63,6 +63,15 @@ def full_f16_gguf(built, tmp_path_factory):
 
 
 @pytest.fixture(scope="session")
+def full_q8_gguf(built, tmp_path_factory):
+    """the Qwen3-ASR-0.6B-shaped synthetic Q8_0 GGUF (seed 42; configs[2]'s weights)"""
+    import qasr
+    p = str(tmp_path_factory.mktemp("fq8") / "full-q8.gguf")
+    qasr.write_synthetic_gguf(p, "full", 42, 8)
+    return p
+
+
+@pytest.fixture(scope="session")
 def tiny_oracle(tiny_gguf):
     import oracle_py as op
     op.set_threads(min(8, os.cpu_count() or 1))

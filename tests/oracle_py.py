@@ -156,6 +156,9 @@ def olib():
         L.qo_align_forward.argtypes = [C.POINTER(QoModel), C.POINTER(C.c_int32), I, F, I, I, C.POINTER(I), I, F, I]
         L.qo_f32_to_f16.argtypes = [C.c_float]
         L.qo_f32_to_f16.restype = C.c_uint16
+        for fn in (L.qo_f16_mad_round1, L.qo_f16_mad_round2):
+            fn.argtypes = [C.c_uint16, C.c_float, C.c_uint16]
+            fn.restype = C.c_uint16
         _olib = L
     return _olib
 
@@ -188,6 +191,7 @@ class OracleModel:
 
     GELU_EXACT = 1
     FA_V_F32 = 2
+    FA_V_ROUND1 = 4   # fp16 V accumulation with one rounding per key (qasr_oracle.h QO_FA_V_ROUND1)
 
     def __init__(self, path: str):
         g = Gguf(path)

@@ -137,6 +137,9 @@ def _queue_worker(rank, world, port, q):
             _t.sleep(0.01 * (1 + 2 * rank))
             out[i] = [i] * b
     res = run_queue(stream, utts, rank, world, 3.5, dist, key="qtest")
+    # every rank's own stream time and utterance count, gathered (the bench's tail imbalance)
+    assert len(res["rank_wall_s"]) == world and res["rank_wall_s"][rank] <= res["wall_s"]
+    assert res["rank_utterances"][rank] == len(res["local"]) and sum(res["rank_utterances"]) == len(utts)
     q.put((rank, sorted(res["local"]), res["tokens"]))
     dist.barrier()
     dist.destroy_process_group()
@@ -229,3 +232,33 @@ def test_bench_batch_group_traffic(tmp_path, monkeypatch):
     assert bench.pmc_group_traffic(3, 64, False) == (33 + 22, "profiles/r9/batch/f16/summary.json")
     assert bench.pmc_group_traffic(2, 32, False) == (None, None)
     assert bench.pmc_group_traffic(2, 64, True) == (None, None)
+
+
+def test_bench_gpus_counts_this_node_under_a_multinode_launch():
+    """--gpus is this node's GPU count -- under a launcher that is
+    LOCAL_WORLD_SIZE, not WORLD_SIZE.  Four ranks as two 'nodes' of two
+    (WORLD_SIZE = 4, LOCAL_WORLD_SIZE = 2) each run `bench.py --gpus 2
+    --dry-run`: all four join the gloo group and rank 0 prints n_gpus = 4;
+    --gpus 4 on the same layout is refused before any work."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import bench_port
+    port = bench_port.free_port()
+    base = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+
+    def launch(gpus):
+        ps = []
+        for r in range(4):
+            env = dict(base, WORLD_SIZE="4", RANK=str(r), LOCAL_RANK=str(r % 2), LOCAL_WORLD_SIZE="2",
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            ps.append(subprocess.Popen([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(gpus), "--dry-run"],
+                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+        return [(p.wait(timeout=300), *p.communicate()) for p in ps]
+    outs = launch(2)
+    assert all(rc == 0 for rc, _, _ in outs), [e[-800:] for _, _, e in outs]
+    lines = [ln for _, o, _ in outs for ln in o.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 4, lines
+    bad = launch(4)
+    assert all(rc != 0 and "LOCAL_WORLD_SIZE" in e for rc, _, e in bad), [(rc, e[-300:]) for rc, _, e in bad]

@@ -154,13 +154,7 @@ def test_full_lds_dma_gemm_bit_identical(full):
     assert np.array_equal(single, out[0][0][3])
 
 
-FUSE_KNOBS = {"QASR_FUSE_FFN": dict(fuse_ffn=0), "QASR_FUSE_QKV": dict(fuse_qkv=0, fuse_o=0), "QASR_FUSE_O": dict(fuse_o=0),
-              "QASR_LFFN": dict(lffn=1),   # (the joined FFN is an option: on against the default's off)
-              # single-wave chain blocks on the default weights path (option): the same bits.  (fx_pipe 1 and 2
-              # sum the softmax denominator S in another order -- per lane / per 32-key group -- so their logits
-              # differ from the default's in the last bits; each equals its own separate-launch path.)
-              "QASR_FX_PIPE3": dict(fx_pipe=3),
-              "QASR_FX_VPF4": dict(fx_vpf=4)}   # the chain's V^T pulled by the o-proj blocks (option): a prefetch only
+FUSE_KNOBS = {"QASR_FUSE_FFN": dict(fuse_ffn=0), "QASR_FUSE_QKV": dict(fuse_qkv=0, fuse_o=0), "QASR_FUSE_O": dict(fuse_o=0)}
 
 
 def _step_state(c, ids, feats, pos, tok=1234):
@@ -223,8 +217,8 @@ def test_full_decode_from_position_zero(full):
             for k, tok in enumerate([151644, 8948, 198]):
                 lg, _ = c1.decode_step([tok], [k])
                 lgs.append(lg[0].copy())
-                # fused: QKV + attention + o-proj (+ the joined FFN, mode 3, when option lffn is on)
-                assert c1.get_option("fused_exact") == fused and c1.get_option("fused_mode") == (2 + c1.get_option("lffn")) * fused
+                # fused: QKV + attention + o-proj (mode 2)
+                assert c1.get_option("fused_exact") == fused and c1.get_option("fused_mode") == 2 * fused
             out[fused] = lgs
     finally:
         c1.close()
@@ -269,7 +263,7 @@ def test_full_fused_wait_timeout_is_an_error(full):
         assert c1.get_option("slots_ffn") >= 1024 + 256 and c1.get_option("slots_qkv") >= 512 + 8 * 4 + 8 + 256
         pcm = qasr.synth_pcm(14000, 2 * SR)
         ref = c1.transcribe([pcm], max_tokens=4, ignore_eos=True).tokens
-        for k, v in (("poll_limit", 1), ("ffn_delay", 0), ("ffn_wdelay", 0), ("qkv_delay", 0), ("o_delay", 0), ("fx_delay", 0)):
+        for k, v in (("poll_limit", 1), ("ffn_delay", 0), ("ffn_wdelay", 0), ("qkv_delay", 0), ("o_delay", 0)):
             c1.set_option(k, v)
         with pytest.raises(qasr.QasrError, match="timed out"):
             c1.transcribe([pcm], max_tokens=4, ignore_eos=True)
@@ -354,15 +348,14 @@ def test_full_configs1_92s(full, parity):
     print("configs[1] decode steps (abs, rel):", [(round(a_, 4), round(r_, 5)) for a_, r_ in errs])
     r = c.transcribe([pcm], max_tokens=16, ignore_eos=True)
     parity("configs1_92s_prefill_and_15_steps", prefill_abs=ab, prefill_rel=rel, steps_abs=[e[0] for e in errs],
-           steps_rel=[e[1] for e in errs], scale=float(np.abs(lo[1]).max()), greedy16_equal=r.tokens[0] == toks,
-           fx_pipe=c.get_option("fx_pipe"))
+           steps_rel=[e[1] for e in errs], scale=float(np.abs(lo[1]).max()), greedy16_equal=r.tokens[0] == toks)
     assert rel <= REL_LOGITS and ab <= ABS_LOGITS, (ab, rel)
     assert max(r_ for _, r_ in errs) <= REL_LOGITS and max(a_ for a_, _ in errs) <= ABS_LOGITS, errs
     assert r.tokens[0] == toks
 
 
 @pytest.mark.timeout(900)
-def test_full_configs2_q8_b64_30s(gpu, tmp_path_factory, parity):
+def test_full_configs2_q8_b64_30s(gpu, full_q8_gguf, parity):
     """configs[2] at its full size: Qwen3-ASR-0.6B Q8_0 (synthetic weights),
     64 x 30 s clips (P = 405 prompt tokens each, 105-token budget).  All 64
     rows bit-identical (identical clips), every budget met, and row 0 against
@@ -371,8 +364,7 @@ def test_full_configs2_q8_b64_30s(gpu, tmp_path_factory, parity):
     oracle's own sensitivity to a 1e-6 perturbation of the encoder features,
     whichever is larger).  The decode attention runs the exact (fp16 V
     accumulation) kernels, the Q8_0 default."""
-    p = str(tmp_path_factory.mktemp("fq8") / "full-q8.gguf")
-    qasr.write_synthetic_gguf(p, "full", 42, 8)
+    p = full_q8_gguf
     op.set_threads(min(16, os.cpu_count() or 1))
     om = op.OracleModel(p)
     m = qasr.Model(p)
@@ -505,3 +497,81 @@ def test_full_skinny_inflight_bit_identical(full):
             assert np.array_equal(out[0], out[1]), (B, float(np.abs(out[0] - out[1]).max()))
         finally:
             c.close()
+
+
+def test_full_q8_skinny_inflight_bit_identical(gpu, full_q8_gguf):
+    """the Q8_0 skinny GEMMs (gemm_skinny_q8_kernel, CPW chunks in
+    flight with hand-counted vmcnt waits) against the one-chunk loop
+    (skinny_inf = 0) at 16 and 64 rows of the full-size Q8_0 model (K = 1024 /
+    2048 / 3072: 1-3 chunks a wave): bit-identical decode-step logits."""
+    m = qasr.Model(full_q8_gguf)
+    try:
+        rng = np.random.default_rng(31)
+        ids = [int(t) for t in rng.integers(0, 151643, 40)]
+        for B in (16, 64):
+            c = qasr.Context(m, max_batch=B, max_ctx=64)
+            try:
+                toks = [int(t) for t in np.random.default_rng(B).integers(0, 151643, B)]
+                out = {}
+                for inf in (1, 0):
+                    c.set_option("skinny_inf", inf)
+                    c.prefill([ids] * B, want_logits=False)
+                    lg, _ = c.decode_step(toks, [len(ids)] * B)
+                    out[inf] = lg.copy()
+                assert np.isfinite(out[1]).all()
+                assert np.array_equal(out[0], out[1]), (B, float(np.abs(out[0] - out[1]).max()))
+            finally:
+                c.close()
+    finally:
+        m.close()
+
+
+# Every per-context option that engine.hip's fuse_options() reads from the
+# environment (QASR_<NAME>) and no other test switches: the value a user could
+# set against the default, and what it must give.  "bits": the same arithmetic
+# in another launch shape, schedule or prefetch -- decode-step logits, prefill
+# logits and greedy tokens bit-identical to the default; "oracle": another
+# arithmetic (the oracle switch named) within the decoder bars.  Batch-1
+# options run on a 1-row context (the fused launches), batch options on 16 rows.
+OPTION_CASES = {
+    "ffn_delay": (0, "bits", 1), "ffn_wdelay": (0, "bits", 1), "qkv_delay": (0, "bits", 1), "o_delay": (0, "bits", 1),
+    "handoff_fence": (1, "bits", 1), "gran": (0, "bits", 1), "att_spl1": (128, "bits", 1),
+    "fx_vpf": (0, "bits", 1), "fx_vpf=1": (1, "bits", 1), "fx_vpf=3": (3, "bits", 1),
+    "fa_exact_prefill": (0, "oracle", 1),
+    "att_spl": (128, "bits", 16), "lmh": (0, "bits", 16), "skinny": (0, "oracle", 16),
+}
+
+
+@pytest.mark.parametrize("case", list(OPTION_CASES))
+def test_full_option_matches_default(full, case):
+    m, _, om = full
+    name = case.split("=")[0]
+    val, kind, B = OPTION_CASES[case]
+    pcm = qasr.synth_pcm(19000, 2 * SR)
+    feats = om.encode(op.log_mel(pcm))
+    ids, pos = m.build_prompt(feats.shape[0])
+    c = qasr.Context(m, max_batch=B, max_ctx=160)
+    try:
+        def run():
+            lp, _ = c.prefill([ids] * B, [feats] * B, [pos] * B)
+            lp = lp.copy()
+            lg, _ = c.decode_step([1234] * B, [len(ids)] * B)
+            toks = c.transcribe([pcm] * B, max_tokens=8, ignore_eos=True).tokens
+            return lp, lg.copy(), toks
+        base = run()
+        c.set_option(name, val)
+        assert c.get_option(name) == val
+        alt = run()
+    finally:
+        c.close()
+    if kind == "bits":
+        assert np.array_equal(base[0], alt[0]) and np.array_equal(base[1], alt[1]), case
+        assert base[2] == alt[2], case
+    else:
+        flags = op.OracleModel.FA_V_F32 if name == "fa_exact_prefill" else 0
+        d = op.OracleDecoder(om, 160, flags)
+        lo = d.forward(ids, 0, feats, pos)
+        for b in range(B):
+            ab, rel = _err(alt[0][b], lo)
+            assert rel <= REL_LOGITS and ab <= ABS_LOGITS, (case, b, ab, rel)
+        assert all(t == alt[2][0] for t in alt[2])

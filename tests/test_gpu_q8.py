@@ -25,6 +25,7 @@ from test_gpu_parity import _margin_aware_equal, _stats
 pytestmark = pytest.mark.gpu
 
 SR = 16000
+Q8_STEP_ABS = 0.3   # the decode-step bar: measured max 0.19 (profiles/r4/parity.json) with ~50 % margin
 
 
 @pytest.fixture(scope="module")
@@ -95,11 +96,13 @@ def test_q8_prefill_and_decode_match_oracle(tq8, tiny_q8_oracle, parity):
     # the twin's decode steps see the perturbation only through the fp16 KV
     # cache, which absorbs it (noise is usually 0 here), so the bound is the
     # rounding-flip amplitude itself: one int8 quantum flip in an activation
-    # block moves a logit by ~1 % of its range.  Every step <= 2 % of the
-    # scale (a max bar, no typical-step clause).
+    # block moves a logit by ~1 % of its range.  Measured (profiles/r4/parity.json):
+    # max 0.19, median 0.14 at a logit scale of 19.5.  Bars: max <= 0.3 absolute
+    # (and <= 2 % of the scale), median <= 1 % of the scale.
     parity("tiny_q8_prefill_and_12_steps", prefill_abs=float(np.abs(lg0 - lo0).max()), prefill_tol=tol, steps_abs=errs,
            steps_noise=noise, scale=scale)
-    assert max(errs) <= max(2e-2 * scale, 4 * max(noise)), (errs, noise)
+    assert max(errs) <= min(Q8_STEP_ABS, 2e-2 * scale), (errs, noise)
+    assert float(np.median(errs)) <= 1e-2 * scale, errs
 
 
 @pytest.mark.parametrize("path", ["f16", "q8"])

@@ -9,6 +9,8 @@
 //   6: single-rounding chain, VGPR weights (v_fma_mixlo_f16: one op a key)
 //   7: as 2, readlanes batched at the group's start
 //   8/9: LDS broadcast 1 / 2 groups ahead without the memory clobber
+//   17/18: mixlo with LDS weights one / two groups ahead; 19: mixlo, two dimensions a lane;
+//   20/21: two rows x two dimensions (the prefill chain) by mix/cvt_pk and by mixlo
 //   13/14: two dimensions a lane (packed accumulator, v_cvt_pk_f16_f32), LDS / SGPR weights
 //   10/12: weights by s_load_dwordx8 (glc / K$) one group ahead; 11: x16 glc, 16-key double buffer
 // One wave per SIMD (8 workgroups of 4 waves), clock64 around 1024 groups.
@@ -16,8 +18,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
-#include "../../qwen3-asr.cpp_amd/csrc/fx_pipe.h"
-using qasr::fxp_buffer;
+#include "../../qwen3-asr.cpp_amd/csrc/dev_common.h"
 
 
 #define G 1024
@@ -209,15 +210,76 @@ __global__ __launch_bounds__(256) void k(const u32x4 *vin, const float *win, lon
                                [w4] "s"(s4), [w5] "s"(s5), [w6] "s"(s6), [w7] "s"(s7));
             }
             acc = __builtin_bit_cast(f16, (uint16_t)(a2 ^ (a2 >> 16)));
-        } else if constexpr (MODE == 15 || MODE == 16) {
-            // fx_pipe.h's fxp_buffer (8 group blocks, lane-indexed readlanes) on
-            // register V; 15: fast buffer (m64 = 0), 16: the checked form (one record)
-            u32x4 vb8[8] = {v, v, v, v, v, v, v, v};
-            int ww[8] = {s0, s1, s2, s3, s4, s5, s6, s7};
-            fxp_buffer(acc, vb8, ww, wl, wl, MODE == 15 ? 0ull : (unsigned long long)__builtin_amdgcn_readfirstlane(g & 1) << 33);
-            s0 = ww[0]; s1 = ww[1]; s2 = ww[2]; s3 = ww[3]; s4 = ww[4]; s5 = ww[5]; s6 = ww[6]; s7 = ww[7];
-            g += 7;
+        } else if constexpr (MODE == 17 || MODE == 18) {
+            // single rounding with the weights by LDS broadcast: 17 one group ahead
+            // (as 4, memory clobber), 18 two groups ahead (as 9)
+            constexpr int AH = MODE == 17 ? 1 : 2;
+            const int o = ((g + AH) & 7) * 8;
+            const floatx4 na = *(const floatx4 *)&ws[wid][o], nb = *(const floatx4 *)&ws[wid][o + 4];
+#define MIXLO2(VI, W, SEL) "v_fma_mixlo_f16 %[a], " VI ", " W ", %[a] op_sel:[" SEL ",0,0] op_sel_hi:[1,0,1]\n\t"
+            if constexpr (MODE == 17)
+                asm volatile(MIXLO2("%[v0]", "%[w0]", "0") MIXLO2("%[v0]", "%[w1]", "1") MIXLO2("%[v1]", "%[w2]", "0")
+                             MIXLO2("%[v1]", "%[w3]", "1") MIXLO2("%[v2]", "%[w4]", "0") MIXLO2("%[v2]", "%[w5]", "1")
+                             MIXLO2("%[v3]", "%[w6]", "0") MIXLO2("%[v3]", "%[w7]", "1")
+                             : [a] "+v"(acc)
+                             : [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [w0] "v"(wa[0]), [w1] "v"(wa[1]),
+                               [w2] "v"(wa[2]), [w3] "v"(wa[3]), [w4] "v"(wb[0]), [w5] "v"(wb[1]), [w6] "v"(wb[2]), [w7] "v"(wb[3])
+                             : "memory");
+            else
+                asm volatile(MIXLO2("%[v0]", "%[w0]", "0") MIXLO2("%[v0]", "%[w1]", "1") MIXLO2("%[v1]", "%[w2]", "0")
+                             MIXLO2("%[v1]", "%[w3]", "1") MIXLO2("%[v2]", "%[w4]", "0") MIXLO2("%[v2]", "%[w5]", "1")
+                             MIXLO2("%[v3]", "%[w6]", "0") MIXLO2("%[v3]", "%[w7]", "1")
+                             : [a] "+v"(acc)
+                             : [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [w0] "v"(wa[0]), [w1] "v"(wa[1]),
+                               [w2] "v"(wa[2]), [w3] "v"(wa[3]), [w4] "v"(wb[0]), [w5] "v"(wb[1]), [w6] "v"(wb[2]), [w7] "v"(wb[3]));
+            if constexpr (AH == 1) {
+                wa = na;
+                wb = nb;
+            } else {
+                wa = wc;
+                wb = wd;
+                wc = na;
+                wd = nb;
+            }
             (void)t;
+        } else if constexpr (MODE == 19 || MODE == 20 || MODE == 21) {
+            // several independent chains a lane, per key: 19 two dimensions, one
+            // mixlo each (separate registers); 20 two rows x two dimensions as the
+            // prefill chain (mix, mix, cvt_pk per row); 21 the same four chains by mixlo
+            uint32_t c0 = __builtin_bit_cast(uint16_t, acc), c1 = c0 ^ 1u, c2 = c0 ^ 2u, c3 = c0 ^ 3u;
+#define ML(A, VI, W, SEL) "v_fma_mixlo_f16 " A ", " VI ", " W ", " A " op_sel:[" SEL ",0,0] op_sel_hi:[1,0,1]\n\t"
+#define K19(VI, VJ, W, SEL) ML("%[c0]", VI, W, SEL) ML("%[c1]", VJ, W, SEL)
+#define K21(VI, VJ, W, SEL) ML("%[c0]", VI, W, SEL) ML("%[c1]", VJ, W, SEL) ML("%[c2]", VI, W, SEL) ML("%[c3]", VJ, W, SEL)
+#define K20(VA, VB, W, SEL)                                                                     \
+    "v_fma_mix_f32 %[t], " VA ", " W ", %[c0] op_sel:[" SEL ",0,0] op_sel_hi:[1,0,1]\n\t"        \
+    "v_fma_mix_f32 %[u], " VB ", " W ", %[c0] op_sel:[" SEL ",0,1] op_sel_hi:[1,0,1]\n\t"        \
+    "v_cvt_pk_f16_f32 %[c0], %[t], %[u]\n\t"                                                     \
+    "v_fma_mix_f32 %[t], " VA ", " W ", %[c1] op_sel:[" SEL ",0,0] op_sel_hi:[1,0,1]\n\t"        \
+    "v_fma_mix_f32 %[u], " VB ", " W ", %[c1] op_sel:[" SEL ",0,1] op_sel_hi:[1,0,1]\n\t"        \
+    "v_cvt_pk_f16_f32 %[c1], %[t], %[u]\n\t"
+            float u;
+            if constexpr (MODE == 19)
+                asm volatile(K19("%[v0]", "%[v1]", "%[w0]", "0") K19("%[v0]", "%[v1]", "%[w1]", "1") K19("%[v1]", "%[v2]", "%[w2]", "0")
+                             K19("%[v1]", "%[v2]", "%[w3]", "1") K19("%[v2]", "%[v3]", "%[w4]", "0") K19("%[v2]", "%[v3]", "%[w5]", "1")
+                             K19("%[v3]", "%[v0]", "%[w6]", "0") K19("%[v3]", "%[v0]", "%[w7]", "1")
+                             : [c0] "+v"(c0), [c1] "+v"(c1)
+                             : [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [w0] "s"(s0), [w1] "s"(s1), [w2] "s"(s2),
+                               [w3] "s"(s3), [w4] "s"(s4), [w5] "s"(s5), [w6] "s"(s6), [w7] "s"(s7));
+            else if constexpr (MODE == 20)
+                asm volatile(K20("%[v0]", "%[v1]", "%[w0]", "0") K20("%[v0]", "%[v1]", "%[w1]", "1") K20("%[v1]", "%[v2]", "%[w2]", "0")
+                             K20("%[v1]", "%[v2]", "%[w3]", "1") K20("%[v2]", "%[v3]", "%[w4]", "0") K20("%[v2]", "%[v3]", "%[w5]", "1")
+                             K20("%[v3]", "%[v0]", "%[w6]", "0") K20("%[v3]", "%[v0]", "%[w7]", "1")
+                             : [c0] "+v"(c0), [c1] "+v"(c1), [t] "=&v"(t), [u] "=&v"(u)
+                             : [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [w0] "s"(s0), [w1] "s"(s1), [w2] "s"(s2),
+                               [w3] "s"(s3), [w4] "s"(s4), [w5] "s"(s5), [w6] "s"(s6), [w7] "s"(s7));
+            else
+                asm volatile(K21("%[v0]", "%[v1]", "%[w0]", "0") K21("%[v0]", "%[v1]", "%[w1]", "1") K21("%[v1]", "%[v2]", "%[w2]", "0")
+                             K21("%[v1]", "%[v2]", "%[w3]", "1") K21("%[v2]", "%[v3]", "%[w4]", "0") K21("%[v2]", "%[v3]", "%[w5]", "1")
+                             K21("%[v3]", "%[v0]", "%[w6]", "0") K21("%[v3]", "%[v0]", "%[w7]", "1")
+                             : [c0] "+v"(c0), [c1] "+v"(c1), [c2] "+v"(c2), [c3] "+v"(c3)
+                             : [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [w0] "s"(s0), [w1] "s"(s1), [w2] "s"(s2),
+                               [w3] "s"(s3), [w4] "s"(s4), [w5] "s"(s5), [w6] "s"(s6), [w7] "s"(s7));
+            acc = __builtin_bit_cast(f16, (uint16_t)(c0 ^ c1 ^ c2 ^ c3));
         } else if constexpr (MODE == 6) {
 #define MIXLO(VI, W, SEL) "v_fma_mixlo_f16 %[a], " VI ", " W ", %[a] op_sel:[" SEL ",0,0] op_sel_hi:[1,0,1]\n\t"
             asm volatile(MIXLO("%[v0]", "%[w0]", "0") MIXLO("%[v0]", "%[w1]", "1") MIXLO("%[v1]", "%[w2]", "0")
@@ -255,8 +317,10 @@ int main() {
                            "LDS broadcast one group ahead", "LDS + S add", "single rounding (mixlo), VGPR", "readlanes batched first",
                            "LDS 1 ahead, no clobber", "LDS 2 ahead, no clobber", "SMEM x8 glc, wait each group", "SMEM x16 glc, 16-key double buffer",
                            "SMEM x8 no glc (K$ hits)", "2 dims a lane, LDS weights", "2 dims a lane, SGPR weights",
-                           "fxp_buffer fast (8 blocks)", "fxp_buffer checked (1 record/2 buffers)"};
-    for (int mode = 0; mode < 17; mode++) {
+                           "(removed: fx_pipe.h)", "(removed: fx_pipe.h)",
+                           "mixlo, LDS 1 ahead", "mixlo, LDS 2 ahead", "mixlo, 2 dims (2 instr/key)",
+                           "2 rows x 2 dims mix/cvt_pk (6/key)", "2 rows x 2 dims mixlo (4/key)"};
+    for (int mode = 0; mode < 22; mode++) {
         double best = 1e30;
         for (int rep = 0; rep < 4; rep++) {
             switch (mode) {
@@ -275,8 +339,12 @@ int main() {
             case 12: hipLaunchKernelGGL(k<12>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
             case 13: hipLaunchKernelGGL(k<13>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
             case 14: hipLaunchKernelGGL(k<14>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
-            case 15: hipLaunchKernelGGL(k<15>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
-            case 16: hipLaunchKernelGGL(k<16>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
+            case 15: case 16: continue;   // (fx_pipe.h's buffer, removed in round 5)
+            case 17: hipLaunchKernelGGL(k<17>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
+            case 18: hipLaunchKernelGGL(k<18>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
+            case 19: hipLaunchKernelGGL(k<19>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
+            case 20: hipLaunchKernelGGL(k<20>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
+            case 21: hipLaunchKernelGGL(k<21>, dim3(8), dim3(256), 0, 0, v, w, c, o); break;
             }
             (void)hipDeviceSynchronize();
             long long hc[32];
