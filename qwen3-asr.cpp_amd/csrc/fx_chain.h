@@ -125,12 +125,6 @@ __device__ __forceinline__ void fx_step1_m(const u32x4 *v, int j0, int n, const 
 // against 17.1 with an s_nop 0 -- the padding hipcc adds in front of an asm
 // statement that reads a just-written VGPR)
 #define FX_CVT "v_cvt_f16_f32 %1, %0\n\t"
-#ifdef FX_R1_DIAG   // (timing diagnostic, tools/r5: single-rounding v_fma_mixlo_f16 chain)
-#undef FX_MIX
-#undef FX_CVT
-#define FX_MIX(VI, W, SEL) "v_fma_mixlo_f16 %1, " VI ", " W ", %1 op_sel:[" SEL ",0,0] op_sel_hi:[1,0,1]\n\t"
-#define FX_CVT ""
-#endif
 __device__ __forceinline__ void fx8_fast(f16 &acc, const u32x4 v, const floatx4 wa, const floatx4 wb) {
     float t;
     asm volatile(FX_MIX("%2", "%6", "0") FX_CVT FX_MIX("%2", "%7", "1") FX_CVT FX_MIX("%3", "%8", "0") FX_CVT
