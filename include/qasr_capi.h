@@ -123,6 +123,12 @@ int qasr_mel(qasr_ctx *c, const float *const *pcm, const int *n, int B, float *m
 int qasr_encode(qasr_ctx *c, const float *mel, const int *T, int B, float *feats);
 /* conv front-end + positional embedding only: [sum N_b][d_model] */
 int qasr_encode_conv(qasr_ctx *c, const float *mel, const int *T, int B, float *out);
+/* AudioEncoder::encode_no_chunk (src/audio_encoder.cpp:603-852): the conv stack
+ * over each clip's T_b frames as ONE chunk (no 100-frame split), sinusoidal PE
+ * positions 0 .. N_b - 1, then the same transformer; feats [sum N_b][hidden]
+ * with N_b = qasr_encoder_frames_no_chunk(T_b).  ASR models only. */
+int qasr_encode_no_chunk(qasr_ctx *c, const float *mel, const int *T, int B, float *feats);
+int qasr_encoder_frames_no_chunk(int n_mel_frames);
 /* Prefill B sequences from n_past = 0 (the KV cache of sequence b is reset).
  * ids: sum P_b tokens back to back; feats: sum N_b rows of [hidden];
  * audio_pos[b]: first pad index (splice rows [audio_pos, audio_pos+N_b));
@@ -135,6 +141,12 @@ int qasr_prefill(qasr_ctx *c, const int32_t *ids, const int *P, const float *fea
  *    src/text_decoder.h:125-126 / .cpp:392-581, 583-586 */
 int qasr_prefill_chunk(qasr_ctx *c, const int32_t *ids, const int *P, const int *n_past, int B,
                        float *logits_last, int32_t *argmax);
+/* The same chunk with audio rows spliced in (feats: sum N_b rows of [hidden];
+ * rows [audio_pos[b], audio_pos[b] + N_b) of chunk b when they fit in it).
+ * <- TextDecoder::forward_with_audio(tokens, n, audio, n_audio, pos, n_past)
+ *    at any n_past, src/text_decoder.cpp:588-644 (splice :431-459) */
+int qasr_prefill_chunk_audio(qasr_ctx *c, const int32_t *ids, const int *P, const int *n_past, const float *feats,
+                             const int *audio_pos, const int *N, int B, float *logits_last, int32_t *argmax);
 /* One decode step for B sequences at positions n_past[b] (token tok[b]). */
 int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_past, int B,
                      float *logits, int32_t *argmax);

@@ -589,22 +589,25 @@ static void conv2d_s2(const float *in, int IC, int H, int W, const uint16_t *w,
 
 /* src/audio_encoder.cpp:85-160 + :348-409: per 100-frame chunk (last one
  * short, not padded): conv x3 -> [W][C*16] (feature c*16+h) -> conv_out ->
- * + sinusoidal PE restarting at position 0 in every chunk. */
+ * + sinusoidal PE restarting at position 0 in every chunk.
+ * QO_ENC_NO_CHUNK (AudioEncoder::encode_no_chunk, src/audio_encoder.cpp:603-663):
+ * one chunk over all T frames, PE positions 0 .. N-1. */
 int qo_encode_conv(const qo_model *m, const float *mel, int T, float *out, int flags) {
     gelu_lut_init();
     const int C = m->conv_ch, D = m->d_model, NM = m->n_mel;
+    const int CH = (flags & QO_ENC_NO_CHUNK) ? (T > 0 ? T : 1) : 100;
     int n_out = 0;
-    for (int s = 0; s < T; s += 100) {
+    for (int s = 0; s < T; s += CH) {
         /* ASR: the chunk on its own length.  Aligner: one batched graph over
          * chunks zero-padded to 100 frames (src/forced_aligner.cpp:633-698);
          * the short last chunk keeps chunk_out_len(true length) frames (:725-733). */
-        const int Lv = (T - s) < 100 ? (T - s) : 100;
-        const int L = m->aligner ? 100 : Lv;
+        const int Lv = (T - s) < CH ? (T - s) : CH;
+        const int L = m->aligner ? CH : Lv;
         float *x0 = (float *)calloc((size_t)NM * L, sizeof(float));
         for (int mm = 0; mm < NM; mm++)
             for (int f = 0; f < Lv; f++) x0[mm * L + f] = mel[(size_t)mm * T + s + f];
         int H1, W1, H2, W2, H3, W3;
-        float *x1 = (float *)malloc((size_t)C * 64 * 50 * sizeof(float));
+        float *x1 = (float *)malloc((size_t)C * ((NM - 1) / 2 + 1) * ((L - 1) / 2 + 1) * sizeof(float));
         conv2d_s2(x0, 1, NM, L, m->conv1_w, m->conv1_b, C, x1, &H1, &W1, flags);
         float *x2 = (float *)malloc((size_t)C * H1 * W1 * sizeof(float));
         conv2d_s2(x1, C, H1, W1, m->conv2_w, m->conv2_b, C, x2, &H2, &W2, flags);
@@ -689,7 +692,7 @@ static void enc_attention_seg(const float *qkv_q, const float *qkv_k, const floa
 /* src/audio_encoder.cpp:411-555 */
 int qo_encode(const qo_model *m, const float *mel, int T, float *out, int flags) {
     const int D = m->d_model, H = m->enc_heads, FF = m->enc_ffn, HID = m->hidden;
-    const int N = qo_enc_frames(T);
+    const int N = (flags & QO_ENC_NO_CHUNK) ? chunk_out_len(T) : qo_enc_frames(T);
     float *x = (float *)malloc((size_t)N * D * sizeof(float));
     qo_encode_conv(m, mel, T, x, flags);
     float *cur = (float *)malloc((size_t)N * D * sizeof(float));

@@ -97,6 +97,8 @@ typedef struct {
 #define QO_FA_V_ROUND1  4   /* fp16 V accumulation, each key's fma rounded once
                                (fp16 of the exact v*vs + acc) instead of ggml's
                                x86 fp32-fma-then-fp16; the scale by ms unchanged */
+#define QO_ENC_NO_CHUNK 8   /* AudioEncoder::encode_no_chunk: the conv stack over all
+                               frames as one chunk, PE positions 0..N-1 (ASR model) */
 
 /* the V-accumulator step: ggml (F16C) fp16(fmaf(x, v, y)), and the single-
  * rounding variant of QO_FA_V_ROUND1 (fp16 RNE of the exact x * v + y) */

@@ -1132,6 +1132,11 @@ __global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int QD = a.n_head * 128, KD = a.n_kv_head * 128;
     const int q4 = lane >> 4, c16 = lane & 15, sub = lane >> 4, dl = (lane & 15) * 8;
+    // dev trace (QASR_DEV_TRACE, decode batches): row g + n_kv_head b: [start, q/k/v ready, scores done, chain done]
+    auto mark = [&](int slot) {
+        if (a.trace && tid == 0) a.trace[((long)b * a.n_kv_head + g) * 8 + slot] = rt_now();
+    };
+    mark(0);
     const long cbase = ((long)b * a.n_kv_head + g) * a.max_ctx;
     uint16_t *kc = a.kc + cbase * 128, *vc = a.vc + cbase * 128;
     const int pos = a.pos[b], nkv = pos + 1, kcap = min(pos, a.max_ctx - 1);
@@ -1169,6 +1174,7 @@ __global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) 
         }
     }
     __syncthreads();
+    mark(1);
     half8 qa[4];
 #pragma unroll
     for (int s4 = 0; s4 < 4; s4++)
@@ -1188,7 +1194,10 @@ __global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) 
     }
     if constexpr (FX) {
         __syncthreads();   // both heads' scores in LDS; the new V^T row stored (this workgroup's own writes)
+        mark(2);
         decode_attn_exact_body(a, 2 * g + (wid >> 1), b, wid & 1, fxs + (wid >> 1) * a.max_ctx);
+        if (a.trace) __syncthreads();
+        mark(3);
         stamp_end(a.stamp);
         return;
     }

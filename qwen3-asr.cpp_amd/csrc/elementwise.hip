@@ -72,10 +72,10 @@ __global__ __launch_bounds__(256) void conv1_kernel(const float *__restrict__ me
 }
 
 void launch_conv1(const float *mel, const ChunkDesc *chunks, const int *row1_start, int n_chunks, int rows1,
-                  const uint16_t *w, const float *b, const uint16_t *gelu, int C, uint16_t *act1, hipStream_t s) {
+                  const uint16_t *w, const float *b, const uint16_t *gelu, int C, uint16_t *act1, hipStream_t s, int max_w1) {
     if (rows1 <= 0) return;
     const int per_block = 4 * CONV1_ROWS;
-    const int max_loc = 64 * ((100 - 1) / 2 + 1);   // chunks hold <= 100 mel frames (ASR and aligner)
+    const int max_loc = 64 * max_w1;   // the widest chunk's conv1 outputs (100-frame chunks: W1 = 50)
     hipLaunchKernelGGL(conv1_kernel, dim3((max_loc + per_block - 1) / per_block, n_chunks), dim3(256), 0, s, mel, chunks,
                        row1_start, n_chunks, rows1, w, b, gelu, C, act1);
 }

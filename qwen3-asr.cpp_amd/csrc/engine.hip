@@ -103,6 +103,8 @@ struct qasr_ctx {
     // grow-on-demand scratch
     DevBuf pcm, spcm, mel, meltmp, melmax, melclips, melblocks;   // (spcm: qasr_run_stream's host clips)
     DevBuf chunks, rs1, rs2, rs3, pepos, act1, act2, act3;
+    DevBuf pebig;                  // encode_no_chunk: sinusoidal PE over a whole clip's frames
+    int pebig_rows = 0;
     DevBuf ex, exh, eqkv, eatt, eff, feats, segs;
     DevBuf px, pxh, pqkv, pq, patt, pact, prow, plast, pids, pxl;
     DevBuf pq32, pk32;             // ForcedAligner prefill: fp32 Q / K rows
@@ -887,8 +889,10 @@ static int run_mel(qasr_ctx *c, const std::vector<long> &off, const std::vector<
 
 // encoder over B clips whose mel sits at d_mel + mel_off[b] ([128][T_b]).
 // conv_only: stop after conv_out + PE (output [sum N][d_model] in c->ex).
+// no_chunk: AudioEncoder::encode_no_chunk (src/audio_encoder.cpp:603-852): the
+// conv stack over each clip's frames as one chunk, PE positions 0 .. N-1 (ASR)
 static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> &mel_off, const std::vector<int> &T,
-                       bool conv_only, std::vector<int> &Nb) {
+                       bool conv_only, std::vector<int> &Nb, bool no_chunk = false) {
     qasr_model *m = c->m;
     const Hparams &hp = m->hp;
     const int B = (int)T.size(), C = hp.conv_ch, D = hp.d_model, FF = hp.enc_ffn;
@@ -904,14 +908,16 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     // every padded row (PE position = row within its chunk, as for the valid
     // ones) and the valid rows are gathered after it.
     const bool al = hp.aligner;
+    if (no_chunk && al) return fail(QASR_ERR_ARG, "encode_no_chunk: ASR models only");
     const bool al_gather = al && B > 1;
     std::vector<int> pepos_pad, gidx;
     for (int b = 0; b < B; b++) {
-        for (int s = 0; s < T[b]; s += 100) {
+        const int CH = no_chunk ? std::max(T[b], 1) : 100;
+        for (int s = 0; s < T[b]; s += CH) {
             ChunkDesc d;
             d.mel_off = mel_off[b] + s;
             d.T = T[b];
-            d.Lv = std::min(100, T[b] - s);
+            d.Lv = std::min(CH, T[b] - s);
             d.L = al ? 100 : d.Lv;
             d.W1 = (d.L - 1) / 2 + 1;
             d.W2 = (d.W1 - 1) / 2 + 1;
@@ -932,6 +938,19 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     const int NC = (int)ch.size(), N = er;
     if (N == 0) return 0;
     int rc;
+    const float *pe_tab = m->pe;   // 13 positions: a 100-frame chunk's
+    if (no_chunk) {
+        int npos = 0;
+        for (int v : Nb) npos = std::max(npos, v);
+        if (npos > c->pebig_rows) {
+            std::vector<float> pe;
+            sinusoidal_pe(pe, npos, D);
+            if ((rc = ensure(c, c->pebig, pe.size() * 4))) return rc;
+            HIPCHK(hipMemcpy(c->pebig.p, pe.data(), pe.size() * 4, hipMemcpyHostToDevice));
+            c->pebig_rows = npos;
+        }
+        pe_tab = c->pebig.as<float>();
+    }
     const int NP = r3 / 16;   // conv_out rows over every (padded) chunk row
     if (al_gather && ((rc = upload(c, c->gidx, gidx)) || (rc = ensure(c, c->exp_, (size_t)NP * D * 4)))) return rc;
     if ((rc = upload(c, c->chunks, ch)) || (rc = upload(c, c->rs1, s1)) || (rc = upload(c, c->rs2, s2)) ||
@@ -943,8 +962,10 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
         (rc = ensure(c, c->feats, (size_t)N * hp.hidden * 4)))
         return rc;
     hipStream_t s = c->st;
+    int max_w1 = 0;
+    for (const ChunkDesc &d : ch) max_w1 = std::max(max_w1, d.W1);
     launch_conv1(d_mel, c->chunks.as<ChunkDesc>(), c->rs1.as<int>(), NC, r1, m->conv1_w, m->conv1_b, m->gelu, C,
-                 c->act1.as<uint16_t>(), s);
+                 c->act1.as<uint16_t>(), s, max_w1);
     GemmArgs g{};
     g.chunks = c->chunks.as<ChunkDesc>();
     g.n_chunks = NC;
@@ -964,7 +985,7 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     // conv_out (no bias) + per-chunk sinusoidal PE (src/audio_encoder.cpp:147-149, :400-404)
     GemmArgs o{};
     o.M = MO; o.N = D; o.K = 16 * C;
-    o.out_f32 = al_gather ? c->exp_.as<float>() : c->ex.as<float>(); o.ldo = D; o.pe = m->pe; o.pe_pos = c->pepos.as<int>();
+    o.out_f32 = al_gather ? c->exp_.as<float>() : c->ex.as<float>(); o.ldo = D; o.pe = pe_tab; o.pe_pos = c->pepos.as<int>();
     if (q8) {
         gemm_q8(c, EPI_F32, o, nullptr, c->act3.as<uint16_t>(), 16 * C, C, m->conv_out_w, m->conv_out_d, s);
     } else {
@@ -1708,7 +1729,7 @@ extern "C" int qasr_mel_engine_run(qasr_mel_engine *e, const float *pcm, int n, 
     return 0;
 }
 
-static int encode_common(qasr_ctx *c, const float *mel, const int *T, int B, float *outp, bool conv_only) {
+static int encode_common(qasr_ctx *c, const float *mel, const int *T, int B, float *outp, bool conv_only, bool no_chunk = false) {
     if (!c || !mel || !T || B <= 0 || !outp) return fail(QASR_ERR_ARG, "bad arguments");
     HIPCHK(hipSetDevice(c->m->device));
     HIPCHK(hipStreamSynchronize(c->st));
@@ -1721,7 +1742,7 @@ static int encode_common(qasr_ctx *c, const float *mel, const int *T, int B, flo
     if (rc) return rc;
     if (tot) HIPCHK(hipMemcpyAsync(c->mel.p, mel, tot * 4, hipMemcpyHostToDevice, c->st));
     std::vector<int> Nb;
-    if ((rc = run_encoder(c, c->mel.as<float>(), mo, Tv, conv_only, Nb))) return rc;
+    if ((rc = run_encoder(c, c->mel.as<float>(), mo, Tv, conv_only, Nb, no_chunk))) return rc;
     long N = 0;
     for (int v : Nb) N += v;
     const int width = conv_only ? c->m->hp.d_model : c->m->hp.hidden;
@@ -1735,6 +1756,15 @@ extern "C" int qasr_encode(qasr_ctx *c, const float *mel, const int *T, int B, f
 }
 extern "C" int qasr_encode_conv(qasr_ctx *c, const float *mel, const int *T, int B, float *out) {
     return encode_common(c, mel, T, B, out, true);
+}
+extern "C" int qasr_encode_no_chunk(qasr_ctx *c, const float *mel, const int *T, int B, float *feats) {
+    return encode_common(c, mel, T, B, feats, false, true);
+}
+extern "C" int qasr_encoder_frames_no_chunk(int n_mel_frames) {
+    int L = n_mel_frames;
+    if (L <= 0) return 0;
+    for (int i = 0; i < 3; i++) L = (L - 1) / 2 + 1;   // src/audio_encoder.cpp:304-310 over the whole length
+    return L;
 }
 
 extern "C" int qasr_prefill(qasr_ctx *c, const int32_t *ids, const int *P, const float *feats, const int *audio_pos,
@@ -1770,25 +1800,48 @@ extern "C" int qasr_prefill(qasr_ctx *c, const int32_t *ids, const int *P, const
 // 392-581 builds one graph for the chunk): the chunk's rows through the
 // prefill layers at positions n_past[b] .. n_past[b] + P[b] - 1, causal
 // attention over the cached keys and the chunk's own; logits of each chunk's
-// last row.  n_past[b] = 0 is the plain prefill without audio.
-extern "C" int qasr_prefill_chunk(qasr_ctx *c, const int32_t *ids, const int *P, const int *n_past, int B, float *logits_last,
-                                  int32_t *argmax) {
+// last row.  n_past[b] = 0 is the plain prefill.  With feats: forward_with_audio
+// at any n_past (src/text_decoder.cpp:588-644, the splice of :431-459) -- rows
+// [audio_pos[b], audio_pos[b] + N[b]) of the chunk take the audio embeddings
+// when they fit inside it, as the reference's condition.
+static int prefill_chunk_common(qasr_ctx *c, const int32_t *ids, const int *P, const int *n_past, const float *feats,
+                                const int *audio_pos, const int *N, int B, float *logits_last, int32_t *argmax) {
     if (!c || !ids || !P || !n_past || B <= 0) return fail(QASR_ERR_ARG, "bad arguments");
     HIPCHK(hipSetDevice(c->m->device));
     HIPCHK(hipStreamSynchronize(c->st));
     c->pin_used = 0;
+    const int H = c->m->hp.hidden;
     std::vector<int> Pv(P, P + B), Nv(B, 0), ap(B, -1), p0(n_past, n_past + B);
-    long nid = 0;
-    for (int b = 0; b < B; b++) nid += P[b];
+    long nid = 0, nf = 0;
+    for (int b = 0; b < B; b++) {
+        nid += P[b];
+        if (feats && N) { Nv[b] = N[b]; nf += N[b]; }
+        if (audio_pos) ap[b] = audio_pos[b];
+    }
     for (long i = 0; i < nid; i++)
         if (ids[i] < 0 || ids[i] >= c->m->hp.vocab) return fail(QASR_ERR_ARG, "token id out of range");
     std::vector<int32_t> idv(ids, ids + nid);
     int rc;
-    if ((rc = run_prefill(c, idv, Pv, nullptr, ap, Nv, logits_last != nullptr, nullptr, &p0))) return rc;
+    if (nf) {
+        if ((rc = ensure(c, c->feats, (size_t)nf * H * 4))) return rc;
+        HIPCHK(hipMemcpyAsync(c->feats.p, feats, (size_t)nf * H * 4, hipMemcpyHostToDevice, c->st));
+    }
+    if ((rc = run_prefill(c, idv, Pv, nf ? c->feats.as<float>() : nullptr, ap, Nv, logits_last != nullptr, nullptr, &p0)))
+        return rc;
     if (logits_last) HIPCHK(hipMemcpyAsync(logits_last, c->d_logits, (size_t)B * c->m->hp.vocab * 4, hipMemcpyDeviceToHost, c->st));
     if (argmax) HIPCHK(hipMemcpyAsync(argmax, c->d_tok, B * 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;
+}
+
+extern "C" int qasr_prefill_chunk(qasr_ctx *c, const int32_t *ids, const int *P, const int *n_past, int B, float *logits_last,
+                                  int32_t *argmax) {
+    return prefill_chunk_common(c, ids, P, n_past, nullptr, nullptr, nullptr, B, logits_last, argmax);
+}
+
+extern "C" int qasr_prefill_chunk_audio(qasr_ctx *c, const int32_t *ids, const int *P, const int *n_past, const float *feats,
+                                        const int *audio_pos, const int *N, int B, float *logits_last, int32_t *argmax) {
+    return prefill_chunk_common(c, ids, P, n_past, feats, audio_pos, N, B, logits_last, argmax);
 }
 
 extern "C" int qasr_decode_step(qasr_ctx *c, const int32_t *tok, const int *n_past, int B, float *logits, int32_t *argmax) {

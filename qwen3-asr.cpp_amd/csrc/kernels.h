@@ -36,7 +36,8 @@ struct ChunkDesc {
 
 // conv1 (1 -> C, 3x3, s2, p1) + bias + GELU(LUT) -> act1 NHWC fp16 [rows1][C]
 void launch_conv1(const float *mel, const ChunkDesc *chunks, const int *row1_start, int n_chunks, int rows1,
-                  const uint16_t *w /*[C][9]*/, const float *b, const uint16_t *gelu, int C, uint16_t *act1, hipStream_t s);
+                  const uint16_t *w /*[C][9]*/, const float *b, const uint16_t *gelu, int C, uint16_t *act1, hipStream_t s,
+                  int max_w1 = 50 /* the widest chunk's W1 */);
 
 // ---------------------------------------------------------------- GEMM
 enum GemmEpi {

@@ -288,9 +288,22 @@ bool AudioEncoder::encode(const float *mel_data, int n_mel, int n_frames, std::v
 bool AudioEncoder::encode_conv_only(const float *mel_data, int n_mel, int n_frames, std::vector<float> &output) {
     return run(mel_data, n_mel, n_frames, output, true);
 }
-bool AudioEncoder::encode_no_chunk(const float *, int, int, std::vector<float> &) {
-    error_msg_ = "encode_no_chunk is not provided: the encoder runs the reference's 100-frame chunking (encode)";
-    return false;
+// src/audio_encoder.cpp:603-852: the conv stack over all frames, PE 0..N-1
+bool AudioEncoder::encode_no_chunk(const float *mel_data, int n_mel, int n_frames, std::vector<float> &output) {
+    if (!ctx_) {
+        error_msg_ = "Model not loaded";
+        return false;
+    }
+    if (!mel_data || n_mel != hparams_.n_mel_bins || n_frames <= 0) {
+        error_msg_ = "Mel bins mismatch";
+        return false;
+    }
+    output.assign((size_t)qasr_encoder_frames_no_chunk(n_frames) * text_hparams_.hidden_size, 0.0f);
+    if (qasr_encode_no_chunk(ctx_, mel_data, &n_frames, 1, output.data()) != 0) {
+        error_msg_ = std::string("Failed to compute encoder graph: ") + qasr_last_error();
+        return false;
+    }
+    return true;
 }
 
 // =============================================================== decoder
@@ -372,9 +385,9 @@ bool TextDecoder::forward_with_audio(const int32_t *tokens, int32_t n_tokens, co
     if (n_past == 0) {
         const int P = n_tokens, N = splice ? n_audio : 0, ap = splice ? audio_start_pos : -1;
         rc = qasr_prefill(ctx_, tokens, &P, splice ? audio_embd : nullptr, &ap, &N, 1, output.data(), nullptr);
-    } else if (splice) {
-        error_msg_ = "audio embeddings are spliced by the prefill: forward_with_audio needs n_past = 0";
-        return false;
+    } else if (splice) {   // the audio rows of a chunk after cached tokens (src/text_decoder.cpp:588-644)
+        const int P = n_tokens, N = n_audio, ap = audio_start_pos;
+        rc = qasr_prefill_chunk_audio(ctx_, tokens, &P, &n_past, audio_embd, &ap, &N, 1, output.data(), nullptr);
     } else if (n_tokens == 1) {
         rc = qasr_decode_step(ctx_, tokens, &n_past, 1, output.data(), nullptr);
     } else {
@@ -411,9 +424,15 @@ std::vector<int32_t> TextDecoder::tokenize(const std::string &text) const {
     return ids;
 }
 
-bool TextDecoder::forward_debug(const int32_t *, int32_t, int32_t, std::vector<float> &, std::map<std::string, std::vector<float>> &) {
-    error_msg_ = "forward_debug is not provided: read intermediate decode state with qasr_debug_read";
-    return false;
+// src/text_decoder.cpp:686-760: forward without audio, then the graph tensors
+// named debug_norm0, debug_q0_raw, ... -- which the reference's build_graph
+// never names (none of them exists in its graph: its map comes back empty) --
+// and the logits tensor, which holds the LAST row only (:564-566): the same here
+// (the last row's logits; an empty debug map)
+bool TextDecoder::forward_debug(const int32_t *tokens, int32_t n_tokens, int32_t n_past, std::vector<float> &output,
+                                std::map<std::string, std::vector<float>> &debug_tensors) {
+    debug_tensors.clear();
+    return forward_with_audio(tokens, n_tokens, nullptr, 0, -1, n_past, output);
 }
 
 // ======================================================= audio injection

@@ -23,7 +23,8 @@ EXPORTS = [
     "qasr_model_load", "qasr_model_free", "qasr_model_hparams", "qasr_model_device_bytes",
     "qasr_ctx_create", "qasr_ctx_free",
     "qasr_mel_frames", "qasr_encoder_frames", "qasr_prompt_len", "qasr_build_prompt",
-    "qasr_mel", "qasr_encode", "qasr_encode_conv", "qasr_prefill", "qasr_prefill_chunk", "qasr_decode_step",
+    "qasr_mel", "qasr_encode", "qasr_encode_conv", "qasr_encode_no_chunk", "qasr_encoder_frames_no_chunk",
+    "qasr_prefill", "qasr_prefill_chunk", "qasr_prefill_chunk_audio", "qasr_decode_step",
     "qasr_stage_audio", "qasr_run", "qasr_run_staged", "qasr_run_stream", "qasr_run_stream_staged", "qasr_set_system_prompt", "qasr_transcribe_batch",
     "qasr_set_probe", "qasr_get_probe", "qasr_get_probe_device",
     "qasr_ctx_set_option", "qasr_ctx_get_option", "qasr_debug_read",
@@ -85,9 +86,11 @@ def lib() -> C.CDLL:
             "qasr_build_prompt": ([P, I, I32P, IP], I),
             "qasr_mel": ([P, C.POINTER(F), IP, I, F], I),
             "qasr_encode": ([P, F, IP, I, F], I), "qasr_encode_conv": ([P, F, IP, I, F], I),
+            "qasr_encode_no_chunk": ([P, F, IP, I, F], I), "qasr_encoder_frames_no_chunk": ([I], I),
             "qasr_prefill": ([P, I32P, IP, F, IP, IP, I, F, I32P], I),
             "qasr_decode_step": ([P, I32P, IP, I, F, I32P], I),
             "qasr_prefill_chunk": ([P, I32P, IP, IP, I, F, I32P], I),
+            "qasr_prefill_chunk_audio": ([P, I32P, IP, IP, F, IP, IP, I, F, I32P], I),
             "qasr_stage_audio": ([P, C.POINTER(F), IP, I], I),
             "qasr_run": ([P, I, I, I32P, IP, C.POINTER(Timings)], I),
             "qasr_run_staged": ([P, IP, I, I, I, I32P, IP, C.POINTER(Timings)], I),
@@ -338,13 +341,13 @@ class Context:
             o += 128 * t
         return res
 
-    def _encode(self, mels: Sequence[np.ndarray], conv_only: bool) -> List[np.ndarray]:
+    def _encode(self, mels: Sequence[np.ndarray], conv_only: bool, no_chunk: bool = False) -> List[np.ndarray]:
         T = np.array([m.shape[1] for m in mels], np.int32)
         flat = np.ascontiguousarray(np.concatenate([np.ascontiguousarray(m, np.float32).ravel() for m in mels]))
-        N = [encoder_frames(int(t)) for t in T]
+        N = [lib().qasr_encoder_frames_no_chunk(int(t)) if no_chunk else encoder_frames(int(t)) for t in T]
         width = self.model.hp.d_model if conv_only else self.model.hp.hidden_size
         out = np.zeros(max(1, sum(N) * width), np.float32)
-        fn = lib().qasr_encode_conv if conv_only else lib().qasr_encode
+        fn = lib().qasr_encode_no_chunk if no_chunk else lib().qasr_encode_conv if conv_only else lib().qasr_encode
         _check(fn(self.h, _f(flat), _i(T), len(mels), _f(out)), "qasr_encode")
         res, o = [], 0
         for k in N:
@@ -354,6 +357,10 @@ class Context:
 
     def encode(self, mels):
         return self._encode(mels, False)
+
+    def encode_no_chunk(self, mels):
+        """AudioEncoder::encode_no_chunk: the conv stack over all frames at once, PE 0..N-1"""
+        return self._encode(mels, False, True)
 
     def encode_conv(self, mels):
         return self._encode(mels, True)
@@ -385,9 +392,11 @@ class Context:
                "qasr_decode_step")
         return logits, am
 
-    def prefill_chunk(self, ids_list, n_past, want_logits=True):
+    def prefill_chunk(self, ids_list, n_past, want_logits=True, feats_list=None, audio_pos=None):
         """qasr_prefill_chunk: sequence b's tokens ids_list[b] after n_past[b]
         cached ones, one causal chunk (TextDecoder::forward, n_tokens > 1);
+        with feats_list / audio_pos: qasr_prefill_chunk_audio, the audio rows
+        spliced at audio_pos[b] of the chunk (forward_with_audio at n_past > 0);
         returns (logits of each chunk's last row, argmax)"""
         P = np.array([len(x) for x in ids_list], np.int32)
         ids = np.ascontiguousarray(np.concatenate([np.asarray(x, np.int32) for x in ids_list]), np.int32)
@@ -395,8 +404,15 @@ class Context:
         B = len(P)
         logits = np.zeros((B, self.model.hp.vocab_size), np.float32) if want_logits else None
         am = np.zeros(B, np.int32)
-        _check(lib().qasr_prefill_chunk(self.h, _i32(ids), _i(P), _i(npast), B, _f(logits) if want_logits else None, _i32(am)),
-               "qasr_prefill_chunk")
+        if feats_list is None:
+            _check(lib().qasr_prefill_chunk(self.h, _i32(ids), _i(P), _i(npast), B, _f(logits) if want_logits else None,
+                                            _i32(am)), "qasr_prefill_chunk")
+            return logits, am
+        N = np.array([f.shape[0] for f in feats_list], np.int32)
+        feats = np.ascontiguousarray(np.concatenate([np.asarray(f, np.float32) for f in feats_list]))
+        ap = np.ascontiguousarray(audio_pos, np.int32)
+        _check(lib().qasr_prefill_chunk_audio(self.h, _i32(ids), _i(P), _i(npast), _f(feats), _i(ap), _i(N), B,
+                                              _f(logits) if want_logits else None, _i32(am)), "qasr_prefill_chunk_audio")
         return logits, am
 
     # ---- whole path --------------------------------------------------------

@@ -192,6 +192,7 @@ class OracleModel:
     GELU_EXACT = 1
     FA_V_F32 = 2
     FA_V_ROUND1 = 4   # fp16 V accumulation with one rounding per key (qasr_oracle.h QO_FA_V_ROUND1)
+    ENC_NO_CHUNK = 8  # AudioEncoder::encode_no_chunk: the conv stack over all frames, PE 0..N-1
 
     def __init__(self, path: str):
         g = Gguf(path)
@@ -291,10 +292,18 @@ class OracleModel:
         self.vocab = m.vocab
         self.hidden = m.hidden
 
+    @staticmethod
+    def frames(T: int, flags: int = 0) -> int:
+        if flags & OracleModel.ENC_NO_CHUNK:   # src/audio_encoder.cpp:304-310 over the whole length
+            for _ in range(3):
+                T = (T - 1) // 2 + 1
+            return T
+        return olib().qo_enc_frames(T)
+
     def encode(self, mel: np.ndarray, flags: int = 0) -> np.ndarray:
         mel = np.ascontiguousarray(mel, np.float32)
         T = mel.shape[1]
-        N = olib().qo_enc_frames(T)
+        N = self.frames(T, flags)
         out = np.zeros(max(1, N * self.hidden), np.float32)
         olib().qo_encode(C.byref(self.m), _f(mel), T, _f(out), flags)
         return out[:N * self.hidden].reshape(N, self.hidden)
@@ -302,7 +311,7 @@ class OracleModel:
     def encode_conv(self, mel: np.ndarray, flags: int = 0) -> np.ndarray:
         mel = np.ascontiguousarray(mel, np.float32)
         T = mel.shape[1]
-        N = olib().qo_enc_frames(T)
+        N = self.frames(T, flags)
         D = self.m.d_model
         out = np.zeros(max(1, N * D), np.float32)
         olib().qo_encode_conv(C.byref(self.m), _f(mel), T, _f(out), flags)

@@ -575,3 +575,43 @@ def test_full_option_matches_default(full, case):
             ab, rel = _err(alt[0][b], lo)
             assert rel <= REL_LOGITS and ab <= ABS_LOGITS, (case, b, ab, rel)
         assert all(t == alt[2][0] for t in alt[2])
+
+
+@pytest.mark.timeout(900)
+def test_full_stream_34_slots_refills_across_split_buckets(full):
+    """continuous batching at full size with more than 8
+    slots -- 34 slots take the decode-batch kernels (skinny GEMMs, the
+    one-launch LM head, the per-sequence exact attention indexed by slot) --
+    48 clips of 2-19 s with ragged budgets, so refills land mid-stream and
+    several clips' contexts cross a 256-key split bucket (prompt < 256 <=
+    prompt + budget).  Every clip's tokens equal the same clip's in a static
+    batch of 34 clips (the same decode kernels, run to the batch's longest
+    budget and truncated): a clip's result depends neither on its slot nor on
+    when the slot was refilled."""
+    m, _, _ = full
+    S, n = 34, 48
+    rng = np.random.default_rng(77)
+    secs = rng.uniform(2.0, 19.0, n)
+    secs[:4] = [18.0, 17.5, 17.9, 2.0]   # prompts 249, 243, 248: each crosses 256 within its budget
+    lens = [int(s * 100) * 160 for s in secs]
+    budgets = [int(b) for b in rng.integers(3, 28, n)]
+    budgets[:3] = [27, 20, 26]
+    prompts = [qasr.lib().qasr_prompt_len(qasr.encoder_frames(qasr.mel_frames(L))) for L in lens]
+    assert sum(P < 256 <= P + b for P, b in zip(prompts, budgets)) >= 2
+    clips = [qasr.synth_pcm(7600 + i, L) for i, L in enumerate(lens)]
+    c = qasr.Context(m, max_batch=S, max_ctx=max(prompts) + max(budgets) + 8)
+    try:
+        it = iter([(i, clips[i], budgets[i]) for i in range(n)])
+        out, st = c.run_stream(lambda: next(it, None), max_tokens=max(budgets), ignore_eos=True)
+        assert st.n_clips == n and st.n_errors == 0 and st.n_prefills >= 2
+        ref = {}
+        for k in range(0, n, S):
+            idx = list(range(k, min(k + S, n)))
+            pad = [i for i in range(n) if i not in idx][:S - len(idx)]   # a full batch: the same kernels as the stream
+            r = c.transcribe([clips[i] for i in idx + pad], max_tokens=max(budgets[i] for i in idx), ignore_eos=True)
+            for j, i in enumerate(idx):
+                ref[i] = r.tokens[j][:budgets[i]]
+    finally:
+        c.close()
+    for i in range(n):
+        assert len(out[i]) == budgets[i] and out[i] == ref[i], i

@@ -253,3 +253,46 @@ def test_chunk_prefill_after_cached_tokens(tiny, tiny_oracle, parity):
     d0 = op.OracleDecoder(tiny_oracle, 64)
     lo = d0.forward(chunk, 0)
     assert float(np.abs(lg[0] - lo).max()) <= 1e-2 * float(np.abs(lo).max())
+
+
+def test_forward_with_audio_after_cached_tokens(tiny, tiny_oracle, parity):
+    """TextDecoder::forward_with_audio at n_past > 0 (src/text_decoder.cpp:588-644;
+    the splice of :431-459 applies to the chunk's own rows) = qasr_prefill_chunk_audio:
+    the prompt's text head prefilled first (n_past = 0, no audio), then the rest
+    of the prompt as one chunk with the audio rows spliced at their offset in the
+    chunk, and a decode step -- against the oracle doing the same two calls, and
+    the chunked result against the one-shot prefill"""
+    m, c = tiny
+    feats = tiny_oracle.encode(op.log_mel(qasr.synth_pcm(6400, int(1.7 * SR))))
+    ids, pos = m.build_prompt(feats.shape[0])
+    k = pos - 2   # the head stops two tokens before the audio pads
+    d = op.OracleDecoder(tiny_oracle, 512)
+    lg0, _ = c.prefill([ids[:k]])
+    lo0 = d.forward(ids[:k], 0)
+    lg1, am = c.prefill_chunk([ids[k:]], [k], feats_list=[feats], audio_pos=[pos - k])
+    lo1 = d.forward(ids[k:], k, feats, pos - k)
+    tok = int(am[0])
+    lg2, _ = c.decode_step([tok], [len(ids)])
+    lo2 = d.forward([tok], len(ids))
+    errs = [float(np.abs(g[0] - o).max()) / float(np.abs(o).max()) for g, o in ((lg0, lo0), (lg1, lo1), (lg2, lo2))]
+    parity("tiny_forward_with_audio_at_n_past", rel_max=errs)
+    assert max(errs) <= 1e-2, errs
+    assert tok == int(np.argmax(lo1))
+    full, _ = c.prefill([ids], [feats], [pos])   # the same prompt in one call: the same rows up to rounding
+    assert float(np.abs(full[0] - lg1[0]).max()) <= 1e-2 * float(np.abs(lo1).max())
+
+
+@pytest.mark.parametrize("secs", [0.9, 3.1, 9.5])
+def test_encode_no_chunk_matches_oracle(tiny, tiny_oracle, secs):
+    """AudioEncoder::encode_no_chunk (src/audio_encoder.cpp:603-852): the conv
+    stack over every frame as one chunk and PE positions 0..N-1, against the
+    oracle's QO_ENC_NO_CHUNK at the encoder bar; up to 100 frames it equals encode"""
+    _, c = tiny
+    mel = op.log_mel(qasr.synth_pcm(6500, int(secs * SR)))
+    g = c.encode_no_chunk([mel])[0]
+    o = tiny_oracle.encode(mel, op.OracleModel.ENC_NO_CHUNK)
+    assert g.shape == o.shape
+    mx, mean = _stats(g, o)
+    assert mx <= 2e-2 and mean <= 1e-3, (mx, mean)
+    if mel.shape[1] <= 100:
+        assert np.array_equal(g, c.encode([mel])[0])

@@ -71,3 +71,19 @@ def test_argmax_tie_rule(built):
     x = np.zeros(16, np.float32)
     x[[3, 7, 11]] = 5.0
     assert op.olib().qo_argmax(op._f(x), 16) == 3
+
+
+def test_encode_no_chunk_structure(om):
+    """QO_ENC_NO_CHUNK (AudioEncoder::encode_no_chunk, src/audio_encoder.cpp:603-852):
+    up to 100 frames it is the chunked encoder itself; past 100 the conv stack
+    sees across chunk edges and the PE keeps counting, so the rows differ from
+    the chunked ones after the first chunk but not before its edge region."""
+    mel = op.log_mel(qasr.synth_pcm(7, 16000))   # 100 frames: one chunk
+    assert np.array_equal(om.encode_conv(mel), om.encode_conv(mel, om.ENC_NO_CHUNK))
+    mel = op.log_mel(qasr.synth_pcm(8, 3 * 16000 + 480))   # 303 frames
+    a, b = om.encode_conv(mel), om.encode_conv(mel, om.ENC_NO_CHUNK)
+    assert b.shape == (om.frames(303, om.ENC_NO_CHUNK), om.m.d_model) == (38, om.m.d_model) and a.shape[0] == 40
+    assert np.array_equal(a[:12], b[:12])          # rows whose receptive field stays inside chunk 0
+    assert not np.allclose(a[13:20], b[13:20])     # PE position 13.. vs the restarted 0..
+    f = om.encode(mel, om.ENC_NO_CHUNK)
+    assert f.shape == (38, om.hidden) and np.isfinite(f).all()

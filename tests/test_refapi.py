@@ -136,3 +136,21 @@ def test_reference_decoder_driver_last_pos(gpu, full_f16_gguf, tmp_path):
         m.close()
     assert int(top.group(1)) == int(am[0])
     assert abs(float(top.group(2)) - float(lg[0][int(am[0])])) <= 1e-3 * max(1.0, abs(float(top.group(2))))
+
+
+@pytest.mark.gpu
+def test_reference_encoder_no_chunk_driver(gpu, full_f16_gguf, tmp_path):
+    """test_encoder_no_chunk.cpp unchanged: AudioEncoder::encode_no_chunk on the
+    full-size model (its hard-coded models/qwen3-asr-0.6b-f16.gguf, here the
+    synthetic one) against tests/reference/encoder_no_chunk.npy, which the
+    oracle's QO_ENC_NO_CHUNK writes; the driver's own 2e-2 max |delta| bar"""
+    exe = _need("test_encoder_no_chunk")
+    om = op.OracleModel(full_f16_gguf)
+    mel = op.log_mel(qasr.synth_pcm(4344, int(2.6 * SR)))   # 260 frames: three chunks in encode()
+    (tmp_path / "tests" / "reference").mkdir(parents=True)
+    (tmp_path / "models").mkdir()
+    os.symlink(full_f16_gguf, tmp_path / "models" / "qwen3-asr-0.6b-f16.gguf")
+    _npy(tmp_path / "tests" / "reference" / "mel.npy", mel)
+    _npy(tmp_path / "tests" / "reference" / "encoder_no_chunk.npy", om.encode(mel, op.OracleModel.ENC_NO_CHUNK))
+    r = _run([exe], str(tmp_path))
+    assert r.returncode == 0 and "TEST PASSED" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]

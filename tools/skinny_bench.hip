@@ -16,7 +16,11 @@ using namespace qasr;
 
 struct Shape { const char *name; int N, K, epi; };
 
-template <int MT, int NT, int KW, int EPI, int VAR>
+__global__ void empty_kernel(int *p) {
+    if (p && threadIdx.x == 1000) p[0] = 1;
+}
+
+template <int MT, int NT, int KW, int EPI, int VAR, int CPW = 0>
 static double time_cfg(GemmArgs g, const std::vector<uint16_t *> &ws, hipStream_t s, const char *tag) {
     const int NREP = 64;
     dim3 grid(g.N / (16 * NT), (g.M + 16 * MT - 1) / (16 * MT));
@@ -24,7 +28,7 @@ static double time_cfg(GemmArgs g, const std::vector<uint16_t *> &ws, hipStream_
     CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
     for (int r = 0; r < NREP; r++) {
         g.W = ws[r % ws.size()];
-        hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, EPI, VAR>), grid, dim3(64 * KW), 0, s, g);
+        hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, EPI, VAR, CPW>), grid, dim3(64 * KW), 0, s, g);
     }
     CK(hipStreamEndCapture(s, &graph));
     CK(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
@@ -47,7 +51,7 @@ static double time_cfg(GemmArgs g, const std::vector<uint16_t *> &ws, hipStream_
         std::vector<float> h(no); CK(hipMemcpy(h.data(), g.out_f32, no * 4, hipMemcpyDeviceToHost));
         for (size_t i = 0; i < no; i++) cs += (double)h[i] * (double)((i % 97) + 1);
     }
-    printf("  %-28s MT%d NT%d KW%d VAR%d  %7.2f us  %6.0f GB/s  grid %4dx%d  sum %.9g\n", tag, MT, NT, KW, VAR, us, bytes / us * 1e-3, grid.x,
+    printf("  %-28s MT%d NT%d KW%d VAR%d CPW%d  %7.2f us  %6.0f GB/s  grid %4dx%d  sum %.9g\n", tag, MT, NT, KW, VAR, CPW, us, bytes / us * 1e-3, grid.x,
            grid.y, cs);
     CK(hipGraphExecDestroy(ex)); CK(hipGraphDestroy(graph));
     return us;
@@ -69,6 +73,21 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&out, (size_t)128 * 8192 * 4)); CK(hipMalloc(&res, (size_t)128 * 8192 * 4)); CK(hipMalloc(&out16, (size_t)128 * 8192 * 2));
     CK(hipMemset(res, 0, (size_t)128 * 8192 * 4));
     printf("M = %d\n", M);
+    {   // the graph's per-launch floor: an empty kernel of 256 workgroups, 64 dependent launches
+        hipGraph_t graph; hipGraphExec_t ex;
+        CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+        for (int r = 0; r < 64; r++) hipLaunchKernelGGL(empty_kernel, dim3(256), dim3(512), 0, s, nullptr);
+        CK(hipStreamEndCapture(s, &graph));
+        CK(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
+        hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+        CK(hipGraphLaunch(ex, s)); CK(hipStreamSynchronize(s));
+        float best = 1e30f;
+        for (int it = 0; it < 5; it++) {
+            CK(hipEventRecord(a, s)); CK(hipGraphLaunch(ex, s)); CK(hipEventRecord(b, s)); CK(hipEventSynchronize(b));
+            float ms; CK(hipEventElapsedTime(&ms, a, b)); best = ms < best ? ms : best;
+        }
+        printf("empty kernel (256 x 512 threads) in a graph: %.2f us per launch\n", best * 1e3 / 64);
+    }
     for (const Shape &sh : shapes) {
         const size_t wb = (size_t)sh.N * sh.K * 2;
         const int NL = (int)((600ull << 20) / wb) + 1;
@@ -78,37 +97,27 @@ int main(int argc, char **argv) {
         g.A = A; g.lda = sh.K; g.ldw = sh.K; g.M = M; g.N = sh.N; g.K = sh.K;
         g.out_f32 = out; g.ldo = sh.N; g.res = res; g.ldr = sh.N; g.out_f16 = out16; g.ldo16 = sh.N;
         printf("%s (%zu MB, %d copies)\n", sh.name, wb >> 20, NL);
-        if (sh.epi == EPI_F32) {
-            time_cfg<4, 1, 8, EPI_F32, 0>(g, ws, s, "full");
-            time_cfg<4, 1, 8, EPI_F32, 4>(g, ws, s, "A via LDS-DMA");
-            time_cfg<1, 1, 8, EPI_F32, 0>(g, ws, s, "full");
-            time_cfg<1, 1, 8, EPI_F32, 4>(g, ws, s, "A via LDS-DMA");
-            time_cfg<2, 1, 8, EPI_F32, 4>(g, ws, s, "A via LDS-DMA");
-            time_cfg<4, 1, 4, EPI_F32, 0>(g, ws, s, "full");
-            time_cfg<4, 1, 4, EPI_F32, 1>(g, ws, s, "no A");
-            time_cfg<4, 1, 4, EPI_F32, 2>(g, ws, s, "no W");
-            time_cfg<4, 1, 4, EPI_F32, 3>(g, ws, s, "no loads");
-            time_cfg<2, 1, 4, EPI_F32, 0>(g, ws, s, "full");
-            time_cfg<1, 1, 4, EPI_F32, 0>(g, ws, s, "full");
-            time_cfg<1, 1, 8, EPI_F32, 0>(g, ws, s, "full");
-            time_cfg<1, 1, 8, EPI_F32, 1>(g, ws, s, "no A");
-            time_cfg<1, 1, 16, EPI_F32, 0>(g, ws, s, "full");
-            time_cfg<2, 1, 8, EPI_F32, 0>(g, ws, s, "full");
-            time_cfg<4, 1, 8, EPI_F32, 0>(g, ws, s, "full");
-            time_cfg<4, 1, 2, EPI_F32, 0>(g, ws, s, "full");
-            time_cfg<4, 2, 4, EPI_F32, 0>(g, ws, s, "full");
-        } else {
-            time_cfg<4, 2, 4, EPI_SWIGLU_F16, 0>(g, ws, s, "full");
-            time_cfg<4, 2, 4, EPI_SWIGLU_F16, 4>(g, ws, s, "A via LDS-DMA");
-            time_cfg<2, 2, 4, EPI_SWIGLU_F16, 4>(g, ws, s, "A via LDS-DMA");
-            time_cfg<2, 2, 8, EPI_SWIGLU_F16, 4>(g, ws, s, "A via LDS-DMA");
-            time_cfg<4, 2, 4, EPI_SWIGLU_F16, 1>(g, ws, s, "no A");
-            time_cfg<4, 2, 4, EPI_SWIGLU_F16, 2>(g, ws, s, "no W");
-            time_cfg<2, 2, 4, EPI_SWIGLU_F16, 0>(g, ws, s, "full");
-            time_cfg<1, 2, 4, EPI_SWIGLU_F16, 0>(g, ws, s, "full");
-            time_cfg<1, 2, 8, EPI_SWIGLU_F16, 0>(g, ws, s, "full");
-            time_cfg<4, 2, 8, EPI_SWIGLU_F16, 0>(g, ws, s, "full");
-            time_cfg<4, 2, 2, EPI_SWIGLU_F16, 0>(g, ws, s, "full");
+        if (sh.N == 4096) {   // QKV: the engine's <4,1,8> with all chunks in flight (K = 1024: 1 chunk a wave)
+            time_cfg<4, 1, 8, EPI_F32, 4, 1>(g, ws, s, "engine (CPW 1)");
+            time_cfg<4, 1, 8, EPI_F32, 3>(g, ws, s, "no loads");
+            time_cfg<4, 1, 4, EPI_F32, 4, 2>(g, ws, s, "KW4 CPW2");
+            time_cfg<2, 1, 8, EPI_F32, 4, 1>(g, ws, s, "MT2 CPW1");
+        } else if (sh.N == 1024 && sh.K == 2048) {   // o-proj: <1,1,8> CPW 2
+            time_cfg<1, 1, 8, EPI_F32, 4, 2>(g, ws, s, "engine (CPW 2)");
+            time_cfg<1, 1, 8, EPI_F32, 3>(g, ws, s, "no loads");
+            time_cfg<2, 1, 8, EPI_F32, 4, 2>(g, ws, s, "MT2 CPW2");
+            time_cfg<1, 1, 16, EPI_F32, 4, 1>(g, ws, s, "KW16 CPW1");
+        } else if (sh.epi == EPI_F32) {   // down: <1,1,8> CPW 3
+            time_cfg<1, 1, 8, EPI_F32, 4, 3>(g, ws, s, "engine (CPW 3)");
+            time_cfg<1, 1, 8, EPI_F32, 3>(g, ws, s, "no loads");
+            time_cfg<1, 1, 16, EPI_F32, 4, 0>(g, ws, s, "KW16 (1.5 chunks: loop)");
+        } else {   // gate/up: <2,2,4> CPW 2
+            time_cfg<2, 2, 4, EPI_SWIGLU_F16, 4, 2>(g, ws, s, "engine (CPW 2)");
+            time_cfg<2, 2, 4, EPI_SWIGLU_F16, 3>(g, ws, s, "no loads");
+            time_cfg<2, 2, 8, EPI_SWIGLU_F16, 4, 1>(g, ws, s, "KW8 CPW1");
+            time_cfg<4, 2, 8, EPI_SWIGLU_F16, 4, 1>(g, ws, s, "MT4 KW8 CPW1");
+            time_cfg<1, 2, 8, EPI_SWIGLU_F16, 4, 1>(g, ws, s, "MT1 KW8 CPW1");
+            time_cfg<4, 2, 4, EPI_SWIGLU_F16, 4, 2>(g, ws, s, "MT4 KW4 CPW2");
         }
         for (auto &w : ws) CK(hipFree(w));
     }
