@@ -307,12 +307,23 @@ static int run_transcription_sharded(const cli_params &p) {
     std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return size[a] > size[b]; });
     fprintf(stderr, "qwen3-asr-cli (sharded)\n  Model: %s\n  Files: %zu over %d GPU(s), %d slots each, shared queue\n\n",
             p.model_path.c_str(), N, G, p.batch);
-    // the context: the longest file's prompt + the budget (16-bit PCM: at most
-    // size / 2 samples), so long files transcribe as in the reference, which
-    // sizes its context per clip (src/qwen3_asr.cpp:223)
-    const long long max_samples = N ? size[order[0]] / 2 : 0;
+    // the stream's context: the longest file's prompt + the budget (16-bit PCM:
+    // at most size / 2 samples), capped at kStreamSecs of audio -- every slot
+    // gets that length, so one long file must not multiply the whole cache
+    // (ADVICE r4).  Longer files go to a second queue that the device threads
+    // take one at a time after their streams, each in a context sized to that
+    // file as the reference sizes its context per clip (src/qwen3_asr.cpp:223).
+    constexpr long long kStreamSecs = 120;
+    std::vector<size_t> longq;
+    while (!order.empty() && size[order.front()] / 2 > kStreamSecs * 16000) {
+        longq.push_back(order.front());
+        order.erase(order.begin());
+    }
+    const size_t NS = order.size();
+    const long long max_samples = NS ? size[order[0]] / 2 : 0;
     const int n_ctx = qasr_prompt_len(qasr_encoder_frames(qasr_mel_frames((int)std::min<long long>(max_samples, 1LL << 30)))) +
                       p.max_tokens + 64;
+    std::atomic<size_t> next_long{0};
     std::vector<qwen3_asr::transcribe_result> results(N);
     std::vector<std::string> errors(G);
     std::atomic<size_t> next{0};
@@ -333,7 +344,7 @@ static int run_transcription_sharded(const cli_params &p) {
             auto fetch = [&](int &id, std::vector<float> &pcm) {
                 for (;;) {
                     const size_t k = next++;
-                    if (k >= N) return false;
+                    if (k >= NS) return false;
                     const size_t i = order[k];
                     int sr = 0;
                     if (qwen3_asr::load_audio_file(p.audio_paths[i], pcm, sr) && sr == 16000) {
@@ -349,7 +360,14 @@ static int run_transcription_sharded(const cli_params &p) {
                 std::lock_guard<std::mutex> lk(res_mu);
                 results[id] = std::move(r);
             };
-            if (!asr.transcribe_stream(fetch, sink, tp, n_ctx)) errors[g] = asr.get_error();
+            if (NS && !asr.transcribe_stream(fetch, sink, tp, n_ctx)) { errors[g] = asr.get_error(); return; }
+            for (size_t k; (k = next_long++) < longq.size();) {   // files past the stream's cap, one at a time
+                const size_t i = longq[k];
+                qwen3_asr::transcribe_result r = asr.transcribe(p.audio_paths[i], tp);
+                std::lock_guard<std::mutex> lk(res_mu);
+                if (r.success) samples += size[i] / 2;
+                results[i] = std::move(r);
+            }
         });
     }
     for (auto &t : th) t.join();

@@ -75,7 +75,12 @@ bool Qwen3ASR::load_model(const std::string &model_path) {
 bool Qwen3ASR::ensure_ctx(int batch, int n_ctx) {
     if (ctx_ && ctx_batch_ >= batch && ctx_len_ >= n_ctx) return true;
     if (ctx_) { qasr_ctx_free(ctx_); ctx_ = nullptr; }
-    const int nb = std::max(batch, ctx_batch_), nl = std::max(n_ctx, ctx_len_);
+    // keep the larger shape only while the KV cache stays in bounds: a long
+    // single clip after a many-slot stream gets (1, its length), not (slots,
+    // its length) -- that product multiplies the cache (CLI sharding)
+    const long long kMaxCells = 1LL << 22;   // slots x positions (~0.7 TB of f16 KV at 0.6B would be absurd)
+    int nb = std::max(batch, ctx_batch_), nl = std::max(n_ctx, ctx_len_);
+    if ((long long)nb * nl > kMaxCells) { nb = batch; nl = n_ctx; }
     if (qasr_ctx_create(model_, nb, nl, &ctx_) != 0) {
         error_msg_ = std::string("Failed to initialize KV cache: ") + qasr_last_error();
         ctx_ = nullptr;

@@ -95,10 +95,11 @@ def test_staged_pool_subsets(tiny):
 def test_cli_sharded_file_list(tiny, tmp_path, tiny_gguf):
     """qwen3-asr-cli --devices / --file-list / --batch: outputs in input
     order, identical to one file at a time (a 40 s file included: the
-    sharded path sizes its context to the longest file); --profile prints
-    the report"""
+    sharded stream sizes its context to the longest file up to 120 s; the
+    130 s file goes to the long-file queue, its own context -- ADVICE r4);
+    --profile prints the report"""
     paths = []
-    for i, secs in enumerate((1.2, 2.2, 40.0, 3.2)):
+    for i, secs in enumerate((1.2, 2.2, 40.0, 130.0, 3.2)):
         p = str(tmp_path / f"c{i}.wav")
         qasr.write_wav(p, qasr.synth_pcm(33000 + i, int(secs * SR)))
         paths.append(p)
