@@ -79,7 +79,7 @@ def parse():
                          "ranks (0: skip)")
     ap.add_argument("--set-seconds", type=float, default=30.0)
     ap.add_argument("--set-pool", type=int, default=128, help="distinct seeded clips staged per GPU (utterance i = clip i mod pool)")
-    ap.add_argument("--set-slots", type=int, default=64, help="continuous-batching slots per GPU")
+    ap.add_argument("--set-slots", type=int, default=128, help="continuous-batching slots per GPU")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous check without a GPU: ranks join a gloo group, time a barrier and rank 0 "
                          "prints the JSON line with value 0 (tests/test_dist.py)")

@@ -1245,7 +1245,7 @@ static int decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange r
     float *x = c->d_x;
     const bool skinny = B <= 8;
     // decode batches: the LM head as one launch (lmhead.hip's shape conditions)
-    const bool lmh_one = !skinny && B <= 64 && c->fuse.lmh && H == 1024 && hp.vocab % 16 == 0;
+    const bool lmh_one = !skinny && B <= 128 && c->fuse.lmh && H == 1024 && hp.vocab % 16 == 0;
     const size_t layer_kv = (size_t)c->max_batch * hp.n_kv_head * c->max_ctx * 128;
     const int nl = step_layers(c);   // diagnostic layer cap
     // probed group (emitted alone): every launch in it folds its block times into one record

@@ -122,9 +122,10 @@ struct GemvArgs {
     unsigned long long *stamp;           // kernel-duration probe record (dev_common.h stamp_start/end) or null
     int *nkv;                            // launch_lmhead_batch: n_kv[b] += 1 with pos[b] (decode batches) or null
     int n_valid;                         // launch_lmhead_batch: columns >= n_valid never win; 0 = N
+    int keep_step;                       // lmhead_batch_kernel: leave *step as it is (a first row-half launch)
 };
 void launch_gemv(int epi, const GemvArgs &g, hipStream_t s);
-// lmhead.hip: decode-batch LM head in one launch (9..64 rows, K = 1024, f16 W):
+// lmhead.hip: decode-batch LM head in one launch (9..64 rows; 65..128 rows: two, one per row half; K = 1024, f16 W):
 // RMS norm of x with norm_w, GEMM against W [N][K], optional fp32 logits,
 // per-row first-index argmax, and the fused bookkeeping of EPI_ARGMAX above
 // (plus nkv); amax and done zero at rest.  false = shape not covered

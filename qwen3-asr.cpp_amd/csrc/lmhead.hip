@@ -188,7 +188,7 @@ __global__ __launch_bounds__(64 * WPG) void lmhead_batch_kernel(GemvArgs g) {
             __hip_atomic_store(g.amax + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (tid == 0) {
-            *g.step = st + 1;
+            if (!g.keep_step) *g.step = st + 1;
             __hip_atomic_store(g.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
@@ -216,10 +216,37 @@ void run_lmhead(const GemvArgs &g, hipStream_t s) {
 
 }  // namespace
 
+static void lmhead_rows(const GemvArgs &g, hipStream_t s) {   // <= 64 rows
+    const int mt = (g.M + 15) / 16;
+    if (mt == 1) run_lmhead<1>(g, s);
+    else if (mt == 2) run_lmhead<2>(g, s);
+    else if (mt == 3) run_lmhead<3>(g, s);
+    else run_lmhead<4>(g, s);
+}
+
 bool launch_lmhead_batch(const GemvArgs &g, hipStream_t s) {
-    if (g.M < 1 || g.M > 64 || g.K != LMH_K || g.N % 16 != 0 || !g.x || !g.norm_w || !g.amax || !g.done || !g.tok_out ||
+    if (g.M < 1 || g.M > 128 || g.K != LMH_K || g.N % 16 != 0 || !g.x || !g.norm_w || !g.amax || !g.done || !g.tok_out ||
         !g.step || !g.pos || g.Wd)
         return false;
+    if (g.M > 64) {   // 65..128 rows: the activation image of 128 rows (256 KB) exceeds the LDS, so one launch
+                      // per 64-row half; the first leaves the step counter to the second (both read the same step)
+        GemvArgs a = g;
+        a.M = 64;
+        a.keep_step = 1;
+        lmhead_rows(a, s);
+        GemvArgs b = g;
+        b.M = g.M - 64;
+        b.x = g.x + (long)64 * g.ldx;
+        if (g.out_f32) b.out_f32 = g.out_f32 + (long)64 * g.ldo;
+        b.amax = g.amax + 64;
+        b.tok_out = g.tok_out + 64;
+        if (g.hist) b.hist = g.hist + (long)64 * g.hist_stride;
+        b.pos = g.pos + 64;
+        if (g.nkv) b.nkv = g.nkv + 64;
+        b.keep_step = 0;
+        lmhead_rows(b, s);
+        return true;
+    }
     const int mt = (g.M + 15) / 16;
     if (mt == 1) run_lmhead<1>(g, s);
     else if (mt == 2) run_lmhead<2>(g, s);

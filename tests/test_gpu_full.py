@@ -539,13 +539,14 @@ OPTION_CASES = {
     "fx_vpf": (0, "bits", 1), "fx_vpf=1": (1, "bits", 1), "fx_vpf=3": (3, "bits", 1),
     "fa_exact_prefill": (0, "oracle", 1),
     "att_spl": (128, "bits", 16), "lmh": (0, "bits", 16), "skinny": (0, "oracle", 16),
+    "lmh@100": (0, "bits", 100),   # 65..128 rows: the one-launch LM head as two row-half launches
 }
 
 
 @pytest.mark.parametrize("case", list(OPTION_CASES))
 def test_full_option_matches_default(full, case):
     m, _, om = full
-    name = case.split("=")[0]
+    name = case.split("=")[0].split("@")[0]
     val, kind, B = OPTION_CASES[case]
     pcm = qasr.synth_pcm(19000, 2 * SR)
     feats = om.encode(op.log_mel(pcm))
