@@ -17,6 +17,7 @@
 // NHWC conv activations (3x3, stride 2, pad 1) so conv2/conv3 of the audio
 // encoder never materialise im2col buffers (src/audio_encoder.cpp:116-128).
 #include "gemm_epi.h"
+#include "gemm8p.h"
 
 namespace qasr {
 
@@ -350,7 +351,18 @@ static void dispatch_tiles(const GemmArgs &g, hipStream_t s) {
         // waves, 4-stage ring, for the wide projections of one clip (~1.2k rows:
         // prefill gate/up 39.6 -> 29.4, qkv 27.3 -> 25.1, encoder fc1 22.6 -> 21.3,
         // encoder qkv 19.8 -> 18.9; the narrow deep ones stay on 64 x 64 x 4)
+        // round 5 (tools/micro/g8_bench.hip, MI355X, us per launch at 64 x 30 s): the 256 x
+        // 256 8-phase tile (gemm8p.h) for every >= 2048-row projection it takes --
+        // prefill qkv 370 -> 280, o 167 -> 125, gate/up 510 -> 351, down 220 -> 166,
+        // encoder fc1 383 -> 258, fc2 251 -> 176, qkv 219 -> 164
         const bool big = g.M >= 2048 && g.N % 128 == 0;
+        if constexpr (EPI != EPI_ARGMAX) {
+            if (g.M >= 2048 && g.N >= 256 && g.N % 32 == 0 && g.K % 128 == 0 && g.lda % 8 == 0 && g.ldw % 8 == 0 && g.ldo % 4 == 0 &&
+                g.ldo16 % 4 == 0 && (!g.res || g.ldr % 4 == 0) && !g.regs_staged) {
+                run_gemm8p<EPI>(g, s);
+                return;
+            }
+        }
         if (big && !g.regs_staged && g.N % 256 == 0) {
             run_glds<256, 256, 1, 3, AMODE, EPI, 4>(g, s);
         } else if (big && !g.regs_staged) {   // LDS-DMA stages (tools/micro/glds_gemm_bench.hip: +5-10 %)

@@ -60,13 +60,26 @@ static void glds(GemmArgs g, hipStream_t s) {
            2.0 * g.M * g.N * g.K / us * 1e-6, maxdiff(g.out_f32, (size_t)g.M * g.N));
 }
 
+template <int EPI = EPI_F32>
+static void g8(GemmArgs g, hipStream_t s) {
+    if (g.K % 128) { printf("  8p    256x256 n/a\n"); return; }
+    CK(hipMemset(g.out_f32, 0, (size_t)g.M * g.N * 4));
+    double us = timeit([&] { run_gemm8p<EPI>(g, s); }, s);
+    printf("  8p    256x256 BK64      %8.1f us  %7.1f TFLOP/s  maxdiff %.3g\n", us, 2.0 * g.M * g.N * g.K / us * 1e-6,
+           maxdiff(g.out_f32, (size_t)g.M * g.N));
+    us = timeit([&] { run_gemm8p<G8_EPI_NONE>(g, s); }, s);
+    printf("  8p    no stores             %8.1f us  %7.1f TFLOP/s\n", us, 2.0 * g.M * g.N * g.K / us * 1e-6);
+}
+
 int main(int argc, char **argv) {
     hipStream_t s; CK(hipStreamCreate(&s));
     struct Sh { const char *name; int M, N, K; };
     Sh shapes[] = {{"enc qkv b64", 24960, 2688, 896}, {"enc fc1 b64", 24960, 3584, 896}, {"enc fc2 b64", 24960, 896, 3584},
                    {"enc o b64", 24960, 896, 896},     {"prefill qkv b64", 25920, 4096, 1024}, {"prefill dn b64", 25920, 1024, 3072},
-                   {"enc fc1 b1", 1196, 3584, 896}};
-    const size_t MA = (size_t)25920 * 4096, MW = (size_t)4096 * 4096, MO = (size_t)25920 * 4096;
+                   {"prefill o b64", 25920, 1024, 2048}, {"prefill gu b64", 25920, 6144, 1024}, {"enc fc1 b1", 1196, 3584, 896},
+                   {"odd M", 2500, 1024, 1024}, {"qkv K2048", 25920, 4096, 2048}, {"qkv K4096", 25920, 4096, 4096},
+                   {"4096^3", 4096, 4096, 4096}, {"8192x4096x4096", 8192, 4096, 4096}};
+    const size_t MA = (size_t)25920 * 4096, MW = (size_t)4096 * 4096, MO = (size_t)25920 * 6144;   // the largest M x N below (prefill gu)
     uint16_t *A, *W; float *out;
     CK(hipMalloc(&A, MA * 2)); CK(hipMalloc(&W, MW * 2)); CK(hipMalloc(&out, MO * 4)); CK(hipMalloc(&g_ref, MO * 4));
     {
@@ -77,6 +90,7 @@ int main(int argc, char **argv) {
         CK(hipMemcpy(W, h.data() + 7, MW * 2, hipMemcpyHostToDevice));
     }
     const bool b1only = argc > 1 && argv[1][0] == '1';
+    const bool quick = argc > 1 && argv[1][0] == 'q';   // the 8-phase kernel only (against the reference tile)
     if (b1only) {   // single-clip (configs[1]) shapes: the dispatch's register tiles against 8-wave LDS-DMA tiles
         Sh b1[] = {{"enc qkv b1", 1196, 2688, 896}, {"enc fc1 b1", 1196, 3584, 896}, {"enc fc2 b1", 1196, 896, 3584},
                    {"enc o b1", 1196, 896, 896},    {"pre qkv b1", 1211, 4096, 1024}, {"pre o b1", 1211, 1024, 2048},
@@ -103,15 +117,11 @@ int main(int argc, char **argv) {
         g.A = A; g.lda = sh.K; g.W = W; g.ldw = sh.K; g.M = sh.M; g.N = sh.N; g.K = sh.K; g.out_f32 = out; g.ldo = sh.N;
         printf("%s  M=%d N=%d K=%d\n", sh.name, sh.M, sh.N, sh.K);
         ref<128, 128, 1>(g, s);
-        glds<128, 128, 1, 2>(g, s);
-        glds<256, 256, 1, 4, 4>(g, s);
-        glds<256, 256, 1, 3, 4>(g, s);
-        glds<256, 256, 2, 2, 4>(g, s);
-        glds<256, 128, 1, 4, 4>(g, s);
-        glds<256, 128, 2, 3, 4>(g, s);
-        glds<256, 128, 1, 4, 2>(g, s);
-        glds<128, 256, 1, 4, 4>(g, s);
-        glds<128, 128, 1, 4, 4>(g, s);
+        if (!quick) {
+            glds<128, 128, 1, 2>(g, s);
+            glds<256, 256, 1, 3, 4>(g, s);
+        }
+        g8(g, s);
     }
     return 0;
 }
