@@ -1120,7 +1120,7 @@ __device__ __forceinline__ void kvc_step(const DecodeAttnArgs &a, const half8 *q
 // kernel boundary, the scores' round trip through HBM and the second
 // launch's ramp go, and one CU's workgroups overlap their K and V^T streams.
 template <int FX>
-__global__ __launch_bounds__(256) void decode_attn_seq_kernel(DecodeAttnArgs a) {
+__global__ __launch_bounds__(256, FX ? 4 : 1) void decode_attn_seq_kernel(DecodeAttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) float fxs[];
     __shared__ __attribute__((aligned(16))) uint16_t qs[2][128];
     __shared__ __attribute__((aligned(16))) uint16_t knew[128];

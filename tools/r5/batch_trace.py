@@ -12,3 +12,5 @@ print(f"workgroups {len(x)}: start {us(x[:, 0].min()):.2f}..{us(x[:, 0].max()):.
 for name, a, b in (("q/k/v + norm/rope", 0, 1), ("K stream + scores", 1, 2), ("weights + chain", 2, 3), ("whole", 0, 3)):
     d = (x[:, b] - x[:, a]) / 100.0
     print(f"  {name:20s} median {np.median(d):6.2f}  p10 {np.percentile(d, 10):6.2f}  p90 {np.percentile(d, 90):6.2f}  max {d.max():6.2f} us")
+starts = np.sort(us(x[:, 0]))
+print("start-time deciles (us):", " ".join(f"{v:.1f}" for v in np.percentile(starts, [0, 10, 25, 50, 75, 90, 100])))
