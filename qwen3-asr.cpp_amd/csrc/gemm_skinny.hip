@@ -128,6 +128,7 @@ __global__ __launch_bounds__(64 * KW) void gemm_skinny_kernel(GemmArgs g) {
     // row) per wave (CPW of them with CPW > 0), in the same LDS as the
     // partial-tile reduction after the loop
     constexpr int RED_B = KW * NTILE * 64 * 16, ALDS_B = ALDS ? KW * MT * 16 * 128 * 2 * (CPW > 0 ? CPW : 1) : 0;
+    static_assert((RED_B > ALDS_B ? RED_B : ALDS_B) + 512 <= 160 * 1024, "LDS per workgroup");
     __shared__ __attribute__((aligned(16))) unsigned char lds_raw[RED_B > ALDS_B ? RED_B : ALDS_B];
     floatx4 (*red)[NTILE][64] = reinterpret_cast<floatx4 (*)[NTILE][64]>(lds_raw);
     uint16_t *alds = reinterpret_cast<uint16_t *>(lds_raw);
@@ -535,8 +536,14 @@ bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s) {
         case EPI_F32:
         case EPI_F16:
             if (g.N % 16 != 0) return false;
-            // tilings picked with tools/skinny_bench.hip at M = 64
-            if (g.N >= 4096) {   // QKV: 256 column tiles, all rows per block, K over 8 waves
+            // tilings picked with tools/skinny_bench.hip at M = 64; 65..128 rows (round 5, M = 128,
+            // us a launch): QKV 32-column tiles of 64 rows 9.55 -> 7.30, o / down 32-row blocks
+            // 8.01 -> 6.14 / 12.64 -> 8.81 -- fewer activation re-reads per weight byte
+            if (g.M > 64 && g.N >= 4096 && g.N % 32 == 0) {
+                if (epi == EPI_F32) run_skinny<4, 2, 8, EPI_F32>(g, s); else run_skinny<4, 2, 8, EPI_F16>(g, s);
+            } else if (g.M > 64) {
+                if (epi == EPI_F32) run_skinny<2, 1, 8, EPI_F32>(g, s); else run_skinny<2, 1, 8, EPI_F16>(g, s);
+            } else if (g.N >= 4096) {   // QKV: 256 column tiles, all rows per block, K over 8 waves
                 if (epi == EPI_F32) skinny_mt<4, 1, 8, EPI_F32>(g, s); else skinny_mt<4, 1, 8, EPI_F16>(g, s);
             } else {             // o / down projections: 64 column tiles x 16-row blocks, K over 8 waves
                 if (epi == EPI_F32) skinny_mt<1, 1, 8, EPI_F32>(g, s); else skinny_mt<1, 1, 8, EPI_F16>(g, s);
@@ -548,7 +555,10 @@ bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s) {
             // 33..64 rows: all of them in one row block, K over 8 waves (one chunk each at K = 1024):
             // every weight byte read once instead of once per 32-row block (tools/skinny_bench.hip,
             // 64 rows, 6144 x 1024: 9.31 -> 7.13 us a launch, round 5)
-            if (g.M > 32 && g.M <= 64) {
+            // 65..128 rows: 64-row blocks of 64 columns, 12.95 -> 10.38 us at M = 128 (round 5)
+            if (g.M > 64 && g.N % 64 == 0) {
+                if (epi == EPI_SWIGLU_F16) run_skinny<4, 4, 8, EPI_SWIGLU_F16>(g, s); else run_skinny<4, 4, 8, EPI_SWIGLU_F32>(g, s);
+            } else if (g.M > 32 && g.M <= 64) {
                 if (epi == EPI_SWIGLU_F16) run_skinny<4, 2, 8, EPI_SWIGLU_F16>(g, s); else run_skinny<4, 2, 8, EPI_SWIGLU_F32>(g, s);
             } else if (epi == EPI_SWIGLU_F16) {
                 skinny_mt<2, 2, 4, EPI_SWIGLU_F16>(g, s);

@@ -540,6 +540,7 @@ OPTION_CASES = {
     "fa_exact_prefill": (0, "oracle", 1),
     "att_spl": (128, "bits", 16), "lmh": (0, "bits", 16), "skinny": (0, "oracle", 16),
     "lmh@100": (0, "bits", 100),   # 65..128 rows: the one-launch LM head as two row-half launches
+    "skinny@100": (0, "oracle", 100),   # 65..128 rows: the skinny GEMMs' 128-row tilings (default) and the tiled GEMMs
 }
 
 
@@ -569,13 +570,21 @@ def test_full_option_matches_default(full, case):
         assert np.array_equal(base[0], alt[0]) and np.array_equal(base[1], alt[1]), case
         assert base[2] == alt[2], case
     else:
+        # the option's run against the oracle (prefill rows and the decode step's rows), and the
+        # default's decode rows too: the default path differs from the option's only there
         flags = op.OracleModel.FA_V_F32 if name == "fa_exact_prefill" else 0
         d = op.OracleDecoder(om, 160, flags)
         lo = d.forward(ids, 0, feats, pos)
+        ld = d.forward([1234], len(ids))
         for b in range(B):
             ab, rel = _err(alt[0][b], lo)
             assert rel <= REL_LOGITS and ab <= ABS_LOGITS, (case, b, ab, rel)
+            if name != "fa_exact_prefill":
+                for run in (base, alt):
+                    ab, rel = _err(run[1][b], ld)
+                    assert rel <= REL_LOGITS and ab <= ABS_LOGITS, (case, "decode", b, ab, rel)
         assert all(t == alt[2][0] for t in alt[2])
+        assert all(t == base[2][0] for t in base[2])
 
 
 @pytest.mark.timeout(900)

@@ -97,7 +97,31 @@ int main(int argc, char **argv) {
         g.A = A; g.lda = sh.K; g.ldw = sh.K; g.M = M; g.N = sh.N; g.K = sh.K;
         g.out_f32 = out; g.ldo = sh.N; g.res = res; g.ldr = sh.N; g.out_f16 = out16; g.ldo16 = sh.N;
         printf("%s (%zu MB, %d copies)\n", sh.name, wb >> 20, NL);
-        if (sh.N == 4096) {   // QKV: the engine's <4,1,8> with all chunks in flight (K = 1024: 1 chunk a wave)
+        if (M > 64) {   // 65..128 rows (round 5): fewer activation re-reads (NT 2) against more row blocks
+            if (sh.N == 4096) {
+                time_cfg<4, 1, 8, EPI_F32, 4, 1>(g, ws, s, "engine (MT4 NT1 CPW1)");
+                time_cfg<4, 2, 8, EPI_F32, 4, 1>(g, ws, s, "MT4 NT2 CPW1");
+                time_cfg<2, 2, 8, EPI_F32, 4, 1>(g, ws, s, "MT2 NT2 CPW1");
+                time_cfg<4, 4, 8, EPI_F32, 4, 1>(g, ws, s, "MT4 NT4 CPW1");
+                time_cfg<2, 4, 8, EPI_F32, 4, 1>(g, ws, s, "MT2 NT4 CPW1");
+            } else if (sh.N == 1024 && sh.K == 2048) {
+                time_cfg<1, 1, 8, EPI_F32, 4, 2>(g, ws, s, "engine (MT1 NT1 CPW2)");
+                time_cfg<2, 1, 8, EPI_F32, 4, 2>(g, ws, s, "MT2 NT1 CPW2");
+                time_cfg<2, 2, 8, EPI_F32, 4, 2>(g, ws, s, "MT2 NT2 CPW2");
+                time_cfg<1, 2, 8, EPI_F32, 4, 2>(g, ws, s, "MT1 NT2 CPW2");
+            } else if (sh.epi == EPI_F32) {
+                time_cfg<1, 1, 8, EPI_F32, 4, 3>(g, ws, s, "engine (MT1 NT1 CPW3)");
+                time_cfg<1, 2, 8, EPI_F32, 4, 3>(g, ws, s, "MT1 NT2 CPW3");
+                time_cfg<2, 1, 8, EPI_F32, 4, 0>(g, ws, s, "MT2 NT1 (chunk loop)");
+                time_cfg<2, 2, 8, EPI_F32, 4, 0>(g, ws, s, "MT2 NT2 (chunk loop)");
+            } else {
+                time_cfg<2, 2, 4, EPI_SWIGLU_F16, 4, 2>(g, ws, s, "engine (MT2 NT2 KW4 CPW2)");
+                time_cfg<4, 2, 8, EPI_SWIGLU_F16, 4, 1>(g, ws, s, "MT4 NT2 KW8 CPW1");
+                time_cfg<4, 4, 8, EPI_SWIGLU_F16, 4, 1>(g, ws, s, "MT4 NT4 KW8 CPW1");
+                time_cfg<2, 4, 8, EPI_SWIGLU_F16, 4, 1>(g, ws, s, "MT2 NT4 KW8 CPW1");
+                time_cfg<2, 2, 8, EPI_SWIGLU_F16, 4, 1>(g, ws, s, "MT2 NT2 KW8 CPW1");
+            }
+        } else if (sh.N == 4096) {   // QKV: the engine's <4,1,8> with all chunks in flight (K = 1024: 1 chunk a wave)
             time_cfg<4, 1, 8, EPI_F32, 4, 1>(g, ws, s, "engine (CPW 1)");
             time_cfg<4, 1, 8, EPI_F32, 3>(g, ws, s, "no loads");
             time_cfg<4, 1, 4, EPI_F32, 4, 2>(g, ws, s, "KW4 CPW2");
