@@ -588,6 +588,13 @@ def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
     assert len(toks) == n_utt and all(len(t) == bud for t in toks.values()), "utterance set: a budget was not met"
     walls = res["rank_wall_s"]
     st = stats[0]
+    # the encoder at batch: rank 0's clips' encoder FLOPs over the refills' encoder
+    # device time (HIP events around run_encoder; mel excluded), against the dense fp16 MFMA peak
+    ef = st.n_clips * encoder_flops(m.hp, ns)
+    enc = ({"bound": "mfma", "achieved": round(ef / (st.t_encode_ms / 1e3) / 1e12, 1), "peak": MFMA_F16_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(ef / (st.t_encode_ms / 1e3) / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
+            "encoder_ms": round(st.t_encode_ms, 1), "mel_ms": round(st.t_mel_ms, 1), "clips": st.n_clips}
+           if st.t_encode_ms > 0 else None)
     return {
         "workload": f"configs[3]: {n_utt} x {secs:g} s utterances (16 kHz, a pool of {pool} distinct seeded clips per "
                     f"GPU), one shared longest-first queue feeding {args.set_slots} continuous-batching slots per GPU, "
@@ -602,6 +609,7 @@ def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
         "rank0_stream": {"clips": st.n_clips, "refill_prefills": st.n_prefills, "decode_steps": st.n_steps,
                          "slot_utilisation": round(st.live_steps / max(1, st.slot_steps), 4),
                          "prefill_ms": round(st.t_prefill_ms, 1), "decode_ms": round(st.t_decode_ms, 1)},
+        "encoder_roofline": enc,
         "collectives": "barrier + max wall time + all_gather of per-rank times and token ids (RCCL); the queue is a "
                        "TCPStore counter (one add per utterance)",
     }

@@ -211,6 +211,8 @@ typedef struct {
     int64_t n_steps;                        /* decode steps (each over all the slots) */
     int64_t slot_steps, live_steps;         /* slot-steps run, of which decoding a live clip */
     double t_prefill_ms, t_decode_ms, t_total_ms;  /* host wall time: refills, decode chunks, call */
+    double t_mel_ms, t_encode_ms;           /* device time (HIP events) of the refills' mel / encoder stages,
+                                               parts of t_prefill_ms */
 } qasr_stream_stats;
 int qasr_run_stream(qasr_ctx *c, int slots, qasr_fetch_fn fetch, qasr_sink_fn sink, void *user, int max_tokens, int ignore_eos,
                     qasr_stream_stats *stats);

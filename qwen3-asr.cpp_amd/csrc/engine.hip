@@ -472,16 +472,19 @@ extern "C" int qasr_model_load(const char *path, int device, qasr_model **out) {
         size_t bytes = t->nbytes;
         ups.push_back({n, bytes, (void **)dst, [t, bytes](uint8_t *o) { memcpy(o, t->data, bytes); }});
     };
-    // conv kernels: [oc][ic][kh][kw] -> [oc][kh][kw][ic] (im2col K order of the implicit GEMM)
+    // conv kernels: [oc][ic][kh][kw] -> [oc][kh][kw][ic] (im2col K order of the implicit GEMM),
+    // rows zero-padded to conv_kpad(IC) (the 8-phase tile's K % 128; gemm8p.h)
     auto conv_w = [&](const std::string &n, int IC, uint16_t **dst) {
         const gguf_tensor *t = need(n, {3, 3, IC, C}, DT_F16);
         if (!t) return;
-        ups.push_back({n, (size_t)C * IC * 9 * 2, (void **)dst, [t, IC, C](uint8_t *o) {
+        const int KP = conv_kpad(IC);
+        ups.push_back({n, (size_t)C * KP * 2, (void **)dst, [t, IC, C, KP](uint8_t *o) {
                            const uint16_t *s = (const uint16_t *)t->data;
                            uint16_t *d = (uint16_t *)o;
+                           memset(d, 0, (size_t)C * KP * 2);
                            for (int oc = 0; oc < C; oc++)
                                for (int ic = 0; ic < IC; ic++)
-                                   for (int k = 0; k < 9; k++) d[((size_t)oc * 9 + k) * IC + ic] = s[((size_t)oc * IC + ic) * 9 + k];
+                                   for (int k = 0; k < 9; k++) d[(size_t)oc * KP + (size_t)k * IC + ic] = s[((size_t)oc * IC + ic) * 9 + k];
                        }});
     };
     copy_f16("audio.encoder.conv1.weight", {3, 3, 1, C}, &m->conv1_w);
@@ -972,7 +975,7 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     g.C = C;
     g.gelu = m->gelu;
     // conv2: act1 (NHWC, H=64) -> act2 (NHWC, H=32)
-    g.A = c->act1.as<uint16_t>(); g.W = m->conv2_w; g.ldw = 9 * C; g.M = r2; g.N = C; g.K = 9 * C;
+    g.A = c->act1.as<uint16_t>(); g.W = m->conv2_w; g.ldw = conv_kpad(C); g.M = r2; g.N = C; g.K = 9 * C;
     g.row_start = c->rs2.as<int>(); g.bias = m->conv2_b; g.out_f16 = c->act2.as<uint16_t>(); g.ldo16 = C;
     launch_gemm_c(c, AM_CONV2, EPI_GELU_F16, g, s);
     // conv3: act2 -> act3 rows ordered (chunk, w, h) so conv_out's A is dense
@@ -2119,6 +2122,12 @@ static int run_stream(qasr_ctx *c, int slots, const std::function<bool(StreamCli
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     };
     qasr_stream_stats st{};
+    // device time of each refill's mel and encoder stages (the utterance set's encoder roofline)
+    struct StageEvents {
+        hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+        ~StageEvents() { for (hipEvent_t x : e) if (x) (void)hipEventDestroy(x); }
+    } ev;
+    for (hipEvent_t &x : ev.e) HIPCHK(hipEventCreate(&x));
     std::vector<StreamSlot> sl(S);
     bool open = true;
     int rc;
@@ -2181,9 +2190,11 @@ static int run_stream(qasr_ctx *c, int slots, const std::function<bool(StreamCli
             }
             std::vector<long> mo;
             std::vector<int> T, Nb;
-            if ((rc = run_mel(c, off, ns, mo, T, staged ? c->pcm.as<float>() : c->spcm.as<float>())) ||
-                (rc = run_encoder(c, c->mel.as<float>(), mo, T, false, Nb)))
-                return rc;
+            HIPCHK(hipEventRecord(ev.e[0], s));
+            if ((rc = run_mel(c, off, ns, mo, T, staged ? c->pcm.as<float>() : c->spcm.as<float>()))) return rc;
+            HIPCHK(hipEventRecord(ev.e[1], s));
+            if ((rc = run_encoder(c, c->mel.as<float>(), mo, T, false, Nb))) return rc;
+            HIPCHK(hipEventRecord(ev.e[2], s));
             std::vector<int32_t> pids;
             std::vector<int> P(R), ap(R);
             for (int r = 0; r < R; r++) {
@@ -2199,6 +2210,11 @@ static int run_stream(qasr_ctx *c, int slots, const std::function<bool(StreamCli
             if ((rc = check_dev_err(c))) return rc;
             st.n_prefills++;
             st.t_prefill_ms += ms_since(t0);
+            float mel_ms = 0.f, enc_ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&mel_ms, ev.e[0], ev.e[1]));
+            HIPCHK(hipEventElapsedTime(&enc_ms, ev.e[1], ev.e[2]));
+            st.t_mel_ms += mel_ms;
+            st.t_encode_ms += enc_ms;
             for (int r = 0; r < R; r++) {
                 StreamSlot &x = sl[slots[r]];
                 x.id = ids[r];

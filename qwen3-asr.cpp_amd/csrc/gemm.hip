@@ -327,6 +327,15 @@ static void run_glds(const GemmArgs &g, hipStream_t s) {
 template <int AMODE, int EPI>
 static void dispatch_tiles(const GemmArgs &g, hipStream_t s) {
     if constexpr (AMODE != AM_DENSE) {
+        // round 5: the 8-phase tile over the implicit im2col (weights zero-padded to g.ldw = K
+        // rounded up to 128; tools/micro/g8_bench.hip) for >= 2048 output rows
+        if (g.M >= 2048 && g.N >= 256 && g.N % 32 == 0 && g.C % 8 == 0 && g.ldw % 128 == 0 && g.ldw >= g.K &&
+            g.ldw - g.K < 128 && g.ldo16 % 4 == 0 && !g.regs_staged) {
+            GemmArgs h = g;
+            h.K = g.ldw;
+            run_gemm8p<EPI, AMODE>(h, s);
+            return;
+        }
         // conv: K = 9*C, slab group must stay inside one tap -> C % (32*KS) == 0
         static const int wide = [] { const char *e = getenv("QASR_CONV_WIDE"); return e ? atoi(e) : 1; }();
         if (wide && g.N == 480) {

@@ -30,6 +30,14 @@
 // retired those reads before its first barrier (B0: lgkmcnt(8) after the 4 B
 // reads), two phases after otherwise.
 //
+// AMODE AM_CONV2 / AM_CONV3: the audio encoder's 3x3 stride-2 convs as implicit
+// GEMMs over NHWC fp16 activations (gemm_kernel's gather): K = (tap, channel),
+// each lane's 16-B piece is 8 channels of one tap, so the tap / channel split is
+// per lane (channels % 8 == 0); a lane keeps its 4 rows' input origin (chunk base
+// row, 2oh - 1, 2ow - 1, input width) in 8 registers, and taps in the padding --
+// or in K past 9 * C, up to the weights' zero-padded row length (K % 128 == 0) --
+// fetch a zero line.
+//
 // Every accumulator takes its K in the order of gemm_kernel / gemm_glds_kernel
 // (32-deep steps, k ascending) with the same MFMA, so the outputs are
 // bit-identical to theirs.  A last row (column) tile that would run past M (N)
@@ -44,6 +52,7 @@ namespace qasr {
 typedef __attribute__((address_space(3))) void lds_void_8p;
 typedef __attribute__((address_space(1))) void glb_void_8p;
 
+__device__ __attribute__((aligned(64))) uint32_t g8_zero_line[16];
 constexpr int G8_EPI_NONE = 99;    // tools/micro/g8_bench.hip: no output stores
 constexpr int G8_HALF = 128 * 64;   // halves per [128][64] image (16 KiB)
 // image of half-tile hid (0 A0, 1 A1, 2 B0, 3 B1) of buffer buf, in halves
@@ -172,8 +181,9 @@ __device__ __forceinline__ void g8_epilogue(const GemmArgs &g, floatx4 (&acc)[2]
 }
 
 // grid: one workgroup per 256 x 256 tile, 1-D, ceil(N/256) * ceil(M/256); host
-// guarantees M >= 256, N >= 256, K % 128 == 0, N % 32 == 0, EPI not EPI_ARGMAX
-template <int EPI>
+// guarantees M >= 256, N >= 256, K % 128 == 0, N % 32 == 0, EPI not EPI_ARGMAX;
+// conv modes: C % 8 == 0, K >= 9 * C, weight rows zero beyond 9 * C
+template <int EPI, int AMODE = AM_DENSE>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
     __shared__ __attribute__((aligned(16))) uint16_t smem[8 * G8_HALF];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -195,9 +205,54 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
     const int pchk = ((lane & 7) ^ ((prow >> 1) & 7)) * 8;
     // rows h*128 + p*64 + prow of the tile for half h, piece p: uniform offsets from one base
     const int aoff = (m0 + prow) * g.lda + pchk, woff = (n0 + prow) * g.ldw + pchk;
+    // conv modes, per row j of this lane's 4 [half * 2 + piece]: the input position of tap (0, 0)
+    // in 16-B units (8 channels: int32 holds a batch's whole activation), and the row's input
+    // width << 9 | bit t = tap t inside the image
+    int rbase[AMODE == AM_DENSE ? 1 : 4], rinfo[AMODE == AM_DENSE ? 1 : 4];
+    if constexpr (AMODE != AM_DENSE) {
+        constexpr int Hin = AMODE == AM_CONV2 ? 64 : 32;
+        const int C8 = g.C >> 3;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int row = m0 + (j >> 1) * 128 + (j & 1) * 64 + prow;
+            const int c = find_chunk(g.row_start, g.n_chunks, row);
+            const ChunkDesc cd = g.chunks[c];
+            const int local = row - g.row_start[c];
+            int oh, ow, cb, Win;
+            if constexpr (AMODE == AM_CONV2) {
+                ow = local % cd.W2; oh = local / cd.W2; cb = cd.row1; Win = cd.W1;
+            } else {
+                oh = local % 16; ow = local / 16; cb = cd.row2; Win = cd.W2;
+            }
+            int mask = 0;
+#pragma unroll
+            for (int t = 0; t < 9; t++) {
+                const int ih = 2 * oh - 1 + t / 3, iw = 2 * ow - 1 + t % 3;
+                mask |= (ih >= 0 && ih < Hin && iw >= 0 && iw < Win) << t;
+            }
+            rbase[j] = (cb + (2 * oh - 1) * Win + (2 * ow - 1)) * C8;
+            rinfo[j] = (Win << 9) | mask;
+        }
+    }
     // half-tile id: 0 A0, 1 A1, 2 B0, 3 B1
     auto issue = [&](int hid, int buf, int kt) {
         const bool isa = hid < 2;
+        if (AMODE != AM_DENSE && isa) {
+            const int C8 = g.C >> 3, k = kt * 64 + pchk;       // this lane's first channel of the tile, as a K index
+            const int tap = (int)((k + 0.5f) * (1.0f / g.C));   // exact: k < 2^16, C >= 8
+            const int ic8 = (k - tap * g.C) >> 3, kh = (tap * 11) >> 5, kw = tap - 3 * kh;   // tap / 3 for tap <= 10
+#pragma unroll
+            for (int p = 0; p < 2; p++) {
+                const int j = (hid & 1) * 2 + p, info = rinfo[j];
+                const int off = rbase[j] + (kh * (info >> 9) + kw) * C8 + ic8;   // tap <= 8 when used
+                const bool ok = (info >> tap) & 1;                                // 0 for tap >= 9 (K padding)
+                const uint16_t *pa = g.A + 8 * (long)off;
+                const uint16_t *src = ok ? pa : (const uint16_t *)g8_zero_line;
+                __builtin_amdgcn_global_load_lds((glb_void_8p *)src, (lds_void_8p *)(smem + g8_img(hid, buf) + (wid + 8 * p) * 512),
+                                                 16, 0, 0);
+            }
+            return;
+        }
         const int ld = isa ? g.lda : g.ldw;
         const uint16_t *base = (isa ? g.A : g.W) + kt * 64 + (isa ? aoff : woff);
 #pragma unroll
@@ -337,10 +392,10 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
     g8_epilogue<EPI>(g, acc, smem, m0, n0, mlo, nlo, wr, wc, lane);
 }
 
-template <int EPI>
+template <int EPI, int AMODE = AM_DENSE>
 static inline void run_gemm8p(const GemmArgs &g, hipStream_t s) {
     const int tiles = ((g.N + 255) / 256) * ((g.M + 255) / 256);
-    hipLaunchKernelGGL((gemm8p_kernel<EPI>), dim3(tiles), dim3(512), 0, s, g);
+    hipLaunchKernelGGL((gemm8p_kernel<EPI, AMODE>), dim3(tiles), dim3(512), 0, s, g);
 }
 
 }  // namespace qasr

@@ -23,6 +23,9 @@ int mel_frames_per_block();
 
 // ---------------------------------------------------------------- conv front-end
 // One entry per 100-frame mel chunk (src/audio_encoder.cpp:331-409).
+// conv2 / conv3 weight row length: 9 * channels rounded up to 128, zeros past 9 * channels
+inline constexpr int conv_kpad(int channels) { return (9 * channels + 127) / 128 * 128; }
+
 struct ChunkDesc {
     long mel_off;   // element offset of mel[clip][0][chunk_start]
     int T;          // mel row stride (frames of the clip)

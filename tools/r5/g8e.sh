@@ -6,5 +6,5 @@ tail -3 gpurun_out/g8e_t.log; [ $rc -ne 0 ] && { grep -E "FAIL|Error|assert" gpu
 timeout -k 10 400 python -u bench.py --steps 2 --warmup 1 --no-probe --no-cpu-baseline > gpurun_out/g8e_b.json 2> gpurun_out/g8e_b.log || { tail -5 gpurun_out/g8e_b.log; exit 1; }
 python3 -c "
 import json; d=json.loads(open('gpurun_out/g8e_b.json').read().strip().splitlines()[-1]); u=d['utterance_set']
-print('headline', d['value'], d.get('stages_ms')); print('set', u['value'], u['rank0_stream'])"
+print('headline', d['value'], d.get('stages_ms')); print('set', u['value'], u['rank0_stream'], u.get('encoder_roofline'))"
 exit 0
