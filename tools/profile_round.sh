@@ -45,6 +45,6 @@ step prof_stats 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/stats" -o r
 DEC="gemv|qkv_attn1|ffn1|decode_attn"
 step prof_fetch 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$DEC" -f csv -d "$OUT/fetch" -o run -- ./qwen3-asr.cpp_amd/qasr-bench --steps 1 --warmup 0 --tok-rate 0.5 $ARGS
 step prof_write 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$DEC" -f csv -d "$OUT/write" -o run -- ./qwen3-asr.cpp_amd/qasr-bench --steps 1 --warmup 0 --tok-rate 0.5 $ARGS
-ENC="gemm_kernel|gemm_glds|gemm_q8|enc_attn|prefill_attn|conv1"
+ENC="gemm_kernel|gemm_glds|gemm8p|gemm_q8|enc_attn|prefill_attn|conv1"
 step prof_mfma 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_I8 GRBM_GUI_ACTIVE --kernel-include-regex "$ENC" -f csv -d "$OUT/mfma" -o run -- ./qwen3-asr.cpp_amd/qasr-bench --steps 1 --warmup 0 --tok-rate 0.05 $ARGS
 python3 tools/prof_report.py "$OUT" > "$OUT/summary.json"
