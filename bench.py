@@ -79,7 +79,10 @@ def parse():
                          "ranks (0: skip)")
     ap.add_argument("--set-seconds", type=float, default=30.0)
     ap.add_argument("--set-pool", type=int, default=128, help="distinct seeded clips staged per GPU (utterance i = clip i mod pool)")
-    ap.add_argument("--set-slots", type=int, default=128, help="continuous-batching slots per GPU")
+    ap.add_argument("--set-slots", type=int, default=128, help="continuous-batching slots per context")
+    ap.add_argument("--set-contexts", type=int, default=2,
+                    help="continuous-batching contexts per GPU, each on its own HIP stream and host thread, all fed by "
+                         "the rank's queue (one context's refill prefill overlaps another's decode steps)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous check without a GPU: ranks join a gloo group, time a barrier and rank 0 "
                          "prints the JSON line with value 0 (tests/test_dist.py)")
@@ -554,8 +557,14 @@ def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
     subset (graph capture), then one timed pass: barrier -> streams -> barrier,
     wall = max over ranks; each rank's own stream time and utterance count are
     gathered for the tail imbalance.  Budget ceil(3.5 tok/s x 30 s) = 105
-    tokens a clip, EOS ignored (every budget is asserted)."""
+    tokens a clip, EOS ignored (every budget is asserted).  Each rank runs
+    --set-contexts contexts of --set-slots slots concurrently (own HIP stream,
+    own host thread, one lock around the rank's queue): a context's refill
+    prefill (compute-bound) overlaps the others' decode steps (latency / HBM
+    bound) -- 1 x 128 slots 7780, 2 x 128 8500, 3 x 128 8690 RTFx, tokens equal
+    (tools/r5/two_ctx.py; 4 contexts exceed the box's 4 hardware queues)."""
     import concurrent.futures as cf
+    import threading
 
     import qasr_dist as qd
     n_utt, secs = args.set_utterances, args.set_seconds
@@ -563,41 +572,62 @@ def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
     utts = [(50000 + i, ns) for i in range(n_utt)]
     bud = qd.budget(ns, args.tok_rate)
     P = qasr.lib().qasr_prompt_len(qasr.encoder_frames(qasr.mel_frames(ns)))
-    ctx = qasr.Context(m, max_batch=args.set_slots, max_ctx=P + bud + 8)
+    nctx = max(1, args.set_contexts)
+    ctxs = [qasr.Context(m, max_batch=args.set_slots, max_ctx=P + bud + 8) for _ in range(nctx)]
     pool = min(args.set_pool, n_utt)
     with cf.ThreadPoolExecutor(16) as ex:   # (ctypes releases the GIL: the C synthesiser runs in parallel)
         pcm = list(ex.map(lambda i: qasr.synth_pcm(utts[i][0], ns), range(pool)))
-    ctx.stage_audio(pcm)
+    for c in ctxs:
+        c.stage_audio(pcm)
     stats = []
 
     def stream(next_clip):
-        out, st = ctx.run_stream_staged(next_clip, bud, ignore_eos=True, slots=args.set_slots)
-        bad = [i for i, t in out.items() if isinstance(t, Exception)]
-        assert not bad, (bad[:4], out[bad[0]] if bad else None)
-        stats.append(st)
-        return out
+        lock = threading.Lock()
+
+        def take():   # the rank's queue (a TCPStore client) is not shared between threads unguarded
+            with lock:
+                return next_clip()
+
+        def one(c):
+            out, st = c.run_stream_staged(take, bud, ignore_eos=True, slots=args.set_slots)
+            bad = [i for i, t in out.items() if isinstance(t, Exception)]
+            assert not bad, (bad[:4], out[bad[0]] if bad else None)
+            return out, st
+        with cf.ThreadPoolExecutor(nctx) as ex:
+            res = list(ex.map(one, ctxs))
+        merged = {}
+        for out, st in res:
+            merged.update(out)
+            stats.append(st)
+        return merged
     dev = f"cuda:{local}" if dist else None
-    warm = utts[:min(n_utt, 2 * args.set_slots * world)]
+    warm = utts[:min(n_utt, 2 * args.set_slots * nctx * world)]
     qd.run_queue(stream, warm, rank, world, args.tok_rate, dist, dev, key="utt_set_warm")
     stats.clear()
     res = qd.run_queue(stream, utts, rank, world, args.tok_rate, dist, dev, key="utt_set_timed")
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if rank != 0:
         return {}
     toks = res["tokens"]
     assert len(toks) == n_utt and all(len(t) == bud for t in toks.values()), "utterance set: a budget was not met"
     walls = res["rank_wall_s"]
-    st = stats[0]
     # the encoder at batch: rank 0's clips' encoder FLOPs over the refills' encoder
-    # device time (HIP events around run_encoder; mel excluded), against the dense fp16 MFMA peak
-    ef = st.n_clips * encoder_flops(m.hp, ns)
-    enc = ({"bound": "mfma", "achieved": round(ef / (st.t_encode_ms / 1e3) / 1e12, 1), "peak": MFMA_F16_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(ef / (st.t_encode_ms / 1e3) / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
-            "encoder_ms": round(st.t_encode_ms, 1), "mel_ms": round(st.t_mel_ms, 1), "clips": st.n_clips}
-           if st.t_encode_ms > 0 else None)
+    # device time (HIP events around run_encoder on each context's stream; mel excluded; with several
+    # contexts a span also holds the other contexts' overlapping decode kernels), against the dense
+    # fp16 MFMA peak
+    clips = sum(x.n_clips for x in stats)
+    enc_ms = sum(x.t_encode_ms for x in stats)
+    ef = clips * encoder_flops(m.hp, ns)
+    enc = ({"bound": "mfma", "achieved": round(ef / (enc_ms / 1e3) / 1e12, 1), "peak": MFMA_F16_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(ef / (enc_ms / 1e3) / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
+            "encoder_ms": round(enc_ms, 1), "mel_ms": round(sum(x.t_mel_ms for x in stats), 1), "clips": clips,
+            "contexts": nctx}
+           if enc_ms > 0 else None)
     return {
         "workload": f"configs[3]: {n_utt} x {secs:g} s utterances (16 kHz, a pool of {pool} distinct seeded clips per "
-                    f"GPU), one shared longest-first queue feeding {args.set_slots} continuous-batching slots per GPU, "
+                    f"GPU), one shared longest-first queue feeding {nctx} concurrent continuous-batching context(s) of "
+                    f"{args.set_slots} slots per GPU (own HIP stream each), "
                     f"greedy budget {bud} tokens (3.5 tok/s), EOS ignored",
         "scaling": "strong", "n_gpus": world, "utterances": n_utt, "audio_s": res["audio_s"],
         "value": round(res["audio_s"] / res["wall_s"], 3), "unit": "audio-sec/wall-sec",
@@ -606,9 +636,9 @@ def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
         "per_rank_wall_s": [round(w, 4) for w in walls],
         "per_rank_utterances": [int(u) for u in res["rank_utterances"]],
         "tail_imbalance": round((max(walls) - min(walls)) / max(walls), 4) if max(walls) > 0 else 0.0,
-        "rank0_stream": {"clips": st.n_clips, "refill_prefills": st.n_prefills, "decode_steps": st.n_steps,
-                         "slot_utilisation": round(st.live_steps / max(1, st.slot_steps), 4),
-                         "prefill_ms": round(st.t_prefill_ms, 1), "decode_ms": round(st.t_decode_ms, 1)},
+        "rank0_stream": [{"clips": st.n_clips, "refill_prefills": st.n_prefills, "decode_steps": st.n_steps,
+                          "slot_utilisation": round(st.live_steps / max(1, st.slot_steps), 4),
+                          "prefill_ms": round(st.t_prefill_ms, 1), "decode_ms": round(st.t_decode_ms, 1)} for st in stats],
         "encoder_roofline": enc,
         "collectives": "barrier + max wall time + all_gather of per-rank times and token ids (RCCL); the queue is a "
                        "TCPStore counter (one add per utterance)",

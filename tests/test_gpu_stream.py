@@ -117,3 +117,35 @@ def test_stream_fetch_exception_is_raised(tiny_model):
         assert out[5] == _single(tiny_model, clips[0], 4, True)
     finally:
         c.close()
+
+
+def test_concurrent_streams_equal_single(tiny_model):
+    """bench.py's utterance_set runs several continuous-batching contexts of one
+    model at once, each on its own HIP stream and host thread, fed by one
+    locked queue: every clip's tokens equal its one-clip run whichever context
+    took it, and every clip is delivered exactly once."""
+    import concurrent.futures as cf
+    import threading
+    lens = [SR + 160 * i for i in range(10)]
+    budgets = [4 + (i % 5) for i in range(10)]
+    clips = [qasr.synth_pcm(7300 + i, n) for i, n in enumerate(lens)]
+    items = iter([(20 + i, p, b) for i, (p, b) in enumerate(zip(clips, budgets))])
+    lock = threading.Lock()
+
+    def take():
+        with lock:
+            return next(items, None)
+    ctxs = [qasr.Context(tiny_model, max_batch=3, max_ctx=640) for _ in range(2)]
+    try:
+        with cf.ThreadPoolExecutor(2) as ex:
+            res = list(ex.map(lambda c: c.run_stream(take, max_tokens=16, ignore_eos=True), ctxs))
+    finally:
+        for c in ctxs:
+            c.close()
+    out = {}
+    for o, st in res:
+        assert not set(o) & set(out)
+        out.update(o)
+    assert sorted(out) == [20 + i for i in range(len(clips))]
+    for i, (p, b) in enumerate(zip(clips, budgets)):
+        assert out[20 + i] == _single(tiny_model, p, b, True), i
