@@ -23,7 +23,7 @@ with cf.ThreadPoolExecutor(16) as ex:
     pcm = list(ex.map(lambda i: qasr.synth_pcm(50000 + i, ns), range(POOL)))
 
 
-def run(nctx: int, slots: int, n_utt: int):
+def run(nctx: int, slots: int, n_utt: int, stagger_s: float = 0.0):
     ctxs = [qasr.Context(m, max_batch=slots, max_ctx=P + bud + 8) for _ in range(nctx)]
     for c in ctxs:
         c.stage_audio(pcm)
@@ -38,12 +38,15 @@ def run(nctx: int, slots: int, n_utt: int):
             nxt[0] += 1
             return i
 
-    def one(c):
+    def one(k_c):
+        k, c = k_c
+        if k and stagger_s > 0:
+            time.sleep(k * stagger_s)   # context k starts k staggers late: refills alternate with the others' decode
         out, st = c.run_stream_staged(next_clip, bud, ignore_eos=True, slots=slots)
         return out, st
     t0 = time.perf_counter()
     with cf.ThreadPoolExecutor(nctx) as ex:
-        res = list(ex.map(one, ctxs))
+        res = list(ex.map(one, list(enumerate(ctxs))))
     wall = time.perf_counter() - t0
     n = sum(len(o) for o, _ in res)
     for c in ctxs:
@@ -56,11 +59,11 @@ def run(nctx: int, slots: int, n_utt: int):
 
 
 ref = None
-for nctx, slots in [(1, 128), (2, 128), (3, 128), (4, 128), (3, 96)]:
+for nctx, slots, stg in [(1, 128, 0.0), (2, 128, 0.0), (2, 128, 0.2), (2, 128, 0.35), (2, 128, 0.5), (3, 128, 0.0), (3, 128, 0.15)]:
     run(nctx, slots, min(N_UTT, 2 * nctx * slots))   # warm-up (graphs, buffers)
-    v, st, toks = run(nctx, slots, N_UTT)
+    v, st, toks = run(nctx, slots, N_UTT, stg)
     if ref is None:
         ref = toks
     same = all(toks[i] == ref[i] for i in ref)
-    print(f"{nctx} ctx x {slots} slots: {v:.1f} RTFx  tokens equal to 1 x 128: {same}  per ctx (refills, prefill ms, "
-          f"decode ms) {st}", flush=True)
+    print(f"{nctx} ctx x {slots} slots, stagger {stg} s: {v:.1f} RTFx  tokens equal to 1 x 128: {same}  per ctx (refills, "
+          f"prefill ms, decode ms) {st}", flush=True)
