@@ -97,7 +97,7 @@ int main(int argc, char **argv) {
         g.A = A; g.lda = sh.K; g.ldw = sh.K; g.M = M; g.N = sh.N; g.K = sh.K;
         g.out_f32 = out; g.ldo = sh.N; g.res = res; g.ldr = sh.N; g.out_f16 = out16; g.ldo16 = sh.N;
         printf("%s (%zu MB, %d copies)\n", sh.name, wb >> 20, NL);
-        if (M > 64) {   // 65..128 rows (round 5): fewer activation re-reads (NT 2) against more row blocks
+        if (M > 64 || getenv("SKINNY_ALT")) {   // 65..128 rows (round 5; SKINNY_ALT: the same set at any M): fewer activation re-reads (NT 2) against more row blocks
             if (sh.N == 4096) {
                 time_cfg<4, 1, 8, EPI_F32, 4, 1>(g, ws, s, "engine (MT4 NT1 CPW1)");
                 time_cfg<4, 2, 8, EPI_F32, 4, 1>(g, ws, s, "MT4 NT2 CPW1");
