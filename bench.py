@@ -573,7 +573,11 @@ def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
     bud = qd.budget(ns, args.tok_rate)
     P = qasr.lib().qasr_prompt_len(qasr.encoder_frames(qasr.mel_frames(ns)))
     nctx = max(1, args.set_contexts)
-    ctxs = [qasr.Context(m, max_batch=args.set_slots, max_ctx=P + bud + 8) for _ in range(nctx)]
+    # slots per context: --set-slots, or fewer when the rank's share of the set cannot fill them
+    # (strong scaling: 1000 utterances over 8 ranks x 2 contexts is ~63 a context; parked slots
+    # would still cost a decode step its full-batch GEMMs)
+    slots = max(1, min(args.set_slots, -(-n_utt // (world * nctx))))
+    ctxs = [qasr.Context(m, max_batch=slots, max_ctx=P + bud + 8) for _ in range(nctx)]
     pool = min(args.set_pool, n_utt)
     with cf.ThreadPoolExecutor(16) as ex:   # (ctypes releases the GIL: the C synthesiser runs in parallel)
         pcm = list(ex.map(lambda i: qasr.synth_pcm(utts[i][0], ns), range(pool)))
@@ -589,7 +593,7 @@ def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
                 return next_clip()
 
         def one(c):
-            out, st = c.run_stream_staged(take, bud, ignore_eos=True, slots=args.set_slots)
+            out, st = c.run_stream_staged(take, bud, ignore_eos=True, slots=slots)
             bad = [i for i, t in out.items() if isinstance(t, Exception)]
             assert not bad, (bad[:4], out[bad[0]] if bad else None)
             return out, st
@@ -601,7 +605,7 @@ def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
             stats.append(st)
         return merged
     dev = f"cuda:{local}" if dist else None
-    warm = utts[:min(n_utt, 2 * args.set_slots * nctx * world)]
+    warm = utts[:min(n_utt, 2 * slots * nctx * world)]
     qd.run_queue(stream, warm, rank, world, args.tok_rate, dist, dev, key="utt_set_warm")
     stats.clear()
     res = qd.run_queue(stream, utts, rank, world, args.tok_rate, dist, dev, key="utt_set_timed")
@@ -627,7 +631,7 @@ def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
     return {
         "workload": f"configs[3]: {n_utt} x {secs:g} s utterances (16 kHz, a pool of {pool} distinct seeded clips per "
                     f"GPU), one shared longest-first queue feeding {nctx} concurrent continuous-batching context(s) of "
-                    f"{args.set_slots} slots per GPU (own HIP stream each), "
+                    f"{slots} slots per GPU (own HIP stream each), "
                     f"greedy budget {bud} tokens (3.5 tok/s), EOS ignored",
         "scaling": "strong", "n_gpus": world, "utterances": n_utt, "audio_s": res["audio_s"],
         "value": round(res["audio_s"] / res["wall_s"], 3), "unit": "audio-sec/wall-sec",
