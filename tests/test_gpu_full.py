@@ -154,6 +154,26 @@ def test_full_lds_dma_gemm_bit_identical(full):
     assert np.array_equal(single, out[0][0][3])
 
 
+def test_full_encoder_ragged_tiles_bit_identical(full):
+    """Ragged clips (short last chunks, row counts no multiple of 256): the
+    8-phase tile's shifted last row / column tiles and its implicit-im2col
+    convs against the register-staged tiles (option gemm_regs), bit for bit."""
+    m, _, _ = full
+    secs = [29.37, 17.71, 8.13, 30.0, 3.05]
+    clips = [qasr.synth_pcm(15500 + i, int(s * SR)) for i, s in enumerate(secs)]
+    cb = qasr.Context(m, max_batch=len(clips), max_ctx=512)
+    try:
+        mels = cb.mel(clips)
+        out = {}
+        for regs in (1, 0):
+            cb.set_option("gemm_regs", regs)
+            out[regs] = cb.encode(mels)
+    finally:
+        cb.close()
+    for a, b in zip(out[0], out[1]):
+        assert a.shape == b.shape and np.array_equal(a, b)
+
+
 FUSE_KNOBS = {"QASR_FUSE_FFN": dict(fuse_ffn=0), "QASR_FUSE_QKV": dict(fuse_qkv=0, fuse_o=0), "QASR_FUSE_O": dict(fuse_o=0)}
 
 
