@@ -380,6 +380,19 @@ static void gemm_q8_pre(qasr_ctx *c, int epi, GemmArgs g, const uint16_t *W, con
     launch_gemm_q8(epi, g, s);
 }
 
+// decode batches: SwiGLU gate/up with the output quantised to Q8_0 (q / d, row
+// length N / 2) in the skinny GEMM's epilogue; false (nothing launched) where
+// the skinny GEMM declines the shape or is switched off
+static bool gemm_q8_pre_swiglu_q8(qasr_ctx *c, GemmArgs g, const uint16_t *W, const uint16_t *Wd, hipStream_t s, const int8_t *qa,
+                                  const float *qd, int8_t *q, float *d) {
+    g.Aq = qa; g.lda = g.K; g.Ad = qd; g.ldad = g.K / 32;
+    g.Wq = (const int8_t *)W; g.ldw = g.K; g.Wd = Wd;
+    g.no_skinny = !c->fuse.skinny;
+    g.skinny_inflight = c->fuse.skinny_inf;
+    g.out_q = q; g.out_d = d; g.ldoq = g.N / 2;
+    return launch_gemm_skinny_q8(EPI_SWIGLU_Q8, g, s);
+}
+
 static int ensure_q8(qasr_ctx *c, size_t rows, size_t kmax, size_t x32_cols) {
     int rc;
     if ((rc = ensure(c, c->q8a, rows * kmax)) || (rc = ensure(c, c->q8d, rows * (kmax / 32) * 4)) ||
@@ -1383,10 +1396,16 @@ static int decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange r
             launch_rmsnorm_q8(x, H, B, H, L.ffn_norm, hp.rms_eps, c->d_q8n, c->d_q8nd, s);
             GemmArgs gu{};
             gu.M = B; gu.N = 2 * F; gu.K = H; gu.out_f32 = c->d_x32; gu.ldo = F;
-            gemm_q8_pre(c, EPI_SWIGLU_F32, gu, L.wgu, L.wgu_d, s, c->d_q8n, c->d_q8nd);
             GemmArgs dn{};
             dn.M = B; dn.N = H; dn.K = F; dn.res = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
-            gemm_q8(c, EPI_F32, dn, c->d_x32, nullptr, F, 0, L.wd, L.wd_d, s, c->d_q8a, c->d_q8d, true);
+            // the down projection's Q8_0 input quantised in the gate/up epilogue (one launch
+            // fewer a layer, the same bits); the two-launch form where the skinny GEMM declines
+            if (gemm_q8_pre_swiglu_q8(c, gu, L.wgu, L.wgu_d, s, c->d_q8n, c->d_q8nd, c->d_q8a, c->d_q8d)) {
+                gemm_q8_pre(c, EPI_F32, dn, L.wd, L.wd_d, s, c->d_q8a, c->d_q8d);
+            } else {
+                gemm_q8_pre(c, EPI_SWIGLU_F32, gu, L.wgu, L.wgu_d, s, c->d_q8n, c->d_q8nd);
+                gemm_q8(c, EPI_F32, dn, c->d_x32, nullptr, F, 0, L.wd, L.wd_d, s, c->d_q8a, c->d_q8d, true);
+            }
         } else {
             GemmArgs ob{};
             ob.A = c->d_att; ob.lda = QD; ob.W = L.wo; ob.ldw = QD; ob.M = B; ob.N = H; ob.K = QD; ob.res = x; ob.ldr = H; ob.out_f32 = x; ob.ldo = H;

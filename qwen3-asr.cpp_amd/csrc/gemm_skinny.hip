@@ -62,7 +62,35 @@ struct SkinnyEpi {
             for (int w = 1; w < KW; w++) v += red[w][t][l][r];
             return v;
         };
-        if constexpr (EPI == EPI_SWIGLU_F16 || EPI == EPI_SWIGLU_F32) {
+        if constexpr (EPI == EPI_SWIGLU_Q8) {
+            // silu(g) * u of the block's NT / 2 * 16 output columns (whole Q8_0
+            // blocks: NT % 4 == 0) through LDS, then quantize_q8_rows_kernel's
+            // arithmetic per 32-block: 8 lanes of 4 values, amax by xor shuffles
+            static_assert(NT % 4 == 0, "whole 32-column blocks (and MT * NT * 32 lane groups: whole waves)");
+            constexpr int OC = NT / 2 * 16;
+            __shared__ __attribute__((aligned(16))) float vq[MT * 16][OC];
+            for (int e = tid; e < MT * (NT / 2) * 256; e += 64 * KW) {
+                const int tp = e >> 8, rin = (e >> 4) & 15, cin = e & 15;
+                const int i = tp / (NT / 2), p = tp - i * (NT / 2);
+                const float gt = tile_val(i * NT + 2 * p, rin, cin), up = tile_val(i * NT + 2 * p + 1, rin, cin);
+                vq[i * 16 + rin][p * 16 + cin] = silu_s(gt) * up;
+            }
+            __syncthreads();
+            for (int u = tid; u < MT * 16 * OC / 4; u += 64 * KW) {   // wave-uniform trip count
+                const int rl = u / (OC / 4), c4 = u - rl * (OC / 4), row = m0 + rl;
+                const float4 v = *(const float4 *)&vq[rl][4 * c4];
+                float am = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+                am = fmaxf(am, __shfl_xor(am, 1, 64));
+                am = fmaxf(am, __shfl_xor(am, 2, 64));
+                am = fmaxf(am, __shfl_xor(am, 4, 64));
+                if (row >= M) continue;
+                const int col = n0 / 2 + 4 * c4;
+                *(uint32_t *)(g.out_q + (long)row * g.ldoq + col) =
+                    (uint32_t)(uint8_t)q8_quant(v.x, am) | (uint32_t)(uint8_t)q8_quant(v.y, am) << 8 |
+                    (uint32_t)(uint8_t)q8_quant(v.z, am) << 16 | (uint32_t)(uint8_t)q8_quant(v.w, am) << 24;
+                if ((c4 & 7) == 0) g.out_d[(long)row * (g.ldoq / 32) + col / 32] = q8_scale(am);
+            }
+        } else if constexpr (EPI == EPI_SWIGLU_F16 || EPI == EPI_SWIGLU_F32) {
             // interleaved 16-row [gate | up] weight blocks: tiles 2p / 2p+1
             for (int e = tid; e < MT * (NT / 2) * 256; e += 64 * KW) {
                 const int tp = e >> 8, rin = (e >> 4) & 15, cin = e & 15;
@@ -589,6 +617,13 @@ bool launch_gemm_skinny_q8(int epi, const GemmArgs &g, hipStream_t s) {
         case EPI_SWIGLU_F32:
             if (g.N % 32 != 0) return false;
             skinny_q8_mt<2, 2, 4, EPI_SWIGLU_F32>(g, s);
+            return true;
+        case EPI_SWIGLU_Q8:
+            // 64-column blocks: 32 output columns, one Q8_0 block a row; K over 8 waves
+            // (tools/skinny_q8_bench.hip, 64 rows: 10.16 us against 10.43 for the fp32
+            // SwiGLU form alone, which the separate quantisation launch then followed)
+            if (g.N % 64 != 0 || !g.out_q || !g.out_d || g.ldoq % 32 != 0) return false;
+            skinny_q8_mt<2, 4, 8, EPI_SWIGLU_Q8>(g, s);
             return true;
         default:
             return false;

@@ -50,6 +50,8 @@ enum GemmEpi {
     EPI_ARGMAX = 3,     // optional out_f32 logits + per-row packed argmax (atomicMax)
     EPI_F16 = 4,        // out_f16 = acc (+bias)
     EPI_SWIGLU_F32 = 5, // as EPI_SWIGLU_F16 with fp32 out_f32 (input of a Q8_0 layer)
+    EPI_SWIGLU_Q8 = 6,  // as EPI_SWIGLU_F32, quantised to Q8_0 in the epilogue: out_q / out_d
+                        // (the bits of EPI_SWIGLU_F32 + launch_quantize_q8); skinny Q8_0 GEMM only
 };
 enum GemmAMode {
     AM_DENSE = 0,       // A [M][lda] fp16 row-major
@@ -79,12 +81,13 @@ struct GemmArgs {
     int regs_staged;                      // 1: register-staged tiles instead of the LDS-DMA ones (A/B option)
     int no_skinny;                        // 1: launch_gemm_skinny / _q8 decline (per-context option skinny = 0)
     int skinny_inflight;                  // skinny GEMMs: every K chunk of a wave requested at entry (FuseCfg::skinny_inf)
+    int8_t *out_q; float *out_d; int ldoq;   // EPI_SWIGLU_Q8: int8 [M][ldoq], fp32 block scales [M][ldoq / 32]
 };
 void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s);
 // decode-batch GEMM (gemm_skinny.hip): dense A, M <= 128, K % 128 == 0; returns
 // false (nothing launched) for shapes it does not take, or when g.no_skinny.
 bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s);
-// the same for Q8_0 weights (Aq/Ad quantised activations, Wq/Wd): EPI_F32, EPI_SWIGLU_F32
+// the same for Q8_0 weights (Aq/Ad quantised activations, Wq/Wd): EPI_F32, EPI_SWIGLU_F32, EPI_SWIGLU_Q8
 bool launch_gemm_skinny_q8(int epi, const GemmArgs &g, hipStream_t s);
 // ggml_mul_mat with Q8_0 weights: exact int8 block dots (v_mfma_i32_16x16x32_i8
 // per 32-wide K block), each scaled by d_w * d_x into an fp32 accumulator.
