@@ -611,7 +611,10 @@ bool launch_gemm_skinny_q8(int epi, const GemmArgs &g, hipStream_t s) {
     switch (epi) {
         case EPI_F32:
             if (g.N % 16 != 0) return false;
-            if (g.N >= 4096) skinny_q8_mt<2, 1, 8, EPI_F32>(g, s);   // MT <= 2: the block scales cost 16 VGPRs per row tile
+            // QKV: all 64 rows a block (tools/skinny_q8_bench.hip, 64 rows: 7.18 -> 6.53 us a
+            // launch with every chunk in flight; the same K split, so the same bits); o / down:
+            // 16-row blocks (32- and 64-row blocks 1.3-3.7 us slower)
+            if (g.N >= 4096) skinny_q8_mt<4, 1, 8, EPI_F32>(g, s);
             else skinny_q8_mt<1, 1, 8, EPI_F32>(g, s);
             return true;
         case EPI_SWIGLU_F32:

@@ -110,5 +110,46 @@ int main(int argc, char **argv) {
     time_cfg<1, 4, 8, EPI_SWIGLU_Q8, 1>(g, ws, wds, s, "fused q8 MT1 NT4 KW8");
     time_cfg<4, 4, 8, EPI_SWIGLU_Q8, 1>(g, ws, wds, s, "fused q8 MT4 NT4 KW8");
     time_cfg<2, 8, 4, EPI_SWIGLU_Q8, 2>(g, ws, wds, s, "fused q8 MT2 NT8 KW4");
+    for (int w = 0; w < NL; w++) { CK(hipFree(ws[w])); CK(hipFree(wds[w])); }
+    // the fp32-output projections (QKV, o, down): the engine's tilings and alternatives
+    struct Sh { const char *name; int N, K; };
+    const Sh shs[] = {{"qkv 4096x1024", 4096, 1024}, {"o 1024x2048", 1024, 2048}, {"down 1024x3072", 1024, 3072}};
+    float *res; int8_t *A2; float *Ad2;
+    CK(hipMalloc(&res, (size_t)64 * 4096 * 4)); CK(hipMemset(res, 0, (size_t)64 * 4096 * 4));
+    CK(hipMalloc(&A2, (size_t)64 * 3072)); CK(hipMemset(A2, 0x13, (size_t)64 * 3072));
+    CK(hipMalloc(&Ad2, (size_t)64 * 96 * 4)); CK(hipMemset(Ad2, 0x3a, (size_t)64 * 96 * 4));
+    CK(hipFree(o32)); CK(hipMalloc(&o32, (size_t)64 * 4096 * 4));
+    for (const Sh &sh : shs) {
+        const size_t wb2 = (size_t)sh.N * sh.K;
+        const int NL2 = (int)((600ull << 20) / wb2) + 1;
+        std::vector<int8_t *> w2(NL2);
+        std::vector<uint16_t *> d2(NL2);
+        for (int i = 0; i < NL2; i++) {
+            CK(hipMalloc(&w2[i], wb2)); CK(hipMemset(w2[i], 0x21, wb2));
+            CK(hipMalloc(&d2[i], wb2 / 16)); CK(hipMemset(d2[i], 0x11, wb2 / 16));
+        }
+        GemmArgs h{};
+        h.Aq = A2; h.lda = sh.K; h.Ad = Ad2; h.ldad = sh.K / 32; h.ldw = sh.K; h.M = M; h.N = sh.N; h.K = sh.K;
+        h.out_f32 = o32; h.ldo = sh.N; h.res = res; h.ldr = sh.N; h.skinny_inflight = 1;
+        printf("%s (%d copies)\n", sh.name, NL2);
+        if (sh.N == 4096) {
+            time_cfg<2, 1, 8, EPI_F32, 1>(h, w2, d2, s, "engine (MT2 NT1 KW8)");
+            time_cfg<4, 1, 8, EPI_F32, 1>(h, w2, d2, s, "MT4 NT1 KW8");
+            time_cfg<2, 2, 8, EPI_F32, 1>(h, w2, d2, s, "MT2 NT2 KW8");
+            time_cfg<4, 2, 8, EPI_F32, 1>(h, w2, d2, s, "MT4 NT2 KW8");
+            time_cfg<2, 1, 4, EPI_F32, 2>(h, w2, d2, s, "MT2 NT1 KW4");
+        } else if (sh.K == 2048) {
+            time_cfg<1, 1, 8, EPI_F32, 2>(h, w2, d2, s, "engine (MT1 NT1 KW8)");
+            time_cfg<2, 1, 8, EPI_F32, 2>(h, w2, d2, s, "MT2 NT1 KW8");
+            time_cfg<4, 1, 8, EPI_F32, 2>(h, w2, d2, s, "MT4 NT1 KW8");
+            time_cfg<1, 1, 16, EPI_F32, 1>(h, w2, d2, s, "MT1 NT1 KW16");
+            time_cfg<2, 1, 16, EPI_F32, 1>(h, w2, d2, s, "MT2 NT1 KW16");
+        } else {
+            time_cfg<1, 1, 8, EPI_F32, 3>(h, w2, d2, s, "engine (MT1 NT1 KW8)");
+            time_cfg<2, 1, 8, EPI_F32, 3>(h, w2, d2, s, "MT2 NT1 KW8");
+            time_cfg<2, 1, 12, EPI_F32, 2>(h, w2, d2, s, "MT2 NT1 KW12");
+        }
+        for (int i = 0; i < NL2; i++) { CK(hipFree(w2[i])); CK(hipFree(d2[i])); }
+    }
     return 0;
 }
