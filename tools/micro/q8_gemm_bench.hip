@@ -1,8 +1,11 @@
 // q8_gemm_bench.hip -- the Q8_0 block GEMM of the encoder / prefill projections
 // (csrc/gemm_q8.hip, included directly): us per launch of the engine's
 // register-staged tile against an LDS-DMA ring form of the same tile (defined
-// here; measured no faster at any (KS, NB)), each output compared
-// bit for bit with the engine tile's.
+// here; measured no faster at any (KS, NB)) and against the same
+// products on the fp16 MFMA (int8 quants held as fp16 values: exact; also
+// defined here, also slower), each output compared bit for bit with the engine
+// tile's.  The fp16 form reads GemmArgs::A / W as the fp16 quants and its own
+// wd32 argument as the fp32 W scales.
 // Build: hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -mllvm -amdgpu-mfma-vgpr-form=1
 #include "../../qwen3-asr.cpp_amd/csrc/gemm_q8.hip"
 
@@ -161,6 +164,153 @@ static void run_gemm_q8_glds(const GemmArgs &g, hipStream_t s) {
     hipLaunchKernelGGL((gemm_q8_glds_kernel<BM, BN, KS, NB, EPI>), grid, dim3(256), 0, s, g);
 }
 
+
+// ---------------------------------------- Q8_0 GEMM on the fp16 MFMA, LDS-DMA
+// gemm_glds_kernel's ring, pieces, swizzle and epilogue (gemm.hip) over fp16
+// operands that hold int8 quants, one 32-deep slab a Q8_0 block: per slab and
+// fragment one v_mfma_f32_16x16x32_f16 from a zero accumulator -- exact, the
+// (float)sumi of v_mfma_i32_16x16x32_i8 + v_cvt -- scaled into the fp32
+// accumulator as gemm_q8_kernel does (q8_scale_acc's packed mul + fma), so the
+// same bits, with 4 VALU a MFMA instead of 8 and the f16 tile's staging.  The
+// block scales ride the ring as dword LDS-DMA pieces (64 rows each, fp32 row
+// vectors per slab: the C layout's 4 consecutive A rows are one ds_read_b128).
+typedef __attribute__((address_space(3))) void lds_void_h;
+typedef __attribute__((address_space(1))) void glb_void_h;
+__device__ __attribute__((aligned(64))) uint32_t g_zero_line_h[16];
+
+template <int N>
+__device__ __forceinline__ void wait_vm_h() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int KS, int NB, int EPI, int WNW>
+__global__ __launch_bounds__(128 * WNW) void gemm_q8h_kernel(GemmArgs g, const float *wd32) {
+    constexpr int NWAVE = 2 * WNW;
+    constexpr int FM = BM / 32, FN = BN / (16 * WNW);
+    constexpr int ROWS = BM + BN;
+    constexpr int SLAB = ROWS * 32;                  // halves per 32-deep slab
+    constexpr int RG = ROWS / 16;                    // 1-KiB quant pieces per slab
+    constexpr int SP = ROWS / 64;                    // scale pieces per slab (A rows, then W rows)
+    constexpr int NP = KS * (RG + SP);               // pieces per stage
+    constexpr int NW = (NP + NWAVE - 1) / NWAVE;     // per wave (uniform: vmcnt counts)
+    constexpr int STG = KS * SLAB * 2 + KS * ROWS * 4;   // bytes per stage
+    static_assert(BM % 64 == 0 && BN % 64 == 0 && NB >= 2 && NB <= 4 && (NB - 2) * NW < 64, "tile");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NB * STG + 1024];
+    uint8_t *scratch = smem + NB * STG;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid / WNW, wc = wid % WNW;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int M = g.M, K = g.K, nbw = K / 32;
+    const uint16_t *A = g.A, *W = g.W;
+
+    floatx4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int lrow = lane >> 2, lpos = lane & 3;
+    auto issue = [&](int kb0, int buf) {   // kb0: the stage's first 32-block
+        uint8_t *st = smem + buf * STG;
+#pragma unroll
+        for (int p = 0; p < NW; p++) {
+            const int i = wid + NWAVE * p;   // wave-uniform
+            if (i < KS * RG) {
+                const int s = i / RG, rg = i - s * RG;
+                const int r = rg * 16 + lrow;
+                const int k = (kb0 + s) * 32 + ((lpos ^ ((r >> 1) & 3)) << 3);
+                const uint16_t *src = (const uint16_t *)g_zero_line_h;
+                if (rg * 16 < BM) {
+                    if (m0 + r < M) src = A + (long)(m0 + r) * g.lda + k;
+                } else {
+                    src = W + (long)(n0 + r - BM) * g.ldw + k;
+                }
+                __builtin_amdgcn_global_load_lds((glb_void_h *)src, (lds_void_h *)(st + (s * SLAB + rg * 512) * 2), 16, 0, 0);
+            } else if (i < NP) {
+                const int j = i - KS * RG, s = j / SP, h = j - s * SP;
+                const int r = h * 64 + lane;   // scale row of the slab: A rows, then W rows
+                const float *src = (const float *)g_zero_line_h;
+                if (r < BM) {
+                    if (m0 + r < M) src = g.Ad + (long)(m0 + r) * g.ldad + kb0 + s;
+                } else {
+                    src = wd32 + (long)(n0 + r - BM) * nbw + kb0 + s;
+                }
+                __builtin_amdgcn_global_load_lds((glb_void_h *)src, (lds_void_h *)(st + KS * SLAB * 2 + (s * ROWS + h * 64) * 4), 4, 0, 0);
+            } else {
+                __builtin_amdgcn_global_load_lds((glb_void_h *)g_zero_line_h, (lds_void_h *)scratch, 16, 0, 0);
+            }
+        }
+    };
+
+    const int nk = K / (32 * KS);
+#pragma unroll
+    for (int st = 0; st < NB - 1; st++)
+        if (st < nk) issue(st * KS, st);
+    const int q = lane >> 4;
+    int buf = 0;
+    for (int kt = 0; kt < nk; kt++) {
+        const int ahead = nk - 1 - kt;
+        if constexpr (NB >= 4) {
+            if (ahead >= 2) wait_vm_h<2 * NW>();
+            else if (ahead == 1) wait_vm_h<NW>();
+            else wait_vm_h<0>();
+        } else if constexpr (NB == 3) {
+            if (ahead >= 1) wait_vm_h<NW>();
+            else wait_vm_h<0>();
+        } else {
+            wait_vm_h<0>();
+        }
+        asm volatile("s_barrier" ::: "memory");   // every wave's pieces landed; stage kt-1's readers done
+        if (kt + NB - 1 < nk) {
+            int nb = buf + NB - 1;
+            if (nb >= NB) nb -= NB;
+            issue((kt + NB - 1) * KS, nb);
+        }
+        const uint8_t *st = smem + buf * STG;
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+            const uint16_t *sl = (const uint16_t *)st + s * SLAB;
+            const float *sc = (const float *)(st + KS * SLAB * 2) + s * ROWS;
+            half8 af[FM], bf[FN];
+            floatx4 sa[FM];
+            float sb[FN];
+#pragma unroll
+            for (int i = 0; i < FM; i++) {
+                const int r = wr * (BM / 2) + i * 16 + (lane & 15);
+                af[i] = *(const half8 *)(sl + r * 32 + ((q ^ ((r >> 1) & 3)) << 3));
+                sa[i] = *(const floatx4 *)(sc + wr * (BM / 2) + i * 16 + 4 * q);
+            }
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                const int r = BM + wc * (BN / WNW) + j * 16 + (lane & 15);
+                bf[j] = *(const half8 *)(sl + r * 32 + ((q ^ ((r >> 1) & 3)) << 3));
+                sb[j] = sc[r];
+            }
+#pragma unroll
+            for (int i = 0; i < FM; i++)
+#pragma unroll
+                for (int j = 0; j < FN; j++) {
+                    const floatx4 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                    const floatx2 w2 = {sb[j], sb[j]};
+                    const floatx2 s01 = w2 * floatx2{sa[i][0], sa[i][1]}, s23 = w2 * floatx2{sa[i][2], sa[i][3]};
+                    const floatx2 a01 = __builtin_elementwise_fma(s01, floatx2{c[0], c[1]}, floatx2{acc[i][j][0], acc[i][j][1]});
+                    const floatx2 a23 = __builtin_elementwise_fma(s23, floatx2{c[2], c[3]}, floatx2{acc[i][j][2], acc[i][j][3]});
+                    acc[i][j] = floatx4{a01[0], a01[1], a23[0], a23[1]};
+                }
+        }
+        if (++buf == NB) buf = 0;
+    }
+    gemm_epilogue<BM, BN, EPI, WNW>(g, acc, m0, n0, wr, wc, lane);
+}
+
+template <int BM, int BN, int KS, int NB, int EPI, int WNW>
+static void run_gemm_q8h(const GemmArgs &g, const float *wd32, hipStream_t s) {
+    dim3 grid(g.N / BN, (g.M + BM - 1) / BM);
+    hipLaunchKernelGGL((gemm_q8h_kernel<BM, BN, KS, NB, EPI, WNW>), grid, dim3(128 * WNW), 0, s, g, wd32);
+}
+
 }  // namespace qasr
 
 #include <cstdio>
@@ -215,10 +365,29 @@ int main() {
         for (auto &v : w) { _Float16 h = (_Float16)(0.001f + 0.00005f * (float)(rnd() % 100)); memcpy(&v, &h, 2); }
         CK(hipMemcpy(Wd, w.data(), w.size() * 2, hipMemcpyHostToDevice));
     }
+    // the fp16-MFMA form's operands: the same quants as fp16 values, W scales in fp32
+    uint16_t *Ah, *Wh; float *Wd32;
+    CK(hipMalloc(&Ah, MA * 2)); CK(hipMalloc(&Wh, MW * 2)); CK(hipMalloc(&Wd32, MW / 32 * 4));
+    {
+        std::vector<int8_t> q(MA);
+        CK(hipMemcpy(q.data(), Aq, MA, hipMemcpyDeviceToHost));
+        std::vector<_Float16> h(MA);
+        for (size_t i = 0; i < MA; i++) h[i] = (_Float16)q[i];
+        CK(hipMemcpy(Ah, h.data(), MA * 2, hipMemcpyHostToDevice));
+        CK(hipMemcpy(q.data(), Wq, MW, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < MW; i++) h[i] = (_Float16)q[i];
+        CK(hipMemcpy(Wh, h.data(), MW * 2, hipMemcpyHostToDevice));
+        std::vector<uint16_t> d(MW / 32);
+        CK(hipMemcpy(d.data(), Wd, d.size() * 2, hipMemcpyDeviceToHost));
+        std::vector<float> f(MW / 32);
+        for (size_t i = 0; i < f.size(); i++) { _Float16 x; memcpy(&x, &d[i], 2); f[i] = (float)x; }
+        CK(hipMemcpy(Wd32, f.data(), f.size() * 4, hipMemcpyHostToDevice));
+    }
     for (const Sh &sh : shapes) {
         GemmArgs g{};
         g.Aq = Aq; g.lda = sh.K; g.Ad = Ad; g.ldad = sh.K / 32; g.Wq = Wq; g.ldw = sh.K; g.Wd = Wd;
         g.M = sh.M; g.N = sh.N; g.K = sh.K; g.ldo = sh.N;
+        g.A = Ah; g.W = Wh;
         const double ops = 2.0 * sh.M * sh.N * sh.K;
         printf("%s  M=%d N=%d K=%d\n", sh.name, sh.M, sh.N, sh.K);
         g.out_f32 = o1;
@@ -234,10 +403,14 @@ int main() {
             const bool same = memcmp(ref.data(), got.data(), ref.size() * 4) == 0;
             printf("  %-22s %8.1f us %6.1f TOP/s  %s\n", name, us, ops / us * 1e-6, same ? "bit-identical" : "DIFFERENT");
         };
+        if (sh.N % 128 == 0) {
+            var([&] { run_gemm_q8h<128, 128, 1, 4, EPI_F32, 2>(g, Wd32, s); }, "f16 MFMA 128x128 KS1 NB4 4w");
+            var([&] { run_gemm_q8h<128, 128, 1, 3, EPI_F32, 4>(g, Wd32, s); }, "f16 MFMA 128x128 KS1 NB3 8w");
+            var([&] { run_gemm_q8h<128, 128, 2, 2, EPI_F32, 4>(g, Wd32, s); }, "f16 MFMA 128x128 KS2 NB2 8w");
+            var([&] { run_gemm_q8h<128, 128, 1, 4, EPI_F32, 4>(g, Wd32, s); }, "f16 MFMA 128x128 KS1 NB4 8w");
+        }
+        var([&] { run_gemm_q8h<128, 64, 1, 4, EPI_F32, 2>(g, Wd32, s); }, "f16 MFMA 128x64 KS1 NB4 4w");
         var([&] { run_gemm_q8_glds<128, 64, 2, 2, EPI_F32>(g, s); }, "glds KS2 NB2");
-        var([&] { run_gemm_q8_glds<128, 64, 2, 3, EPI_F32>(g, s); }, "glds KS2 NB3");
-        var([&] { run_gemm_q8_glds<128, 64, 2, 4, EPI_F32>(g, s); }, "glds KS2 NB4");
-        var([&] { run_gemm_q8_glds<128, 64, 4, 2, EPI_F32>(g, s); }, "glds KS4 NB2");
     }
     return 0;
 }
