@@ -10,21 +10,37 @@ namespace qasr {
 // kernel.  K = 9 is below ggml's SIMD step, so ggml's vec_dot_f16 sums the 9
 // exact fp16 products in double (its scalar leftover loop); we do the same.
 // One wave per CONV1_ROWS consecutive output positions; lane l owns output
-// channels 8l .. 8l+7 (its 72 fp16 weights and 8 biases stay in registers), so
-// each position costs one broadcast 9-tap input gather and one 16-byte NHWC
-// store per lane.
+// channels 8l .. 8l+7 (its 72 fp16 weights and 8 biases stay in registers).
+// The rows' 9-tap inputs are fetched by one load per lane (lane 9r + t: tap t
+// of row r) and broadcast by v_readlane, so every row's loads are in flight at
+// once; the rows' GELU-table gathers likewise, before the 16-byte NHWC stores
+// (one dependent load / gather / store round per row measured 0.9 TB/s of
+// output).  The same operations per output, so the same bits.
 #define CONV1_ROWS 4
 __global__ __launch_bounds__(256) void conv1_kernel(const float *__restrict__ mel, const ChunkDesc *__restrict__ chunks,
                                                     const int *__restrict__ row1_start, int n_chunks, int rows1,
                                                     const uint16_t *__restrict__ w, const float *__restrict__ b,
                                                     const uint16_t *__restrict__ lut, int C, uint16_t *__restrict__ act1) {
+    static_assert(9 * CONV1_ROWS <= 64, "one tap per lane");
     // grid (positions / 16, chunk): no row -> chunk search
     const ChunkDesc cd = chunks[blockIdx.y];
     const int nloc = 64 * cd.W1;
     const int loc0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * CONV1_ROWS;
     const int lane = threadIdx.x & 63;
-    if (loc0 >= nloc || lane * 8 >= C) return;
-    const int oc0 = lane * 8;
+    if (loc0 >= nloc) return;   // wave-uniform
+    float tap = 0.0f;
+    if (lane < 9 * CONV1_ROWS) {
+        const int r = lane / 9, t = lane - r * 9, kh = t / 3, kw = t - kh * 3;
+        const int local = loc0 + r;
+        if (local < nloc) {
+            const int oh = local / cd.W1, ow = local - oh * cd.W1;
+            const int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;   // ih: mel bin, iw: frame in chunk
+            if (ih >= 0 && ih < 128 && iw >= 0 && iw < cd.Lv) tap = mel[cd.mel_off + (long)ih * cd.T + iw];
+        }
+        tap = h2f(f2h(tap));
+    }
+    const bool active = lane * 8 < C;
+    const int oc0 = active ? lane * 8 : 0;
     float wf[8][9];
     {
         const u32x4 *wp = (const u32x4 *)(w + oc0 * 9);   // 72 consecutive halves
@@ -42,32 +58,26 @@ __global__ __launch_bounds__(256) void conv1_kernel(const float *__restrict__ me
     }
     const float4 b0 = *(const float4 *)(b + oc0), b1 = *(const float4 *)(b + oc0 + 4);
     const float bias[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    uint32_t hv[CONV1_ROWS][8];
+#pragma unroll
     for (int r = 0; r < CONV1_ROWS; r++) {
-        const int local = loc0 + r;
-        if (local >= nloc) break;
-        const int row = cd.row1 + local;
-        const int oh = local / cd.W1, ow = local - oh * cd.W1;
         float in[9];
 #pragma unroll
-        for (int kh = 0; kh < 3; kh++)
-#pragma unroll
-            for (int kw = 0; kw < 3; kw++) {
-                const int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;   // ih: mel bin, iw: frame in chunk
-                float v = 0.0f;
-                if (ih >= 0 && ih < 128 && iw >= 0 && iw < cd.Lv) v = mel[cd.mel_off + (long)ih * cd.T + iw];
-                in[kh * 3 + kw] = h2f(f2h(v));
-            }
-        uint32_t packed[4];
+        for (int t = 0; t < 9; t++) in[t] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tap), r * 9 + t));
 #pragma unroll
         for (int o = 0; o < 8; o++) {
             double sd = 0.0;
 #pragma unroll
             for (int t = 0; t < 9; t++) sd += (double)(in[t] * wf[o][t]);
-            const float v = fadd_rn((float)sd, bias[o]);
-            const uint32_t h = gelu_lut_bits(v, lut);
-            if (o & 1) packed[o >> 1] |= h << 16; else packed[o >> 1] = h;
+            hv[r][o] = gelu_lut_bits(fadd_rn((float)sd, bias[o]), lut);
         }
-        *(u32x4 *)(act1 + (long)row * C + oc0) = u32x4{packed[0], packed[1], packed[2], packed[3]};
+    }
+#pragma unroll
+    for (int r = 0; r < CONV1_ROWS; r++) {
+        const int local = loc0 + r;
+        if (!active || local >= nloc) continue;
+        const u32x4 v = {hv[r][0] | hv[r][1] << 16, hv[r][2] | hv[r][3] << 16, hv[r][4] | hv[r][5] << 16, hv[r][6] | hv[r][7] << 16};
+        *(u32x4 *)(act1 + (long)(cd.row1 + local) * C + oc0) = v;
     }
 }
 
