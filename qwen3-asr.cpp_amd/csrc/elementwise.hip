@@ -15,8 +15,15 @@ namespace qasr {
 // of row r) and broadcast by v_readlane, so every row's loads are in flight at
 // once; the rows' GELU-table gathers likewise, before the 16-byte NHWC stores
 // (one dependent load / gather / store round per row measured 0.9 TB/s of
-// output).  The same operations per output, so the same bits.
-#define CONV1_ROWS 4
+// output).  The same operations per output, so the same bits.  64 x 30 s
+// (tools/micro/conv1_bench.hip, 5.9 GB of output): one row a round 5.77 ms;
+// batched 2 / 4 / 6 / 7 rows 5.34 / 4.37 / 4.11 / 3.94 ms (7: 63 tap lanes, the
+// most one wave holds); without the GELU gather 3.0 ms, and with each product as a
+// double FMA over double weights (half the FP64 ops) 4.11 -- neither the gather
+// nor the FP64 sums alone bound it.
+#ifndef CONV1_ROWS
+#define CONV1_ROWS 7
+#endif
 __global__ __launch_bounds__(256) void conv1_kernel(const float *__restrict__ mel, const ChunkDesc *__restrict__ chunks,
                                                     const int *__restrict__ row1_start, int n_chunks, int rows1,
                                                     const uint16_t *__restrict__ w, const float *__restrict__ b,
