@@ -43,18 +43,18 @@ static double time_cfg(GemmArgs g, const std::vector<int8_t *> &ws, const std::v
 int main(int argc, char **argv) {
     const int M = argc > 1 ? atoi(argv[1]) : 64;
     const int N = 6144, K = 1024, F = N / 2;
-    if (M < 1 || M > 64) { printf("M in 1..64\n"); return 1; }
+    if (M < 1 || M > 128) { printf("M in 1..128\n"); return 1; }
     hipStream_t s; CK(hipStreamCreate(&s));
     // activations: int8 [M][K] + fp32 (fp16-valued) block scales [M][K/32]
     int8_t *Aq, *oq; float *Ad, *o32, *od;
-    CK(hipMalloc(&Aq, (size_t)64 * K)); CK(hipMalloc(&Ad, (size_t)64 * (K / 32) * 4));
-    CK(hipMalloc(&o32, (size_t)64 * F * 4)); CK(hipMalloc(&oq, (size_t)64 * F)); CK(hipMalloc(&od, (size_t)64 * (F / 32) * 4));
+    CK(hipMalloc(&Aq, (size_t)128 * K)); CK(hipMalloc(&Ad, (size_t)128 * (K / 32) * 4));
+    CK(hipMalloc(&o32, (size_t)128 * F * 4)); CK(hipMalloc(&oq, (size_t)128 * F)); CK(hipMalloc(&od, (size_t)128 * (F / 32) * 4));
     unsigned x = 4321u;
     auto rnd = [&] { x = x * 1664525u + 1013904223u; return x >> 8; };
     {
-        std::vector<int8_t> q((size_t)64 * K);
+        std::vector<int8_t> q((size_t)128 * K);
         for (auto &v : q) v = (int8_t)((int)(rnd() % 255) - 127);
-        std::vector<float> d((size_t)64 * (K / 32));
+        std::vector<float> d((size_t)128 * (K / 32));
         for (auto &v : d) v = (float)(_Float16)(0.002f + 0.0001f * (float)(rnd() % 100));
         CK(hipMemcpy(Aq, q.data(), q.size(), hipMemcpyHostToDevice));
         CK(hipMemcpy(Ad, d.data(), d.size() * 4, hipMemcpyHostToDevice));
@@ -81,7 +81,7 @@ int main(int argc, char **argv) {
     // bits: the fused epilogue against the fp32 output quantised on the host
     {
         GemmArgs g1 = g; g1.Wq = ws[0]; g1.Wd = wds[0];
-        CK(hipMemset(oq, 0x55, (size_t)64 * F)); CK(hipMemset(od, 0x55, (size_t)64 * (F / 32) * 4));
+        CK(hipMemset(oq, 0x55, (size_t)128 * F)); CK(hipMemset(od, 0x55, (size_t)128 * (F / 32) * 4));
         // the engine's tiling (K over 8 waves) and the fp32 form with the same K split
         hipLaunchKernelGGL((gemm_skinny_q8_kernel<2, 2, 8, EPI_SWIGLU_F32, 4, 1>), dim3(N / 32, (M + 31) / 32), dim3(512), 0, s, g1);
         hipLaunchKernelGGL((gemm_skinny_q8_kernel<2, 4, 8, EPI_SWIGLU_Q8, 4, 1>), dim3(N / 64, (M + 31) / 32), dim3(512), 0, s, g1);
@@ -115,10 +115,10 @@ int main(int argc, char **argv) {
     struct Sh { const char *name; int N, K; };
     const Sh shs[] = {{"qkv 4096x1024", 4096, 1024}, {"o 1024x2048", 1024, 2048}, {"down 1024x3072", 1024, 3072}};
     float *res; int8_t *A2; float *Ad2;
-    CK(hipMalloc(&res, (size_t)64 * 4096 * 4)); CK(hipMemset(res, 0, (size_t)64 * 4096 * 4));
-    CK(hipMalloc(&A2, (size_t)64 * 3072)); CK(hipMemset(A2, 0x13, (size_t)64 * 3072));
-    CK(hipMalloc(&Ad2, (size_t)64 * 96 * 4)); CK(hipMemset(Ad2, 0x3a, (size_t)64 * 96 * 4));
-    CK(hipFree(o32)); CK(hipMalloc(&o32, (size_t)64 * 4096 * 4));
+    CK(hipMalloc(&res, (size_t)128 * 4096 * 4)); CK(hipMemset(res, 0, (size_t)128 * 4096 * 4));
+    CK(hipMalloc(&A2, (size_t)128 * 3072)); CK(hipMemset(A2, 0x13, (size_t)128 * 3072));
+    CK(hipMalloc(&Ad2, (size_t)128 * 96 * 4)); CK(hipMemset(Ad2, 0x3a, (size_t)128 * 96 * 4));
+    CK(hipFree(o32)); CK(hipMalloc(&o32, (size_t)128 * 4096 * 4));
     for (const Sh &sh : shs) {
         const size_t wb2 = (size_t)sh.N * sh.K;
         const int NL2 = (int)((600ull << 20) / wb2) + 1;
