@@ -614,7 +614,11 @@ bool launch_gemm_skinny_q8(int epi, const GemmArgs &g, hipStream_t s) {
             // QKV: all 64 rows a block (tools/skinny_q8_bench.hip, 64 rows: 7.18 -> 6.53 us a
             // launch with every chunk in flight; the same K split, so the same bits); o / down:
             // 16-row blocks (32- and 64-row blocks 1.3-3.7 us slower)
-            if (g.N >= 4096) skinny_q8_mt<4, 1, 8, EPI_F32>(g, s);
+            // 65..128 rows (tools/skinny_q8_bench.hip at 128 rows): QKV 32-column tiles of 64
+            // rows 9.17 -> 8.60 us, o / down 32-row blocks 8.97 -> 7.27 / 12.55 -> 9.42 us
+            if (g.M > 64 && g.N >= 4096 && g.N % 32 == 0) run_skinny_q8<4, 2, 8, EPI_F32>(g, s);
+            else if (g.M > 64) run_skinny_q8<2, 1, 8, EPI_F32>(g, s);
+            else if (g.N >= 4096) skinny_q8_mt<4, 1, 8, EPI_F32>(g, s);
             else skinny_q8_mt<1, 1, 8, EPI_F32>(g, s);
             return true;
         case EPI_SWIGLU_F32:
@@ -625,8 +629,10 @@ bool launch_gemm_skinny_q8(int epi, const GemmArgs &g, hipStream_t s) {
             // 64-column blocks: 32 output columns, one Q8_0 block a row; K over 8 waves
             // (tools/skinny_q8_bench.hip, 64 rows: 10.16 us against 10.43 for the fp32
             // SwiGLU form alone, which the separate quantisation launch then followed)
+            // (65..128 rows: 64-row blocks, 18.30 -> 12.52 us at 128 rows)
             if (g.N % 64 != 0 || !g.out_q || !g.out_d || g.ldoq % 32 != 0) return false;
-            skinny_q8_mt<2, 4, 8, EPI_SWIGLU_Q8>(g, s);
+            if (g.M > 64) run_skinny_q8<4, 4, 8, EPI_SWIGLU_Q8>(g, s);
+            else skinny_q8_mt<2, 4, 8, EPI_SWIGLU_Q8>(g, s);
             return true;
         default:
             return false;

@@ -528,7 +528,7 @@ def test_full_q8_skinny_inflight_bit_identical(gpu, full_q8_gguf):
     try:
         rng = np.random.default_rng(31)
         ids = [int(t) for t in rng.integers(0, 151643, 40)]
-        for B in (16, 64):
+        for B in (16, 64, 100):   # 100: the 65..128-row tilings
             c = qasr.Context(m, max_batch=B, max_ctx=64)
             try:
                 toks = [int(t) for t in np.random.default_rng(B).integers(0, 151643, B)]
