@@ -583,6 +583,7 @@ def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
         pcm = list(ex.map(lambda i: qasr.synth_pcm(utts[i][0], ns), range(pool)))
     for c in ctxs:
         c.stage_audio(pcm)
+        c.set_option("staged_wrap", 1)   # utterance ids past the pool reuse its clips (id % pool)
     stats = []
 
     def stream(next_clip):

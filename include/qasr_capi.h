@@ -218,7 +218,9 @@ int qasr_run_stream(qasr_ctx *c, int slots, qasr_fetch_fn fetch, qasr_sink_fn si
                     qasr_stream_stats *stats);
 /* The same over the staged pool (qasr_stage_audio; inputs already in HBM):
  * fetch(user, &max_tokens) returns the next clip's id (>= 0), or < 0 when the
- * queue is empty; the clip is staged clip id % (pool size), so an utterance
+ * queue is empty; the clip is staged clip id.  An id outside the pool fails
+ * that clip (QASR_ERR_ARG through the sink) unless the context option
+ * "staged_wrap" is 1: then it is staged clip id % (pool size), so an utterance
  * set larger than the pool reuses its clips, each under its own id. */
 typedef int (*qasr_fetch_staged_fn)(void *user, int *max_tokens);
 int qasr_run_stream_staged(qasr_ctx *c, int slots, qasr_fetch_staged_fn fetch, qasr_sink_fn sink, void *user,
@@ -302,6 +304,11 @@ int qasr_align_tokenize(const qasr_model *m, const char *text, const char *langu
  * returns the length, writes at most cap-1 bytes + NUL */
 int qasr_align_words(const qasr_model *m, const char *text, const char *language, char *out, int cap);
 int qasr_model_load_korean_dict(qasr_model *m, const char *path);
+/* Host policy of the Qwen3ASR class (no reference counterpart): the shape a
+ * context (cur_b slots x cur_l positions) is recreated with for a call that
+ * needs (batch, n_ctx) -- the union of both while its KV cells do not exceed
+ * the larger shape's own, else exactly (batch, n_ctx). */
+void qasr_ctx_grow_shape(int cur_b, int cur_l, int batch, int n_ctx, int *nb, int *nl);
 /* LIS repair of raw classes (in -> out, n values) */
 int qasr_fix_timestamps(const int32_t *classes, int n, int32_t *out);
 /* prompt length of an alignment: n_text + 2 + pads(mel frames of n_samples) */

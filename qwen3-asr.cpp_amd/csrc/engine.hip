@@ -37,6 +37,14 @@ static int fail(int code, const std::string &msg) {
     return code;
 }
 
+// a GEMM / GEMV launch that found no kernel for its (mode, epilogue) pair
+// (gemm.hip note_declined) fails the stage that issued it
+static int declined_check(const char *stage) {
+    std::string msg;
+    if (qasr::take_declined(&msg)) return fail(QASR_ERR_STATE, std::string(stage) + ": " + msg);
+    return 0;
+}
+
 #define HIPCHK(x)                                                                                  \
     do {                                                                                           \
         hipError_t e_ = (x);                                                                       \
@@ -137,7 +145,7 @@ struct qasr_ctx {
     std::vector<int> staged_n;
     std::vector<long> staged_off;
     bool eager = false;            // QASR_NO_GRAPH=1: launch the decode step eagerly (profilers)
-    int dev_skip = 0;              // QASR_DEV_SKIP bitmask: profiling only, omits decode kernels
+    int dev_skip = 0;              // QASR_DEV_SKIP bitmask (-DQASR_DIAG_SKIP builds only): omits decode kernels
     FuseCfg fuse;                  // batch-1 fused launches: switches, delays, co-residency of this device
     unsigned int *d_err = nullptr; // sticky device error word of the fused launches (DevErr bits)
     int dbg_layers = 0;            // diagnostic: decode steps run only the first n decoder layers (0 = all)
@@ -229,6 +237,8 @@ static const std::vector<FuseOption> &fuse_options() {
         {"lmh", "QASR_LMH", &FuseCfg::lmh},
         {"fx_seq", "QASR_FX_SEQ", &FuseCfg::fx_seq},
         {"skinny_inf", "QASR_SKINNY_INF", &FuseCfg::skinny_inf},
+        {"staged_wrap", "QASR_STAGED_WRAP", &FuseCfg::staged_wrap},
+        {"poison_scratch", "QASR_POISON_SCRATCH", &FuseCfg::poison},
     };
     return v;
 }
@@ -324,6 +334,7 @@ static int ensure(qasr_ctx *c, DevBuf &b, size_t bytes) {
     HIPCHK(hipMalloc(&b.p, n));
     b.n = n;
     c->owned.push_back({b.p, n});
+    if (c->fuse.poison) HIPCHK(hipMemsetAsync(b.p, 0xFF, n, c->st));
     return 0;
 }
 
@@ -711,8 +722,9 @@ extern "C" int qasr_ctx_create(qasr_model *m, int max_batch, int max_ctx, qasr_c
         return fail(QASR_ERR_ARG, "max_ctx exceeds " + std::to_string(decode_max_splits() * decode_split_len()));
     const char *ng = getenv("QASR_NO_GRAPH");
     c->eager = ng && ng[0] == '1';
-    const char *ds = getenv("QASR_DEV_SKIP");
-    if (ds) c->dev_skip = atoi(ds);
+#ifdef QASR_DIAG_SKIP   // diagnostic builds only (tools/): drops decode kernels to price them -- wrong tokens
+    if (const char *ds = getenv("QASR_DEV_SKIP")) c->dev_skip = atoi(ds);
+#endif
     // fused-launch options: environment defaults, per-context overrides via qasr_ctx_set_option
     for (const auto &o : fuse_options()) {
         if (const char *e = getenv(o.env)) c->fuse.*(o.field) = atoi(e);
@@ -1068,7 +1080,7 @@ static int run_encoder(qasr_ctx *c, const float *d_mel, const std::vector<long> 
     p2.M = N; p2.N = hp.hidden; p2.K = D; p2.bias = m->proj2_b; p2.out_f32 = c->feats.as<float>(); p2.ldo = hp.hidden;
     linear(EPI_F32, p2, nullptr, c->eatt.as<uint16_t>(), D, m->proj2_w, m->proj2_d);
     HIPCHK(hipGetLastError());
-    return 0;
+    return declined_check("encoder");
 }
 
 // embedding gather + audio splice + decoder layer stack over the prompt rows of
@@ -1176,7 +1188,7 @@ static int prefill_layers(qasr_ctx *c, const std::vector<int32_t> &ids, const st
         if (q8) gemm_q8(c, EPI_F32, dn, x32, nullptr, F, 0, L.wd, L.wd_d, s);
         else { dn.A = c->pact.as<uint16_t>(); dn.lda = F; dn.W = L.wd; dn.ldw = F; launch_gemm_c(c, AM_DENSE, EPI_F32, dn, s); }
     }
-    return 0;
+    return declined_check("prefill");
 }
 
 // prefill (src/text_decoder.cpp:588-684): layers, then the LAST row of each
@@ -1223,7 +1235,7 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
     HIPCHK(hipMemcpyAsync(c->d_nkv, nkv.data(), B * 4, hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));   // pos/nkv host vectors go out of scope
     HIPCHK(hipGetLastError());
-    return 0;
+    return declined_check("prefill LM head");
 }
 
 // decode-batch projections: the weight-streaming skinny GEMM where it takes
@@ -1267,7 +1279,7 @@ static int decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange r
     // probed group (emitted alone): every launch in it folds its block times into one record
     unsigned long long *stamp = r.hi - r.lo == 1 ? c->cur_stamp : nullptr;
     if (r.in(0) && !skinny) launch_embed(c->d_tok, B, m->embd, H, nullptr, nullptr, x, s);
-    const int skip = c->dev_skip;   // profiling only (QASR_DEV_SKIP): drop kernels to price them
+    const int skip = c->dev_skip;   // 0 unless built with -DQASR_DIAG_SKIP (QASR_DEV_SKIP): drop kernels to price them
     if (c->d_trace && r.in(0)) (void)hipMemsetAsync(c->d_trace, 0, 6 * 4096 * 8 * 8, s);
     for (int l = 0; l < nl; l++) {
         const bool ga = r.in(1 + 2 * l), gb = r.in(2 + 2 * l);
@@ -1451,7 +1463,7 @@ static int decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange r
         launch_argmax_finish(c->d_amax, B, c->d_tok, c->d_hist, c->hist_cap, c->d_step, s);
         launch_fill_u64(c->d_amax, B, 0ull, s);   // re-arm (zero at rest)
     }
-    return 0;
+    return declined_check("decode step");
 }
 
 // Kernel probes (qasr_set_probe): HIP events on the context stream around one
@@ -1829,6 +1841,9 @@ extern "C" int qasr_prefill(qasr_ctx *c, const int32_t *ids, const int *P, const
 static int prefill_chunk_common(qasr_ctx *c, const int32_t *ids, const int *P, const int *n_past, const float *feats,
                                 const int *audio_pos, const int *N, int B, float *logits_last, int32_t *argmax) {
     if (!c || !ids || !P || !n_past || B <= 0) return fail(QASR_ERR_ARG, "bad arguments");
+    if (feats && (!N || !audio_pos)) return fail(QASR_ERR_ARG, "audio features need N and audio_pos");
+    for (int b = 0; b < B; b++)
+        if (P[b] < 0 || n_past[b] < 0 || (feats && N[b] < 0)) return fail(QASR_ERR_ARG, "negative P / n_past / N");
     HIPCHK(hipSetDevice(c->m->device));
     HIPCHK(hipStreamSynchronize(c->st));
     c->pin_used = 0;
@@ -2318,7 +2333,9 @@ extern "C" int qasr_run_stream_staged(qasr_ctx *c, int slots, qasr_fetch_staged_
     const int pool = (int)c->staged_n.size();
     return run_stream(c, slots, [&](StreamClip &k) {
         k.id = fetch(user, &k.budget);
-        k.staged = k.id >= 0 && pool > 0 ? k.id % pool : k.id;   // (ids past the pool reuse its clips)
+        // ids past the pool reuse its clips only when asked for (option staged_wrap); else run_stream
+        // rejects them as out of range
+        k.staged = k.id >= 0 && pool > 0 && c->fuse.staged_wrap ? k.id % pool : k.id;
         return k.id >= 0;
     }, sink, user, max_tokens, ignore_eos, stats);
 }
@@ -2460,6 +2477,7 @@ static int align_classes(qasr_ctx *c, const float *const *pcm, const int *n, con
         g.amax = c->aam.as<unsigned long long>(); g.n_valid = hp.classify_num;
         launch_gemm_c(c, AM_DENSE, EPI_ARGMAX, g, s);
         HIPCHK(hipGetLastError());
+        if ((rc = declined_check("aligner head"))) return rc;
         HIPCHK(hipMemcpyAsync(keys.data(), c->aam.p, (size_t)NT * 8, hipMemcpyDeviceToHost, s));
     }
     HIPCHK(hipEventRecord(c->ev[3], s));

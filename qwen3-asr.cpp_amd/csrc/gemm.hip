@@ -337,8 +337,7 @@ static void dispatch_tiles(const GemmArgs &g, hipStream_t s) {
             return;
         }
         // conv: K = 9*C, slab group must stay inside one tap -> C % (32*KS) == 0
-        static const int wide = [] { const char *e = getenv("QASR_CONV_WIDE"); return e ? atoi(e) : 1; }();
-        if (wide && g.N == 480) {
+        if (g.N == 480) {
             // all 480 output channels per block: the gathered A tile is read once
             // (N/96 = 5 re-reads of the im2col rows otherwise), W stays L2-resident
             if (g.regs_staged) run_gemm<64, 480, 1, AMODE, EPI>(g, s);
@@ -404,14 +403,23 @@ void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s) {
         case AM_DENSE * 8 + EPI_SWIGLU_F32: dispatch_tiles<AM_DENSE, EPI_SWIGLU_F32>(g, s); break;
         case AM_CONV2 * 8 + EPI_GELU_F16: dispatch_tiles<AM_CONV2, EPI_GELU_F16>(g, s); break;
         case AM_CONV3 * 8 + EPI_GELU_F16: dispatch_tiles<AM_CONV3, EPI_GELU_F16>(g, s); break;
-        default: break;
+        default: note_declined("launch_gemm", amode, epi); break;
     }
 }
 
-// QASR_GEMV1=0 keeps the multi-row kernel for one-row calls (A/B timing)
-static bool getenv_gemv1() {
-    static const int on = [] { const char *e = getenv("QASR_GEMV1"); return e && e[0] == '0' ? 0 : 1; }();
-    return on;
+// a (mode, epilogue) pair no dispatcher instantiates: recorded per host thread
+// (each context is driven by one thread) and turned into an error by the
+// engine after the stage that launched it (take_declined), never skipped silently
+static thread_local std::string t_declined;
+void note_declined(const char *what, int mode, int epi) {
+    if (t_declined.empty())
+        t_declined = std::string(what) + " has no kernel for mode " + std::to_string(mode) + " / epilogue " + std::to_string(epi);
+}
+bool take_declined(std::string *msg) {
+    if (t_declined.empty()) return false;
+    if (msg) *msg = t_declined;
+    t_declined.clear();
+    return true;
 }
 
 // ===================================================================== GEMV
@@ -834,8 +842,7 @@ template <int EPI, int CPW, int MR, int NK>
 static void run_gemv(const GemvArgs &g, hipStream_t s) {
     const int per_block = 4 * CPW;
     int blocks = (g.N + per_block - 1) / per_block;
-    static const int cap = [] { const char *e = getenv("QASR_GEMV_BLOCKS"); return e ? atoi(e) : 1024; }();
-    if (blocks > cap) blocks = cap;   // 256 CUs x 4 resident workgroups, grid-stride beyond
+    if (blocks > 1024) blocks = 1024;   // 256 CUs x 4 resident workgroups, grid-stride beyond
     const size_t lds = (size_t)MR * g.K * 2;
     hipLaunchKernelGGL((gemv_kernel<EPI, CPW, MR, NK>), dim3(blocks), dim3(256), lds, s, g);
 }
@@ -868,12 +875,12 @@ static void gemv_mr(const GemvArgs &g, hipStream_t s) {
 
 void launch_gemv(int epi, const GemvArgs &g, hipStream_t s) {
     if (g.M <= 0) return;
-    if (getenv_gemv1() && launch_gemv1(epi, g, s)) return;
+    if (launch_gemv1(epi, g, s)) return;
     if (g.Wd) {   // Q8_0 weights: fp32 x only
         switch (epi) {
             case EPI_F32: gemv_q8_mr<EPI_F32>(g, s); break;
             case EPI_SWIGLU_F32: gemv_q8_mr<EPI_SWIGLU_F32>(g, s); break;
-            default: break;
+            default: note_declined("launch_gemv (Q8_0)", 0, epi); break;
         }
         return;
     }
@@ -882,7 +889,7 @@ void launch_gemv(int epi, const GemvArgs &g, hipStream_t s) {
         case EPI_SWIGLU_F16: gemv_mr<EPI_SWIGLU_F16>(g, s); break;
         case EPI_ARGMAX: gemv_mr<EPI_ARGMAX>(g, s); break;
         case EPI_F16: gemv_mr<EPI_F16>(g, s); break;
-        default: break;
+        default: note_declined("launch_gemv", 0, epi); break;
     }
 }
 

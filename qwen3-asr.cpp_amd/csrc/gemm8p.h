@@ -207,7 +207,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
     const int aoff = (m0 + prow) * g.lda + pchk, woff = (n0 + prow) * g.ldw + pchk;
     // conv modes, per row j of this lane's 4 [half * 2 + piece]: the input position of tap (0, 0)
     // in 16-B units (8 channels: int32 holds a batch's whole activation), and the row's input
-    // width << 9 | bit t = tap t inside the image
+    // width << 16 | bit t = tap t inside the image (bits 9..15 stay 0: the K-padding taps read the zero line)
     int rbase[AMODE == AM_DENSE ? 1 : 4], rinfo[AMODE == AM_DENSE ? 1 : 4];
     if constexpr (AMODE != AM_DENSE) {
         constexpr int Hin = AMODE == AM_CONV2 ? 64 : 32;
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
                 mask |= (ih >= 0 && ih < Hin && iw >= 0 && iw < Win) << t;
             }
             rbase[j] = (cb + (2 * oh - 1) * Win + (2 * ow - 1)) * C8;
-            rinfo[j] = (Win << 9) | mask;
+            rinfo[j] = (Win << 16) | mask;
         }
     }
     // half-tile id: 0 A0, 1 A1, 2 B0, 3 B1
@@ -244,8 +244,8 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
 #pragma unroll
             for (int p = 0; p < 2; p++) {
                 const int j = (hid & 1) * 2 + p, info = rinfo[j];
-                const int off = rbase[j] + (kh * (info >> 9) + kw) * C8 + ic8;   // tap <= 8 when used
-                const bool ok = (info >> tap) & 1;                                // 0 for tap >= 9 (K padding)
+                const int off = rbase[j] + (kh * (info >> 16) + kw) * C8 + ic8;   // tap <= 8 when used
+                const bool ok = (info >> tap) & 1;                                 // 0 for tap >= 9 (K padding)
                 const uint16_t *pa = g.A + 8 * (long)off;
                 const uint16_t *src = ok ? pa : (const uint16_t *)g8_zero_line;
                 __builtin_amdgcn_global_load_lds((glb_void_8p *)src, (lds_void_8p *)(smem + g8_img(hid, buf) + (wid + 8 * p) * 512),

@@ -3,6 +3,8 @@
 // are graph-capturable (no allocation, no synchronisation).
 #pragma once
 
+#include <string>
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -84,6 +86,11 @@ struct GemmArgs {
     int8_t *out_q; float *out_d; int ldoq;   // EPI_SWIGLU_Q8: int8 [M][ldoq], fp32 block scales [M][ldoq / 32]
 };
 void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s);
+// an unsupported (mode, epilogue) pair launches nothing and is recorded for the
+// calling host thread; take_declined returns (and clears) it -- the engine
+// fails the call with it (QASR_ERR_STATE) instead of running short
+void note_declined(const char *what, int mode, int epi);
+bool take_declined(std::string *msg);
 // decode-batch GEMM (gemm_skinny.hip): dense A, M <= 128, K % 128 == 0; returns
 // false (nothing launched) for shapes it does not take, or when g.no_skinny.
 bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s);
@@ -179,6 +186,10 @@ struct FuseCfg {
                                         // (decode_attn_seq_kernel<1>) where the per-sequence kernel is taken
     int lmh = 1;                        // decode batches of f16 models (9..64 rows): the LM head in one launch (lmhead.hip)
     int skinny_inf = 1;                 // decode-batch skinny GEMMs: all of a wave's K chunks in flight (gemm_skinny.hip CPW)
+    int staged_wrap = 0;                // qasr_run_stream_staged: ids past the staged pool reuse clip id % pool (bench
+                                        // utterance sets over a smaller pool); 0: such an id is rejected as out of range
+    int poison = 0;                     // test only: scratch buffers grown by the context are filled with 0xFF bytes
+                                        // (fp16 NaN) so a kernel reading rows it never wrote shows up in its outputs
     unsigned int *err = nullptr;        // sticky device error word (DevErr bits)
 };
 // co-resident workgroup capacity of the fused kernels on the current device

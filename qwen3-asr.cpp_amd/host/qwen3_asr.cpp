@@ -72,15 +72,24 @@ bool Qwen3ASR::load_model(const std::string &model_path) {
     return true;
 }
 
+// The shape a context is recreated with when (batch, n_ctx) does not fit the
+// current (cur_b, cur_l): the union of both only while its KV cells (slots x
+// positions) are no more than the larger of the two shapes' own -- a long
+// single clip after a many-slot stream gets (1, its length), not (slots, its
+// length), which multiplies the cache (128 slots x 16k positions of
+// a 20-min file is ~240 GB of KV at 0.6B).
+extern "C" void qasr_ctx_grow_shape(int cur_b, int cur_l, int batch, int n_ctx, int *nb, int *nl) {
+    const long long cur = (long long)cur_b * cur_l, want = (long long)batch * n_ctx;
+    const int ub = std::max(batch, cur_b), ul = std::max(n_ctx, cur_l);
+    if ((long long)ub * ul <= std::max(cur, want)) { *nb = ub; *nl = ul; }
+    else { *nb = batch; *nl = n_ctx; }
+}
+
 bool Qwen3ASR::ensure_ctx(int batch, int n_ctx) {
     if (ctx_ && ctx_batch_ >= batch && ctx_len_ >= n_ctx) return true;
     if (ctx_) { qasr_ctx_free(ctx_); ctx_ = nullptr; }
-    // keep the larger shape only while the KV cache stays in bounds: a long
-    // single clip after a many-slot stream gets (1, its length), not (slots,
-    // its length) -- that product multiplies the cache (CLI sharding)
-    const long long kMaxCells = 1LL << 22;   // slots x positions (~0.7 TB of f16 KV at 0.6B would be absurd)
-    int nb = std::max(batch, ctx_batch_), nl = std::max(n_ctx, ctx_len_);
-    if ((long long)nb * nl > kMaxCells) { nb = batch; nl = n_ctx; }
+    int nb = 0, nl = 0;
+    qasr_ctx_grow_shape(ctx_batch_, ctx_len_, batch, n_ctx, &nb, &nl);
     if (qasr_ctx_create(model_, nb, nl, &ctx_) != 0) {
         error_msg_ = std::string("Failed to initialize KV cache: ") + qasr_last_error();
         ctx_ = nullptr;

@@ -33,6 +33,7 @@ EXPORTS = [
     "qasr_load_wav", "qasr_write_wav", "qasr_synth_pcm", "qasr_write_synthetic_gguf", "qasr_synthetic_gguf_version",
     "qasr_align", "qasr_align_tokenize", "qasr_model_load_korean_dict", "qasr_fix_timestamps",
     "qasr_align_prompt_len", "qasr_align_json", "qasr_align_json_batch", "qasr_align_words",
+    "qasr_ctx_grow_shape",
 ]
 
 
@@ -115,6 +116,7 @@ def lib() -> C.CDLL:
             "qasr_align_tokenize": ([P, C.c_char_p, C.c_char_p, I32P, I, IP], I),
             "qasr_model_load_korean_dict": ([P, C.c_char_p], I),
             "qasr_fix_timestamps": ([I32P, I, I32P], I),
+            "qasr_ctx_grow_shape": ([I, I, I, I, IP, IP], None),
             "qasr_align_prompt_len": ([I, I], I),
             "qasr_align_words": ([P, C.c_char_p, C.c_char_p, C.c_char_p, I], I),
             "qasr_align_json": ([P, F, I, C.c_char_p, C.c_char_p, C.c_char_p, I, C.POINTER(Timings)], I),

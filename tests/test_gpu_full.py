@@ -174,6 +174,33 @@ def test_full_encoder_ragged_tiles_bit_identical(full):
         assert a.shape == b.shape and np.array_equal(a, b)
 
 
+def test_full_encoder_poisoned_scratch(full):
+    """the implicit-im2col convs must never read activation rows they
+    did not write (the 8-phase tile's K-padding taps read the zero line).  With
+    option poison_scratch every scratch buffer the context grows starts as 0xFF
+    bytes (fp16 NaN): odd-width chunks (ragged clips, conv3 at W2 = 25) and a
+    long odd-length encode_no_chunk clip (conv2 through the 8-phase tile at odd
+    W1) give the same finite features as a clean context, bit for bit."""
+    m, _, _ = full
+    secs = [29.37, 17.71, 30.0]
+    clips = [qasr.synth_pcm(15600 + i, int(s * SR)) for i, s in enumerate(secs)]
+    long_clip = qasr.synth_pcm(15650, int(47.31 * SR))
+    out = {}
+    for poison in (0, 1):
+        cb = qasr.Context(m, max_batch=len(clips), max_ctx=512)
+        try:
+            cb.set_option("poison_scratch", poison)
+            mels = cb.mel(clips)
+            f = cb.encode(mels)
+            nc = cb.encode_no_chunk(cb.mel([long_clip]))[0]
+            out[poison] = (f, nc)
+        finally:
+            cb.close()
+    for a, b in zip(out[0][0], out[1][0]):
+        assert np.isfinite(b).all() and np.array_equal(a, b)
+    assert np.isfinite(out[1][1]).all() and np.array_equal(out[0][1], out[1][1])
+
+
 FUSE_KNOBS = {"QASR_FUSE_FFN": dict(fuse_ffn=0), "QASR_FUSE_QKV": dict(fuse_qkv=0, fuse_o=0), "QASR_FUSE_O": dict(fuse_o=0)}
 
 

@@ -119,6 +119,24 @@ def test_stream_fetch_exception_is_raised(tiny_model):
         c.close()
 
 
+def test_stream_staged_ids_outside_pool(tiny_model):
+    """a staged id outside the pool fails that clip (out of range)
+    unless option staged_wrap asks for id % pool reuse (bench.py's utterance
+    sets over a 128-clip pool); the other clips are transcribed either way"""
+    clips = [qasr.synth_pcm(7500 + i, SR + 300 * i) for i in range(2)]
+    c = qasr.Context(tiny_model, max_batch=2, max_ctx=640)
+    try:
+        c.stage_audio(clips)
+        out, st = c.run_stream_staged(_queue([0, 5, 1]), max_tokens=4, ignore_eos=True)
+        assert isinstance(out[5], qasr.QasrError) and "out of range" in str(out[5])
+        assert st.n_errors == 1 and out[0] == _single(tiny_model, clips[0], 4, True)
+        c.set_option("staged_wrap", 1)
+        out, st = c.run_stream_staged(_queue([0, 5, 1]), max_tokens=4, ignore_eos=True)
+        assert st.n_errors == 0 and out[5] == out[1] == _single(tiny_model, clips[1], 4, True)
+    finally:
+        c.close()
+
+
 def test_concurrent_streams_equal_single(tiny_model):
     """bench.py's utterance_set runs several continuous-batching contexts of one
     model at once, each on its own HIP stream and host thread, fed by one
@@ -149,3 +167,29 @@ def test_concurrent_streams_equal_single(tiny_model):
     assert sorted(out) == [20 + i for i in range(len(clips))]
     for i, (p, b) in enumerate(zip(clips, budgets)):
         assert out[20 + i] == _single(tiny_model, p, b, True), i
+
+
+def test_env_eager_and_trace_paths_equal_default(tiny_model, tmp_path, monkeypatch):
+    """the environment switches outside fuse_options().
+    QASR_NO_GRAPH=1 (decode steps launched eagerly, for profilers) and
+    QASR_DEV_TRACE (per-block timestamps of one layer's kernels) change how the
+    step is launched, never what it computes: tokens of a batch-1 and a
+    batch-3 run equal the default context's, and the trace file is written."""
+    clips = [qasr.synth_pcm(7600 + i, SR + 700 * i) for i in range(3)]
+
+    def run():
+        c = qasr.Context(tiny_model, max_batch=3, max_ctx=640)
+        try:
+            return (c.transcribe(clips[:1], max_tokens=10, ignore_eos=True).tokens,
+                    c.transcribe(clips, max_tokens=10, ignore_eos=True).tokens)
+        finally:
+            c.close()
+    base = run()
+    monkeypatch.setenv("QASR_NO_GRAPH", "1")
+    assert run() == base
+    monkeypatch.delenv("QASR_NO_GRAPH")
+    tr = tmp_path / "trace.bin"
+    monkeypatch.setenv("QASR_DEV_TRACE", str(tr))
+    monkeypatch.setenv("QASR_DEV_TRACE_LAYER", "0")
+    assert run() == base
+    assert tr.exists() and tr.stat().st_size > 0

@@ -126,3 +126,23 @@ def test_stream_fetch_guard_stores_exception():
     assert len(n) == 1 and isinstance(failed[0], KeyError)
     ok = qasr._guarded_fetch(lambda *a: 7, [])
     assert ok(None) == 7
+
+
+def test_ctx_grow_shape_bounds_kv_cells(built):
+    """ADVICE r5 (Qwen3ASR::ensure_ctx): a context is recreated with the union
+    of the old and the requested shape only while that union's KV cells do not
+    exceed the larger of the two shapes -- 128 stream slots followed by a long
+    single clip (16k positions) gives (1, 16k), not (128, 16k) (~240 GB of KV)"""
+    import ctypes as C
+
+    def grow(cb, cl, b, n):
+        nb, nl = C.c_int(0), C.c_int(0)
+        qasr.lib().qasr_ctx_grow_shape(cb, cl, b, n, C.byref(nb), C.byref(nl))
+        return nb.value, nl.value
+    assert grow(128, 600, 1, 16000) == (1, 16000)
+    assert grow(1, 16000, 128, 600) == (128, 600)
+    assert grow(0, 0, 4, 512) == (4, 512)
+    assert grow(4, 512, 4, 600) == (4, 600)          # longer context, same slots: union
+    assert grow(4, 512, 8, 512) == (8, 512)
+    assert grow(64, 500, 128, 480) == (128, 480)     # union 64k cells > max(32k, 61.4k): the request alone
+    assert grow(128, 480, 64, 500) == (64, 500)

@@ -27,6 +27,7 @@ def run(nctx: int, slots: int, n_utt: int, stagger_s: float = 0.0):
     ctxs = [qasr.Context(m, max_batch=slots, max_ctx=P + bud + 8) for _ in range(nctx)]
     for c in ctxs:
         c.stage_audio(pcm)
+        c.set_option("staged_wrap", 1)
     lock = threading.Lock()
     nxt = [0]
 
