@@ -545,6 +545,36 @@ def utterance_main(args, m, rank, local, world, dist, model_path):
     print(json.dumps(out), flush=True)
 
 
+def pmc_batch_kernel(kernel_prefix: str, batch: int, sub: str = "f16"):
+    """HBM bytes per launch of one decode-batch kernel from the newest committed
+    single-context batch PMC summary (profiles/<round>/batch*/<sub>/summary.json,
+    tools/profile_batch.sh) whose bench line ran this batch size"""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "batch*", sub, "summary.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+            bl = json.load(open(os.path.join(os.path.dirname(f), "bench.json")))
+        except (OSError, ValueError):
+            continue
+        if bl.get("config", {}).get("clips_per_gpu") != batch:
+            continue
+        for k in d.get("kernels", []):
+            if k["name"].startswith(kernel_prefix) and "hbm_read_bytes" in k:
+                return k["hbm_read_bytes"] + k.get("hbm_write_bytes", 0), os.path.relpath(f, ROOT)
+    return None, None
+
+
+def set_decode_bytes(hp, stats) -> float:
+    """Algorithmic HBM bytes of the contexts' decode steps: per
+    step the decoder weights and the tied LM head once (shared by the slots),
+    plus every slot's K / V cache rows 0..n_kv-1 (qasr_stream_stats.kv_keys)"""
+    H, hd = hp.hidden_size, hp.head_dim
+    per_layer = (hp.n_heads * hd + 2 * hp.n_kv_heads * hd) * H + H * hp.n_heads * hd + 3 * hp.dec_ffn * H
+    w = hp.dec_layers * per_layer * 2 + hp.vocab_size * H * 2
+    kv_row = hp.dec_layers * 2 * hp.n_kv_heads * hd * 2
+    return float(sum(st.n_steps * w + st.kv_keys * kv_row for st in stats))
+
+
 def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
     """configs[3] inside the default run (1000 x 30 s f16
     utterances; north_star's "throughput on synthetic 30 s / 16 kHz audio at
@@ -562,7 +592,14 @@ def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
     own host thread, one lock around the rank's queue): a context's refill
     prefill (compute-bound) overlaps the others' decode steps (latency / HBM
     bound) -- 1 x 128 slots 7780, 2 x 128 8500, 3 x 128 8690 RTFx, tokens equal
-    (tools/r5/two_ctx.py; 4 contexts exceed the box's 4 hardware queues)."""
+    (tools/r5/two_ctx.py; 4 contexts exceed the box's 4 hardware queues).
+    Round 6: the set's own rooflines from one untimed
+    single-context pass after the timed one (so the contexts do not contend):
+    the dominant decode kernel (decode_attn_seq_kernel<1>, layer probe_layer,
+    device clock) and the encoder by its HIP events; the timed pass's decode
+    bytes (weights + every slot's K / V rows) over the contexts' decode time;
+    and SURVEY.md §8(d)'s ragged form: --set-utterances x U[5, 30] s with
+    natural-length budgets through the same queue (`ragged`)."""
     import concurrent.futures as cf
     import threading
 
@@ -610,25 +647,99 @@ def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
     qd.run_queue(stream, warm, rank, world, args.tok_rate, dist, dev, key="utt_set_warm")
     stats.clear()
     res = qd.run_queue(stream, utts, rank, world, args.tok_rate, dist, dev, key="utt_set_timed")
+    timed = list(stats)
+
+    # the set's rooflines (untimed, one context alone): one staged refill of `slots` clips at the
+    # set's shape through qasr_run_staged, the layer's attention launch probed by the device clock
+    c0 = ctxs[0]
+    c0.set_option("probe_layer", args.probe_layer)
+    c0.set_option("probe_stride", 4)
+    c0.set_probe(4)
+    pr = c0.run_staged(list(range(min(slots, pool))), bud, ignore_eos=True)
+    att = (*c0.get_probe(), *c0.get_probe_device())
+    c0.set_probe(0)
+
+    # SURVEY.md §8(d)'s ragged set through the same queue: U[5, 30] s, natural budgets (3.5 tok/s of
+    # each utterance's own length), a pool of distinct seeded ragged clips (utterance i = clip i mod pool)
+    rpool = min(2 * args.set_pool, n_utt)
+    rl = [n for _, n in qd.utterance_set(rpool, args.utt_seed + 1, 5.0, secs)]
+    rutts = [(60000 + i, rl[i % rpool]) for i in range(n_utt)]
+    with cf.ThreadPoolExecutor(16) as ex:
+        rpcm = list(ex.map(lambda i: qasr.synth_pcm(60000 + i, rl[i]), range(rpool)))
+    for c in ctxs:
+        c.stage_audio(rpcm)
+    stats.clear()
+    qd.run_queue(stream, rutts[:min(n_utt, 2 * slots * nctx * world)], rank, world, args.tok_rate, dist, dev,
+                 key="utt_set_rwarm")
+    stats.clear()
+    rres = qd.run_queue(stream, rutts, rank, world, args.tok_rate, dist, dev, key="utt_set_rtimed")
+    rstats = list(stats)
     for c in ctxs:
         c.close()
     if rank != 0:
         return {}
     toks = res["tokens"]
     assert len(toks) == n_utt and all(len(t) == bud for t in toks.values()), "utterance set: a budget was not met"
+    rtoks = rres["tokens"]
+    assert len(rtoks) == n_utt and all(len(rtoks[i]) == qd.budget(rutts[i][1], args.tok_rate) for i in range(n_utt)), \
+        "ragged utterance set: a budget was not met"
     walls = res["rank_wall_s"]
-    # the encoder at batch: rank 0's clips' encoder FLOPs over the refills' encoder
-    # device time (HIP events around run_encoder on each context's stream; mel excluded; with several
-    # contexts a span also holds the other contexts' overlapping decode kernels), against the dense
-    # fp16 MFMA peak
-    clips = sum(x.n_clips for x in stats)
-    enc_ms = sum(x.t_encode_ms for x in stats)
-    ef = clips * encoder_flops(m.hp, ns)
-    enc = ({"bound": "mfma", "achieved": round(ef / (enc_ms / 1e3) / 1e12, 1), "peak": MFMA_F16_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(ef / (enc_ms / 1e3) / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
-            "encoder_ms": round(enc_ms, 1), "mel_ms": round(sum(x.t_mel_ms for x in stats), 1), "clips": clips,
-            "contexts": nctx}
-           if enc_ms > 0 else None)
+    hp = m.hp
+
+    # encoder at batch, single context: the probe pass's encoder stage (HIP events around run_encoder)
+    ef = min(slots, pool) * encoder_flops(hp, ns)
+    enc_s = pr.timings.t_encode_ms / 1e3
+    enc = ({"bound": "mfma", "achieved": round(ef / enc_s / 1e12, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ef / enc_s / 1e12 / MFMA_F16_PEAK_TFLOPS, 4), "encoder_ms": round(pr.timings.t_encode_ms, 2),
+            "clips": min(slots, pool), "clock": "hip_events, one context alone (untimed pass)"}
+           if enc_s > 0 else None)
+    # the dominant decode kernel: decode_attn_seq_kernel<1> of layer probe_layer, device clock
+    roof = None
+    if att[4]:
+        avg_s = att[3] / att[4] / 1e3
+        bpl = att[2]
+        traffic, src = pmc_batch_kernel("void qasr::decode_attn_seq_kernel<1>", min(slots, pool))
+        roof = {"kernel": f"decode_attn_seq_kernel<1> (decode batch of {min(slots, pool)}: q/k norm + RoPE + KV write + "
+                          f"MFMA scores + ggml fp16-V chain, one workgroup per kv group and sequence), decoder layer "
+                          f"{args.probe_layer}",
+                "bound": "hbm", "achieved": round(bpl / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(bpl / avg_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
+                "bytes_per_launch": round(bpl), "avg_launch_us": round(avg_s * 1e6, 2), "clock": "device",
+                "launches": att[4], "pass": "untimed, one context alone"}
+    # decode bytes of the timed pass over the contexts' decode time (with the other contexts' refills
+    # running beside each one) and of the probe pass alone
+    db = set_decode_bytes(hp, timed)
+    dsec = sum(st.t_decode_ms for st in timed) / 1e3
+    pb = decode_bytes(hp, False, min(slots, pool), P, bud)
+    ds1 = pr.timings.t_decode_ms / 1e3
+    dh = {"achieved": round(db / dsec / 1e9, 1) if dsec > 0 else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+          "frac": round(db / dsec / 1e9 / HBM_PEAK_GBS, 4) if dsec > 0 else None, "bytes": db,
+          "clock": "host, each context's decode chunks (contexts overlapping)",
+          "single_context": {"achieved": round(pb / ds1 / 1e9, 1) if ds1 > 0 else None,
+                             "frac": round(pb / ds1 / 1e9 / HBM_PEAK_GBS, 4) if ds1 > 0 else None,
+                             "bytes": pb, "decode_ms": round(pr.timings.t_decode_ms, 1)}}
+
+    def streams(ss):
+        return [{"clips": st.n_clips, "refill_prefills": st.n_prefills, "decode_steps": st.n_steps,
+                 "slot_utilisation": round(st.live_steps / max(1, st.slot_steps), 4),
+                 "prefill_ms": round(st.t_prefill_ms, 1), "decode_ms": round(st.t_decode_ms, 1),
+                 "total_ms": round(st.t_total_ms, 1)} for st in ss]
+
+    def tail(w, ss):   # over ranks (N > 1), else over the rank's contexts
+        if len(w) > 1:
+            return round((max(w) - min(w)) / max(w), 4) if max(w) > 0 else 0.0
+        t = [st.t_total_ms for st in ss]
+        return round((max(t) - min(t)) / max(t), 4) if t and max(t) > 0 else 0.0
+    rw = rres["rank_wall_s"]
+    ragged = {"workload": f"{n_utt} x U[5, {secs:g}] s utterances (a pool of {rpool} distinct seeded ragged clips per "
+                          f"GPU, utterance i = clip i mod pool), natural budgets ceil(3.5 tok/s x length), EOS "
+                          f"ignored, the same queue and contexts",
+              "value": round(rres["audio_s"] / rres["wall_s"], 3), "unit": "audio-sec/wall-sec",
+              "audio_s": round(rres["audio_s"], 1), "wall_s": round(rres["wall_s"], 4),
+              "decode_tokens_per_s": round(rres["decode_tokens"] / rres["wall_s"], 2),
+              "slot_utilisation": round(sum(st.live_steps for st in rstats) / max(1, sum(st.slot_steps for st in rstats)), 4),
+              "tail_imbalance": tail(rw, rstats), "per_rank_wall_s": [round(w, 4) for w in rw],
+              "rank0_stream": streams(rstats)}
     return {
         "workload": f"configs[3]: {n_utt} x {secs:g} s utterances (16 kHz, a pool of {pool} distinct seeded clips per "
                     f"GPU), one shared longest-first queue feeding {nctx} concurrent continuous-batching context(s) of "
@@ -640,11 +751,12 @@ def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
         "decode_tokens_per_s": round(res["decode_tokens"] / res["wall_s"], 2),
         "per_rank_wall_s": [round(w, 4) for w in walls],
         "per_rank_utterances": [int(u) for u in res["rank_utterances"]],
-        "tail_imbalance": round((max(walls) - min(walls)) / max(walls), 4) if max(walls) > 0 else 0.0,
-        "rank0_stream": [{"clips": st.n_clips, "refill_prefills": st.n_prefills, "decode_steps": st.n_steps,
-                          "slot_utilisation": round(st.live_steps / max(1, st.slot_steps), 4),
-                          "prefill_ms": round(st.t_prefill_ms, 1), "decode_ms": round(st.t_decode_ms, 1)} for st in stats],
+        "tail_imbalance": tail(walls, timed),
+        "rank0_stream": streams(timed),
+        "roofline": roof,
+        "decode_hbm": dh,
         "encoder_roofline": enc,
+        "ragged": ragged,
         "collectives": "barrier + max wall time + all_gather of per-rank times and token ids (RCCL); the queue is a "
                        "TCPStore counter (one add per utterance)",
     }

@@ -213,6 +213,9 @@ typedef struct {
     double t_prefill_ms, t_decode_ms, t_total_ms;  /* host wall time: refills, decode chunks, call */
     double t_mel_ms, t_encode_ms;           /* device time (HIP events) of the refills' mel / encoder stages,
                                                parts of t_prefill_ms */
+    int64_t kv_keys;                        /* sum over decode steps and slots of the keys each slot's attention
+                                               read (n_kv): the steps' K / V cache bytes = kv_keys x layers x
+                                               n_kv_heads x 128 x 2 B x 2 */
 } qasr_stream_stats;
 int qasr_run_stream(qasr_ctx *c, int slots, qasr_fetch_fn fetch, qasr_sink_fn sink, void *user, int max_tokens, int ignore_eos,
                     qasr_stream_stats *stats);
@@ -278,12 +281,15 @@ int qasr_profile_report(qasr_ctx *c, char *out, int cap);
  * layer's FFN (batch 1: ffn1_kernel).  The rest of each step replays as two
  * graphs around it (one extra graph launch per step); 0 disables.  Setting a
  * probe resets the totals; bytes_per_launch = mean algorithmic HBM bytes of
- * the probed launches (weights + the layer's K/V rows at each step's n_kv). */
+ * the probed launches (weights + the layer's K/V rows at each step's n_kv).
+ * 4 = at decode batches (9..128 rows) that layer's attention launch alone
+ * (decode_attn_seq_kernel: K / V^T rows + q / output rows), by the device
+ * clock (qasr_get_probe_device). */
 int qasr_set_probe(qasr_ctx *c, int kernel);
 int qasr_get_probe(qasr_ctx *c, double *total_ms, int64_t *launches, double *bytes_per_launch);
 /* The same launches timed by the device clock (first workgroup start -> last
  * workgroup end, 100 MHz s_memrealtime, folded in-kernel by the batch <= 8
- * decode kernels): the kernels' own duration, without the ~2.5 us of dispatch
+ * decode kernels and the decode-batch attention): the kernels' own duration, without the ~2.5 us of dispatch
  * and event processing an event pair around one launch includes. */
 int qasr_get_probe_device(qasr_ctx *c, double *total_ms, int64_t *launches);
 

@@ -185,7 +185,7 @@ struct qasr_ctx {
     // decode graphs, one set per attention split-grid bucket (the grid must
     // cover the longest sequence's context: it grows by 64 keys per split)
     struct StepGraphs { hipGraphExec_t full = nullptr, pre = nullptr, post = nullptr; };
-    std::map<int, StepGraphs> graphs;
+    std::map<int, StepGraphs> graphs;   // key: batch * 65536 + split bucket
     int graph_B = -1;
     bool graph_logits = false;
     int graph_base = 0;            // max prompt length of the current run: step k feeds position base + k
@@ -237,6 +237,9 @@ static const std::vector<FuseOption> &fuse_options() {
         {"lmh", "QASR_LMH", &FuseCfg::lmh},
         {"fx_seq", "QASR_FX_SEQ", &FuseCfg::fx_seq},
         {"skinny_inf", "QASR_SKINNY_INF", &FuseCfg::skinny_inf},
+        {"skinny_wdef", "QASR_SKINNY_WDEF", &FuseCfg::skinny_wdef},
+        {"refill_group", "QASR_REFILL_GROUP", &FuseCfg::refill_group},
+        {"live_prefix", "QASR_LIVE_PREFIX", &FuseCfg::live_prefix},
         {"staged_wrap", "QASR_STAGED_WRAP", &FuseCfg::staged_wrap},
         {"poison_scratch", "QASR_POISON_SCRATCH", &FuseCfg::poison},
     };
@@ -1243,6 +1246,7 @@ static int run_prefill(qasr_ctx *c, const std::vector<int32_t> &ids, const std::
 static void dec_gemm(qasr_ctx *c, int epi, GemmArgs g, hipStream_t s) {
     g.no_skinny = !c->fuse.skinny;
     g.skinny_inflight = c->fuse.skinny_inf;
+    g.wdef = c->fuse.skinny_wdef;
     if (launch_gemm_skinny(epi, g, s)) return;
     launch_gemm(AM_DENSE, epi, g, s);
 }
@@ -1474,9 +1478,14 @@ static int decode_step_kernels(qasr_ctx *c, int B, bool want_logits, StepRange r
 //       fused qkv_attn1_kernel, the dominant kernel of the headline decode
 //   3 = layer probe_layer's o-projection (if separate) + FFN: at batch 1 the
 //       fused ffn1_kernel
+//   4 = decode batches (9..128 rows): layer probe_layer's attention launch
+//       alone (decode_attn_seq_kernel: the only launch of group 2's set that
+//       records device stamps at these batches; its bytes are the K / V^T rows
+//       of every sequence plus its q / output rows -- the utterance set's
+//       dominant decode kernel, bench.py utterance_set.roofline)
 static int probe_group(const qasr_ctx *c) {
     const int nl = step_layers(c), pl = std::min(c->probe_layer, nl - 1);
-    return c->probe == 1 ? 1 + 2 * nl : c->probe == 2 ? 1 + 2 * pl : 2 + 2 * pl;
+    return c->probe == 1 ? 1 + 2 * nl : (c->probe == 2 || c->probe == 4) ? 1 + 2 * pl : 2 + 2 * pl;
 }
 
 // algorithmic HBM bytes of one launch of the probed group at decode step k
@@ -1487,6 +1496,11 @@ static double probe_bytes(const qasr_ctx *c, int B, int k) {
     const double H = hp.hidden, QD = hp.n_head * 128.0, KD = hp.n_kv_head * 128.0, F = hp.dec_ffn;
     const double wb = c->m->q8 ? 34.0 / 32.0 : 2.0;   // bytes per linear weight (Q8_0 block: 34 B / 32)
     if (c->probe == 1) return (double)hp.vocab * H * 2 + B * H * 4 + B * 8.0;
+    if (c->probe == 4) {   // the attention launch: K and V^T rows (fp16) + q / k / v rows (fp32) in + output (fp16) out
+        double kv = 0;
+        for (int b = 0; b < B; b++) kv += (double)(c->run_P[b] + k + 1) * KD * 2 * 2;
+        return kv + B * (QD + 2 * KD) * 4 + B * QD * 2;
+    }
     if (c->probe == 2) {
         double kv = 0;
         for (int b = 0; b < B; b++) kv += (double)(c->run_P[b] + k + 1) * KD * 2 * 2;
@@ -1520,7 +1534,8 @@ static int split_bucket(qasr_ctx *c, int pos) {
 // prepare decode graphs for batch B; base = longest prompt (step k feeds base + k)
 static int decode_graph(qasr_ctx *c, int B, bool want_logits, int base) {
     const int pg = c->probe ? probe_group(c) : -1;
-    if (c->graph_B != B || c->graph_logits != want_logits || c->graph_probe_group != pg) c->drop_graphs();
+    // (graphs are kept per (batch, split bucket): a stream's decode chunks switch between live-prefix batches)
+    if (c->graph_logits != want_logits || c->graph_probe_group != pg) c->drop_graphs();
     c->graph_B = B;
     c->graph_logits = want_logits;
     c->graph_base = base;
@@ -1529,8 +1544,8 @@ static int decode_graph(qasr_ctx *c, int B, bool want_logits, int base) {
 }
 
 static int step_graphs(qasr_ctx *c, int splits, qasr_ctx::StepGraphs **out) {
-    auto &gs = c->graphs[splits];
     const int B = c->graph_B;
+    auto &gs = c->graphs[B * 65536 + splits];
     int rc;
     if (!gs.full && (rc = capture(c, B, c->graph_logits, kWholeStep, splits, &gs.full))) return rc;
     if (c->probe && !gs.pre) {
@@ -1615,7 +1630,7 @@ static int probe_collect(qasr_ctx *c, int B, int nsteps) {
 }
 
 extern "C" int qasr_set_probe(qasr_ctx *c, int kernel) {
-    if (!c || kernel < 0 || kernel > 3) return fail(QASR_ERR_ARG, "bad probe id");
+    if (!c || kernel < 0 || kernel > 4) return fail(QASR_ERR_ARG, "bad probe id");
     c->probe = kernel;
     c->probe_ms = 0.0;
     c->probe_n = 0;
@@ -2181,11 +2196,14 @@ static int run_stream(qasr_ctx *c, int slots, const std::function<bool(StreamCli
     };
     // fill free slots from the queue until every slot holds a live clip or the queue is empty
     auto refill = [&]() -> int {
+        bool refilled = false;
         for (;;) {
             std::vector<int> freeS;
             for (int i = 0; i < S; i++)
                 if (sl[i].id < 0) freeS.push_back(i);
             if (freeS.empty() || !open) return 0;
+            if (refilled && c->fuse.refill_group > 0) return 0;   // one group a refill: decode steps come between groups
+            if (c->fuse.refill_group > 0 && (int)freeS.size() > c->fuse.refill_group) freeS.resize(c->fuse.refill_group);
             const auto t0 = std::chrono::steady_clock::now();
             std::vector<int> ids, ns, budgets, slots;
             std::vector<float> pcm;   // host clips of this refill, packed (-> c->spcm)
@@ -2242,6 +2260,7 @@ static int run_stream(qasr_ctx *c, int slots, const std::function<bool(StreamCli
             HIPCHK(hipMemcpyAsync(first.data(), c->d_tok, R * 4, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));   // (pcm host vector in flight until here)
             if ((rc = check_dev_err(c))) return rc;
+            refilled = true;
             st.n_prefills++;
             st.t_prefill_ms += ms_since(t0);
             float mel_ms = 0.f, enc_ms = 0.f;
@@ -2265,11 +2284,12 @@ static int run_stream(qasr_ctx *c, int slots, const std::function<bool(StreamCli
     if ((rc = decode_graph(c, S, false, 0))) return rc;
     for (;;) {
         if ((rc = refill())) return rc;
-        int live = 0, chunk = c->tok_cb ? 1 : 8, maxpos = 0;
+        int live = 0, chunk = c->tok_cb ? 1 : 8, maxpos = 0, hi = 0;
         for (int i = 0; i < S; i++) {
             const StreamSlot &x = sl[i];
             if (x.id < 0) { pos[i] = 0; nkv[i] = 1; tok[i] = 0; continue; }   // parked
             live++;
+            hi = i + 1;
             pos[i] = x.P + (int)x.toks.size() - 1;   // the last token is fed at this position
             nkv[i] = pos[i] + 1;
             tok[i] = x.toks.back();
@@ -2277,6 +2297,11 @@ static int run_stream(qasr_ctx *c, int slots, const std::function<bool(StreamCli
             maxpos = std::max(maxpos, pos[i]);
         }
         if (live == 0) break;
+        // option live_prefix: decode only the slots up to the last live one (rounded up to 16 rows, at least
+        // 16 -- the batch kernels' shapes), so a context filling in refill groups or draining at the end of the
+        // queue does not run every step at full width; the slots past it are parked and untouched
+        const int Bq = c->fuse.live_prefix && S > 8 ? std::min(S, std::max(16, (hi + 15) / 16 * 16)) : S;
+        if ((rc = decode_graph(c, Bq, false, 0))) return rc;
         HIPCHK(hipMemcpyAsync(c->d_pos, pos.data(), S * 4, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->d_nkv, nkv.data(), S * 4, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->d_tok, tok.data(), S * 4, hipMemcpyHostToDevice, s));
@@ -2285,7 +2310,7 @@ static int run_stream(qasr_ctx *c, int slots, const std::function<bool(StreamCli
         for (int k = 0; k < chunk; k++) {
             const int splits = split_bucket(c, maxpos + k);
             if (c->eager) {
-                if ((rc = decode_step_kernels(c, S, false, kWholeStep, splits))) return rc;
+                if ((rc = decode_step_kernels(c, Bq, false, kWholeStep, splits))) return rc;
             } else {
                 qasr_ctx::StepGraphs *gs = nullptr;
                 if ((rc = step_graphs(c, splits, &gs))) return rc;
@@ -2300,6 +2325,7 @@ static int run_stream(qasr_ctx *c, int slots, const std::function<bool(StreamCli
         st.t_decode_ms += ms_since(t0);
         st.n_steps += chunk;
         st.slot_steps += (int64_t)S * chunk;
+        for (int i = 0; i < S; i++) st.kv_keys += (int64_t)nkv[i] * chunk + (int64_t)chunk * (chunk - 1) / 2;   // step k: n_kv + k
         for (int i = 0; i < S; i++) {
             StreamSlot &x = sl[i];
             if (x.id < 0) continue;

@@ -55,7 +55,7 @@ class StreamStats(C.Structure):
     _fields_ = [("n_clips", C.c_int32), ("n_errors", C.c_int32), ("n_prefills", C.c_int32), ("n_steps", C.c_int64),
                 ("slot_steps", C.c_int64), ("live_steps", C.c_int64), ("t_prefill_ms", C.c_double),
                 ("t_decode_ms", C.c_double), ("t_total_ms", C.c_double), ("t_mel_ms", C.c_double),
-                ("t_encode_ms", C.c_double)]
+                ("t_encode_ms", C.c_double), ("kv_keys", C.c_int64)]
 
 
 _lib = None

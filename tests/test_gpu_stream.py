@@ -60,6 +60,46 @@ def test_stream_ragged_budgets_equal_single(tiny_model, slots):
     assert st.slot_steps < static or slots == 1
 
 
+def test_stream_refill_groups_equal_single(tiny_model):
+    """option refill_group: at most g clips a refill, decode
+    steps between the groups -- a different schedule, the same tokens per clip"""
+    lens = [SR, 2 * SR + 333, 4 * SR, SR // 2, 3 * SR, 5 * SR + 7, SR + 999, 2 * SR]
+    budgets = [3, 9, 5, 16, 1, 7, 12, 10]
+    clips = [qasr.synth_pcm(7150 + i, n) for i, n in enumerate(lens)]
+    c = qasr.Context(tiny_model, max_batch=5, max_ctx=640)
+    try:
+        c.set_option("refill_group", 2)
+        out, st = c.run_stream(_queue([(30 + i, p, b) for i, (p, b) in enumerate(zip(clips, budgets))]), max_tokens=32,
+                               ignore_eos=True)
+    finally:
+        c.close()
+    for i, (p, b) in enumerate(zip(clips, budgets)):
+        assert out[30 + i] == _single(tiny_model, p, b, True), i
+    assert st.n_clips == len(clips) and st.n_prefills >= 4   # groups of at most 2
+
+
+def test_stream_live_prefix_batches_equal_single(tiny_model):
+    """option live_prefix: decode chunks run over the slots up to the last live
+    one (16-row granules) -- with refill groups of 5 into 40 slots the chunks
+    switch between 16-, 32- and 40-row batches; every clip's tokens equal its
+    one-clip run"""
+    n = 23
+    lens = [SR // 2 + 2311 * i for i in range(n)]
+    budgets = [2 + (7 * i) % 13 for i in range(n)]
+    clips = [qasr.synth_pcm(7170 + i, m) for i, m in enumerate(lens)]
+    c = qasr.Context(tiny_model, max_batch=40, max_ctx=640)
+    try:
+        c.set_option("refill_group", 5)
+        c.set_option("live_prefix", 1)
+        out, st = c.run_stream(_queue([(50 + i, p, b) for i, (p, b) in enumerate(zip(clips, budgets))]), max_tokens=32,
+                               ignore_eos=True)
+    finally:
+        c.close()
+    for i, (p, b) in enumerate(zip(clips, budgets)):
+        assert out[50 + i] == _single(tiny_model, p, b, True), i
+    assert st.n_clips == n and st.n_prefills >= 5
+
+
 def test_stream_natural_eos_and_per_clip_errors(tiny_model):
     good = [qasr.synth_pcm(7200 + i, n) for i, n in enumerate([SR, 3 * SR, 2 * SR])]
     items = [(0, good[0], 8), (1, qasr.synth_pcm(7300, 100), 8), (2, good[1], 8), (3, qasr.synth_pcm(7301, SR), 10000),
