@@ -86,31 +86,37 @@ __device__ __forceinline__ void fx_weights(const float *src, float *sc, float *m
     for (int i = 0; i < KPL; i++) lm = fmaxf(lm, v[i]);
     const float inc = wave_scan_max(lm);   // inclusive prefix maximum over the lanes
     float Mp = fmaxf(M, dpp_ninf<0x138, 0xF>(inc));   // wave_shr:1 -> the exclusive prefix (lane 0: -inf)
+    const float Mn = fmaxf(M, lane_f(inc, 63));
+    // one expf a key, branch-free (a new maximum: ms = expf(Mold - M), 0 before the first key,
+    // vs = 1; any other key: vs = expf(s - M)); round 6: the per-key if / else compiled to divergent
+    // blocks around each expf (tools/micro/px_bench PMC: 2.5x the chain's VALU instructions)
     bool nm = false;
+    float t[KPL];   // this chunk's S terms expf(s - Mn)
 #pragma unroll
     for (int i = 0; i < KPL; i++) {
         const int j = lane * KPL + i;
         const float s = v[i];
-        float m1 = 1.0f, w = 0.0f;
-        if (s > Mp) {   // new maximum: ms = expf(Mold - M) (0 before the first key), vs = 1
-            m1 = expf(Mp - s);
-            w = 1.0f;
-            Mp = s;
-            nm = true;
-        } else if (s != -INFINITY) {
-            w = expf(s - Mp);
-        }
+        const bool gt = s > Mp;
+        const float e = expf(gt ? Mp - s : s - Mp);
+        const float m1 = gt ? e : 1.0f, w = gt ? 1.0f : (s != -INFINITY ? e : 0.0f);
+        Mp = fmaxf(Mp, s);
+        nm = nm || gt;
         if (j < n) {
             sc[j] = w;
             ms[j] = m1;
         }
+        // where the running maximum after this key is already the chunk's, expf(s - Mn) is the weight
+        // just computed (the same operands: w, or 1 = expf(0) at the maximum itself); the others
+        // (keys before a later new maximum, mostly the first chunks of a row) take their own expf
+        t[i] = s == -INFINITY ? 0.0f : w;
+        if (Mp != Mn && s != -INFINITY) t[i] = expf(s - Mn);
     }
-    const float Mn = fmaxf(M, lane_f(inc, 63));
     float ps = 0.0f;
 #pragma unroll
-    for (int i = 0; i < KPL; i++) ps += v[i] == -INFINITY ? 0.0f : expf(v[i] - Mn);
+    for (int i = 0; i < KPL; i++) ps += t[i];
     ps = wave_sum(ps);
-    S = (M == -INFINITY ? 0.0f : S * expf(M - Mn)) + ps;
+    // (S * expf(0) = S exactly: no rescale when the chunk held no new maximum)
+    S = (M == -INFINITY ? 0.0f : M == Mn ? S : S * expf(M - Mn)) + ps;
     M = Mn;
     constexpr int LPB = FX_B / KPL;   // lanes per batch
     const unsigned long long bal = __ballot(nm);

@@ -565,141 +565,6 @@ static void skinny_mt(const GemmArgs &g, hipStream_t s) {
 }
 
 
-// ------------------------------------------------------------ RMS norm fold
-// Decode batches (9..128 rows), f16 weights, K = 1024: the layer's RMS norm
-// (ggml_rms_norm + ggml_mul, src/text_decoder.cpp:480-485 / :542-545) in the
-// GEMM's prologue instead of a launch of its own.  The workgroup's 16 MT rows
-// of x (fp32) are normalised with rms_row's arithmetic (the values
-// launch_rmsnorm_f16 writes) and rounded to fp16 straight into an LDS image
-// (row r's 16-B chunk ch at ch ^ (r & 15), lmhead.hip's layout, so the 16
-// rows of a fragment read hit distinct banks); wave w then multiplies K chunk
-// w of that image against its weight fragments (requested at entry, before
-// the prologue) in gemm_skinny_kernel<MT, NT, 8, EPI, 4, 1>'s order -- the
-// same fragments, accumulation order and wave-order reduction, so the outputs
-// are bit-identical to the two launches.  The rows come from L2 as fp32 (twice
-// the fp16 copy's bytes per block), which costs less than the norm launch and
-// its kernel boundary (tools/skinny_bench.hip).
-template <int MT, int NT, int EPI, int WDEF>
-__global__ __launch_bounds__(512) void gemm_skinny_norm_kernel(GemmArgs g) {
-    constexpr int KW = 8, NTILE = MT * NT, ROWS = MT * 16, KN = 1024;
-    constexpr int IMG_B = ROWS * KN * 2, RED_B = KW * NTILE * 64 * 16;
-    static_assert((IMG_B > RED_B ? IMG_B : RED_B) + 512 <= 160 * 1024, "LDS per workgroup");
-    __shared__ __attribute__((aligned(16))) unsigned char lds_raw[IMG_B > RED_B ? IMG_B : RED_B];
-    uint16_t *xs = reinterpret_cast<uint16_t *>(lds_raw);
-    floatx4 (*red)[NTILE][64] = reinterpret_cast<floatx4 (*)[NTILE][64]>(lds_raw);
-    __shared__ unsigned long long rmax[64];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int n0 = blockIdx.x * 16 * NT, m0 = blockIdx.y * ROWS;
-    const int M = g.M;
-    const int q = lane >> 4, c16 = lane & 15;
-    auto img = [&](int row, int k) { return row * KN + ((((k >> 3) ^ (row & 15))) << 3) + (k & 7); };
-
-    // this wave's weight fragments (K chunk wid), requested first: they land under the prologue
-    u32x4 wq[NT][4];
-#pragma unroll
-    for (int t = 0; t < NT; t++) {
-        const u32x4 *wr = (const u32x4 *)(g.W + (long)(n0 + t * 16 + c16) * g.ldw + q * 8) + wid * 16;
-#pragma unroll
-        for (int s4 = 0; s4 < 4; s4++) wq[t][s4] = WDEF ? wr[4 * s4] : __builtin_nontemporal_load(wr + 4 * s4);
-    }
-    SkinnyEpi<MT, NT, KW, EPI> epi;
-    epi.prefetch(g, m0, n0, tid);
-
-    // prologue: wave wid normalises rows wid + 8 r, RB at a time (all of a batch's loads in flight)
-    constexpr int R = ROWS / KW, RB = R % 4 == 0 ? 4 : R % 3 == 0 ? 3 : R % 2 == 0 ? 2 : 1;
-    float4 nw[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) nw[i] = *(const float4 *)(g.norm_w + 4 * lane + 256 * i);
-#pragma unroll
-    for (int r0 = 0; r0 < R; r0 += RB) {
-        float4 v[RB][4];
-#pragma unroll
-        for (int r = 0; r < RB; r++) {
-            const int m = m0 + wid + KW * (r0 + r);
-            const float *xr = g.xn + (long)(m < M ? m : 0) * g.ldxn;
-#pragma unroll
-            for (int i = 0; i < 4; i++) v[r][i] = *(const float4 *)(xr + 4 * lane + 256 * i);
-        }
-#pragma unroll
-        for (int r = 0; r < RB; r++) {   // rms_row<1024>'s arithmetic
-            const int rl = wid + KW * (r0 + r);
-            double sd = 0.0;
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                sd += ((double)fmul_rn(v[r][i].x, v[r][i].x) + (double)fmul_rn(v[r][i].y, v[r][i].y)) +
-                      ((double)fmul_rn(v[r][i].z, v[r][i].z) + (double)fmul_rn(v[r][i].w, v[r][i].w));
-            sd = wave_sum_d(sd);
-            const float mean = (float)(sd / KN);
-            const float scale = 1.0f / sqrtf(mean + g.eps);
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                uint32_t lo = f_to_u16(fmul_rn(fmul_rn(v[r][i].x, scale), nw[i].x)) |
-                              ((uint32_t)f_to_u16(fmul_rn(fmul_rn(v[r][i].y, scale), nw[i].y)) << 16);
-                uint32_t hi = f_to_u16(fmul_rn(fmul_rn(v[r][i].z, scale), nw[i].z)) |
-                              ((uint32_t)f_to_u16(fmul_rn(fmul_rn(v[r][i].w, scale), nw[i].w)) << 16);
-                if (m0 + rl >= M) lo = hi = 0u;   // rows past M: zeros (the LDS-DMA path's zero line)
-                *(uint2 *)(xs + img(rl, 4 * lane + 256 * i)) = make_uint2(lo, hi);
-            }
-        }
-    }
-    __syncthreads();
-
-    floatx4 acc[MT][NT];
-#pragma unroll
-    for (int i = 0; i < MT; i++)
-#pragma unroll
-        for (int j = 0; j < NT; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s4 = 0; s4 < 4; s4++)
-#pragma unroll
-        for (int i = 0; i < MT; i++) {
-            const half8 a8 = *(const half8 *)(xs + img(i * 16 + c16, wid * 128 + 32 * s4 + 8 * q));
-#pragma unroll
-            for (int j = 0; j < NT; j++)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a8, __builtin_bit_cast(half8, wq[j][s4]), acc[i][j], 0, 0, 0);
-        }
-    __syncthreads();   // every wave's image reads done before the reduction reuses the LDS
-#pragma unroll
-    for (int i = 0; i < MT; i++)
-#pragma unroll
-        for (int j = 0; j < NT; j++) red[wid][i * NT + j][lane] = acc[i][j];
-    __syncthreads();
-    epi.run(g, red, rmax, m0, n0, tid);
-}
-
-template <int MT, int NT, int EPI>
-static void run_skinny_norm(const GemmArgs &g, hipStream_t s) {
-    dim3 grid(g.N / (16 * NT), (g.M + 16 * MT - 1) / (16 * MT));
-    if (g.wdef) hipLaunchKernelGGL((gemm_skinny_norm_kernel<MT, NT, EPI, 1>), grid, dim3(512), 0, s, g);
-    else hipLaunchKernelGGL((gemm_skinny_norm_kernel<MT, NT, EPI, 0>), grid, dim3(512), 0, s, g);
-}
-
-bool launch_gemm_skinny_norm(int epi, const GemmArgs &g, hipStream_t s) {
-    if (g.no_skinny || !g.xn || !g.norm_w || g.M < 9 || g.M > 128 || g.K != 1024 || g.ldxn % 4 != 0 || g.ldw % 8 != 0 ||
-        g.Wq || g.res)
-        return false;
-    const int mt = (g.M + 15) / 16;
-    switch (epi) {
-        case EPI_F32:
-            if (g.N % 32 != 0) return false;
-            // the tilings of launch_gemm_skinny for K = 1024 at these rows (QKV: one K chunk a wave)
-            if (g.M > 64) run_skinny_norm<4, 2, EPI_F32>(g, s);
-            else if (mt <= 1) run_skinny_norm<1, 1, EPI_F32>(g, s);
-            else if (mt <= 2) run_skinny_norm<2, 1, EPI_F32>(g, s);
-            else if (mt <= 3) run_skinny_norm<3, 1, EPI_F32>(g, s);
-            else run_skinny_norm<4, 1, EPI_F32>(g, s);
-            return true;
-        case EPI_SWIGLU_F16:
-            if (g.N % 64 != 0) return false;
-            if (g.M > 64) run_skinny_norm<4, 4, EPI_SWIGLU_F16>(g, s);
-            else if (g.M > 32) run_skinny_norm<4, 2, EPI_SWIGLU_F16>(g, s);
-            else run_skinny_norm<2, 2, EPI_SWIGLU_F16>(g, s);
-            return true;
-        default:
-            return false;
-    }
-}
-
 bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s) {
     const bool off = g.no_skinny != 0;
     if (off || g.M <= 0 || g.M > 128 || g.K % 128 != 0 || g.lda % 8 != 0 || g.ldw % 8 != 0) return false;

@@ -84,9 +84,6 @@ struct GemmArgs {
     int no_skinny;                        // 1: launch_gemm_skinny / _q8 decline (per-context option skinny = 0)
     int skinny_inflight;                  // skinny GEMMs: every K chunk of a wave requested at entry (FuseCfg::skinny_inf)
     int8_t *out_q; float *out_d; int ldoq;   // EPI_SWIGLU_Q8: int8 [M][ldoq], fp32 block scales [M][ldoq / 32]
-    // launch_gemm_skinny_norm: A = fp16(rms_norm(xn) * norm_w) computed in the prologue from the
-    // fp32 rows xn [M][ldxn] (K = 1024; the values launch_rmsnorm_f16 writes)
-    const float *xn; int ldxn; const float *norm_w; float eps;
     int wdef;                             // skinny GEMMs: weights with the default cache policy (1) or nontemporal (0)
 };
 void launch_gemm(int amode, int epi, const GemmArgs &g, hipStream_t s);
@@ -98,10 +95,6 @@ bool take_declined(std::string *msg);
 // decode-batch GEMM (gemm_skinny.hip): dense A, M <= 128, K % 128 == 0; returns
 // false (nothing launched) for shapes it does not take, or when g.no_skinny.
 bool launch_gemm_skinny(int epi, const GemmArgs &g, hipStream_t s);
-// the same with the layer's RMS norm folded into the prologue (g.xn, g.norm_w,
-// g.eps; f16 weights, K == 1024, 9..128 rows, EPI_F32 / EPI_SWIGLU_F16): one
-// launch instead of launch_rmsnorm_f16 + launch_gemm_skinny, the same bits
-bool launch_gemm_skinny_norm(int epi, const GemmArgs &g, hipStream_t s);
 // the same for Q8_0 weights (Aq/Ad quantised activations, Wq/Wd): EPI_F32, EPI_SWIGLU_F32, EPI_SWIGLU_Q8
 bool launch_gemm_skinny_q8(int epi, const GemmArgs &g, hipStream_t s);
 // ggml_mul_mat with Q8_0 weights: exact int8 block dots (v_mfma_i32_16x16x32_i8
