@@ -80,9 +80,10 @@ def parse():
     ap.add_argument("--set-seconds", type=float, default=30.0)
     ap.add_argument("--set-pool", type=int, default=128, help="distinct seeded clips staged per GPU (utterance i = clip i mod pool)")
     ap.add_argument("--set-slots", type=int, default=128, help="continuous-batching slots per context")
-    ap.add_argument("--set-contexts", type=int, default=2,
+    ap.add_argument("--set-contexts", type=int, default=0,
                     help="continuous-batching contexts per GPU, each on its own HIP stream and host thread, all fed by "
-                         "the rank's queue (one context's refill prefill overlaps another's decode steps)")
+                         "the rank's queue (one context's refill prefill overlaps another's decode steps); 0 = by the "
+                         "rank's share of the set (set_contexts)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous check without a GPU: ranks join a gloo group, time a barrier and rank 0 "
                          "prints the JSON line with value 0 (tests/test_dist.py)")
@@ -575,6 +576,19 @@ def set_decode_bytes(hp, stats) -> float:
     return float(sum(st.n_steps * w + st.kv_keys * kv_row for st in stats))
 
 
+def set_contexts(share: int, slots: int = 128) -> int:
+    """Contexts per GPU for a rank's share of the utterance set (round 6,
+    tools/r6/set_run.py on one MI355X, RTFx; profiles/r6/set_contexts.txt):
+    125 utterances (N = 8) 1 x 125 slots 7849, 2 x 63 7603, 3 x 42 7369 --
+    every context's decode step costs about a full-width step, so splitting a
+    small share only adds steps (asymmetric splits 32 + 93 etc.: 7295-7546);
+    250: 2 x 125 8721, 3 x 84 8343; 500: 2 x 128 8688, 3 x 128 8736; 1000:
+    2 x 128 8678-8814, 3 x 128 8851-9097 alone but 8733 vs 8788 in the bench
+    line (ragged 9152 vs 8984): two, which also leaves a hardware queue for
+    RCCL's stream beside the default one (GPU_MAX_HW_QUEUES = 4)."""
+    return 1 if share <= slots else 2
+
+
 def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
     """configs[3] inside the default run (1000 x 30 s f16
     utterances; north_star's "throughput on synthetic 30 s / 16 kHz audio at
@@ -609,7 +623,7 @@ def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
     utts = [(50000 + i, ns) for i in range(n_utt)]
     bud = qd.budget(ns, args.tok_rate)
     P = qasr.lib().qasr_prompt_len(qasr.encoder_frames(qasr.mel_frames(ns)))
-    nctx = max(1, args.set_contexts)
+    nctx = args.set_contexts if args.set_contexts > 0 else set_contexts(-(-n_utt // world), args.set_slots)
     # slots per context: --set-slots, or fewer when the rank's share of the set cannot fill them
     # (strong scaling: 1000 utterances over 8 ranks x 2 contexts is ~63 a context; parked slots
     # would still cost a decode step its full-batch GEMMs)
@@ -778,6 +792,10 @@ def main():
         return
     dist = None
     if world > 1:
+        # torch ships its own HIP / HSA runtimes (torch/lib): they must initialise before libqasr.so loads,
+        # which then binds to torch's libamdhip64.so.7 by soname -- loaded the other way round, two HSA
+        # runtimes share the process and the second finds no device (tools/r6/set_run.py RCCL=1)
+        assert qasr._lib is None, "libqasr.so loaded before torch's HIP runtime"
         import torch
         import torch.distributed as dist_mod
         torch.cuda.set_device(local)
@@ -861,6 +879,11 @@ def main():
             extra[kind] = (*ctx.get_probe(), *ctx.get_probe_device())
         ctx.set_probe(0)
     assert all(len(x) == ntok for x in res.tokens), "decode budget not met"
+    attn_path = ctx.get_option("attn_path")
+    # the configs[1] context's HIP stream goes before the utterance set's contexts take theirs: the set
+    # contexts + the default stream (+ RCCL's at N > 1) share the box's four hardware queues
+    # (GPU_MAX_HW_QUEUES); with it open, three set contexts gave 8590 RTFx against 8768 for two
+    ctx.close()
     uset = utterance_set_leg(args, m, rank, local, world, dist) if args.set_utterances > 0 and not actx else None
     if rank != 0:
         if dist is not None:
@@ -890,7 +913,7 @@ def main():
                    "clip_seconds": args.seconds, "decode_tokens": ntok, "parallelism": f"dp{N} (utterance sharding)"},
         "decode_tokens_per_s": round(N * args.batch * ntok * args.steps / dt, 2),
         # from the launches the last step actually made (read-only option attn_path)
-        "decode_attention": ATTN_LABEL.get(ctx.get_option("attn_path"), "unknown"),
+        "decode_attention": ATTN_LABEL.get(attn_path, "unknown"),
         "stage_ms_per_step_rank0": {k: round(v / args.steps, 3) for k, v in tm.items()},
     }
     if probe and probe[1]:

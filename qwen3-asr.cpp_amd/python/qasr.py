@@ -70,7 +70,12 @@ SINK_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int32), 
 
 
 def lib() -> C.CDLL:
-    """Load the in-tree libqasr.so (raises if it was not built)."""
+    """Load the in-tree libqasr.so (raises if it was not built).  A process
+    that also uses torch's HIP (torch.distributed over RCCL) initialises that
+    first: torch bundles its own libamdhip64 / libhsa-runtime, which
+    libqasr.so then binds to by soname; loaded before them, two HSA runtimes
+    end up in one process and torch's, initialised second, sees no device
+    (or the other way round)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):

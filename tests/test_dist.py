@@ -262,3 +262,12 @@ def test_bench_gpus_counts_this_node_under_a_multinode_launch():
     assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 4, lines
     bad = launch(4)
     assert all(rc != 0 and "LOCAL_WORLD_SIZE" in e for rc, _, e in bad), [(rc, e[-300:]) for rc, _, e in bad]
+
+
+def test_set_contexts_policy():
+    """bench.set_contexts (round 6, profiles/r6/set_contexts.txt): contexts per
+    GPU by the rank's share of the utterance set -- 1 x 125 at N = 8, two
+    contexts from N = 4 down"""
+    import bench
+    assert [bench.set_contexts(-(-1000 // n)) for n in (1, 2, 4, 8)] == [2, 2, 2, 1]
+    assert bench.set_contexts(128) == 1 and bench.set_contexts(129) == 2 and bench.set_contexts(10000) == 2

@@ -193,3 +193,30 @@ def _check_dumped_alignment(d):
     clear = (srt[:, -1] - srt[:, -2]) > 5e-3 * float(np.abs(olg).max())
     same = np.array(cls) == np.array(ocls)
     assert same[clear].all(), (cls, list(ocls), clear)
+
+
+def test_engine_after_torch_rccl_in_one_process(tmp_path):
+    """bench.py's N > 1 order: torch's HIP runtime and a one-rank RCCL group
+    initialised first, then libqasr.so loads (binding to torch's libamdhip64
+    by soname) and transcribes -- the multi-GPU bench's control path on one
+    GPU.  (The reverse order puts two HSA runtimes in one process.)"""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import os, sys\n"
+        f"sys.path.insert(0, {os.path.join(root, 'qwen3-asr.cpp_amd', 'python')!r})\n"
+        "import torch, torch.distributed as dist\n"
+        "os.environ['MASTER_ADDR'] = '127.0.0.1'; os.environ['MASTER_PORT'] = '29581'\n"
+        "torch.cuda.set_device(0)\n"
+        "dist.init_process_group('nccl', rank=0, world_size=1); dist.barrier()\n"
+        "import qasr\n"
+        f"p = {str(tmp_path / 'tiny.gguf')!r}\n"
+        "qasr.write_synthetic_gguf(p, 'tiny', 42, 1)\n"
+        "m = qasr.Model(p, 0); c = qasr.Context(m, max_batch=1, max_ctx=256)\n"
+        "r = c.transcribe([qasr.synth_pcm(5, 16000)], max_tokens=4, ignore_eos=True)\n"
+        "t = torch.tensor([float(len(r.tokens[0]))], device='cuda:0'); dist.all_reduce(t)\n"
+        "print('ok', int(t.item()))\n"
+        "c.close(); m.close(); dist.destroy_process_group()\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0 and "ok 4" in out.stdout, (out.stdout[-800:], out.stderr[-1500:])

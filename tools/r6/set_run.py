@@ -18,9 +18,22 @@ import bench  # noqa: E402
 import qasr  # noqa: E402
 import qasr_dist as qd  # noqa: E402
 
+# a one-rank RCCL process group, initialised before libqasr.so loads -- bench.py's N > 1 order
+if os.environ.get("RCCL") == "1":
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29571")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    dist.barrier()
+
 N_UTT = int(os.environ.get("N_UTT", "1000"))
 NCTX = int(os.environ.get("CTX", "2"))
-SLOTS = int(os.environ.get("SLOTS", "128"))
+# SLOTS: slots per context, one value or one per context ("32,93": asymmetric contexts)
+SLOTV = [int(x) for x in os.environ.get("SLOTS", "128").split(",")]
+SLOTV = SLOTV * NCTX if len(SLOTV) == 1 else SLOTV
+SLOTS = max(SLOTV)
 SECS = float(os.environ.get("SECS", "30"))
 RAGGED = os.environ.get("RAGGED", "0") == "1"
 REPS = int(os.environ.get("REPS", "1"))
@@ -37,7 +50,7 @@ P = qasr.lib().qasr_prompt_len(qasr.encoder_frames(qasr.mel_frames(nmax)))
 m = qasr.Model(bench.synthetic_model(0))
 with cf.ThreadPoolExecutor(16) as ex:
     pcm = list(ex.map(lambda i: qasr.synth_pcm(50000 + i, lens[i]), range(POOL)))
-ctxs = [qasr.Context(m, max_batch=SLOTS, max_ctx=P + bud_max + 8) for _ in range(NCTX)]
+ctxs = [qasr.Context(m, max_batch=SLOTV[k], max_ctx=P + bud_max + 8) for k in range(NCTX)]
 for c in ctxs:
     c.stage_audio(pcm)
     c.set_option("staged_wrap", 1)
@@ -60,11 +73,11 @@ def run(n_utt):
             nxt[0] += 1
             return i, qd.budget(lens[i % POOL], 3.5)
 
-    def one(c):
-        return c.run_stream_staged(take, bud_max, ignore_eos=True, slots=SLOTS)
+    def one(k):
+        return ctxs[k].run_stream_staged(take, bud_max, ignore_eos=True, slots=SLOTV[k])
     t0 = time.perf_counter()
     with cf.ThreadPoolExecutor(NCTX) as ex:
-        res = list(ex.map(one, ctxs))
+        res = list(ex.map(one, range(NCTX)))
     wall = time.perf_counter() - t0
     n = sum(len(o) for o, _ in res)
     assert n == n_utt, n
@@ -73,10 +86,10 @@ def run(n_utt):
                                  round(st.live_steps / max(1, st.slot_steps), 3)) for _, st in res]
 
 
-run(min(N_UTT, 2 * NCTX * SLOTS))   # warm-up: graphs, buffers
+run(min(N_UTT, 2 * sum(SLOTV)))   # warm-up: graphs, buffers
 for _ in range(REPS):
     v, wall, st = run(N_UTT)
-    print(f"set {N_UTT} x {'U[5,30]' if RAGGED else SECS} s, {NCTX} ctx x {SLOTS} slots, opts {OPTS}: {v:.1f} RTFx  wall {wall:.3f} s  "
+    print(f"set {N_UTT} x {'U[5,30]' if RAGGED else SECS} s, {NCTX} ctx x {SLOTV} slots, opts {OPTS}: {v:.1f} RTFx  wall {wall:.3f} s  "
           f"per ctx (clips, refills, steps, prefill ms, decode ms, slot util) {st}", flush=True)
 for c in ctxs:
     c.close()
