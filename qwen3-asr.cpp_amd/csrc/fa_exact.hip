@@ -28,9 +28,10 @@
 // conversions); the single-value form converts in inline asm.
 //
 // Prefill: one workgroup = 16 query rows of one head (one MFMA column each);
-// keys in chunks of PX_KC: (1) scores on MFMA -> LDS, (2) per row the (ms, vs)
-// weights by wave scans -> LDS, (3) the chain, wave w running rows 2w, 2w + 1
-// with two dimensions per lane, V staged in LDS once for all rows.
+// keys in chunks of PX_KC: (1) scores on MFMA -> LDS, (2) wave w derives the
+// weights of its rows 2w, 2w + 1 (one half-wave a row) -> LDS, (3) wave w
+// runs the chain of those rows with two dimensions per lane, V staged in LDS
+// once for all rows.
 // Decode: launch_decode_attention in scores mode writes the scaled scores;
 // then one workgroup per (query head, sequence): both waves derive the
 // weights, each runs the chain for 64 dimensions, one per lane (the shortest
@@ -61,140 +62,6 @@ __device__ __forceinline__ half2v fx_mad2(half2v acc, uint32_t v, float vs) {
     const float f1 = fmaf((float)vv.y, vs, (float)acc.y);
     return __builtin_convertvector((floatx2){f0, f1}, half2v);
 }
-// ggml_vec_scale_f16: fp16(acc * ms)
-__device__ __forceinline__ half2v fx_scale2(half2v acc, float ms) {
-    return __builtin_convertvector((floatx2){(float)acc.x * ms, (float)acc.y * ms}, half2v);
-}
-// Weights of n keys (n <= KPL * 64) of one row, one wave: src[j] = the scaled
-// score (src may be sc itself), sc[j] = vs_j on return, ms[j] = ms_j (1 where no new
-// maximum; a masked key (-inf) gives vs = 0, ms = 1 -- ggml skips it, and a
-// zero weight leaves the fp16 accumulator unchanged); fl[b * fls] = 1 where
-// batch b (FX_B keys) holds a new maximum.  M: running maximum (in/out);
-// S: rescaled to the new maximum, plus this chunk's sum.
-template <int KPL>
-__device__ __forceinline__ void fx_weights(const float *src, float *sc, float *ms, uint32_t *fl, int fls, int n, float &M,
-                                           float &S) {
-    const int lane = threadIdx.x & 63;
-    float v[KPL];
-    float lm = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < KPL; i++) {   // independent loads (src: LDS, or the scores in global memory)
-        const int j = lane * KPL + i;
-        v[i] = j < n ? src[j] : -INFINITY;
-    }
-#pragma unroll
-    for (int i = 0; i < KPL; i++) lm = fmaxf(lm, v[i]);
-    const float inc = wave_scan_max(lm);   // inclusive prefix maximum over the lanes
-    float Mp = fmaxf(M, dpp_ninf<0x138, 0xF>(inc));   // wave_shr:1 -> the exclusive prefix (lane 0: -inf)
-    const float Mn = fmaxf(M, lane_f(inc, 63));
-    // one expf a key, branch-free (a new maximum: ms = expf(Mold - M), 0 before the first key,
-    // vs = 1; any other key: vs = expf(s - M)); round 6: the per-key if / else compiled to divergent
-    // blocks around each expf (tools/micro/px_bench PMC: 2.5x the chain's VALU instructions)
-    bool nm = false;
-    float t[KPL];   // this chunk's S terms expf(s - Mn)
-#pragma unroll
-    for (int i = 0; i < KPL; i++) {
-        const int j = lane * KPL + i;
-        const float s = v[i];
-        const bool gt = s > Mp;
-        const float e = expf(gt ? Mp - s : s - Mp);
-        const float m1 = gt ? e : 1.0f, w = gt ? 1.0f : (s != -INFINITY ? e : 0.0f);
-        Mp = fmaxf(Mp, s);
-        nm = nm || gt;
-        if (j < n) {
-            sc[j] = w;
-            ms[j] = m1;
-        }
-        // where the running maximum after this key is already the chunk's, expf(s - Mn) is the weight
-        // just computed (the same operands: w, or 1 = expf(0) at the maximum itself); the others
-        // (keys before a later new maximum, mostly the first chunks of a row) take their own expf
-        t[i] = s == -INFINITY ? 0.0f : w;
-        if (Mp != Mn && s != -INFINITY) t[i] = expf(s - Mn);
-    }
-    float ps = 0.0f;
-#pragma unroll
-    for (int i = 0; i < KPL; i++) ps += t[i];
-    ps = wave_sum(ps);
-    // (S * expf(0) = S exactly: no rescale when the chunk held no new maximum)
-    S = (M == -INFINITY ? 0.0f : M == Mn ? S : S * expf(M - Mn)) + ps;
-    M = Mn;
-    constexpr int LPB = FX_B / KPL;   // lanes per batch
-    const unsigned long long bal = __ballot(nm);
-    if (lane % LPB == 0 && lane * KPL < n) {
-        const unsigned long long grp = (bal >> lane) & ((1ull << LPB) - 1ull);
-        fl[(lane / LPB) * fls] = grp != 0ull;
-    }
-}
-
-// One full batch of FX_B keys for R rows, two dimensions per lane: v[i] = the
-// lane's V dword of key j0 + i; row r's weights at vs / ms + r * ld + j0.
-// Rows whose bit is set in SCALE hold a new maximum in the batch and scale
-// every key of it (ggml_vec_scale_f16 runs only on a new maximum, but ms = 1
-// is exact: an fp16 value times 1, rounded to fp16); the others take three
-// VALU instructions per key.
-template <int R, int SCALE>
-__device__ __forceinline__ void fx_body2(const uint32_t *v, const float *vs, const float *ms, int ld, int j0, half2v *acc) {
-#pragma unroll
-    for (int i = 0; i < FX_B; i++)
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            if constexpr (SCALE != 0)
-                if ((SCALE >> r) & 1) acc[r] = fx_scale2(acc[r], ms[r * ld + j0 + i]);
-            acc[r] = fx_mad2(acc[r], v[i], vs[r * ld + j0 + i]);
-        }
-}
-template <int R>
-__device__ __forceinline__ void fx_batch2(const uint32_t *v, const float *vs, const float *ms, int ld, int j0, int nb,
-                                          uint32_t mask, half2v *acc) {
-    static_assert(R == 2, "row-mask dispatch written for two rows a wave");
-    if (nb == FX_B) {
-        switch (mask) {   // uniform
-        case 0: fx_body2<R, 0>(v, vs, ms, ld, j0, acc); break;
-        case 1: fx_body2<R, 1>(v, vs, ms, ld, j0, acc); break;
-        case 2: fx_body2<R, 2>(v, vs, ms, ld, j0, acc); break;
-        default: fx_body2<R, 3>(v, vs, ms, ld, j0, acc); break;
-        }
-    } else {   // the chunk's partial last batch
-#pragma unroll
-        for (int i = 0; i < FX_B; i++) {
-            if (i < nb) {
-#pragma unroll
-                for (int r = 0; r < R; r++) {
-                    acc[r] = fx_scale2(acc[r], ms[r * ld + j0 + i]);
-                    acc[r] = fx_mad2(acc[r], v[i], vs[r * ld + j0 + i]);
-                }
-            }
-        }
-    }
-}
-// the chain over keys [0, n) of a chunk for R rows, V from the chunk's LDS
-// image (vl = this lane's dword of key 0, 64 dwords per key); row r's batch
-// flags at fl[b * PX_ROWS + r]
-template <int R>
-__device__ __forceinline__ void fx_chain2(const uint32_t *vl, int n, const float *vs, const float *ms, int ld,
-                                          const uint32_t *fl, half2v *acc) {
-    for (int j0 = 0; j0 < n; j0 += FX_B) {
-        uint32_t v[FX_B];
-#pragma unroll
-        for (int i = 0; i < FX_B; i++) v[i] = vl[(j0 + i) * 64];   // rows past n: staged padding, unused
-        uint32_t mask = 0;
-#pragma unroll
-        for (int r = 0; r < R; r++) mask |= (fl[(j0 / FX_B) * PX_ROWS + r] ? 1u : 0u) << r;
-        fx_batch2<R>(v, vs, ms, ld, j0, min(FX_B, n - j0), __builtin_amdgcn_readfirstlane(mask), acc);
-    }
-}
-
-// FX_STAMPS (tools/micro/fx_bench.hip only): per-workgroup phase cycles of the
-// prefill kernel, wave 0: [start, end, scores, weights, chain, chunks]
-#ifdef FX_STAMPS
-__device__ unsigned long long fx_stamps[1 << 16][8];
-#define FX_CLK(v) const unsigned long long v = clock64()
-#define FX_ADD(i, d) tsum[i] += (d)
-#else
-#define FX_CLK(v)
-#define FX_ADD(i, d)
-#endif
-
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
@@ -212,64 +79,110 @@ typedef __attribute__((address_space(1))) void glb_void;
 #ifndef PX_MINW
 #define PX_MINW 1   // minimum waves per SIMD asked of the register allocator
 #endif
+// Round 6: the same arithmetic per (row, key) as the round-5 kernel (kept as
+// tools/micro/px_v0.h, the A/B baseline of tools/micro/px_bench) -- scores,
+// (ms, vs), S and the chain -- in 24 % fewer VALU instructions (the kernel is
+// VALU-issue bound: tools/micro/px_bench PMC, ~80 % of its cycles issue VALU):
+//  * the weights of the wave's two rows at once, lanes 0-31 row 2w and 32-63
+//    row 2w + 1, four keys a lane: one LDS read of the four scores, a 32-lane
+//    prefix-maximum scan, one shared sum tree -- S is the same balanced
+//    pairwise sum over the chunk's 128 keys in key order (lane pairs there,
+//    lane quads here: the same tree), so the same fp32 value;
+//  * expf(gt ? Mp - s : s - Mp) as expf(-|s - Mp|) (a - b = -(b - a) exactly)
+//    through px_expf_nonpos, the device expf without its overflow clamp;
+//  * one word a key: vs, or -ms at a new maximum (vs = 1 there); the
+//    new-maximum keys of each 16-key batch as a bit mask per row, so the
+//    chain scales the accumulator only at those keys (ggml's order: scale,
+//    then the mad with vs = 1), by v_fma_mix_f32 with a -0 addend (= the fp32
+//    product) -- the other keys of such a batch keep the 3-instruction body;
+//  * the chunk's partial last batch runs the full body with v = -0 past the
+//    wave's last key (fma(-0, vs, acc) = acc exactly, as skipping the key);
+//  * wave-uniform loop bounds (the wave index through readfirstlane) and no
+//    barrier between a wave's weights and its chain (its own rows only).
+// Bit-identical to the round-5 kernel on every tools/micro/px_bench case
+// (causal batches, a key-0 attention sink, cached prefixes, the aligner's
+// fp32 scores); 1.13-1.31x faster (2.57 -> 1.99 ms a layer at 128 x 405).
+//
+// fp16(fp32(acc) * ms) with ms = -x (v_fma_mix_f32 negates its f32 operand)
+__device__ __forceinline__ half2v fx_scale2n(half2v acc, float x) {
+    float lo, hi;
+    const float nz = -0.0f;
+    asm("v_fma_mix_f32 %0, %1, -%2, %3 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(acc), "v"(x), "v"(nz));
+    asm("v_fma_mix_f32 %0, %1, -%2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(hi) : "v"(acc), "v"(x), "v"(nz));
+    return __builtin_convertvector((floatx2){lo, hi}, half2v);
+}
+// expf at x <= 0 (or NaN): the instruction sequence of this ROCm's device
+// expf (__ocml_exp_f32: x log2(e) split in two fp32 parts, v_exp_f32 of the
+// fraction, v_ldexp_f32 by the rounded integer part, 0 below -103.28) without
+// its overflow clamp, which never applies at x <= 0; the same bits as expf on
+// every x <= 0 (tools/micro/px_bench checks all 2^31 of them)
+__device__ __forceinline__ float px_expf_nonpos(float x) {
+    const float l2e = __uint_as_float(0x3fb8aa3bu), l2e_lo = __uint_as_float(0x32a5705fu);
+    const float ph = x * l2e;
+    float pl = __builtin_fmaf(x, l2e, -ph);
+    pl = __builtin_fmaf(x, l2e_lo, pl);
+    const float e = __builtin_rintf(ph);
+    const float f = (ph - e) + pl;
+    const float r = __builtin_ldexpf(__builtin_amdgcn_exp2f(f), (int)e);
+    return x < __uint_as_float(0xc2ce8ed0u) ? 0.0f : r;
+}
+// the chain step of one row at key i of a batch whose new-maximum keys are
+// the bits of mk: x = the key's word (vs, or -ms at a new maximum)
+__device__ __forceinline__ half2v fx_key(half2v acc, uint32_t v, float x, uint32_t mk, int i) {
+    float vs = x;
+    if ((mk >> i) & 1u) {   // uniform
+        acc = fx_scale2n(acc, x);
+        vs = 1.0f;
+    }
+    return fx_mad2(acc, v, vs);
+}
+
 template <bool F32S>   // fp32 Q / K scores (the aligner)
 __global__ __launch_bounds__(64 * PX_W, PX_MINW) void prefill_attn_exact_kernel(PrefillAttnArgs a) {
-    __shared__ __attribute__((aligned(16))) float sc[PX_ROWS][PX_SCS];   // scores, then vs
-    __shared__ __attribute__((aligned(16))) float msw[PX_ROWS][PX_SCS];
-    __shared__ __attribute__((aligned(16))) uint32_t fl[PX_KC / FX_B][PX_ROWS];
-    __shared__ __attribute__((aligned(16))) uint32_t vsh[PX_KC * 64];    // the chunk's V rows
+    __shared__ __attribute__((aligned(16))) float sc[PX_ROWS][PX_SCS];   // scores, then vs / -ms
+    __shared__ __attribute__((aligned(16))) uint32_t fl[PX_KC / FX_B][PX_ROWS];   // new-maximum key masks
+    __shared__ __attribute__((aligned(16))) uint32_t vsh[PX_KC * 64];
+    static_assert(FX_B == 16 && PX_KC == 128 && PX_R == 2, "four keys a lane, four lanes a batch, two rows a wave");
     const int sq = blockIdx.z, h = blockIdx.y;
     const int L = a.seq_len[sq];
     const int nqb = (a.max_len + PX_ROWS - 1) / PX_ROWS;
     const int q0 = (nqb - 1 - (int)blockIdx.x) * PX_ROWS;
     if (q0 >= L) return;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, ql = lane & 15;
     const int hk = h / (a.n_head / a.n_kv_head);
     const int row0 = a.seq_row0[sq];
     const int QD = a.n_head * 128;
     const long cbase = ((long)a.seq_slot[sq] * a.n_kv_head + hk) * a.max_ctx;
     const uint16_t *kc = a.kc + cbase * 128, *vc = a.vc + cbase * 128;
-    // B fragment of query column ql (row q0 + ql; zero past the sequence)
     half8 qf[4];
     const bool qv = q0 + ql < L;
 #pragma unroll
     for (int s = 0; s < 4; s++)
         qf[s] = qv ? *(const half8 *)(a.q + (long)(row0 + q0 + ql) * QD + h * 128 + 32 * s + 8 * g) : half8{};
-    // a chunk after P0 cached tokens (TextDecoder::forward at n_past > 0): row t
-    // at position P0 + t, keys 0 .. P0 + L - 1 (the aligner's fp32 K rows: P0 = 0)
     const int P0 = a.seq_pos0 ? a.seq_pos0[sq] : 0;
-    const int lim = qv ? P0 + q0 + ql : -1;   // causal: keys <= the query's position
+    const int lim = qv ? P0 + q0 + ql : -1;
     const int kend = min(P0 + L, P0 + q0 + PX_ROWS);
-    const int r0 = PX_R * wid;                                     // this wave's first row
-    const int wlast = min(P0 + L - 1, P0 + q0 + r0 + PX_R - 1);    // its last key (its longest row)
-    float M[PX_R], S[PX_R];
+    const int r0 = PX_R * wid;
+    const int wlast = min(P0 + L - 1, P0 + q0 + r0 + PX_R - 1);
+    // weights lanes: half hf = row r0 + hf, keys 4 l32 .. 4 l32 + 3 of the chunk
+    const int hf = lane >> 5, l32 = lane & 31, myrow = r0 + hf;
+    float M = -INFINITY, S = 0.0f;   // row myrow's (uniform in each half)
     half2v acc[PX_R];
 #pragma unroll
-    for (int r = 0; r < PX_R; r++) {
-        M[r] = -INFINITY;
-        S[r] = 0.0f;
-        acc[r] = half2v{0, 0};
-    }
-#ifdef FX_STAMPS
-    unsigned long long tsum[4] = {0, 0, 0, 0};
-    FX_CLK(tk0);
-#endif
+    for (int r = 0; r < PX_R; r++) acc[r] = half2v{0, 0};
     for (int c0 = 0; c0 < kend; c0 += PX_KC) {
         const int n = min(PX_KC, kend - c0);
-        __syncthreads();   // the previous chunk's chains are done with sc / msw / fl / vsh
-        FX_CLK(ta);
-        // V rows c0 .. c0 + PX_KC - 1 -> LDS: 1 KiB (4 rows) per wave-instruction
+        __syncthreads();   // the previous chunk's chains are done with sc / fl / vsh
 #pragma unroll
         for (int it = wid; it < PX_KC / 4; it += PX_W)
             __builtin_amdgcn_global_load_lds((glb_void *)(vc + (long)(c0 + 4 * it + (lane >> 4)) * 128 + 8 * (lane & 15)),
                                              (lds_void *)(vsh + it * 256), 16, 0, 0);
-        // (1) scores: 16-key tile t = wid
-        if constexpr (F32S) {   // fp32 Q and K (the aligner): v_mfma_f32_16x16x4_f32, exact fp32 products
+        // (1) scores: 16-key tile t = wid (as prefill_attn_exact_kernel)
+        if constexpr (F32S) {
             const int t = wid;
             if (t * 16 < n) {
-                // lane (row r = lane & 15, group g): dims 32 g .. 32 g + 31 of key r / query r
-                // (any split of the 128 dims works if A and B use the same one)
                 const int key = min(c0 + t * 16 + ql, kend - 1);
                 const float *kr = a.k32 + (long)(row0 + key) * (a.n_kv_head * 128) + hk * 128 + 32 * g;
                 const float *qr = a.q32 + (long)(row0 + min(q0 + ql, L - 1)) * QD + h * 128 + 32 * g;
@@ -281,7 +194,7 @@ __global__ __launch_bounds__(64 * PX_W, PX_MINW) void prefill_attn_exact_kernel(
                 }
                 floatx4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int kk = 0; kk < 32; kk += 2) {   // two accumulators: the 40-cycle dependent latency
+                for (int kk = 0; kk < 32; kk += 2) {
                     s0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kv[kk], qv2[kk], s0, 0, 0, 0);
                     s1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kv[kk + 1], qv2[kk + 1], s1, 0, 0, 0);
                 }
@@ -302,43 +215,134 @@ __global__ __launch_bounds__(64 * PX_W, PX_MINW) void prefill_attn_exact_kernel(
 #pragma unroll
                 for (int s = 0; s < 4; s++) sacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], qf[s], sacc, 0, 0, 0);
 #pragma unroll
-                for (int i = 0; i < 4; i++) {   // C row = key 4g + i of the tile, column = query ql
+                for (int i = 0; i < 4; i++) {
                     const int k = c0 + t * 16 + 4 * g + i;
                     sc[ql][t * 16 + 4 * g + i] = k <= lim ? sacc[i] * a.scale : -INFINITY;
                 }
             }
         }
-        __syncthreads();
-        FX_CLK(tb);
-        FX_ADD(0, tb - ta);
-        // (2) weights of the wave's rows
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's V pieces landed
+        __syncthreads();   // every score and every V piece in LDS
+        // (2) weights of rows r0, r0 + 1: fx_weights' arithmetic per key
+        {
+            const float4 s4 = *(const float4 *)&sc[myrow][4 * l32];
+            float v[4] = {s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
-        for (int r = 0; r < PX_R; r++)
-            fx_weights<PX_KC / 64>(sc[r0 + r], sc[r0 + r], msw[r0 + r], &fl[0][r0 + r], PX_ROWS, n, M[r], S[r]);
-        __syncthreads();   // (the V image has landed: the barrier drains the LDS-DMA)
-        FX_CLK(tc);
-        FX_ADD(1, tc - tb);
-        // (3) the chain, up to the wave's longest row (a shorter row sees zero weights)
+            for (int i = 0; i < 4; i++)
+                if (4 * l32 + i >= n) v[i] = -INFINITY;
+            float inc = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+            // inclusive prefix maximum over each half's 32 lanes: row_shr 1, 2, 4, 8, then row 0's
+            // (row 2's) last lane into row 1 (row 3)
+            inc = fmaxf(inc, dpp_ninf<0x111, 0xF>(inc));
+            inc = fmaxf(inc, dpp_ninf<0x112, 0xF>(inc));
+            inc = fmaxf(inc, dpp_ninf<0x114, 0xF>(inc));
+            inc = fmaxf(inc, dpp_ninf<0x118, 0xF>(inc));
+            inc = fmaxf(inc, dpp_ninf<0x142, 0xA>(inc));
+            float ex = dpp_ninf<0x138, 0xF>(inc);   // wave_shr:1: the exclusive prefix
+            if (l32 == 0) ex = -INFINITY;           // (lane 32 got row 2w's total)
+            float Mp = fmaxf(M, ex);
+            const float tA = lane_f(inc, 31), tB = lane_f(inc, 63);
+            const float Mn = fmaxf(M, hf ? tB : tA);
+            float w4[4], t[4];
+            uint32_t gtm = 0, need = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                // fx_weights' per-key values: a new maximum gives ms = expf(Mp - s) (0 before the
+                // row's first key) and vs = 1, any other key vs = expf(s - Mp); a masked key (s = -inf)
+                // of a valid row has a finite Mp (its key 0 is never masked), so expf gives its weight
+                // 0 without a test -- rows past the sequence (every key masked) get NaN weights, and
+                // their outputs are never stored
+                const float s = v[i];
+                const bool gt = s > Mp;
+                const float e = px_expf_nonpos(-fabsf(s - Mp));
+                w4[i] = gt ? -e : e;   // the key's word: -ms, or vs
+                t[i] = gt ? 1.0f : e;
+                Mp = fmaxf(Mp, s);
+                gtm |= (gt ? 1u : 0u) << i;
+                need |= (Mp != Mn ? 1u : 0u) << i;
+            }
+            *(float4 *)&sc[myrow][4 * l32] = make_float4(w4[0], w4[1], w4[2], w4[3]);
+            if (need) {   // keys before a later new maximum of the chunk: their own S term
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if ((need >> i) & 1) t[i] = px_expf_nonpos(v[i] - Mn);
+            }
+            float ps = (t[0] + t[1]) + (t[2] + t[3]);
+            ps = row16_sum(ps);
+            const float psA = lane_f(ps, 0) + lane_f(ps, 16), psB = lane_f(ps, 32) + lane_f(ps, 48);
+            ps = hf ? psB : psA;
+            S = (M == -INFINITY ? 0.0f : M == Mn ? S : S * px_expf_nonpos(M - Mn)) + ps;
+            M = Mn;
+            // batch b = l32 / 4: its 16-bit new-maximum key mask from the four lanes' nibbles
+            uint32_t nib = gtm << (4 * (l32 & 3));
+            nib |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)nib, 0xB1, 0xF, 0xF, true);
+            nib |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)nib, 0x4E, 0xF, 0xF, true);
+            if ((l32 & 3) == 0) fl[l32 >> 2][myrow] = nib;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (LDS ops of one wave complete in order)
+        __builtin_amdgcn_wave_barrier();
+        // (3) the chain, up to the wave's longest row
         const int nw = min(n, wlast + 1 - c0);
-        if (nw > 0) fx_chain2<PX_R>(vsh + lane, nw, sc[r0], msw[r0], PX_SCS, &fl[0][r0], acc);
-        FX_CLK(td);
-        FX_ADD(2, td - tc);
-        FX_ADD(3, 1);
+        const uint32_t *vl = vsh + lane;
+        for (int j0 = 0; j0 < nw; j0 += FX_B) {
+            uint32_t v[FX_B];
+#pragma unroll
+            for (int i = 0; i < FX_B; i++) v[i] = vl[(j0 + i) * 64];
+            const int nb = nw - j0;
+            if (nb < FX_B) {
+#pragma unroll
+                for (int i = 0; i < FX_B; i++)
+                    if (i >= nb) v[i] = 0x80008000u;   // -0: fma(-0, vs, acc) = acc
+            }
+            const uint32_t mA = __builtin_amdgcn_readfirstlane(fl[j0 / FX_B][r0]);
+            const uint32_t mB = __builtin_amdgcn_readfirstlane(fl[j0 / FX_B][r0 + 1]);
+            const float *x0 = sc[r0] + j0, *x1 = sc[r0 + 1] + j0;
+            if ((mA | mB) == 0) {
+#pragma unroll
+                for (int i = 0; i < FX_B; i++) {
+                    acc[0] = fx_mad2(acc[0], v[i], x0[i]);
+                    acc[1] = fx_mad2(acc[1], v[i], x1[i]);
+                }
+            } else {
+                // both rows' words in registers first (left to itself, the compiler sinks each load
+                // into its key's branch: an LDS round trip a key)
+                floatx4 xa[FX_B / 4], xb[FX_B / 4];
+#pragma unroll
+                for (int i = 0; i < FX_B / 4; i++) {
+                    xa[i] = *(const floatx4 *)(x0 + 4 * i);
+                    xb[i] = *(const floatx4 *)(x1 + 4 * i);
+                }
+#pragma unroll
+                for (int i = 0; i < FX_B / 4; i++) asm volatile("" : "+v"(xa[i]), "+v"(xb[i]));
+                // four-key groups: a group without a new maximum runs the plain body, the others test
+                // each key (one new maximum a batch is the common case past a row's first keys)
+#pragma unroll
+                for (int gq = 0; gq < FX_B / 4; gq++) {
+                    const uint32_t ga = (mA >> (4 * gq)) & 15u, gb = (mB >> (4 * gq)) & 15u;
+                    if ((ga | gb) == 0) {
+#pragma unroll
+                        for (int k = 0; k < 4; k++) {
+                            acc[0] = fx_mad2(acc[0], v[4 * gq + k], xa[gq][k]);
+                            acc[1] = fx_mad2(acc[1], v[4 * gq + k], xb[gq][k]);
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 4; k++) {
+                            acc[0] = fx_key(acc[0], v[4 * gq + k], xa[gq][k], ga, k);
+                            acc[1] = fx_key(acc[1], v[4 * gq + k], xb[gq][k], gb, k);
+                        }
+                    }
+                }
+            }
+        }
     }
-#ifdef FX_STAMPS
-    if (tid == 0) {
-        unsigned long long *st = fx_stamps[blockIdx.x + gridDim.x * blockIdx.y];
-        st[0] = tk0;
-        st[1] = clock64();
-        for (int i = 0; i < 4; i++) st[2 + i] = tsum[i];
-        st[6] = q0;
-    }
-#endif
 #pragma unroll
     for (int r = 0; r < PX_R; r++) {
         const int q = q0 + r0 + r;
         if (q >= L) continue;
-        const float inv = S[r] == 0.0f ? 0.0f : 1.0f / S[r];
+        // S of row r0 + r lives in half r
+        const float Sr = lane_f(S, 32 * r);
+        const float inv = Sr == 0.0f ? 0.0f : 1.0f / Sr;
         const float o0 = (float)acc[r].x * inv, o1 = (float)acc[r].y * inv;
         const long o = (long)(row0 + q) * QD + h * 128 + 2 * lane;
         if (a.out32) {

@@ -1,8 +1,9 @@
-// Stand-alone timing of fa_exact.hip's prefill kernel at configs[1]'s shape
+// Stand-alone timing of the round-5 exact prefill kernel (px_v0.h) at configs[1]'s shape
 // (one 1211-row prompt, 16 heads, GQA 2:1, hd 128) with per-workgroup phase
 // stamps (FX_STAMPS).  Build: see tools/micro/Makefile.
 #define FX_STAMPS 1
 #include "../../qwen3-asr.cpp_amd/csrc/fa_exact.hip"
+#include "px_v0.h"   // the round-5 prefill kernel, the one with the phase stamps
 #include <stdio.h>
 #include <stdlib.h>
 #include <vector>
@@ -52,15 +53,18 @@ int main(int argc, char **argv) {
     a.n_head = NH; a.n_kv_head = NKV; a.max_ctx = CTX; a.scale = 1.0f / sqrtf(128.0f); a.out = o;
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
-    for (int i = 0; i < 3; i++) launch_prefill_attention_exact(a, 0);
+    auto launch_r5 = [&]() {
+        hipLaunchKernelGGL(prefill_attn_exact_r5_kernel<false>, dim3((L + PX_ROWS - 1) / PX_ROWS, NH, 1), dim3(64 * PX_W), 0, 0, a);
+    };
+    for (int i = 0; i < 3; i++) launch_r5();
     hipEventRecord(e0, 0);
     const int reps = 10;
-    for (int i = 0; i < reps; i++) launch_prefill_attention_exact(a, 0);
+    for (int i = 0; i < reps; i++) launch_r5();
     hipEventRecord(e1, 0);
     hipEventSynchronize(e1);
     float ms;
     hipEventElapsedTime(&ms, e0, e1);
-    printf("prefill_attn_exact_kernel L=%d: %.1f us per launch\n", L, ms * 1e3 / reps);
+    printf("prefill_attn_exact_r5_kernel L=%d: %.1f us per launch\n", L, ms * 1e3 / reps);
     const int nb = (L + 15) / 16 * NH;
     std::vector<unsigned long long> st((size_t)nb * 8);
     hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(fx_stamps), st.size() * 8);

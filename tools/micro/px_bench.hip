@@ -7,7 +7,16 @@
 // Build: hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize
 //        -I../../include -I../../qwen3-asr.cpp_amd/csrc px_bench.hip -o px_bench
 #include "../../qwen3-asr.cpp_amd/csrc/fa_exact.hip"
+#include "px_v0.h"
+#ifndef PX_ALT
+#define PX_ALT 4   // the kernel compared with the round-5 one (px_v0.h): 3 = px_v3.h's, 4 = fa_exact.hip's (the product)
+#endif
+#if PX_ALT == 3
 #include "px_v3.h"
+#define PX_ALT_KERNEL prefill_attn_exact2_kernel
+#else
+#define PX_ALT_KERNEL prefill_attn_exact_kernel
+#endif
 
 #include <cstdio>
 #include <cstdlib>
@@ -29,6 +38,7 @@ struct Case {
     const char *name;
     std::vector<int> len, pos0;
     bool f32s;
+    bool sink = false;   // key 0 of every sequence aligned with the queries (an attention sink: few new maxima)
 };
 
 static void run_case(const Case &cs, int reps) {
@@ -49,6 +59,12 @@ static void run_case(const Case &cs, int reps) {
     for (auto &x : hq) x = h16(2.0f * frand());
     for (auto &x : hk) x = h16(2.0f * frand());
     for (auto &x : hv) x = h16(frand());
+    if (cs.sink) {   // every query +4 in dimension 0, key 0 of each (sequence, kv head) 8 there: its score tops the row
+        for (int r = 0; r < rows; r++)
+            for (int hh = 0; hh < NH; hh++) hq[(size_t)r * QD + hh * 128] = h16(4.0f + frand());
+        for (int b = 0; b < B; b++)
+            for (int kh = 0; kh < NKV; kh++) hk[((size_t)b * NKV + kh) * max_ctx * 128] = h16(8.0f);
+    }
     uint16_t *q, *k, *v, *o0, *o1;
     float *q32 = nullptr, *k32 = nullptr;
     int *meta;
@@ -86,11 +102,11 @@ static void run_case(const Case &cs, int reps) {
         PrefillAttnArgs av = a;
         av.out = ver ? o1 : o0;
         if (ver == 0) {
-            if (cs.f32s) hipLaunchKernelGGL(prefill_attn_exact_kernel<true>, grid, dim3(64 * PX_W), 0, 0, av);
-            else hipLaunchKernelGGL(prefill_attn_exact_kernel<false>, grid, dim3(64 * PX_W), 0, 0, av);
+            if (cs.f32s) hipLaunchKernelGGL(prefill_attn_exact_r5_kernel<true>, grid, dim3(64 * PX_W), 0, 0, av);
+            else hipLaunchKernelGGL(prefill_attn_exact_r5_kernel<false>, grid, dim3(64 * PX_W), 0, 0, av);
         } else {
-            if (cs.f32s) hipLaunchKernelGGL(prefill_attn_exact2_kernel<true>, grid, dim3(64 * PX_W), 0, 0, av);
-            else hipLaunchKernelGGL(prefill_attn_exact2_kernel<false>, grid, dim3(64 * PX_W), 0, 0, av);
+            if (cs.f32s) hipLaunchKernelGGL(PX_ALT_KERNEL<true>, grid, dim3(64 * PX_W), 0, 0, av);
+            else hipLaunchKernelGGL(PX_ALT_KERNEL<false>, grid, dim3(64 * PX_W), 0, 0, av);
         }
     };
     launch(0);
@@ -136,8 +152,24 @@ static void run_case(const Case &cs, int reps) {
     std::vector<uint16_t> r0((size_t)rows * QD), r1((size_t)rows * QD);
     CK(hipMemcpy(r0.data(), o0, r0.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(r1.data(), o1, r1.size() * 2, hipMemcpyDeviceToHost));
-    size_t diff = 0;
-    for (size_t i = 0; i < r0.size(); i++) diff += r0[i] != r1[i];
+    size_t diff = 0, first = (size_t)-1;
+    for (size_t i = 0; i < r0.size(); i++)
+        if (r0[i] != r1[i]) {
+            if (!diff) first = i;
+            diff++;
+        }
+    if (diff) {   // the first differing element and how far off it is
+        _Float16 a = __builtin_bit_cast(_Float16, r0[first]), b = __builtin_bit_cast(_Float16, r1[first]);
+        long rr = (long)(first / QD);
+        printf("    first diff: row %ld head %ld dim %ld: %04x (%g) vs %04x (%g)\n", rr, (long)(first % QD) / 128, (long)(first % 128),
+               r0[first], (double)a, r1[first], (double)b);
+        double maxrel = 0;
+        for (size_t i = 0; i < r0.size(); i++) {
+            const double x = (double)__builtin_bit_cast(_Float16, r0[i]), y = (double)__builtin_bit_cast(_Float16, r1[i]);
+            maxrel = std::max(maxrel, std::fabs(x - y));
+        }
+        printf("    max |diff| %g\n", maxrel);
+    }
     // chain VALU-issue bound: 3 wave-instructions per (row, key) pair of a head's two dimension
     // halves... = 3 per row-key per 64 lanes x 2 dims = per (row, head, key) 3 x 128 / 128 wave-instr
     double rk = 0;
@@ -153,11 +185,38 @@ static void run_case(const Case &cs, int reps) {
     if (q32) { CK(hipFree(q32)); CK(hipFree(k32)); }
 }
 
+// px_expf_nonpos against the device expf on every x <= 0 (all 2^31 bit patterns with the sign set, and +0)
+__global__ void expf_check(unsigned long long *bad) {
+    const uint32_t base = (blockIdx.x * 256u + threadIdx.x) * 16u;
+    unsigned long long nb = 0;
+    for (uint32_t k = 0; k < 16; k++) {
+        const uint32_t u = (base + k) | 0x80000000u;
+        const float x = __uint_as_float(u);
+        const float a = expf(x), b = px_expf_nonpos(x);
+        if (__float_as_uint(a) != __float_as_uint(b) && !(a != a && b != b)) nb++;
+    }
+    if (base == 0) {
+        const float a = expf(0.0f), b = px_expf_nonpos(0.0f);
+        if (__float_as_uint(a) != __float_as_uint(b)) nb++;
+    }
+    if (nb) atomicAdd(bad, nb);
+}
+
 int main(int argc, char **argv) {
+    {
+        unsigned long long *bad, hb = 0;
+        CK(hipMalloc(&bad, 8));
+        CK(hipMemset(bad, 0, 8));
+        hipLaunchKernelGGL(expf_check, dim3(1u << 19), dim3(256), 0, 0, bad);
+        CK(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
+        printf("px_expf_nonpos vs expf over all 2^31 x <= 0: %llu differ\n", hb);
+        CK(hipFree(bad));
+    }
     const int reps = argc > 1 ? atoi(argv[1]) : 5;
     std::vector<Case> cases;
     cases.push_back({"batch 128 x 405", std::vector<int>(128, 405), {}, false});
     cases.push_back({"configs[1] 1 x 1211", {1211}, {}, false});
+    cases.push_back({"batch 128 x 405, key-0 sink", std::vector<int>(128, 405), {}, false, true});
     {
         Case c{"ragged 24, cached prefixes", {}, {}, false};
         for (int b = 0; b < 24; b++) { c.len.push_back(17 + 37 * b % 400); c.pos0.push_back((b % 3) * 61); }
