@@ -139,7 +139,7 @@ struct GemvArgs {
     int keep_step;                       // lmhead_batch_kernel: leave *step as it is (a first row-half launch)
 };
 void launch_gemv(int epi, const GemvArgs &g, hipStream_t s);
-// lmhead.hip: decode-batch LM head in one launch (9..64 rows; 65..128 rows: two, one per row half; K = 1024, f16 W):
+// lmhead.hip: decode-batch LM head in one launch (9..128 rows; K = 1024, f16 W):
 // RMS norm of x with norm_w, GEMM against W [N][K], optional fp32 logits,
 // per-row first-index argmax, and the fused bookkeeping of EPI_ARGMAX above
 // (plus nkv); amax and done zero at rest.  false = shape not covered

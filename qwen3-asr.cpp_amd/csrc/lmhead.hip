@@ -1,4 +1,4 @@
-// lmhead.hip -- the decode-batch LM head in one launch (9 <= M <= 64 rows):
+// lmhead.hip -- the decode-batch LM head in one launch (9 <= M <= 128 rows):
 // final RMS norm + tied-embedding GEMM (151936 x 1024 f16) + first-index
 // argmax + the greedy step's bookkeeping (src/text_decoder.cpp forward's last
 // ggml_rms_norm / ggml_mul / ggml_mul_mat over model.output, then
@@ -30,6 +30,8 @@ namespace qasr {
 namespace {
 
 constexpr int LMH_K = 1024;   // hidden width this kernel is built for (host checks)
+typedef __attribute__((address_space(3))) void lds_void_l;
+typedef __attribute__((address_space(1))) void glb_void_l;
 
 // LDS row layout: 128 chunks of 16 B per row, chunk ch stored at ch ^ (row & 15)
 // so the 16 rows of a fragment read hit 16 distinct 16-B bank groups
@@ -214,37 +216,195 @@ void run_lmhead(const GemvArgs &g, hipStream_t s) {
     hipLaunchKernelGGL((lmhead_batch_kernel<MT, WPG, D>), dim3(ncu), dim3(64 * WPG), MT * 16 * LMH_K * 2, s, g);
 }
 
-}  // namespace
+// ---- 65..128 rows in one launch, the embedding read once (round 6).  The
+// 128 normalised rows (256 KB fp16) do not fit the LDS, so they live in
+// registers: wave w holds rows 16w .. 16w + 15 as its 32 MFMA A fragments of
+// K (128 VGPRs a lane), staged through LDS 32 rows at a time with
+// lmhead_batch_kernel's norm arithmetic.  The weight units (16 vocabulary rows
+// x 1024, 32 KB) stream through an L128_R-slot LDS ring by LDS-DMA
+// (nontemporal, 16-B chunks XOR-swizzled by row so the fragment reads of 16
+// rows hit distinct banks), two units in flight behind the one being read,
+// and every unit is read by all eight waves: one HBM read of the 311 MB
+// embedding per step instead of one per 64-row half.  Per (row tile, unit)
+// the MFMA order is lmhead_batch_kernel's -- K chunks ascending, even / odd
+// chunks in two accumulators summed at the end -- so the logits, and the
+// tokens, are bit-identical to the two-launch path (tools/micro/lmh128_bench).
+// Each wave owns its rows outright: per row one atomicMax per workgroup, then
+// the last workgroup decodes the tokens as lmhead_batch_kernel does.  (A
+// 9-slot ring of half units, seven in flight, ran slower: 97 against 86 us,
+// profiles/r6/lmhead128_r9ring_ab.txt -- twice the barriers.)
+constexpr int L128_R = 4;                  // ring slots (32 KB each)
+constexpr int L128_UNIT = 16 * LMH_K;      // halves per unit
+constexpr int L128_LDS = L128_R * L128_UNIT * 2;
 
-static void lmhead_rows(const GemvArgs &g, hipStream_t s) {   // <= 64 rows
-    const int mt = (g.M + 15) / 16;
-    if (mt == 1) run_lmhead<1>(g, s);
-    else if (mt == 2) run_lmhead<2>(g, s);
-    else if (mt == 3) run_lmhead<3>(g, s);
-    else run_lmhead<4>(g, s);
+__global__ __launch_bounds__(512) void lmhead128_kernel(GemvArgs g) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t ring[];   // [L128_R][16][LMH_K], swizzled
+    __shared__ int last_wg, st;
+    stamp_start(g.stamp);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int q = lane >> 4, c16 = lane & 15;
+    const int M = g.M;
+    const int U = g.N >> 4;
+    const int u0 = (int)((long)blockIdx.x * U / gridDim.x), u1 = (int)((long)(blockIdx.x + 1) * U / gridDim.x);
+    const int nu = u1 - u0;
+    // unit j of this workgroup -> ring slot j % R: 32 pieces of 1 KB (row r = piece / 2), four per wave
+    auto issue = [&](int j) {
+        const int u = u0 + j;
+        uint16_t *dst = ring + (j % L128_R) * L128_UNIT;
+#pragma unroll
+        for (int ii = 0; ii < 4; ii++) {
+            const int i = wid * 4 + ii, r = i >> 1, p = ((i & 1) << 6) + lane;
+            const uint16_t *src = g.W + ((long)(u * 16 + r) * LMH_K + ((p ^ (r & 15)) << 3));
+            __builtin_amdgcn_global_load_lds((glb_void_l *)src, (lds_void_l *)(dst + i * 512), 16, 0, 2);
+        }
+    };
+    // units 0, 1 land while the rows are normalised (slots 2, 3 hold the staging rows meanwhile)
+    if (nu > 0) issue(0);
+    if (nu > 1) issue(1);
+
+    // ---- prologue: rows 32p .. 32p + 31 -> RMS norm -> fp16 staging (slots 2-3), then the two
+    //      waves owning them take their A fragments; wave w normalises rows 32p + w + 8i
+    uint16_t *xs = ring + 2 * L128_UNIT;   // [32][LMH_K], lmh_off swizzle
+    half8 af[32];                          // K step t: k = 32 t + 8 q .. + 8 of row 16 wid + c16
+    float4 wv[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) wv[i] = *(const float4 *)(g.norm_w + 4 * lane + 256 * i);
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        float4 v[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int m = 32 * p + wid + 8 * r;
+            const float *xr = g.x + (long)(m < M ? m : 0) * g.ldx;
+#pragma unroll
+            for (int i = 0; i < 4; i++) v[r][i] = *(const float4 *)(xr + 4 * lane + 256 * i);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int m = 32 * p + wid + 8 * r, lr = wid + 8 * r;
+            double s = 0.0;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                s += ((double)fmul_rn(v[r][i].x, v[r][i].x) + (double)fmul_rn(v[r][i].y, v[r][i].y)) +
+                     ((double)fmul_rn(v[r][i].z, v[r][i].z) + (double)fmul_rn(v[r][i].w, v[r][i].w));
+            s = wave_sum_d(s);
+            const float mean = (float)(s / LMH_K);
+            const float scale = 1.0f / sqrtf(mean + g.eps);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                uint32_t lo = f_to_u16(fmul_rn(fmul_rn(v[r][i].x, scale), wv[i].x)) |
+                              ((uint32_t)f_to_u16(fmul_rn(fmul_rn(v[r][i].y, scale), wv[i].y)) << 16);
+                uint32_t hi = f_to_u16(fmul_rn(fmul_rn(v[r][i].z, scale), wv[i].z)) |
+                              ((uint32_t)f_to_u16(fmul_rn(fmul_rn(v[r][i].w, scale), wv[i].w)) << 16);
+                if (m >= M) lo = hi = 0u;   // rows past M: zeros
+                *(uint2 *)(xs + lmh_off(lr, 4 * lane + 256 * i)) = make_uint2(lo, hi);
+            }
+        }
+        __syncthreads();
+        if ((wid >> 1) == p) {
+            const int lr = 16 * (wid & 1) + c16;
+#pragma unroll
+            for (int t = 0; t < 32; t++) af[t] = *(const half8 *)(xs + lmh_off(lr, 32 * t + 8 * q));
+        }
+        __syncthreads();
+    }
+    if (nu > 2) issue(2);
+
+    // ---- stream: unit j from slot j % R; unit j + R - 1 issued once every wave is past unit j - 1
+    unsigned long long best[4] = {0ull, 0ull, 0ull, 0ull};
+    const int nvalid = g.n_valid > 0 ? g.n_valid : g.N;
+    for (int j = 0; j < nu; j++) {
+        // this wave's pieces of unit j landed: the units after it still in flight (four pieces each)
+        const int later = min(nu - 1 - j, L128_R - 2);
+        if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();   // every wave's pieces of unit j; every wave done with unit j - 1 (its slot is free)
+        if (j + L128_R - 1 < nu) issue(j + L128_R - 1);
+        const uint16_t *sl = ring + (j % L128_R) * L128_UNIT + c16 * LMH_K;
+        floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int c = 0; c < 8; c++)
+#pragma unroll
+            for (int s4 = 0; s4 < 4; s4++) {
+                const int ch = 16 * c + 4 * s4 + q;
+                const half8 b8 = *(const half8 *)(sl + ((ch ^ c16) << 3));
+                acc[c & 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[4 * c + s4], b8, acc[c & 1], 0, 0, 0);
+            }
+        const int col = (u0 + j) * 16 + c16;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {   // C layout: lane (q, c16) = rows 16 wid + 4q + r, column col
+            const int row = 16 * wid + 4 * q + r;
+            const float v = acc[0][r] + acc[1][r];
+            if (g.out_f32 && row < M) g.out_f32[(long)row * g.ldo + col] = v;
+            const unsigned long long key = col < nvalid ? argmax_key(v, col) : 0ull;
+            best[r] = key > best[r] ? key : best[r];
+        }
+    }
+
+    // ---- per-row best over the 16 column lanes; each row belongs to one wave
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        unsigned long long k = best[r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const unsigned long long t = __shfl_xor(k, o, 64);
+            k = t > k ? t : k;
+        }
+        const int row = 16 * wid + 4 * q + r;
+        if (c16 == 0 && row < M) {
+            const unsigned long long old = atomicMax(g.amax + row, k);
+            asm volatile("" ::"v"(old));   // returned value used: the max has been performed at L2
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) last_wg = __hip_atomic_fetch_add(g.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (last_wg) {
+        if (tid == 0) st = *g.step;
+        __syncthreads();
+        if (tid < M) {
+            const unsigned long long k = __hip_atomic_load(g.amax + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int id = argmax_key_idx(k);
+            g.tok_out[tid] = id;
+            if (g.hist) g.hist[(long)tid * g.hist_stride + st + 1] = id;
+            g.pos[tid] += 1;
+            if (g.nkv) g.nkv[tid] += 1;
+            __hip_atomic_store(g.amax + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (tid == 0) {
+            if (!g.keep_step) *g.step = st + 1;
+            __hip_atomic_store(g.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    stamp_end(g.stamp);
 }
+
+void run_lmhead128(const GemvArgs &g, hipStream_t s) {
+    static int ncu_dev[64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int &ncu = ncu_dev[dev & 63];
+    if (!ncu) {
+        int n = 0;
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipFuncSetAttribute((const void *)lmhead128_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, L128_LDS);
+        ncu = n > 0 ? n : 256;
+    }
+    hipLaunchKernelGGL(lmhead128_kernel, dim3(ncu), dim3(512), L128_LDS, s, g);
+}
+
+}  // namespace
 
 bool launch_lmhead_batch(const GemvArgs &g, hipStream_t s) {
     if (g.M < 1 || g.M > 128 || g.K != LMH_K || g.N % 16 != 0 || !g.x || !g.norm_w || !g.amax || !g.done || !g.tok_out ||
         !g.step || !g.pos || g.Wd)
         return false;
-    if (g.M > 64) {   // 65..128 rows: the activation image of 128 rows (256 KB) exceeds the LDS, so one launch
-                      // per 64-row half; the first leaves the step counter to the second (both read the same step)
-        GemvArgs a = g;
-        a.M = 64;
-        a.keep_step = 1;
-        lmhead_rows(a, s);
-        GemvArgs b = g;
-        b.M = g.M - 64;
-        b.x = g.x + (long)64 * g.ldx;
-        if (g.out_f32) b.out_f32 = g.out_f32 + (long)64 * g.ldo;
-        b.amax = g.amax + 64;
-        b.tok_out = g.tok_out + 64;
-        if (g.hist) b.hist = g.hist + (long)64 * g.hist_stride;
-        b.pos = g.pos + 64;
-        if (g.nkv) b.nkv = g.nkv + 64;
-        b.keep_step = 0;
-        lmhead_rows(b, s);
+    if (g.M > 64) {   // 65..128 rows: the rows in registers, the embedding read once (round 6; until then one
+                      // launch per 64-row half, each streaming all 311 MB: tools/micro/lmh128_bench)
+        run_lmhead128(g, s);
         return true;
     }
     const int mt = (g.M + 15) / 16;

@@ -2,7 +2,8 @@
 bench.utterance_set_leg's contexts / slots / queue without the rest of
 bench.py.  Env: N_UTT (1000), CTX (2), SLOTS (128), SECS (30), RAGGED=1
 (U[5, 30] s lengths from a pool of 256 seeded clips), REPS (1 timed pass after
-one warm-up), OPT="name=value,..." (per-context options, qasr_ctx_set_option).
+one warm-up), OPT="name=value,..." (per-context options, qasr_ctx_set_option),
+STAGGER_MS (context k starts k x STAGGER_MS late).
 Prints one line per pass: RTFx, wall, per-context (clips, refills, steps,
 prefill ms, decode ms).  Dev tool (GPU box)."""
 import concurrent.futures as cf
@@ -38,6 +39,7 @@ SECS = float(os.environ.get("SECS", "30"))
 RAGGED = os.environ.get("RAGGED", "0") == "1"
 REPS = int(os.environ.get("REPS", "1"))
 OPTS = [kv.split("=") for kv in os.environ.get("OPT", "").split(",") if kv]
+STAGGER_MS = float(os.environ.get("STAGGER_MS", "0"))
 POOL = 256 if RAGGED else 128
 
 if RAGGED:
@@ -74,6 +76,8 @@ def run(n_utt):
             return i, qd.budget(lens[i % POOL], 3.5)
 
     def one(k):
+        if STAGGER_MS and k:   # context k starts k x STAGGER_MS late (its refill beside the others' decode)
+            time.sleep(k * STAGGER_MS / 1000.0)
         return ctxs[k].run_stream_staged(take, bud_max, ignore_eos=True, slots=SLOTV[k])
     t0 = time.perf_counter()
     with cf.ThreadPoolExecutor(NCTX) as ex:
@@ -89,7 +93,8 @@ def run(n_utt):
 run(min(N_UTT, 2 * sum(SLOTV)))   # warm-up: graphs, buffers
 for _ in range(REPS):
     v, wall, st = run(N_UTT)
-    print(f"set {N_UTT} x {'U[5,30]' if RAGGED else SECS} s, {NCTX} ctx x {SLOTV} slots, opts {OPTS}: {v:.1f} RTFx  wall {wall:.3f} s  "
+    print(f"set {N_UTT} x {'U[5,30]' if RAGGED else SECS} s, {NCTX} ctx x {SLOTV} slots, opts {OPTS}, stagger {STAGGER_MS} ms: "
+          f"{v:.1f} RTFx  wall {wall:.3f} s  "
           f"per ctx (clips, refills, steps, prefill ms, decode ms, slot util) {st}", flush=True)
 for c in ctxs:
     c.close()
