@@ -578,15 +578,21 @@ def set_decode_bytes(hp, stats) -> float:
 
 def set_contexts(share: int, slots: int = 128) -> int:
     """Contexts per GPU for a rank's share of the utterance set (round 6,
-    tools/r6/set_run.py on one MI355X, RTFx; profiles/r6/set_contexts.txt):
-    125 utterances (N = 8) 1 x 125 slots 7849, 2 x 63 7603, 3 x 42 7369 --
-    every context's decode step costs about a full-width step, so splitting a
-    small share only adds steps (asymmetric splits 32 + 93 etc.: 7295-7546);
-    250: 2 x 125 8721, 3 x 84 8343; 500: 2 x 128 8688, 3 x 128 8736; 1000:
-    2 x 128 8678-8814, 3 x 128 8851-9097 alone but 8733 vs 8788 in the bench
-    line (ragged 9152 vs 8984): two, which also leaves a hardware queue for
-    RCCL's stream beside the default one (GPU_MAX_HW_QUEUES = 4)."""
-    return 1 if share <= slots else 2
+    tools/r6/set_run.py on one MI355X, RTFx; profiles/r6/set_contexts.txt,
+    profiles/r6/set_contexts_r6b.txt): 125 utterances (N = 8) 1 x 125 slots
+    7849, 2 x 63 7603, 3 x 42 7369 -- every context's decode step costs about
+    a full-width step, so splitting a small share only adds steps (asymmetric
+    splits 32 + 93 etc.: 7295-7546; two 63-slot contexts started 60-140 ms
+    apart: 7407-7784 against 8259 for one); 250: 2 x 125 8721, 3 x 84 8343;
+    500: 2 x 128 8688, 3 x 128 8736.  1000, after the round-6 kernels: three
+    contexts of 128 slots 9322-9558 against two 9276-9356 (set_run.py, four
+    runs each), 9343-9601 against 9279-9280 in the bench line, and the ragged
+    set 9753-9828 against 9387-9473 -- a third context's refill fills more of
+    the other two's decode gaps.  So: one context for a share that fits one,
+    two for up to two contexts' slots, three beyond (with the default stream
+    that is the box's four hardware queues, GPU_MAX_HW_QUEUES; RCCL's stream
+    shares one, idle while the streams run)."""
+    return 1 if share <= slots else 2 if share <= 2 * slots else 3
 
 
 def utterance_set_leg(args, m, rank, local, world, dist) -> dict:

@@ -265,9 +265,11 @@ def test_bench_gpus_counts_this_node_under_a_multinode_launch():
 
 
 def test_set_contexts_policy():
-    """bench.set_contexts (round 6, profiles/r6/set_contexts.txt): contexts per
-    GPU by the rank's share of the utterance set -- 1 x 125 at N = 8, two
-    contexts from N = 4 down"""
+    """bench.set_contexts (round 6, profiles/r6/set_contexts.txt and
+    set_contexts_r6b.txt): contexts per GPU by the rank's share of the
+    utterance set -- 1 x 125 at N = 8, 2 x 125 at N = 4, three contexts of 128
+    slots at N = 2 and 1"""
     import bench
-    assert [bench.set_contexts(-(-1000 // n)) for n in (1, 2, 4, 8)] == [2, 2, 2, 1]
-    assert bench.set_contexts(128) == 1 and bench.set_contexts(129) == 2 and bench.set_contexts(10000) == 2
+    assert [bench.set_contexts(-(-1000 // n)) for n in (1, 2, 4, 8)] == [3, 3, 2, 1]
+    assert bench.set_contexts(128) == 1 and bench.set_contexts(129) == 2 and bench.set_contexts(256) == 2
+    assert bench.set_contexts(257) == 3 and bench.set_contexts(10000) == 3
