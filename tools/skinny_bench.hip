@@ -109,11 +109,11 @@ int main(int argc, char **argv) {
                 time_cfg<2, 1, 8, EPI_F32, 4, 2>(g, ws, s, "MT2 NT1 CPW2");
                 time_cfg<2, 2, 8, EPI_F32, 4, 2>(g, ws, s, "MT2 NT2 CPW2");
                 time_cfg<1, 2, 8, EPI_F32, 4, 2>(g, ws, s, "MT1 NT2 CPW2");
-            } else if (sh.epi == EPI_F32) {
-                time_cfg<1, 1, 8, EPI_F32, 4, 3>(g, ws, s, "engine (MT1 NT1 CPW3)");
-                time_cfg<1, 2, 8, EPI_F32, 4, 3>(g, ws, s, "MT1 NT2 CPW3");
-                time_cfg<2, 1, 8, EPI_F32, 4, 0>(g, ws, s, "MT2 NT1 (chunk loop)");
-                time_cfg<2, 2, 8, EPI_F32, 4, 0>(g, ws, s, "MT2 NT2 (chunk loop)");
+            } else if (sh.epi == EPI_F32) {   // down: the engine's MT2 NT1 (its LDS chunk images of three chunks a
+                // wave exceed the LDS, so the chunk loop); round 6 measured every chunk in registers instead
+                // (a kernel form since removed): 10.57 us against 9.10 (profiles/r6/skinny_down_regs_ab.txt)
+                time_cfg<2, 1, 8, EPI_F32, 12, 0>(g, ws, s, "engine (MT2 chunk loop, wdef)");
+                time_cfg<1, 1, 8, EPI_F32, 12, 3>(g, ws, s, "MT1 NT1 CPW3 (LDS, wdef)");
             } else {
                 time_cfg<2, 2, 4, EPI_SWIGLU_F16, 4, 2>(g, ws, s, "engine (MT2 NT2 KW4 CPW2)");
                 time_cfg<4, 2, 8, EPI_SWIGLU_F16, 4, 1>(g, ws, s, "MT4 NT2 KW8 CPW1");
