@@ -586,7 +586,7 @@ OPTION_CASES = {
     "fx_vpf": (0, "bits", 1), "fx_vpf=1": (1, "bits", 1), "fx_vpf=3": (3, "bits", 1),
     "fa_exact_prefill": (0, "oracle", 1),
     "att_spl": (128, "bits", 16), "lmh": (0, "bits", 16), "skinny": (0, "oracle", 16),
-    "lmh@100": (0, "bits", 100),   # 65..128 rows: the one-launch LM head as two row-half launches
+    "lmh@100": (0, "bits", 100),   # 65..128 rows: the one-launch LM head (lmhead128_kernel) against the separate launches
     "skinny@100": (0, "oracle", 100),   # 65..128 rows: the skinny GEMMs' 128-row tilings (default) and the tiled GEMMs
     "skinny_wdef": (0, "bits", 16), "skinny_wdef@100": (0, "bits", 100),   # weights nontemporal (default: cache policy)
 }
