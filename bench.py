@@ -22,6 +22,13 @@ import os
 import sys
 import time
 
+# HIP hardware queues per process (HIP's default, 4 on the GPU box): the utterance set's
+# context streams, the default stream and RCCL's share queues beyond that -- with 8, three
+# contexts 9360-9375 -> 9626-9690 RTFx and four 9986-10031 (profiles/r6/hw_queues.txt).  The
+# HIP runtime reads it at its first call: set before anything below touches the GPU.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "qwen3-asr.cpp_amd", "python"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -588,11 +595,14 @@ def set_contexts(share: int, slots: int = 128) -> int:
     contexts of 128 slots 9322-9558 against two 9276-9356 (set_run.py, four
     runs each), 9343-9601 against 9279-9280 in the bench line, and the ragged
     set 9753-9828 against 9387-9473 -- a third context's refill fills more of
-    the other two's decode gaps.  So: one context for a share that fits one,
-    two for up to two contexts' slots, three beyond (with the default stream
-    that is the box's four hardware queues, GPU_MAX_HW_QUEUES; RCCL's stream
-    shares one, idle while the streams run)."""
-    return 1 if share <= slots else 2 if share <= 2 * slots else 3
+    the other two's decode gaps.  With 8 hardware queues a process
+    (GPU_MAX_HW_QUEUES, set at the top of this file; HIP's default 4 made
+    streams share queues): three contexts 9626-9690, four 9986-10031, the
+    ragged set 9802-9841 / 10078-10205 (profiles/r6/hw_queues.txt).  So: one
+    context for a share that fits one, two for up to two contexts' slots,
+    three up to four contexts' slots (each then refills at least twice, so
+    refills and decode interleave), four beyond."""
+    return 1 if share <= slots else 2 if share <= 2 * slots else 3 if share <= 4 * slots else 4
 
 
 def utterance_set_leg(args, m, rank, local, world, dist) -> dict:
