@@ -89,6 +89,12 @@ typedef struct {
 const char *qasr_last_error(void);                 /* thread-local last message */
 const char *qasr_version(void);
 int qasr_device_count(int *n);
+/* Self-check of the exact prefill attention's expf (fa_exact.hip px_expf_nonpos,
+ * the device expf's instruction sequence without its overflow clamp) against the
+ * device expf on every non-positive fp32 input (2^31 + 1 values) on `device`:
+ * *mismatches = the number of differing results (0 = the kernel's weights are
+ * ggml's expf bits).  No reference counterpart (a property of this build). */
+int qasr_check_expf_nonpos(int device, uint64_t *mismatches);
 
 /* ---- model ---------------------------------------------------------------- */
 /* device >= 0: upload weights to that HIP device.  device = QASR_HOST_ONLY:

@@ -424,6 +424,20 @@ extern "C" int qasr_device_count(int *n) {
     return 0;
 }
 
+extern "C" int qasr_check_expf_nonpos(int device, uint64_t *mismatches) {
+    if (!mismatches) return fail(QASR_ERR_ARG, "bad arguments");
+    int nd = 0, cur = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return fail(QASR_ERR_DEVICE, "no such HIP device");
+    (void)hipGetDevice(&cur);
+    if (hipSetDevice(device) != hipSuccess) return fail(QASR_ERR_DEVICE, "hipSetDevice failed");
+    unsigned long long bad = ~0ull;
+    const hipError_t e = check_expf_nonpos(&bad);
+    (void)hipSetDevice(cur);
+    if (e != hipSuccess) return fail(QASR_ERR_DEVICE, std::string("expf check: ") + hipGetErrorString(e));
+    *mismatches = bad;
+    return 0;
+}
+
 // -------------------------------------------------------------- loading
 struct Up {
     std::string name;

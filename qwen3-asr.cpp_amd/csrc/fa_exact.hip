@@ -126,6 +126,30 @@ __device__ __forceinline__ float px_expf_nonpos(float x) {
     const float r = __builtin_ldexpf(__builtin_amdgcn_exp2f(f), (int)e);
     return x < __uint_as_float(0xc2ce8ed0u) ? 0.0f : r;
 }
+// px_expf_nonpos against the device expf on every x <= 0: all 2^31 bit
+// patterns with the sign set, and +0 (qasr_check_expf_nonpos, a GPU test)
+__global__ __launch_bounds__(256) void expf_nonpos_check_kernel(unsigned long long *bad) {
+    const uint32_t base = (blockIdx.x * 256u + threadIdx.x) * 16u;
+    unsigned long long nb = 0;
+    for (uint32_t k = 0; k < 16; k++) {
+        const float x = __uint_as_float((base + k) | 0x80000000u);
+        const float a = expf(x), b = px_expf_nonpos(x);
+        if (__float_as_uint(a) != __float_as_uint(b) && !(a != a && b != b)) nb++;
+    }
+    if (base == 0 && __float_as_uint(expf(0.0f)) != __float_as_uint(px_expf_nonpos(0.0f))) nb++;
+    if (nb) atomicAdd(bad, nb);
+}
+hipError_t check_expf_nonpos(unsigned long long *mismatches) {
+    unsigned long long *d = nullptr;
+    hipError_t e = hipMalloc(&d, sizeof(*d));
+    if (e != hipSuccess) return e;
+    if ((e = hipMemset(d, 0, sizeof(*d))) == hipSuccess) {
+        hipLaunchKernelGGL(expf_nonpos_check_kernel, dim3(1u << 19), dim3(256), 0, 0, d);
+        if ((e = hipGetLastError()) == hipSuccess) e = hipMemcpy(mismatches, d, sizeof(*d), hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(d);
+    return e;
+}
 // the chain step of one row at key i of a batch whose new-maximum keys are
 // the bits of mk: x = the key's word (vs, or -ms at a new maximum)
 __device__ __forceinline__ half2v fx_key(half2v acc, uint32_t v, float x, uint32_t mk, int i) {

@@ -282,6 +282,9 @@ void launch_prefill_attention(const PrefillAttnArgs &a, hipStream_t s);
 // the same attention with ggml's CPU flash-attention numerics (fa_exact.hip):
 // keys in order per query row, fp16 V accumulator rounded after every key
 void launch_prefill_attention_exact(const PrefillAttnArgs &a, hipStream_t s);
+// fa_exact.hip: the exact prefill kernel's expf (px_expf_nonpos) against the
+// device expf on all 2^31 non-positive inputs, on the current device
+hipError_t check_expf_nonpos(unsigned long long *mismatches);
 
 // row stride (granules) of the fused exact attention's score granules
 __host__ __device__ inline int sgran_ld(int max_ctx) { return (max_ctx + 63) / 64 * 64; }

@@ -19,7 +19,7 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("QASR_LIB_OVERRIDE") or os.path.join(PKG_DIR, "libqasr.so")   # (override: diagnostic builds only)
 
 EXPORTS = [
-    "qasr_last_error", "qasr_version", "qasr_device_count",
+    "qasr_last_error", "qasr_version", "qasr_device_count", "qasr_check_expf_nonpos",
     "qasr_model_load", "qasr_model_free", "qasr_model_hparams", "qasr_model_device_bytes",
     "qasr_ctx_create", "qasr_ctx_free",
     "qasr_mel_frames", "qasr_encoder_frames", "qasr_prompt_len", "qasr_build_prompt",
@@ -86,6 +86,7 @@ def lib() -> C.CDLL:
         sig = {
             "qasr_last_error": ([], C.c_char_p), "qasr_version": ([], C.c_char_p),
             "qasr_device_count": ([IP], I),
+            "qasr_check_expf_nonpos": ([I, C.POINTER(C.c_uint64)], I),
             "qasr_model_load": ([C.c_char_p, I, C.POINTER(P)], I), "qasr_model_free": ([P], None),
             "qasr_model_hparams": ([P, C.POINTER(Hparams)], I), "qasr_model_device_bytes": ([P], C.c_int64),
             "qasr_ctx_create": ([P, I, I, C.POINTER(P)], I), "qasr_ctx_free": ([P], None),

@@ -28,6 +28,17 @@ def tiny(gpu, tiny_gguf):
     m.close()
 
 
+def test_prefill_expf_replacement_is_bit_exact(gpu):
+    """fa_exact.hip's exact prefill attention takes its weights through
+    px_expf_nonpos (the device expf's instruction sequence without the overflow
+    clamp, round 6): on every non-positive fp32 input its result must be the
+    device expf's bits, so the kernel's (ms, vs) stay the round-5 kernel's"""
+    import ctypes
+    bad = ctypes.c_uint64(12345)
+    assert qasr.lib().qasr_check_expf_nonpos(0, ctypes.byref(bad)) == 0, qasr.lib().qasr_last_error()
+    assert bad.value == 0, bad.value
+
+
 # ------------------------------------------------------------------ mel
 @pytest.mark.parametrize("n", [0, 1, 159, 160, 161, 401, SR, int(2.5 * SR), int(7.3 * SR)])
 def test_mel_matches_oracle(tiny, n):
