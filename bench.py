@@ -598,11 +598,12 @@ def set_contexts(share: int, slots: int = 128) -> int:
     the other two's decode gaps.  With 8 hardware queues a process
     (GPU_MAX_HW_QUEUES, set at the top of this file; HIP's default 4 made
     streams share queues): three contexts 9626-9690, four 9986-10031, the
-    ragged set 9802-9841 / 10078-10205 (profiles/r6/hw_queues.txt).  So: one
-    context for a share that fits one, two for up to two contexts' slots,
-    three up to four contexts' slots (each then refills at least twice, so
-    refills and decode interleave), four beyond."""
-    return 1 if share <= slots else 2 if share <= 2 * slots else 3 if share <= 4 * slots else 4
+    ragged set 9802-9841 / 10078-10205 (profiles/r6/hw_queues.txt); five
+    9690-9776, six (16 queues) 9370-9399; a 500-utterance share (N = 2) four
+    contexts 9936-9950 against three 8492-9362 (profiles/r6/
+    set_contexts_hwq8.txt).  So: one context for a share that fits one, two
+    for up to two contexts' slots, four beyond."""
+    return 1 if share <= slots else 2 if share <= 2 * slots else 4
 
 
 def utterance_set_leg(args, m, rank, local, world, dist) -> dict:

@@ -267,13 +267,12 @@ def test_bench_gpus_counts_this_node_under_a_multinode_launch():
 def test_set_contexts_policy():
     """bench.set_contexts (round 6, profiles/r6/set_contexts.txt and
     set_contexts_r6b.txt): contexts per GPU by the rank's share of the
-    utterance set -- 1 x 125 at N = 8, 2 x 125 at N = 4, 3 x 128 at N = 2,
+    utterance set -- 1 x 125 at N = 8, 2 x 125 at N = 4, 4 x 125 at N = 2,
     4 x 128 at N = 1"""
     import bench
-    assert [bench.set_contexts(-(-1000 // n)) for n in (1, 2, 4, 8)] == [4, 3, 2, 1]
+    assert [bench.set_contexts(-(-1000 // n)) for n in (1, 2, 4, 8)] == [4, 4, 2, 1]
     assert bench.set_contexts(128) == 1 and bench.set_contexts(129) == 2 and bench.set_contexts(256) == 2
-    assert bench.set_contexts(257) == 3 and bench.set_contexts(512) == 3 and bench.set_contexts(513) == 4
-    assert bench.set_contexts(10000) == 4
+    assert bench.set_contexts(257) == 4 and bench.set_contexts(10000) == 4
 
 
 def test_bench_raises_hw_queues():
