@@ -81,9 +81,9 @@ __device__ __forceinline__ void g8_barrier() {
 // 8 B (fp16) a lane: whole 128-B (64-B) row segments per 8 lanes, ~1.2-1.6x
 // faster than element stores from the MFMA layout (tools/micro/g8_bench.hip).
 // The residual rows of the next quadrant are requested before this one is
-// transposed (their HBM latency off the store path; row index clamped so the
-// loads need no branch).  Per-element arithmetic as gemm_epilogue.
-template <int EPI>
+// transposed (their HBM latency off the store path; every row of a tile is < M,
+// the host guarantees M >= 256).  Per-element arithmetic as gemm_epilogue.
+template <int EPI, bool RESV, bool PEV, bool SHIFT>
 __device__ __forceinline__ void g8_epilogue(const GemmArgs &g, floatx4 (&acc)[2][2][4][2], uint16_t *smem, int m0, int n0,
                                             int mlo, int nlo, int wr, int wc, int lane) {
     const int M = g.M;
@@ -99,25 +99,28 @@ __device__ __forceinline__ void g8_epilogue(const GemmArgs &g, floatx4 (&acc)[2]
         return;
     }
     constexpr bool SWIGLU = EPI == EPI_SWIGLU_F16 || EPI == EPI_SWIGLU_F32;
-    constexpr bool RES = EPI == EPI_F32;
     float *st = (float *)smem + (wr * 4 + wc) * 2048;   // this wave's [64][32] fp32 quadrant
     const int lr0 = SWIGLU ? (lane >> 2) : (lane >> 3);   // this lane's first row of a quadrant
-    floatx4 rcur[8], rnext[8];
-    auto load_res = [&](floatx4 (&dst)[8], int q) {
+    floatx4 rcur[RESV ? 8 : 1], rnext[RESV ? 8 : 1];
+    auto load_res = [&](floatx4 (&dst)[RESV ? 8 : 1], int q) {
         const int col = n0 + (q & 1) * 128 + wc * 32 + 4 * (lane & 7);
         const int r0 = m0 + (q >> 1) * 128 + wr * 64 + lr0;
 #pragma unroll
-        for (int it = 0; it < 8; it++) dst[it] = *(const floatx4 *)(g.res + (long)min(r0 + 8 * it, M - 1) * g.ldr + col);
+        for (int it = 0; it < 8; it++) dst[it] = *(const floatx4 *)(g.res + (long)(r0 + 8 * it) * g.ldr + col);
     };
-    const bool has_res = RES && g.res != nullptr;
-    if (has_res) load_res(rcur, 0);
+    if constexpr (RESV) load_res(rcur, 0);
+    floatx4 bias2[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+    if (!SWIGLU && g.bias)
+#pragma unroll
+        for (int j = 0; j < 2; j++) bias2[j] = *(const floatx4 *)(g.bias + n0 + j * 128 + wc * 32 + 4 * (lane & 7));
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int i = q >> 1, j = q & 1;
-        if (has_res && q < 3) load_res(rnext, q + 1);
+        if constexpr (RESV)
+            if (q < 3) load_res(rnext, q + 1);
         const int c0 = n0 + j * 128 + wc * 32;   // this wave's 32-column group
         const int r0 = m0 + i * 128 + wr * 64;
-        if (c0 >= nlo) {                           // (a shifted last column tile leaves the first ones to its neighbour)
+        if (!SHIFT || c0 >= nlo) {                 // (a shifted last column tile leaves the first ones to its neighbour)
 #pragma unroll
             for (int fm = 0; fm < 4; fm++)
 #pragma unroll
@@ -131,7 +134,7 @@ __device__ __forceinline__ void g8_epilogue(const GemmArgs &g, floatx4 (&acc)[2]
                     const int lr = lr0 + 16 * it, row = r0 + lr;
                     const floatx4 gt = *(const floatx4 *)(st + lr * 32 + 4 * (lane & 3));
                     const floatx4 up = *(const floatx4 *)(st + lr * 32 + 16 + 4 * (lane & 3));
-                    if (row < mlo || row >= M) continue;
+                    if (SHIFT && row < mlo) continue;
                     const long o = c0 / 2 + 4 * (lane & 3);
                     floatx4 v;
 #pragma unroll
@@ -145,38 +148,97 @@ __device__ __forceinline__ void g8_epilogue(const GemmArgs &g, floatx4 (&acc)[2]
                 }
             } else {
                 const int col = c0 + 4 * (lane & 7);
-                floatx4 bias = floatx4{0.f, 0.f, 0.f, 0.f};
-                if (g.bias) bias = *(const floatx4 *)(g.bias + col);
+                if constexpr (EPI == EPI_GELU_F16 || EPI == EPI_F16) {
+                    // four rows at a time (GELU: 16 table reads in flight, 32 spilled registers)
 #pragma unroll
-                for (int it = 0; it < 8; it++) {
-                    const int lr = lr0 + 8 * it, row = r0 + lr;
-                    floatx4 v = *(const floatx4 *)(st + lr * 32 + 4 * (lane & 7));
-                    if (row < mlo || row >= M) continue;
-                    if (g.bias)
+                    for (int hh = 0; hh < 2; hh++) {
+                        uint32_t h[4][4];
 #pragma unroll
-                        for (int e = 0; e < 4; e++) v[e] = fadd_rn(v[e], bias[e]);
-                    if constexpr (EPI == EPI_GELU_F16 || EPI == EPI_F16) {
-                        uint32_t h[4];
+                        for (int u = 0; u < 4; u++) {
+                            const int it = 4 * hh + u;
+                            floatx4 v = *(const floatx4 *)(st + (lr0 + 8 * it) * 32 + 4 * (lane & 7));
 #pragma unroll
-                        for (int e = 0; e < 4; e++) h[e] = EPI == EPI_GELU_F16 ? gelu_lut_bits(v[e], g.gelu) : f_to_u16(v[e]);
-                        *(uint2 *)(g.out_f16 + (long)row * g.ldo16 + col) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
-                    } else {
-                        if (g.pe) {
-                            const floatx4 p = *(const floatx4 *)(g.pe + (long)g.pe_pos[row] * g.N + col);
-#pragma unroll
-                            for (int e = 0; e < 4; e++) v[e] = fadd_rn(v[e], p[e]);
+                            for (int e = 0; e < 4; e++) {
+                                const float x = g.bias ? fadd_rn(v[e], bias2[j][e]) : v[e];
+                                const uint32_t b16 = f_to_u16(x);
+                                if constexpr (EPI == EPI_GELU_F16) {
+                                    // gelu_lut_bits with its selects as bit masks: a select on a
+                                    // loaded value becomes a branch around the load (one wait each)
+                                    const uint32_t t = g.gelu[b16];
+                                    const uint32_t hi = 0u - (uint32_t)(x >= 10.0f), lo = 0u - (uint32_t)(x <= -10.0f);
+                                    h[u][e] = ((t & ~hi) | (b16 & hi)) & ~lo;
+                                } else {
+                                    h[u][e] = b16;
+                                }
+                            }
                         }
-                        if (has_res)
 #pragma unroll
-                            for (int e = 0; e < 4; e++) v[e] = fadd_rn(v[e], rcur[it][e]);
+                        for (int u = 0; u < 4; u++) {
+                            const int row = r0 + lr0 + 8 * (4 * hh + u);
+                            if (SHIFT && row < mlo) continue;
+                            *(uint2 *)(g.out_f16 + (long)row * g.ldo16 + col) =
+                                make_uint2(h[u][0] | (h[u][1] << 16), h[u][2] | (h[u][3] << 16));
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int it = 0; it < 8; it++) {
+                        const int row = r0 + lr0 + 8 * it;
+                        floatx4 v = *(const floatx4 *)(st + (lr0 + 8 * it) * 32 + 4 * (lane & 7));
+                        if (SHIFT && row < mlo) continue;
+                        floatx4 pv = floatx4{0.f, 0.f, 0.f, 0.f};
+                        if constexpr (PEV) pv = *(const floatx4 *)(g.pe + (long)g.pe_pos[row] * g.N + col);   // conv_out only
+#pragma unroll
+                        for (int e = 0; e < 4; e++) {
+                            if (g.bias) v[e] = fadd_rn(v[e], bias2[j][e]);
+                            if constexpr (PEV) v[e] = fadd_rn(v[e], pv[e]);
+                            if constexpr (RESV) v[e] = fadd_rn(v[e], rcur[it][e]);
+                        }
                         *(floatx4 *)(g.out_f32 + (long)row * g.ldo + col) = v;
                     }
                 }
             }
         }
-        if (has_res && q < 3)
+        if constexpr (RESV)
+            if (q < 3)
 #pragma unroll
-            for (int it = 0; it < 8; it++) rcur[it] = rnext[it];
+                for (int it = 0; it < 8; it++) rcur[it] = rnext[it];
+    }
+}
+
+// The epilogue in straight-line versions: with a runtime residual / PE / shifted-tile
+// test inside, the compiler's wait analysis merged paths with different numbers of
+// stores and put vmcnt(0) -- one store-to-ack round trip -- ahead of every store
+// (round 6).  Each version issues its loads (bias at entry, residual one quadrant
+// ahead, LUT entries four rows at a time) before the stores that precede their use.
+// 64 x 30 s, same box (profiles/r6/g8_epilogue_pipeline_ab.txt): encode 41.8 -> 32.6 ms,
+// prefill 70.1 -> 60.2, utterance set 9330 -> 10036-10063 RTFx; epilogue cost over the
+// bare loop at prefill qkv 184 -> 94 us (fp32 out), f16 114 -> 44 (g8_epilogue_waits.txt).
+template <int EPI>
+__device__ __forceinline__ void g8_epilogue_any(const GemmArgs &g, floatx4 (&acc)[2][2][4][2], uint16_t *smem, int m0, int n0,
+                                                int mlo, int nlo, int wr, int wc, int lane) {
+    const bool shift = m0 != mlo || n0 != nlo;
+    if constexpr (EPI == EPI_F32) {
+        if (g.res) {
+            if (g.pe) {
+                if (shift) g8_epilogue<EPI, true, true, true>(g, acc, smem, m0, n0, mlo, nlo, wr, wc, lane);
+                else g8_epilogue<EPI, true, true, false>(g, acc, smem, m0, n0, mlo, nlo, wr, wc, lane);
+            } else {
+                if (shift) g8_epilogue<EPI, true, false, true>(g, acc, smem, m0, n0, mlo, nlo, wr, wc, lane);
+                else g8_epilogue<EPI, true, false, false>(g, acc, smem, m0, n0, mlo, nlo, wr, wc, lane);
+            }
+        } else {
+            if (g.pe) {
+                if (shift) g8_epilogue<EPI, false, true, true>(g, acc, smem, m0, n0, mlo, nlo, wr, wc, lane);
+                else g8_epilogue<EPI, false, true, false>(g, acc, smem, m0, n0, mlo, nlo, wr, wc, lane);
+            } else {
+                if (shift) g8_epilogue<EPI, false, false, true>(g, acc, smem, m0, n0, mlo, nlo, wr, wc, lane);
+                else g8_epilogue<EPI, false, false, false>(g, acc, smem, m0, n0, mlo, nlo, wr, wc, lane);
+            }
+        }
+    } else {
+        if (shift) g8_epilogue<EPI, false, false, true>(g, acc, smem, m0, n0, mlo, nlo, wr, wc, lane);
+        else g8_epilogue<EPI, false, false, false>(g, acc, smem, m0, n0, mlo, nlo, wr, wc, lane);
     }
 }
 
@@ -389,7 +451,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
     iteration(niter - 1, std::true_type{});
     if (wr == 0) g8_barrier();   // balance group 1's extra barrier
 
-    g8_epilogue<EPI>(g, acc, smem, m0, n0, mlo, nlo, wr, wc, lane);
+    g8_epilogue_any<EPI>(g, acc, smem, m0, n0, mlo, nlo, wr, wc, lane);
 }
 
 template <int EPI, int AMODE = AM_DENSE>
