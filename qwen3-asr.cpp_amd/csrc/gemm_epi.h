@@ -71,29 +71,76 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs &g, floatx4 (&acc)[
                 if (row < M && (lane & 15) == 0) atomicMax(g.amax + row, best);
             }
     } else {
+        // Every load the values need (bias at entry; residual / PE / GELU table one
+        // 16-row block at a time) is issued before the stores that precede its use: a
+        // load behind a store makes its use wait for that store's write to complete, and
+        // the per-element form compiled to vmcnt(0) ahead of every store (round 6, as
+        // gemm8p.h's epilogue).
+        float bcol[FN];
 #pragma unroll
-        for (int i = 0; i < FM; i++)
+        for (int j = 0; j < FN; j++) bcol[j] = g.bias ? g.bias[cbase + j * 16] : 0.0f;
+        auto stores = [&](int i, const float (&v)[FN][4]) {
 #pragma unroll
             for (int j = 0; j < FN; j++) {
                 const int col = cbase + j * 16;
-                const float bcol = g.bias ? g.bias[col] : 0.0f;
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const int row = rbase + i * 16 + r;
                     if (row >= M) continue;
-                    float v = acc[i][j][r];
-                    if (g.bias) v = fadd_rn(v, bcol);
-                    if constexpr (EPI == EPI_GELU_F16) {
-                        g.out_f16[(long)row * g.ldo16 + col] = f_to_u16(gelu_lut(v, g.gelu));
-                    } else if constexpr (EPI == EPI_F16) {
-                        g.out_f16[(long)row * g.ldo16 + col] = f_to_u16(v);
-                    } else {
-                        if (g.pe) v = fadd_rn(v, g.pe[(long)g.pe_pos[row] * g.N + col]);
-                        if (g.res) v = fadd_rn(v, g.res[(long)row * g.ldr + col]);
-                        g.out_f32[(long)row * g.ldo + col] = v;
-                    }
+                    if constexpr (EPI == EPI_GELU_F16 || EPI == EPI_F16) g.out_f16[(long)row * g.ldo16 + col] = (uint16_t)__float_as_uint(v[j][r]);
+                    else g.out_f32[(long)row * g.ldo + col] = v[j][r];
                 }
             }
+        };
+#pragma unroll
+        for (int i = 0; i < FM; i++) {
+            float v[FN][4];
+#pragma unroll
+            for (int j = 0; j < FN; j++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) v[j][r] = g.bias ? fadd_rn(acc[i][j][r], bcol[j]) : acc[i][j][r];
+            if constexpr (EPI == EPI_GELU_F16 || EPI == EPI_F16) {
+                // fp16 bits carried in the float array (bit cast) up to the stores
+#pragma unroll
+                for (int j = 0; j < FN; j++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const float x = v[j][r];
+                        const uint32_t b16 = f_to_u16(x);
+                        uint32_t h = b16;
+                        if constexpr (EPI == EPI_GELU_F16) {
+                            // gelu_lut's selects as bit masks (a select on a loaded value
+                            // becomes a branch around the load); the table read clamped into
+                            // the table for every value
+                            const uint32_t t = g.gelu[b16];
+                            const uint32_t hi = 0u - (uint32_t)(x >= 10.0f), lo = 0u - (uint32_t)(x <= -10.0f);
+                            h = ((t & ~hi) | (b16 & hi)) & ~lo;
+                        }
+                        v[j][r] = __uint_as_float(h);
+                    }
+                stores(i, v);
+            } else if (g.pe || g.res) {
+                float pv[FN][4], rv[FN][4];
+#pragma unroll
+                for (int j = 0; j < FN; j++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int row = min(rbase + i * 16 + r, M - 1), col = cbase + j * 16;
+                        pv[j][r] = g.pe ? g.pe[(long)g.pe_pos[row] * g.N + col] : 0.0f;
+                        rv[j][r] = g.res ? g.res[(long)row * g.ldr + col] : 0.0f;
+                    }
+#pragma unroll
+                for (int j = 0; j < FN; j++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        if (g.pe) v[j][r] = fadd_rn(v[j][r], pv[j][r]);
+                        if (g.res) v[j][r] = fadd_rn(v[j][r], rv[j][r]);
+                    }
+                stores(i, v);
+            } else {
+                stores(i, v);
+            }
+        }
     }
 }
 
