@@ -538,6 +538,21 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
     auto process = [&](auto bc, int cgi) {
         constexpr int b = decltype(bc)::value;
         const int col0 = cgi * CPW;
+        // bias / residual of this group's outputs requested ahead of the sums and the
+        // stores: a load between two stores makes the later store wait for the earlier
+        // one's write (vmcnt in issue order), one round trip per output column (round 6)
+        float bvv[CPW], rvv[CPW][MR];
+        if constexpr (EPI == EPI_F32 || EPI == EPI_F16) {
+            const float *zero = (const float *)g8_zero_line;
+#pragma unroll
+            for (int c = 0; c < CPW; c++) {
+                const int oc = min(col0 + c, g.N - 1);
+                bvv[c] = *(g.bias ? g.bias + oc : zero);
+                if constexpr (EPI == EPI_F32)
+#pragma unroll
+                    for (int m = 0; m < MR; m++) rvv[c][m] = *(g.res ? g.res + (long)min(m, g.M - 1) * g.ldr + oc : zero);
+            }
+        }
         float acc[CPW][NR][MR];
 #pragma unroll
         for (int c = 0; c < CPW; c++)
@@ -578,11 +593,11 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs g) {
                         g.out_f16[(long)m * g.ldo16 + o] = f_to_u16(silu_f(v[0]) * v[1]);
                     } else {
                         float y = v[0];
-                        if (g.bias) y = fadd_rn(y, g.bias[o]);
+                        if (g.bias) y = fadd_rn(y, bvv[c]);
                         if constexpr (EPI == EPI_F16) {
                             g.out_f16[(long)m * g.ldo16 + o] = f_to_u16(y);
                         } else {
-                            if (g.res) y = fadd_rn(y, g.res[(long)m * g.ldr + o]);
+                            if (g.res) y = fadd_rn(y, rvv[c][m]);
                             g.out_f32[(long)m * g.ldo + o] = y;
                         }
                     }
