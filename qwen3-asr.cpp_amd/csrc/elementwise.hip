@@ -110,12 +110,18 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict_
     if (row >= M) return;
     constexpr int PER = (D + 63) / 64;
     const float *xr = x + (long)row * D;
-    float v[PER];
+    float v[PER], wv[PER], bv[PER];
+    // w / b requested with x (from x's own row when absent: the value is then unused),
+    // so the stores below have no load between them (a load there made each store wait
+    // for the previous one's write: round 6, as the GEMM epilogues)
+    const float *wp = w ? w : xr, *bp = b ? b : xr;
     double s = 0.0;
 #pragma unroll
     for (int i = 0; i < PER; i++) {
         const int k = lane + 64 * i;
         v[i] = k < D ? xr[k] : 0.0f;
+        wv[i] = k < D ? wp[k] : 0.0f;
+        bv[i] = k < D ? bp[k] : 0.0f;
         s += (double)v[i];
     }
     s = wave_sum_d(s);
@@ -137,8 +143,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict_
         const int k = lane + 64 * i;
         if (k < D) {
             float t = fmul_rn(v[i], scale);
-            if (w) t = fmul_rn(t, w[k]);
-            if (b) t = fadd_rn(t, b[k]);
+            if (w) t = fmul_rn(t, wv[i]);
+            if (b) t = fadd_rn(t, bv[i]);
             if (y32) y32[(long)row * D + k] = t;
             else y[(long)row * D + k] = f_to_u16(t);
         }
